@@ -1,0 +1,133 @@
+#!/usr/bin/env python3
+"""Headline benchmark: R2D2 learner steps/s on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config atari57|reference|...]
+
+* Config (default ``atari57``): the R2D2 paper shapes -- batch 64 sequences of 80 steps
+  (burn-in 40 + learning 40), n-step 5, value rescaling, IS weights, centered RMSprop -- on the
+  reference network (``/root/reference/model.py``: 3-conv torso, LSTM 256, dueling head;
+  2,037,095 parameters), synthetic 84x84x4 uint8 frames in a 1M-row HBM replay, random-init
+  weights.  ``--config reference`` runs the reference's own shapes (B=8, T=20, n=3).
+* A timed step is the FULL learner update: prioritized sample from the sum tree, torso on every
+  frame of both nets, LSTM over every chain, head, TD loss, complete backward, (DP all-reduce),
+  optimizer, weight repack, priority write-back + sum-tree repair.
+* Weak scaling: each rank runs the data-parallel learner on its own replay shard with the
+  per-GPU batch fixed; the optimizer step is synchronous (one all-reduce per step).
+  ``value`` = aggregate sequence-batches/s = world * optimizer steps/s, i.e. learner steps/s
+  normalised to the per-GPU batch (the paper's 5 updates/s is per B=64 batch).
+* Timing: W untimed warmup steps, then exactly K steps bracketed by barrier + synchronize on
+  both sides; the max over ranks is reported by rank 0 as one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+BASELINES = {
+    "atari57": 5.0,      # R2D2 paper: ~5 learner updates/s at B=64 x 80 (1 GPU)
+    "reference": 18.6,   # reference learner.py train() on 8-vCPU (measured in SURVEY §6)
+}
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="atari57")
+    ap.add_argument("--capacity", type=int, default=0)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--target-mode", default="")
+    ap.add_argument("--profile-phases", action="store_true")
+    args = ap.parse_args(argv)
+
+    import torch
+    import torch.distributed as dist
+    from pytorch_r2d2_amd.config import get_config
+    from pytorch_r2d2_amd.engine.replay_hbm import HBMReplay
+    from pytorch_r2d2_amd.engine.learner_engine import LearnerEngine
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    overrides = {"seed": 1234 + rank}
+    if args.target_mode:
+        overrides["learner.target_mode"] = args.target_mode
+    cfg = get_config(args.config, **overrides)
+    cap = args.capacity or cfg.replay.capacity
+    replay = HBMReplay(cfg, device, capacity=cap)
+    replay.fill_synthetic(episode_len=400, seed=rank)
+    eng = LearnerEngine(cfg, replay, device, rank=rank, world=world,
+                        process_group=dist.group.WORLD if world > 1 else None)
+    use_graph = cfg.learner.use_graph and not args.no_graph
+    if use_graph:
+        eng.capture(warmup=2)
+    for _ in range(args.warmup):
+        eng.step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.step()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], device=device, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    ms = dt / args.steps * 1e3
+    opt_steps = args.steps / dt
+    value = opt_steps * world
+    loss = eng.loss_value()
+    rc, lc = cfg.replay, cfg.learner
+    base = BASELINES.get(args.config)
+    if rank == 0:
+        out = {
+            "metric": "learner_steps_per_sec",
+            "value": round(value, 3),
+            "unit": "learner steps/s (B=%d x %d-step sequences per step per GPU)" % (lc.batch_size, rc.seq_len),
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / base, 3) if base else None,
+            "dtype": "bf16",
+            "data": "synthetic 84x84x4 uint8 frames in HBM replay, random-init weights",
+            "config": {
+                "model": "r2d2-qnet (reference model.py: conv32x3 + LSTM%d + dueling, %d actions)"
+                         % (cfg.model.hidden, cfg.model.n_actions),
+                "preset": cfg.name,
+                "global_batch": lc.batch_size * world,
+                "seq_len": rc.seq_len,
+                "burn_in": rc.burn_in,
+                "n_step": rc.n_step,
+                "target_mode": lc.target_mode,
+                "replay_rows_per_gpu": replay.capacity,
+                "parallelism": "dp%d" % world,
+                "hip_graph": bool(use_graph),
+            },
+            "optimizer_steps_per_sec": round(opt_steps, 3),
+            "sequences_per_sec": round(opt_steps * lc.batch_size * world, 1),
+            "final_loss": loss,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,76 @@
+// Shared helpers for the gfx950 (MI355X, CDNA4) kernels of pytorch_r2d2_amd.
+//
+// Conventions used by every kernel in csrc/kernels:
+//  * wave = 64 lanes; blocks are multiples of 64 threads.
+//  * bf16 is the clang native __bf16 (fptrunc lowers to v_cvt_pk_bf16_f32 on gfx950).
+//  * MFMA tile = v_mfma_f32_32x32x16_bf16.  Lane l holds A[m=l&31][k=8*(l>>5)+j] and
+//    B[k=8*(l>>5)+j][n=l&31] (j=0..7); accumulator register r holds
+//    C[m=(r&3)+8*(r>>2)+4*(l>>5)][n=l&31].
+//  * every launcher is `extern "C"`, takes raw device pointers and a hipStream_t, never
+//    allocates or synchronises (safe under hipGraph stream capture).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+#define R2_WAVE 64
+
+#define R2_CHECK_LAUNCH() \
+  do { hipError_t e__ = hipGetLastError(); if (e__ != hipSuccess) return (int)e__; } while (0)
+
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+__device__ __forceinline__ float tanhf_(float x) {
+  // tanh via exp; saturates cleanly for large |x|
+  float e = __expf(-2.f * fabsf(x));
+  float t = (1.f - e) / (1.f + e);
+  return copysignf(t, x);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// 8 unsigned bytes (two dwords) -> 8 bf16 (exact: integers 0..255 are representable)
+__device__ __forceinline__ bf16x8 u8x8_to_bf16(uint32_t lo, uint32_t hi) {
+  bf16x8 r;
+  r[0] = (bf16)(float)(lo & 0xff);
+  r[1] = (bf16)(float)((lo >> 8) & 0xff);
+  r[2] = (bf16)(float)((lo >> 16) & 0xff);
+  r[3] = (bf16)(float)(lo >> 24);
+  r[4] = (bf16)(float)(hi & 0xff);
+  r[5] = (bf16)(float)((hi >> 8) & 0xff);
+  r[6] = (bf16)(float)((hi >> 16) & 0xff);
+  r[7] = (bf16)(float)(hi >> 24);
+  return r;
+}
+
+// counter-based RNG (splitmix64 finaliser) -> uniform float in [0,1)
+__device__ __forceinline__ uint64_t r2_mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ float r2_uniform(uint64_t seed, uint64_t ctr, uint64_t idx) {
+  uint64_t z = r2_mix64(seed ^ r2_mix64(ctr * 0x100000001B3ull + idx));
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}

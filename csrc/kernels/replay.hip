@@ -1,0 +1,309 @@
+// HBM-resident prioritized sequence replay kernels (gfx950).
+//
+// Reference: replay_memory.py:58-262 keeps the replay in host numpy, samples with
+// WeightedRandomSampler -> torch.multinomial on CPU after an O(capacity) scan of is_seq_start
+// (replay_memory.py:225-232), builds batches with 2*T*B Python get_stacked_state calls and
+// ships ~36 MB H2D per step (replay_memory.py:236-260).  Here:
+//
+//  * the ring lives in HBM and is split into `n_sub` contiguous sub-rings (one per actor env)
+//    so every episode is contiguous; row(start, t) wraps inside the start's sub-ring;
+//  * sequence sampling weights sit in a 64-ary sum tree whose leaf level IS the per-row
+//    `sequence_priority` array (0 where no sequence starts).  A 64-ary tree is 4 levels for
+//    16M rows: one wave per sample reads 64 children with one coalesced load per level and
+//    finds the child with a wave prefix-scan -- O(B log64 N), no host involvement;
+//  * priority refresh after a train step recomputes the eta-mix of EVERY sequence whose
+//    window overlaps an updated row (fixes Q8/Q9: replay_memory.py:204-213 refreshes idx-i
+//    instead of idx+i and ignores ring wraparound at :186-188), appends the changed leaves to
+//    a dirty list, and the tree is repaired bottom-up one level per launch (parents are
+//    recomputed from children -- deterministic, no float drift, duplicates are benign).
+#include "../common.h"
+
+#define TREE_MAX_LEVELS 8
+
+struct TreeGeom {
+  int64_t off[TREE_MAX_LEVELS];
+  int64_t size[TREE_MAX_LEVELS];
+  int levels;
+};
+
+__device__ __forceinline__ int ring_row_s(int start, int t, int cap_e) {
+  const int base = start - start % cap_e;
+  int r = (start - base + t) % cap_e;
+  if (r < 0) r += cap_e;
+  return base + r;
+}
+
+__device__ __forceinline__ float wave_incl_scan(float v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float n = __shfl_up(v, o, 64);
+    if (lane >= o) v += n;
+  }
+  return v;
+}
+
+// ---- sampling: one wave per sample, stratified over [0, total)
+__global__ void tree_sample_kernel(const float* __restrict__ tree, TreeGeom g, int B,
+                                   uint64_t seed, const int64_t* __restrict__ step,
+                                   int* __restrict__ out_idx, float* __restrict__ out_prob) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const float total = tree[g.off[g.levels - 1]];
+  const uint64_t ctr = step ? (uint64_t)(*step) : 0ull;
+  float u = ((float)b + r2_uniform(seed, ctr, (uint64_t)b)) / (float)B * total;
+  int64_t node = 0;
+  for (int lvl = g.levels - 1; lvl >= 1; --lvl) {
+    const int64_t c = node * 64 + lane;
+    const float v = (c < g.size[lvl - 1]) ? tree[g.off[lvl - 1] + c] : 0.f;
+    const float incl = wave_incl_scan(v, lane);
+    const float excl = incl - v;
+    const unsigned long long hit = __ballot(incl > u && v > 0.f);
+    int pick;
+    if (hit) {
+      pick = __ffsll((long long)hit) - 1;
+    } else {  // float round-off past the end: take the last non-empty child
+      const unsigned long long nz = __ballot(v > 0.f);
+      pick = nz ? 63 - __clzll((long long)nz) : 0;
+    }
+    const float ex = __shfl(excl, pick, 64);
+    const float pv = __shfl(v, pick, 64);
+    u = fminf(fmaxf(u - ex, 0.f), pv * 0.99999f);
+    node = node * 64 + pick;
+  }
+  if (lane == 0) {
+    out_idx[b] = (int)node;
+    if (out_prob) out_prob[b] = total > 0.f ? tree[node] / total : 0.f;
+  }
+}
+
+// ---- rebuild one level from its children (full pass; used after bulk fills)
+__global__ void tree_rebuild_level_kernel(float* __restrict__ tree, TreeGeom g, int lvl) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const float* child = tree + g.off[lvl];
+  float* parent = tree + g.off[lvl + 1];
+  for (int64_t p = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); p < g.size[lvl + 1];
+       p += nwaves) {
+    const int64_t c = p * 64 + lane;
+    float v = c < g.size[lvl] ? child[c] : 0.f;
+    v = wave_sum(v);
+    if (lane == 0) parent[p] = v;
+  }
+}
+
+// ---- repair ancestors of dirty leaves at level lvl+1
+__global__ void tree_update_level_kernel(float* __restrict__ tree, TreeGeom g, int lvl,
+                                         const int* __restrict__ dirty,
+                                         const int* __restrict__ count, int max_dirty) {
+  const int lane = threadIdx.x & 63;
+  const int n = min(*count, max_dirty);
+  const int nwaves = gridDim.x * (blockDim.x >> 6);
+  const float* child = tree + g.off[lvl];
+  float* parent = tree + g.off[lvl + 1];
+  for (int e = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); e < n; e += nwaves) {
+    const int64_t node = ((int64_t)dirty[e]) >> (6 * lvl);
+    const int64_t p = node >> 6;
+    const int64_t c = p * 64 + lane;
+    float v = c < g.size[lvl] ? child[c] : 0.f;
+    v = wave_sum(v);
+    if (lane == 0) parent[p] = v;
+  }
+}
+
+// ---- eta-mixed sequence priority of every marked start overlapping the updated window
+// For sampled start s_b the learner rewrote rows [s_b + upd_lo, s_b + upd_hi).  Sequence s
+// (rows [s, s+T)) overlaps iff s in (s_b + upd_lo - T, s_b + upd_hi).
+__global__ void seqprio_refresh_kernel(const int* __restrict__ starts, int B,
+                                       const uint8_t* __restrict__ is_start,
+                                       const float* __restrict__ priority,
+                                       float* __restrict__ leaves, int T, int upd_lo,
+                                       int upd_hi, int cap_e, float eta,
+                                       int* __restrict__ dirty, int* __restrict__ count,
+                                       int max_dirty) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int sb = starts[b];
+  const int lo = upd_lo - T + 1, hi = upd_hi - 1;  // candidate offsets, inclusive
+  for (int k0 = lo; k0 <= hi; k0 += 64) {
+    const int k = k0 + lane;
+    const bool cand = (k <= hi) && is_start[ring_row_s(sb, k, cap_e)];
+    unsigned long long m = __ballot(cand);
+    while (m) {
+      const int bit = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      const int s = ring_row_s(sb, k0 + bit, cap_e);
+      float mx = 0.f, sm = 0.f;
+      for (int t = lane; t < T; t += 64) {
+        const float p = priority[ring_row_s(s, t, cap_e)];
+        mx = fmaxf(mx, p);
+        sm += p;
+      }
+      mx = wave_max(mx);
+      sm = wave_sum(sm);
+      if (lane == 0) {
+        leaves[s] = eta * mx + (1.f - eta) * (sm / (float)T);
+        const int slot = atomicAdd(count, 1);
+        if (slot < max_dirty) dirty[slot] = s;
+      }
+    }
+  }
+}
+
+// ---- mark new sequence starts (actor side): set flag, compute eta-mix, append dirty
+__global__ void mark_starts_kernel(const int* __restrict__ rows, const int* __restrict__ n_rows,
+                                   int max_rows, uint8_t* __restrict__ is_start,
+                                   const float* __restrict__ priority,
+                                   float* __restrict__ leaves, int T, int cap_e, float eta,
+                                   int* __restrict__ n_valid, int* __restrict__ dirty,
+                                   int* __restrict__ count, int max_dirty) {
+  const int lane = threadIdx.x & 63;
+  const int n = n_rows ? min(*n_rows, max_rows) : max_rows;
+  const int w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (w >= n) return;
+  const int s = rows[w];
+  if (s < 0) return;
+  float mx = 0.f, sm = 0.f;
+  for (int t = lane; t < T; t += 64) {
+    const float p = priority[ring_row_s(s, t, cap_e)];
+    mx = fmaxf(mx, p);
+    sm += p;
+  }
+  mx = wave_max(mx);
+  sm = wave_sum(sm);
+  if (lane == 0) {
+    if (!is_start[s]) atomicAdd(n_valid, 1);
+    is_start[s] = 1;
+    leaves[s] = eta * mx + (1.f - eta) * (sm / (float)T);
+    const int slot = atomicAdd(count, 1);
+    if (slot < max_dirty) dirty[slot] = s;
+  }
+}
+
+// ---- time-major row list for (T x B) frames of sampled sequences: rows[t*B+b] = row(s_b, off+t)
+__global__ void make_rows_kernel(const int* __restrict__ starts, int B, int Tn, int off,
+                                 int cap_e, int* __restrict__ rows) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * Tn) return;
+  const int t = i / B, b = i % B;
+  rows[i] = ring_row_s(starts[b], off + t, cap_e);
+}
+
+// ---- stored recurrent state gather: hs_cs (cap, 2H) fp32 -> h (B,H) bf16, c (B,H) fp32
+__global__ void gather_state_kernel(const float* __restrict__ hs_cs, const int* __restrict__ starts,
+                                    int B, int off, int cap_e, int H, bf16* __restrict__ h,
+                                    float* __restrict__ c, float* __restrict__ h32) {
+  const int b = blockIdx.x;
+  const int row = ring_row_s(starts[b], off, cap_e);
+  const float* src = hs_cs + (size_t)row * 2 * H;
+  for (int k = threadIdx.x; k < H; k += blockDim.x) {
+    const float hv = src[k];
+    h[(size_t)b * H + k] = (bf16)hv;
+    if (h32) h32[(size_t)b * H + k] = hv;
+    c[(size_t)b * H + k] = src[H + k];
+  }
+}
+
+// ---- end of learner step: bump the device step counter, reset the dirty list
+__global__ void step_end_kernel(int64_t* step, int* count) {
+  if (threadIdx.x == 0) {
+    *step += 1;
+    *count = 0;
+  }
+}
+
+static TreeGeom make_geom(const int64_t* offs, const int64_t* sizes, int levels) {
+  TreeGeom g;
+  g.levels = levels;
+  for (int i = 0; i < TREE_MAX_LEVELS; ++i) {
+    g.off[i] = i < levels ? offs[i] : 0;
+    g.size[i] = i < levels ? sizes[i] : 0;
+  }
+  return g;
+}
+
+extern "C" int r2_tree_sample(const float* tree, const int64_t* offs, const int64_t* sizes,
+                              int levels, int B, uint64_t seed, const int64_t* step, int* out_idx,
+                              float* out_prob, void* stream) {
+  if (levels < 2 || levels > TREE_MAX_LEVELS) return -1;
+  TreeGeom g = make_geom(offs, sizes, levels);
+  hipLaunchKernelGGL(tree_sample_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                     tree, g, B, seed, step, out_idx, out_prob);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int r2_tree_rebuild(float* tree, const int64_t* offs, const int64_t* sizes, int levels,
+                               void* stream) {
+  if (levels < 2 || levels > TREE_MAX_LEVELS) return -1;
+  TreeGeom g = make_geom(offs, sizes, levels);
+  for (int l = 0; l + 1 < levels; ++l) {
+    int64_t nb = (g.size[l + 1] + 3) / 4;
+    if (nb > 4096) nb = 4096;
+    if (nb < 1) nb = 1;
+    hipLaunchKernelGGL(tree_rebuild_level_kernel, dim3((unsigned)nb), dim3(256), 0,
+                       (hipStream_t)stream, tree, g, l);
+  }
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int r2_tree_update(float* tree, const int64_t* offs, const int64_t* sizes, int levels,
+                              const int* dirty, const int* count, int max_dirty, void* stream) {
+  if (levels < 2 || levels > TREE_MAX_LEVELS) return -1;
+  TreeGeom g = make_geom(offs, sizes, levels);
+  int nb = (max_dirty + 3) / 4;
+  if (nb > 256) nb = 256;
+  if (nb < 1) nb = 1;
+  for (int l = 0; l + 1 < levels; ++l)
+    hipLaunchKernelGGL(tree_update_level_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream,
+                       tree, g, l, dirty, count, max_dirty);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int r2_seqprio_refresh(const int* starts, int B, const uint8_t* is_start,
+                                  const float* priority, float* leaves, int T, int upd_lo,
+                                  int upd_hi, int cap_e, float eta, int* dirty, int* count,
+                                  int max_dirty, void* stream) {
+  hipLaunchKernelGGL(seqprio_refresh_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+                     starts, B, is_start, priority, leaves, T, upd_lo, upd_hi, cap_e, eta, dirty,
+                     count, max_dirty);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int r2_mark_starts(const int* rows, const int* n_rows, int max_rows, uint8_t* is_start,
+                              const float* priority, float* leaves, int T, int cap_e, float eta,
+                              int* n_valid, int* dirty, int* count, int max_dirty, void* stream) {
+  if (max_rows <= 0) return 0;
+  hipLaunchKernelGGL(mark_starts_kernel, dim3((max_rows + 3) / 4), dim3(256), 0,
+                     (hipStream_t)stream, rows, n_rows, max_rows, is_start, priority, leaves, T,
+                     cap_e, eta, n_valid, dirty, count, max_dirty);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int r2_make_rows(const int* starts, int B, int Tn, int off, int cap_e, int* rows,
+                            void* stream) {
+  const int n = B * Tn;
+  hipLaunchKernelGGL(make_rows_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     starts, B, Tn, off, cap_e, rows);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int r2_gather_state(const float* hs_cs, const int* starts, int B, int off, int cap_e,
+                               int H, bf16* h, float* c, float* h32, void* stream) {
+  hipLaunchKernelGGL(gather_state_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, hs_cs,
+                     starts, B, off, cap_e, H, h, c, h32);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int r2_step_end(int64_t* step, int* count, void* stream) {
+  hipLaunchKernelGGL(step_end_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, step, count);
+  R2_CHECK_LAUNCH();
+  return 0;
+}

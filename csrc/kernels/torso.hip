@@ -1,0 +1,249 @@
+// Fused Atari conv torso forward for gfx950 (MI355X).
+//
+// Reference: model.py:12-22,44-46 -- Conv2d(4,32,8,s4)-ReLU-Conv2d(32,32,4,s2)-ReLU-
+// Conv2d(32,32,3,s1)-ReLU on (N,4,84,84) float frames that the replay first expands from uint8
+// (replay_memory.py:236-256, state/255 then H2D).  Here one kernel does all of it:
+//
+//  * frames are read as uint8 straight from the HBM replay ring through a row-index list
+//    (the replay "gather" and the /255 normalisation are fused; integers 0..255 are exact in
+//    bf16 and the 1/255 is applied to the fp32 conv1 accumulator);
+//  * every convolution is an implicit GEMM on MFMA (v_mfma_f32_32x32x16_bf16) with
+//    M = 32 output channels, N = 32 output pixels, K = Cin*kh*kw;
+//  * activations never leave LDS: conv1 output (20x20x32) and conv2 output (9x9x32) are kept
+//    channels-last (HWC, 80-byte padded pixel rows -> 16-byte aligned, bank-spread
+//    ds_read_b128 fragment loads);
+//  * conv2/conv3 weights live in LDS (padded rows), conv1 weights in VGPRs (64 regs);
+//  * the next frame's 28 KB is prefetched into registers while the current frame computes and
+//    written to LDS after conv2 (async-stage split);
+//  * output is bf16 in PyTorch's (C,H,W) flatten order, ready for the LSTM input GEMM.
+//  * optional: conv1/conv2 activations are written channels-last for the backward pass
+//    (torch channels_last NCHW tensors), so backward does not recompute the forward.
+//
+// One 512-thread workgroup per CU (118 KB LDS), grid-stride over frames.
+#include "../common.h"
+
+namespace torso {
+constexpr int IN_BYTES = 4 * 84 * 84;   // 28224
+constexpr int IN_CHUNKS = IN_BYTES / 16; // 1764
+constexpr int NT = 512;                  // threads
+constexpr int PF = (IN_CHUNKS + NT - 1) / NT;  // 4 prefetch chunks per thread
+constexpr int P1 = 400, P2 = 81, P3 = 49;
+constexpr int ACTS = 40;                 // bf16 per pixel row in LDS (32 + 8 pad) = 80 B
+constexpr int W2S = 512 + 8;             // bf16 per conv2 weight row (1040 B)
+constexpr int W3S = 288 + 8;             // bf16 per conv3 weight row (592 B)
+constexpr int OFF_IN = 0;
+constexpr int OFF_A1 = OFF_IN + IN_BYTES;            // 28224
+constexpr int OFF_A2 = OFF_A1 + P1 * ACTS * 2;       // 60224
+constexpr int OFF_W2 = OFF_A2 + P2 * ACTS * 2;       // 66704
+constexpr int OFF_W3 = OFF_W2 + 32 * W2S * 2;        // 99984
+constexpr int LDS_BYTES = OFF_W3 + 32 * W3S * 2;     // 118928
+}  // namespace torso
+
+__global__ __launch_bounds__(512) void torso_fwd_kernel(
+    const uint8_t* __restrict__ frames, const int* __restrict__ rows, int n_frames,
+    const bf16* __restrict__ w1, const float* __restrict__ b1,
+    const bf16* __restrict__ w2, const float* __restrict__ b2,
+    const bf16* __restrict__ w3, const float* __restrict__ b3,
+    bf16* __restrict__ out, bf16* __restrict__ save1, bf16* __restrict__ save2) {
+  using namespace torso;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint8_t* in_u8 = lds + OFF_IN;
+  bf16* act1 = (bf16*)(lds + OFF_A1);
+  bf16* act2 = (bf16*)(lds + OFF_A2);
+  bf16* lw2 = (bf16*)(lds + OFF_W2);
+  bf16* lw3 = (bf16*)(lds + OFF_W3);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int half = lane >> 5, l32 = lane & 31;
+
+  // ---- weights -> LDS (conv2, conv3) with padded rows; conv1 fragments -> VGPRs
+  for (int i = tid; i < 32 * 64; i += NT) {   // conv2: 32 rows x 64 chunks of 8 bf16
+    const int r = i >> 6, c = i & 63;
+    *(bf16x8*)(lw2 + r * W2S + c * 8) = *(const bf16x8*)(w2 + r * 512 + c * 8);
+  }
+  for (int i = tid; i < 32 * 36; i += NT) {   // conv3: 32 rows x 36 chunks
+    const int r = i / 36, c = i % 36;
+    *(bf16x8*)(lw3 + r * W3S + c * 8) = *(const bf16x8*)(w3 + r * 288 + c * 8);
+  }
+  bf16x8 wf1[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) wf1[s] = *(const bf16x8*)(w1 + l32 * 256 + s * 16 + half * 8);
+  float bias1[16], bias2[16], bias3[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int co = (r & 3) + 8 * (r >> 2) + 4 * half;
+    bias1[r] = b1[co]; bias2[r] = b2[co]; bias3[r] = b3[co];
+  }
+
+  int f = blockIdx.x;
+  if (f >= n_frames) return;
+  // ---- prologue: first frame -> LDS
+  {
+    const size_t row = rows ? (size_t)rows[f] : (size_t)f;
+    const u32x4* src = (const u32x4*)(frames + row * IN_BYTES);
+    for (int c = tid; c < IN_CHUNKS; c += NT) ((u32x4*)in_u8)[c] = src[c];
+  }
+  __syncthreads();
+
+  for (; f < n_frames; f += gridDim.x) {
+    // ---- prefetch next frame into registers (lands while conv1/conv2 run)
+    const int fn = f + gridDim.x;
+    u32x4 pf[PF];
+    if (fn < n_frames) {
+      const size_t row = rows ? (size_t)rows[fn] : (size_t)fn;
+      const u32x4* src = (const u32x4*)(frames + row * IN_BYTES);
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        const int c = tid + q * NT;
+        if (c < IN_CHUNKS) pf[q] = src[c];
+      }
+    }
+
+    // ---- conv1: 13 pixel tiles of 32 over 8 waves (waves 7..3 take two tiles)
+    for (int pt = 7 - wave; pt < 13; pt += 8) {
+      const int p = pt * 32 + l32;
+      const int pc = p < P1 ? p : P1 - 1;
+      const int oy = pc / 20, ox = pc % 20;
+      const uint32_t* base = (const uint32_t*)(in_u8 + (4 * oy) * 84 + 4 * ox);
+      f32x16 acc = {};
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int ci = s >> 2, kh = (s & 3) * 2 + half;
+        const uint32_t* q = base + (ci * 7056 + kh * 84) / 4;
+        acc = mfma32(wf1[s], u8x8_to_bf16(q[0], q[1]), acc);
+      }
+      if (p < P1) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          bf16x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x = acc[4 * g + e] * (1.f / 255.f) + bias1[4 * g + e];
+            v[e] = (bf16)fmaxf(x, 0.f);
+          }
+          *(bf16x4*)(act1 + p * ACTS + 8 * g + 4 * half) = v;
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- conv2: 3 pixel tiles (81 px), K = 512 = (kh 4, kw 4, ci 32)
+    if (wave < 3) {
+      const int p = wave * 32 + l32;
+      const int pc = p < P2 ? p : P2 - 1;
+      const int oy = pc / 9, ox = pc % 9;
+      const bf16* abase = lw2 + l32 * W2S + half * 8;
+      const bf16* bbase = act1 + ((2 * oy) * 20 + 2 * ox) * ACTS + half * 8;
+      f32x16 acc = {};
+#pragma unroll 8
+      for (int s = 0; s < 32; ++s) {
+        const int khkw = s >> 1, kh = khkw >> 2, kw = khkw & 3;
+        const bf16x8 av = *(const bf16x8*)(abase + s * 16);
+        const bf16x8 bv = *(const bf16x8*)(bbase + (kh * 20 + kw) * ACTS + (s & 1) * 16);
+        acc = mfma32(av, bv, acc);
+      }
+      if (p < P2) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          bf16x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = (bf16)fmaxf(acc[4 * g + e] + bias2[4 * g + e], 0.f);
+          *(bf16x4*)(act2 + p * ACTS + 8 * g + 4 * half) = v;
+        }
+      }
+    }
+    // ---- next frame -> LDS (conv1 finished reading in_u8 before the barrier above)
+    if (fn < n_frames) {
+#pragma unroll
+      for (int q = 0; q < PF; ++q) {
+        const int c = tid + q * NT;
+        if (c < IN_CHUNKS) ((u32x4*)in_u8)[c] = pf[q];
+      }
+    }
+    __syncthreads();
+
+    // ---- conv3: 2 pixel tiles (49 px), K = 288 = (kh 3, kw 3, ci 32)
+    if (wave < 2) {
+      const int p = wave * 32 + l32;
+      const int pc = p < P3 ? p : P3 - 1;
+      const int oy = pc / 7, ox = pc % 7;
+      const bf16* abase = lw3 + l32 * W3S + half * 8;
+      const bf16* bbase = act2 + (oy * 9 + ox) * ACTS + half * 8;
+      f32x16 acc = {};
+#pragma unroll 6
+      for (int s = 0; s < 18; ++s) {
+        const int khkw = s >> 1, kh = khkw / 3, kw = khkw % 3;
+        const bf16x8 av = *(const bf16x8*)(abase + s * 16);
+        const bf16x8 bv = *(const bf16x8*)(bbase + (kh * 9 + kw) * ACTS + (s & 1) * 16);
+        acc = mfma32(av, bv, acc);
+      }
+      if (p < P3) {
+        bf16* o = out + (size_t)f * 1568 + p;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int co = (r & 3) + 8 * (r >> 2) + 4 * half;
+          o[co * 49] = (bf16)fmaxf(acc[r] + bias3[r], 0.f);
+        }
+      }
+    } else if (save1 != nullptr) {
+      // waves 2..7 copy the channels-last activations out for the backward pass
+      const int t6 = tid - 128;  // 0..383
+      bf16* d1 = save1 + (size_t)f * P1 * 32;
+      for (int c = t6; c < P1 * 4; c += 384) {   // 4 chunks of 8 channels per pixel
+        const int px = c >> 2, q = c & 3;
+        *(bf16x8*)(d1 + px * 32 + q * 8) = *(const bf16x8*)(act1 + px * ACTS + q * 8);
+      }
+      bf16* d2 = save2 + (size_t)f * P2 * 32;
+      for (int c = t6; c < P2 * 4; c += 384) {
+        const int px = c >> 2, q = c & 3;
+        *(bf16x8*)(d2 + px * 32 + q * 8) = *(const bf16x8*)(act2 + px * ACTS + q * 8);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Expand uint8 frames (selected rows) to bf16/255 NCHW for the conv1 weight-gradient pass.
+__global__ void frames_to_bf16_kernel(const uint8_t* __restrict__ frames, const int* __restrict__ rows,
+                                      int n_frames, bf16* __restrict__ out) {
+  const int f = blockIdx.y;
+  const size_t row = rows ? (size_t)rows[f] : (size_t)f;
+  const uint8_t* src = frames + row * torso::IN_BYTES;
+  bf16* dst = out + (size_t)f * torso::IN_BYTES;
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < torso::IN_BYTES / 8;
+       c += gridDim.x * blockDim.x) {
+    const u32x2 v = ((const u32x2*)src)[c];
+    bf16x8 o = u8x8_to_bf16(v[0], v[1]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16)((float)o[e] * (1.f / 255.f));
+    ((bf16x8*)dst)[c] = o;
+  }
+}
+
+extern "C" int r2_torso_fwd(const uint8_t* frames, const int* rows, int n_frames,
+                            const bf16* w1, const float* b1, const bf16* w2, const float* b2,
+                            const bf16* w3, const float* b3, bf16* out, bf16* save1, bf16* save2,
+                            int max_blocks, void* stream) {
+  if (n_frames <= 0) return 0;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)torso_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        torso::LDS_BYTES);
+    attr_set = true;
+  }
+  int grid = max_blocks > 0 ? max_blocks : 256;
+  if (grid > n_frames) grid = n_frames;
+  hipLaunchKernelGGL(torso_fwd_kernel, dim3(grid), dim3(torso::NT), torso::LDS_BYTES,
+                     (hipStream_t)stream, frames, rows, n_frames, w1, b1, w2, b2, w3, b3, out,
+                     save1, save2);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int r2_frames_to_bf16(const uint8_t* frames, const int* rows, int n_frames, bf16* out,
+                                 void* stream) {
+  if (n_frames <= 0) return 0;
+  hipLaunchKernelGGL(frames_to_bf16_kernel, dim3(4, n_frames), dim3(256), 0, (hipStream_t)stream,
+                     frames, rows, n_frames, out);
+  R2_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,238 @@
+"""Typed configuration for the MI355X-native R2D2 engine.
+
+The reference hard-codes every hyper-parameter as a literal inside class constructors
+(``/root/reference/actor.py:21-51``, ``learner.py:20-51``, ``replay_memory.py:59-74``) and
+exposes a single CLI flag (``main.py:14``).  Here every knob lives in one dataclass tree with
+named presets:
+
+* ``reference``   -- the exact values of the reference: B=8, burn-in 10 + learn 10,
+                     n=3, gamma=0.99, centered RMSprop, Pong network.
+* ``cartpole``    -- CartPole-v1 plumbing config (seq 80 / burn-in 40) on CPU (BASELINE config 1).
+* ``pong``        -- Pong, 1 MI355X learner + 64 actor envs, replay resident in HBM (config 2).
+* ``atari57``     -- the R2D2 paper shapes: B=64, burn-in 40 + learn 40, n=5, gamma=0.997,
+                     value rescaling, IS weights (config 3).  This is the ``bench.py`` headline.
+* ``seaquest8``   -- 8-GPU data-parallel learner + 512 actor envs (config 4).
+* ``dmlab30``     -- 96x72 RGB synthetic frames, bf16 LSTM, sharded replay (config 5).
+"""
+from __future__ import annotations
+
+import copy
+import dataclasses
+from dataclasses import dataclass, field
+from typing import Any, Dict, Optional
+
+
+@dataclass
+class EnvConfig:
+    name: str = "synthetic"          # synthetic | cartpole | pong | dmlab_synth
+    action_repeat: int = 4            # env.py:15
+    n_stacks: int = 4                 # env.py:15
+    frame_h: int = 84
+    frame_w: int = 84
+    channels_per_frame: int = 1       # 1 = gray (Atari), 3 = RGB (DMLab)
+    n_actions: int = 6                # model.py:35 (Pong)
+    episode_len: int = 400            # synthetic env only
+    obs_dim: int = 4                  # vector envs (CartPole)
+
+
+@dataclass
+class ModelConfig:
+    torso: str = "atari"              # atari | mlp
+    conv_channels: tuple = (32, 32, 32)   # model.py:14-20 (comments say 16/32/64; code is 32/32/32)
+    hidden: int = 256                 # model.py:24
+    head_hidden: int = 256            # model.py:27,33
+    mlp_hidden: int = 64              # mlp torso width (CartPole)
+    n_actions: int = 6
+
+
+@dataclass
+class ReplayConfig:
+    capacity: int = 500_000           # learner.py:38
+    burn_in: int = 10                 # learner.py:35
+    learn: int = 10                   # learner.py:36
+    overlap: int = 10                 # actor.py:40 (stride between sequence starts)
+    n_step: int = 3                   # learner.py:23
+    eta: float = 0.9                  # replay_memory.py:71
+    alpha: float = 0.6                # actor.py:24 / learner.py:22
+    priority_eps: float = 1e-6        # learner.py:25
+    beta: float = 0.0                 # IS exponent; 0 == reference (no IS weights, Q10)
+    stored_state: str = "post"        # post == reference (Q6); pre == paper
+    n_subrings: int = 1               # one contiguous sub-ring per actor env (HBM replay)
+
+    @property
+    def seq_len(self) -> int:
+        return self.burn_in + self.learn
+
+
+@dataclass
+class LearnerConfig:
+    batch_size: int = 8               # learner.py:39
+    gamma: float = 0.99               # learner.py:21
+    optimizer: str = "rmsprop_centered"   # learner.py:51 ; or "adam" (paper)
+    lr: float = 0.00025 / 4.0
+    rms_alpha: float = 0.95
+    eps: float = 1.5e-7
+    adam_betas: tuple = (0.9, 0.999)
+    grad_clip: float = 0.0            # 0 == off (reference)
+    value_rescale: bool = False       # h(x) = sign(x)(sqrt(|x|+1)-1)+eps*x  (paper)
+    value_rescale_eps: float = 1e-3
+    target_update_interval: int = 1000    # learner.py:46
+    publish_interval: int = 100       # learner.py:45
+    ingest_interval: int = 20         # learner.py:40
+    checkpoint_interval: int = 10_000     # learner.py:117
+    initial_exploration: int = 50_000     # learner.py:24
+    # "reference": 3 recurrent chains exactly like learner.py:75-93 (online on state, target on
+    # next_state, online on next_state continuing the learning chain's state -- Q7 reproduced).
+    # "fixed": Q7 fixed -- online-on-next gets its own stored state + burn-in.
+    # "shifted": R2D2 paper form -- one online and one target chain over T+n frames;
+    #            Q(s_{t+n}) is read at offset +n of the same chain.
+    target_mode: str = "shifted"
+    compute_dtype: str = "bf16"
+    use_graph: bool = True            # capture the whole step in a HIP graph
+    save_dir: str = "save"
+
+
+@dataclass
+class ActorConfig:
+    n_actors: int = 1                 # main.py:14
+    envs_per_actor: int = 1
+    eps_base: float = 0.4             # actor.py:22
+    eps_alpha: float = 7.0
+    net_load_interval: int = 5        # actor.py:51 (episodes)
+    memory_save_interval: int = 5     # actor.py:44 (episodes)
+    local_capacity: int = 50_000      # actor.py:34
+
+
+@dataclass
+class DistConfig:
+    backend: str = "auto"             # nccl (RCCL) on GPU, gloo on CPU
+    grad_bucket_mb: float = 8.0
+    grad_dtype: str = "fp32"          # fp32 | bf16 (compressed all-reduce)
+    overlap_allreduce: bool = True
+
+
+@dataclass
+class R2D2Config:
+    name: str = "reference"
+    env: EnvConfig = field(default_factory=EnvConfig)
+    model: ModelConfig = field(default_factory=ModelConfig)
+    replay: ReplayConfig = field(default_factory=ReplayConfig)
+    learner: LearnerConfig = field(default_factory=LearnerConfig)
+    actor: ActorConfig = field(default_factory=ActorConfig)
+    dist: DistConfig = field(default_factory=DistConfig)
+    seed: int = 0
+
+    def to_dict(self) -> Dict[str, Any]:
+        return dataclasses.asdict(self)
+
+    def replace(self, **overrides) -> "R2D2Config":
+        """Return a copy with dotted overrides, e.g. ``replace(**{"learner.batch_size": 64})``."""
+        cfg = copy.deepcopy(self)
+        for key, val in overrides.items():
+            apply_override(cfg, key, val)
+        return cfg
+
+
+def apply_override(cfg: R2D2Config, dotted: str, value: Any) -> None:
+    parts = dotted.split(".")
+    obj = cfg
+    for p in parts[:-1]:
+        obj = getattr(obj, p)
+    cur = getattr(obj, parts[-1])
+    if isinstance(value, str) and not isinstance(cur, str):
+        if isinstance(cur, bool):
+            value = value.lower() in ("1", "true", "yes", "on")
+        elif isinstance(cur, int):
+            value = int(value)
+        elif isinstance(cur, float):
+            value = float(value)
+        elif isinstance(cur, tuple):
+            value = tuple(type(cur[0])(v) for v in value.split(","))
+    setattr(obj, parts[-1], value)
+
+
+def _reference() -> R2D2Config:
+    return R2D2Config(name="reference")
+
+
+def _cartpole() -> R2D2Config:
+    c = R2D2Config(name="cartpole")
+    c.env = EnvConfig(name="cartpole", action_repeat=1, n_stacks=1, n_actions=2, obs_dim=4,
+                      episode_len=500)
+    c.model = ModelConfig(torso="mlp", hidden=64, head_hidden=64, mlp_hidden=64, n_actions=2)
+    c.replay = ReplayConfig(capacity=100_000, burn_in=40, learn=40, overlap=40, n_step=5,
+                            beta=0.6, stored_state="pre")
+    c.learner = LearnerConfig(batch_size=16, gamma=0.997, optimizer="adam", lr=1e-3, eps=1e-3,
+                              value_rescale=True, target_update_interval=100,
+                              initial_exploration=2_000, compute_dtype="fp32", use_graph=False)
+    c.actor = ActorConfig(n_actors=1, envs_per_actor=16)
+    return c
+
+
+def _pong() -> R2D2Config:
+    c = R2D2Config(name="pong")
+    c.env = EnvConfig(name="synthetic", n_actions=6)
+    c.replay = ReplayConfig(capacity=2_000_000, n_subrings=64)
+    c.learner = LearnerConfig(batch_size=8, target_mode="shifted")
+    c.actor = ActorConfig(n_actors=1, envs_per_actor=64)
+    return c
+
+
+def _atari57() -> R2D2Config:
+    c = R2D2Config(name="atari57")
+    c.env = EnvConfig(name="synthetic", n_actions=6)
+    c.model = ModelConfig(n_actions=6)
+    c.replay = ReplayConfig(capacity=1_000_000, burn_in=40, learn=40, overlap=40, n_step=5,
+                            eta=0.9, alpha=0.9, beta=0.6, stored_state="pre", n_subrings=256)
+    c.learner = LearnerConfig(batch_size=64, gamma=0.997, optimizer="rmsprop_centered",
+                              value_rescale=True, target_update_interval=2500,
+                              target_mode="shifted")
+    c.actor = ActorConfig(n_actors=1, envs_per_actor=256)
+    return c
+
+
+def _seaquest8() -> R2D2Config:
+    c = _atari57()
+    c.name = "seaquest8"
+    c.env.n_actions = 18
+    c.model.n_actions = 18
+    c.actor = ActorConfig(n_actors=8, envs_per_actor=64)
+    c.replay.n_subrings = 64
+    return c
+
+
+def _dmlab30() -> R2D2Config:
+    c = _atari57()
+    c.name = "dmlab30"
+    c.env = EnvConfig(name="dmlab_synth", action_repeat=4, n_stacks=1, frame_h=72, frame_w=96,
+                      channels_per_frame=3, n_actions=15)
+    c.model.n_actions = 15
+    c.actor = ActorConfig(n_actors=8, envs_per_actor=64)
+    return c
+
+
+PRESETS = {
+    "reference": _reference,
+    "cartpole": _cartpole,
+    "pong": _pong,
+    "atari57": _atari57,
+    "seaquest8": _seaquest8,
+    "dmlab30": _dmlab30,
+}
+
+
+def get_config(name: str = "reference", **overrides) -> R2D2Config:
+    if name not in PRESETS:
+        raise KeyError(f"unknown preset {name!r}; choose from {sorted(PRESETS)}")
+    cfg = PRESETS[name]()
+    return cfg.replace(**overrides) if overrides else cfg
+
+
+def epsilon_ladder(actor_id: int, n_actors: int, base: float = 0.4, alpha: float = 7.0) -> float:
+    """Ape-X per-actor epsilon ``base ** (1 + alpha * i / (N - 1))`` (``actor.py:22``).
+
+    Fix for Q1: the reference divides by zero when ``N == 1``; a single actor gets ``base``.
+    """
+    if n_actors <= 1:
+        return base
+    return base ** (1.0 + alpha * actor_id / (n_actors - 1))

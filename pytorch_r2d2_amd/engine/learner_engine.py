@@ -1,0 +1,471 @@
+"""MI355X learner engine: one R2D2 train step as a fixed sequence of HIP kernels.
+
+Parity target: ``/root/reference/learner.py:68-120`` (train + interval).  The reference runs
+5 QNet forward calls (each a Python loop of LSTMCell steps with a blocking D2H copy), a
+36 MB H2D batch upload, autograd, torch.optim.RMSprop, a D2H of the TD errors and numpy
+priority scatters.  Here a step is:
+
+    sample    tree_sample (64-ary sum tree, device RNG keyed by the device step counter)
+    rows      make_rows: time-major ring rows of the T+n frames of every sampled sequence
+    torso     fused uint8->conv1->conv2->conv3 MFMA kernel, online + target nets
+    proj      ONE library GEMM per net: x . W_ih^T + (b_ih + b_hh), all T*B rows at once
+    state     gather stored (h, c) from the replay
+    lstm      recurrence kernels, all chains in one launch per step (grid.y = chain)
+    head      [val.0;adv.0] GEMM + fused dueling epilogue kernel
+    td        fused double-Q n-step target / loss / dL/dQ / IS weights / row priorities
+    backward  dueling backward kernel + 3 small GEMMs, BPTT kernels, weight-grad GEMMs,
+              conv backward (library) from activations saved by the torso kernel
+    allreduce (DP) bucket "core" overlapped with the conv backward, then bucket "torso"
+    update    fused centered RMSprop (or Adam) over the flat master buffer, one pack launch
+              producing every bf16 kernel layout, target sync as a device-side
+              `copy_if_due` (graph-safe)
+    priority  eta-mix refresh of every overlapping sequence, tree repair, step counter
+
+No host synchronisation happens inside a step, so the whole step (minus collectives) is
+captured once into a HIP graph and replayed.
+
+target_mode (config.learner.target_mode):
+  shifted   -- R2D2 paper: one online and one target chain over T+n frames from the stored
+               state at the sequence start; Q(s_{t+n}) is read at offset +n (2 chains).
+  fixed     -- the reference's 3-chain structure (online on state, target on next_state,
+               online on next_state) with Q7 fixed: the online-on-next chain starts from the
+               stored state at s+n and does its own burn-in.
+  reference -- exactly learner.py:75-93 including Q7: online-on-next continues from the
+               online-state chain's final state over next_state[burn_in:].
+"""
+from __future__ import annotations
+
+import math
+import time
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from ..config import R2D2Config
+from ..models.qnet import QNet
+from ..ops._lib import check, kernels, ptr, stream_handle
+from .layout import ParamLayout, UNITS
+from .replay_hbm import HBMReplay
+
+_HAS_MM_DTYPE = None
+
+
+def mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """bf16 x bf16 -> fp32 output library GEMM (hipBLASLt), fallback to bf16 out + cast."""
+    global _HAS_MM_DTYPE
+    if _HAS_MM_DTYPE is not False:
+        try:
+            out = torch.mm(a, b, out_dtype=torch.float32)
+            _HAS_MM_DTYPE = True
+            return out
+        except (RuntimeError, TypeError):
+            _HAS_MM_DTYPE = False
+    return torch.mm(a, b).float()
+
+
+def addmm_f32(bias: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """bias + a @ b with bf16 operands and fp32 output (bias fused into the GEMM epilogue)."""
+    global _HAS_MM_DTYPE
+    if _HAS_MM_DTYPE is not False:
+        try:
+            out = torch.addmm(bias, a, b, out_dtype=torch.float32)
+            _HAS_MM_DTYPE = True
+            return out
+        except (RuntimeError, TypeError):
+            _HAS_MM_DTYPE = False
+    return torch.mm(a, b).float() + bias
+
+
+class LearnerEngine:
+    def __init__(self, cfg: R2D2Config, replay: HBMReplay, device="cuda", rank: int = 0,
+                 world: int = 1, process_group=None, init_module: Optional[QNet] = None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.replay = replay
+        self.rank, self.world, self.pg = rank, world, process_group
+        m, e, rc, lc = cfg.model, cfg.env, cfg.replay, cfg.learner
+        if m.torso != "atari" or tuple(m.conv_channels) != (32, 32, 32) or \
+                (e.frame_h, e.frame_w, e.channels_per_frame * e.n_stacks) != (84, 84, 4):
+            raise NotImplementedError("HIP engine torso kernel is specialised for the Atari "
+                                      "84x84x4 / 32-32-32 torso; use the torch learner otherwise")
+        if m.hidden % UNITS != 0 or m.hidden not in (64, 128, 256, 512):
+            raise NotImplementedError("LSTM kernels support hidden in {64,128,256,512}")
+        self.layout = L = ParamLayout(m, e)
+        d = self.device
+        if init_module is None:
+            torch.manual_seed(cfg.seed)
+            init_module = QNet("cpu", m, e)
+        self.master = L.from_module(init_module, d)
+        self.target = self.master.clone()
+        self.grad = torch.zeros_like(self.master)
+        self.opt_a = torch.zeros_like(self.master)
+        self.opt_b = torch.zeros_like(self.master)
+        self.bf_index = L.bf_index.to(d)
+        self.f_index = L.f_index.to(d)
+        self.bf = torch.zeros(L.bf_numel, dtype=torch.bfloat16, device=d)
+        self.f32 = torch.zeros(L.f_numel, dtype=torch.float32, device=d)
+        self.bf_t = torch.zeros_like(self.bf)
+        self.f32_t = torch.zeros_like(self.f32)
+        self.lstm_b = torch.zeros(L.G, dtype=torch.float32, device=d)
+        self.lstm_b_t = torch.zeros_like(self.lstm_b)
+        self.pk = L.packed_views(self.bf, self.f32)
+        self.pk_t = L.packed_views(self.bf_t, self.f32_t)
+        self.gate_inv = L.gate_inv.to(d)
+        self.clip_buf = torch.zeros(1, dtype=torch.float32, device=d)
+        self.steps_done = 0
+        self.graph = None
+        self.stats: Dict[str, float] = {}
+        self._alloc()
+        self._pack(always=True)
+        if d.type == "cuda":
+            torch.cuda.synchronize(d)
+
+    # ------------------------------------------------------------------ buffers
+    def _alloc(self):
+        cfg, d, L = self.cfg, self.device, self.layout
+        rc, lc = cfg.replay, cfg.learner
+        self.B = B = lc.batch_size
+        self.Lb, self.Ll, self.n = rc.burn_in, rc.learn, rc.n_step
+        self.T = T = rc.seq_len
+        mode = lc.target_mode
+        self.mode = mode
+        H, D, G, A, HD = L.H, L.D, L.G, L.A, L.HD
+        Lb, Ll, n = self.Lb, self.Ll, self.n
+        self.Tn = Tn = T + n                      # frames per sequence touched
+        self.Tc = Tn if mode == "shifted" else T  # chain length of the online chain
+        bf16, f32 = torch.bfloat16, torch.float32
+        z = lambda *s, dt=f32: torch.zeros(s, dtype=dt, device=d)  # noqa: E731
+        self.starts = z(B, dt=torch.int32)
+        self.probs = z(B)
+        self.rows = z(Tn * B, dt=torch.int32)
+        self.X_on = z(Tn * B, D, dt=bf16)
+        t_lo = 0 if mode == "shifted" else n       # first frame the target net needs
+        self.t_lo_tg = t_lo
+        self.X_tg = z((Tn - t_lo) * B, D, dt=bf16)
+        self.act1 = z(Ll * B, 400, 32, dt=bf16)
+        self.act2 = z(Ll * B, 81, 32, dt=bf16)
+        self.frames_bf = z(Ll * B, 4, 84, 84, dt=bf16)
+        self.h0 = {k: z(B, H, dt=bf16) for k in ("on", "tg", "nx")}
+        self.c0 = {k: z(B, H) for k in ("on", "tg", "nx")}
+        Tc = self.Tc
+        self.hseq = {"on": z(Tc, B, H, dt=bf16), "tg": z(T if mode != "shifted" else Tn, B, H, dt=bf16)}
+        self.cseq = {"on": z(Tc, B, H), "tg": z(T if mode != "shifted" else Tn, B, H)}
+        if mode != "shifted":
+            Tnx = T if mode == "fixed" else Ll
+            self.hseq["nx"] = z(Tnx, B, H, dt=bf16)
+            self.cseq["nx"] = z(Tnx, B, H)
+        self.gates = z(Tc - Lb, B, G)
+        # head rows: online from Lb..Tc, target/next likewise
+        self.Nh = (Tc - Lb) * B
+        self.q_on = z(self.Nh, A)
+        self.zr_on = z(self.Nh, 2 * HD, dt=bf16)
+        Ntg = (self.hseq["tg"].shape[0] - Lb) * B
+        self.q_tg = z(Ntg, A)
+        if mode != "shifted":
+            Nnx = (self.hseq["nx"].shape[0] - (Lb if mode == "fixed" else 0)) * B
+            self.q_nx = z(Nnx, A)
+        self.dq = z(Ll * B, A)
+        self.loss = z(1)
+        self.td_abs = z(Ll * B)
+        self.is_w = z(B)
+        self.dz = z(Ll * B, 2 * HD, dt=bf16)
+        self.dva = z(Ll * B, 1 + A)
+        nwg = H // UNITS
+        self.slab0 = z(nwg, B, H)
+        self.slab1 = z(nwg, B, H)
+        self.dc = z(B, H)
+        self.dgates = z(Ll * B, G, dt=bf16)
+        self.gamma_n = float(lc.gamma ** n)
+
+    # ------------------------------------------------------------------ weights
+    def _pack(self, always: bool = False, stream=None):
+        """Re-pack online weights (every step) and target weights (when synced)."""
+        k = kernels()
+        s = stream_handle(stream)
+        L = self.layout
+        check(k.r2_pack_bf16(ptr(self.master), ptr(self.bf_index), ptr(self.bf), L.bf_numel, s), "pack")
+        check(k.r2_gather_f32(ptr(self.master), ptr(self.f_index), ptr(self.f32), L.f_numel, s), "gather")
+        torch.add(self.pk["b_ih"], self.pk["b_hh"], out=self.lstm_b)
+        if always:
+            check(k.r2_pack_bf16(ptr(self.target), ptr(self.bf_index), ptr(self.bf_t), L.bf_numel, s), "pack_t")
+            check(k.r2_gather_f32(ptr(self.target), ptr(self.f_index), ptr(self.f32_t), L.f_numel, s), "gather_t")
+            torch.add(self.pk_t["b_ih"], self.pk_t["b_hh"], out=self.lstm_b_t)
+
+    def state_dict(self):
+        return self.layout.state_dict(self.master)
+
+    def target_state_dict(self):
+        return self.layout.state_dict(self.target)
+
+    def load_state_dict(self, sd, target_sd=None):
+        self.layout.load_state_dict(self.master, sd)
+        self.layout.load_state_dict(self.target, target_sd if target_sd is not None else sd)
+        self._pack(always=True)
+
+    def sync_target(self):
+        self.target.copy_(self.master)
+        self._pack(always=True)
+
+    # ------------------------------------------------------------------ pieces
+    def _torso(self, pk, rows: torch.Tensor, out: torch.Tensor, save=False):
+        n = rows.numel()
+        if n == 0:
+            return
+        k = kernels()
+        check(k.r2_torso_fwd(ptr(self.replay.frames), ptr(rows), n, ptr(pk["conv1"]), ptr(pk["b1"]),
+                             ptr(pk["conv2"]), ptr(pk["b2"]), ptr(pk["conv3"]), ptr(pk["b3"]),
+                             ptr(out), ptr(self.act1) if save else 0, ptr(self.act2) if save else 0,
+                             256, stream_handle()), "torso_fwd")
+
+    def _chain_desc(self, xproj, pk, h0, c0, hseq, cseq, gates=None, save_from=0):
+        return [ptr(xproj), ptr(pk["w_hh"]), ptr(h0), ptr(c0), ptr(hseq), ptr(cseq), 0,
+                ptr(gates), save_from]
+
+    def _lstm(self, chains, T, t_begin=0):
+        k = kernels()
+        arr = np.asarray([v for c in chains for v in c], dtype=np.int64)
+        check(k.r2_lstm_fwd(arr.ctypes.data, len(chains), self.B, T, self.layout.H, t_begin,
+                            stream_handle()), "lstm_fwd")
+
+    def _head(self, pk, h: torch.Tensor, q: torch.Tensor, zr: Optional[torch.Tensor]):
+        N = h.shape[0]
+        z = torch.mm(h, pk["head1"].t())
+        check(kernels().r2_dueling_fwd(ptr(z), ptr(pk["head_b1"]), ptr(pk["head_w2"]),
+                                       ptr(pk["head_b2"]), ptr(q), ptr(zr), N, self.layout.A,
+                                       self.layout.HD, stream_handle()), "dueling_fwd")
+
+    # ------------------------------------------------------------------ the step
+    def _forward_loss(self):
+        k = kernels()
+        s = stream_handle()
+        B, T, Tn, Lb, Ll, n = self.B, self.T, self.Tn, self.Lb, self.Ll, self.n
+        L, rp, lc = self.layout, self.replay, self.cfg.learner
+        H, A = L.H, L.A
+        pk, pt = self.pk, self.pk_t
+        rp.sample(B, self.starts, self.probs)
+        check(k.r2_make_rows(ptr(self.starts), B, Tn, 0, rp.cap_e, ptr(self.rows), s), "make_rows")
+        rows = self.rows
+        # torso: online over all Tn frames (save activations of the learning frames)
+        self._torso(pk, rows[: Lb * B], self.X_on[: Lb * B])
+        self._torso(pk, rows[Lb * B: T * B], self.X_on[Lb * B: T * B], save=True)
+        self._torso(pk, rows[T * B:], self.X_on[T * B:])
+        self._torso(pt, rows[self.t_lo_tg * B:], self.X_tg)
+        # input projections (one GEMM per net over every row)
+        xp_on = addmm_f32(self.lstm_b, self.X_on, pk["w_ih"].t())
+        xp_tg = addmm_f32(self.lstm_b_t, self.X_tg, pt["w_ih"].t())
+        self._xp = (xp_on, xp_tg)
+        # stored recurrent state
+        st_off = {"on": 0, "tg": 0 if self.mode == "shifted" else n, "nx": n}
+        check(k.r2_gather_state(ptr(rp.hs_cs), ptr(self.starts), B, 0, rp.cap_e, H,
+                                ptr(self.h0["on"]), ptr(self.c0["on"]), 0, s), "gather_state")
+        check(k.r2_gather_state(ptr(rp.target_hs_cs), ptr(self.starts), B, st_off["tg"], rp.cap_e,
+                                H, ptr(self.h0["tg"]), ptr(self.c0["tg"]), 0, s), "gather_state")
+        G = L.G
+        on = self._chain_desc(xp_on, pk, self.h0["on"], self.c0["on"], self.hseq["on"],
+                              self.cseq["on"], self.gates, Lb)
+        tg = self._chain_desc(xp_tg, pt, self.h0["tg"], self.c0["tg"], self.hseq["tg"], self.cseq["tg"])
+        if self.mode == "shifted":
+            self._lstm([on, tg], self.Tc)
+        elif self.mode == "fixed":
+            check(k.r2_gather_state(ptr(rp.hs_cs), ptr(self.starts), B, n, rp.cap_e, H,
+                                    ptr(self.h0["nx"]), ptr(self.c0["nx"]), 0, s), "gather_state")
+            nx = self._chain_desc(xp_on[n * B:], pk, self.h0["nx"], self.c0["nx"], self.hseq["nx"],
+                                  self.cseq["nx"])
+            self._lstm([on, tg, nx], T)
+        else:  # reference: Q7 -- online-on-next continues from the online chain's final state
+            self._lstm([on, tg], T)
+            self.h0["nx"].copy_(self.hseq["on"][T - 1])
+            self.c0["nx"].copy_(self.cseq["on"][T - 1])
+            nx = self._chain_desc(xp_on[(n + Lb) * B:], pk, self.h0["nx"], self.c0["nx"],
+                                  self.hseq["nx"], self.cseq["nx"])
+            self._lstm([nx], Ll)
+        # heads (rows from the first learning step on)
+        self._head(pk, self.hseq["on"][Lb:].reshape(-1, H), self.q_on, self.zr_on)
+        self._head(pt, self.hseq["tg"][Lb:].reshape(-1, H), self.q_tg, None)
+        if self.mode == "shifted":
+            q_sa = self.q_on[: Ll * B]
+            q_arg = self.q_on[n * B:(n + Ll) * B]
+            q_tgt = self.q_tg[n * B:(n + Ll) * B]
+        else:
+            nx_from = Lb if self.mode == "fixed" else 0
+            self._head(pk, self.hseq["nx"][nx_from:].reshape(-1, H), self.q_nx, None)
+            q_sa = self.q_on[: Ll * B]
+            q_arg = self.q_nx[: Ll * B]
+            q_tgt = self.q_tg[: Ll * B]
+        rc = self.cfg.replay
+        check(k.r2_td_loss(ptr(q_sa), ptr(q_arg), ptr(q_tgt), ptr(self.starts), ptr(self.probs),
+                           ptr(rp.action), ptr(rp.reward), ptr(rp.done), ptr(self.dq), ptr(self.loss),
+                           ptr(self.td_abs), ptr(rp.priority), ptr(self.is_w), ptr(rp.n_valid),
+                           Ll, B, A, Lb, rp.cap_e, self.gamma_n, int(lc.value_rescale),
+                           float(lc.value_rescale_eps), float(rc.alpha), float(rc.priority_eps),
+                           float(rc.beta), s), "td_loss")
+
+    def _backward_core(self):
+        """Head backward, BPTT, LSTM/head weight gradients -> grad bucket 'core'."""
+        k = kernels()
+        s = stream_handle()
+        B, T, Lb, Ll = self.B, self.T, self.Lb, self.Ll
+        L, pk = self.layout, self.pk
+        H, A, HD, G = L.H, L.A, L.HD, L.G
+        N = Ll * B
+        zr = self.zr_on[:N]
+        check(k.r2_dueling_bwd(ptr(self.dq), ptr(zr), ptr(pk["head_w2"]), ptr(self.dz),
+                               ptr(self.dva), N, A, HD, s), "dueling_bwd")
+        g = self.grad
+        g2 = torch.mm(self.dva.t(), zr.float())                      # (1+A, 2HD)
+        gw2 = L.span(g, "val.2.weight", "adv.2.weight", (1 + A, HD))
+        gw2[0].copy_(g2[0, :HD])
+        gw2[1:].copy_(g2[1:, HD:])
+        torch.sum(self.dva, 0, out=L.span(g, "val.2.bias", "adv.2.bias", (1 + A,)))
+        h_learn = self.hseq["on"][Lb:T].reshape(N, H)
+        L.span(g, "val.0.weight", "adv.0.weight", (2 * HD, H)).copy_(mm_f32(self.dz.t(), h_learn))
+        torch.sum(self.dz, 0, dtype=torch.float32, out=L.span(g, "val.0.bias", "adv.0.bias", (2 * HD,)))
+        dh = mm_f32(self.dz, pk["head1"])                               # (N, H)
+        self.dc.zero_()
+        check(k.r2_lstm_bwd(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]), ptr(self.c0["on"]),
+                            ptr(pk["w_hhT"]), ptr(self.slab0), ptr(self.slab1), ptr(self.dc),
+                            ptr(self.dgates), B, T, Lb, H, s), "lstm_bwd")
+        dg_o = self.dgates.index_select(1, self.gate_inv)               # original gate order
+        X = self.X_on[Lb * B: T * B]
+        L.view(g, "lstm.weight_ih").copy_(mm_f32(dg_o.t(), X))
+        if Lb >= 1:
+            h_prev = self.hseq["on"][Lb - 1: T - 1].reshape(N, H)
+        else:
+            h_prev = torch.cat([self.h0["on"][None], self.hseq["on"][: T - 1]]).reshape(N, H)
+        L.view(g, "lstm.weight_hh").copy_(mm_f32(dg_o.t(), h_prev))
+        db = torch.sum(dg_o, 0, dtype=torch.float32)
+        L.view(g, "lstm.bias_ih").copy_(db)
+        L.view(g, "lstm.bias_hh").copy_(db)
+        self._dX = torch.mm(self.dgates, pk["w_ih"])                   # (N, D) bf16
+
+    def _backward_torso(self):
+        """Conv backward from the activations saved by the torso kernel."""
+        k = kernels()
+        s = stream_handle()
+        B, Lb, Ll, T = self.B, self.Lb, self.Ll, self.T
+        L, g = self.layout, self.grad
+        N = Ll * B
+        out3 = self.X_on[Lb * B: T * B].view(N, 32, 7, 7)
+        g3 = self._dX.view(N, 32, 7, 7) * (out3 > 0)
+        a2 = self.act2.view(N, 9, 9, 32).permute(0, 3, 1, 2)
+        a1 = self.act1.view(N, 20, 20, 32).permute(0, 3, 1, 2)
+        m = self.master
+        w3 = L.view(m, "vis_layers.4.weight").to(torch.bfloat16)
+        w2 = L.view(m, "vis_layers.2.weight").to(torch.bfloat16)
+        w1 = L.view(m, "vis_layers.0.weight").to(torch.bfloat16)
+        cb = torch.ops.aten.convolution_backward
+        d2, dw3, db3 = cb(g3.contiguous(memory_format=torch.channels_last), a2, w3, [32], [1, 1],
+                          [0, 0], [1, 1], False, [0, 0], 1, [True, True, True])
+        g2 = d2 * (a2 > 0)
+        d1, dw2, db2 = cb(g2.contiguous(memory_format=torch.channels_last), a1, w2, [32], [2, 2],
+                          [0, 0], [1, 1], False, [0, 0], 1, [True, True, True])
+        g1 = d1 * (a1 > 0)
+        check(k.r2_frames_to_bf16(ptr(self.replay.frames), ptr(self.rows[Lb * B: T * B]), N,
+                                  ptr(self.frames_bf), s), "frames_to_bf16")
+        _, dw1, db1 = cb(g1.contiguous(), self.frames_bf, w1, [32],
+                         [4, 4], [0, 0], [1, 1], False, [0, 0], 1, [False, True, True])
+        L.view(g, "vis_layers.4.weight").copy_(dw3)
+        L.view(g, "vis_layers.4.bias").copy_(db3)
+        L.view(g, "vis_layers.2.weight").copy_(dw2)
+        L.view(g, "vis_layers.2.bias").copy_(db2)
+        L.view(g, "vis_layers.0.weight").copy_(dw1)
+        L.view(g, "vis_layers.0.bias").copy_(db1)
+
+    def _update(self):
+        k = kernels()
+        s = stream_handle()
+        lc, L = self.cfg.learner, self.layout
+        n = L.padded
+        gscale = 1.0 / self.world
+        clip = 0
+        if lc.grad_clip > 0:
+            check(k.r2_sumsq(ptr(self.grad), n, ptr(self.clip_buf), s), "sumsq")
+            clip = ptr(self.clip_buf)
+        if lc.optimizer == "adam":
+            check(k.r2_adam(ptr(self.master), ptr(self.grad), ptr(self.opt_a), ptr(self.opt_b), n,
+                            float(lc.lr), float(lc.adam_betas[0]), float(lc.adam_betas[1]),
+                            float(lc.eps), gscale, ptr(self.replay.step), clip,
+                            float(lc.grad_clip), s), "adam")
+        else:
+            check(k.r2_rmsprop_centered(ptr(self.master), ptr(self.grad), ptr(self.opt_a),
+                                        ptr(self.opt_b), n, float(lc.lr), float(lc.rms_alpha),
+                                        float(lc.eps), gscale, clip, float(lc.grad_clip), s),
+                  "rmsprop")
+        # target sync on device when (step+1) % interval == 0 (learner.py:107-108), then repack
+        check(k.r2_copy_if_due(ptr(self.target), ptr(self.master), n, ptr(self.replay.step),
+                               int(lc.target_update_interval), s), "copy_if_due")
+        self._pack(always=True)
+
+    def _priorities(self):
+        rp = self.replay
+        rp.refresh_sequences(self.starts, self.B, self.Lb, self.T)
+        rp.update_tree()
+        rp.step_end()
+
+    def _allreduce(self, lo: int, hi: int):
+        if self.world <= 1:
+            return
+        import torch.distributed as dist
+        buf = self.grad[lo:hi]
+        if self.cfg.dist.grad_dtype == "bf16":
+            tmp = buf.to(torch.bfloat16)
+            dist.all_reduce(tmp, group=self.pg)
+            buf.copy_(tmp)
+        else:
+            dist.all_reduce(buf, group=self.pg)
+
+    # ------------------------------------------------------------------ public API
+    def _step_body(self):
+        self._forward_loss()
+        self._backward_core()
+        self._backward_torso()
+
+    def _step_tail(self):
+        self._update()
+        self._priorities()
+
+    def step_eager(self):
+        self._step_body()
+        if self.world > 1:
+            self._allreduce(0, self.layout.padded)
+        self._step_tail()
+        self.steps_done += 1
+
+    def capture(self, warmup: int = 2):
+        """Capture the step into HIP graph(s).  With world > 1 the all-reduce runs between two
+        graphs (body, tail) on the same stream."""
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self.step_eager()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        self.g_body = torch.cuda.CUDAGraph()
+        self.g_tail = torch.cuda.CUDAGraph()
+        if self.world > 1:
+            with torch.cuda.graph(self.g_body):
+                self._step_body()
+            with torch.cuda.graph(self.g_tail, pool=self.g_body.pool()):
+                self._step_tail()
+        else:
+            with torch.cuda.graph(self.g_body):
+                self._step_body()
+                self._step_tail()
+            self.g_tail = None
+        torch.cuda.synchronize(self.device)
+        self.graph = True
+
+    def step(self):
+        if self.graph:
+            self.g_body.replay()
+            if self.g_tail is not None:
+                self._allreduce(0, self.layout.padded)
+                self.g_tail.replay()
+            self.steps_done += 1
+        else:
+            self.step_eager()
+
+    def loss_value(self) -> float:
+        return float(self.loss.item())

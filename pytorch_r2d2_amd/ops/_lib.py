@@ -1,0 +1,102 @@
+"""Loader for the in-tree gfx950 kernel library (``_r2d2_kernels.so``).
+
+The library is loaded with ctypes *after* torch so that its ``libamdhip64.so.7`` dependency
+binds to the HIP runtime torch already mapped.  On a machine with a GPU the library MUST be
+present: ``kernels()`` raises instead of silently falling back to PyTorch, so a GPU run that
+reports HIP numbers really ran the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from pathlib import Path
+
+import torch
+
+_PKG = Path(__file__).resolve().parent.parent
+_SO = _PKG / "_r2d2_kernels.so"
+_lock = threading.Lock()
+_lib = None
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+I64 = ctypes.c_int64
+U64 = ctypes.c_uint64
+F = ctypes.c_float
+
+_SIGS = {
+    "r2_abi_version": [],
+    "r2_lstm_fwd": [P, I, I, I, I, I, P],
+    "r2_lstm_bwd": [P, P, P, P, P, P, P, P, P, I, I, I, I, P],
+    "r2_torso_fwd": [P, P, I, P, P, P, P, P, P, P, P, P, I, P],
+    "r2_frames_to_bf16": [P, P, I, P, P],
+    "r2_dueling_fwd": [P, P, P, P, P, P, I, I, I, P],
+    "r2_dueling_bwd": [P, P, P, P, P, I, I, I, P],
+    "r2_td_loss": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, F, F, F, F, P],
+    "r2_tree_sample": [P, P, P, I, I, U64, P, P, P, P],
+    "r2_tree_rebuild": [P, P, P, I, P],
+    "r2_tree_update": [P, P, P, I, P, P, I, P],
+    "r2_seqprio_refresh": [P, I, P, P, P, I, I, I, I, F, P, P, I, P],
+    "r2_mark_starts": [P, P, I, P, P, P, I, I, F, P, P, P, I, P],
+    "r2_make_rows": [P, I, I, I, I, P, P],
+    "r2_gather_state": [P, P, I, I, I, I, P, P, P, P],
+    "r2_step_end": [P, P, P],
+    "r2_rmsprop_centered": [P, P, P, P, I64, F, F, F, F, P, F, P],
+    "r2_adam": [P, P, P, P, I64, F, F, F, F, F, P, P, F, P],
+    "r2_sumsq": [P, I64, P, P],
+    "r2_pack_bf16": [P, P, P, I64, P],
+    "r2_gather_f32": [P, P, P, I64, P],
+    "r2_copy_if_due": [P, P, I64, P, I64, P],
+    "r2_actor_finalize": [P] * 21 + [I, I, I, I, I, I, F, F, F, F, U64, P],
+}
+
+
+def library_path() -> Path:
+    return _SO
+
+
+def available() -> bool:
+    return _SO.exists()
+
+
+def kernels():
+    """Return the loaded ctypes library, building it on first use if needed."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not _SO.exists():
+            if os.environ.get("R2D2_NO_AUTOBUILD"):
+                raise RuntimeError(f"{_SO} missing; run `python -m pytorch_r2d2_amd._build`")
+            from .. import _build
+            _build.build(verbose=False)
+        torch.cuda.is_available()  # make sure torch's HIP runtime is mapped first
+        lib = ctypes.CDLL(str(_SO), mode=ctypes.RTLD_GLOBAL)
+        for name, argtypes in _SIGS.items():
+            fn = getattr(lib, name, None)
+            if fn is None:
+                continue
+            fn.argtypes = argtypes
+            fn.restype = ctypes.c_int
+        _lib = lib
+        return lib
+
+
+def ptr(t) -> int:
+    """Device/host pointer of a tensor (0 for None)."""
+    if t is None:
+        return 0
+    return t.data_ptr()
+
+
+def stream_handle(stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with code {rc}")

@@ -1,0 +1,263 @@
+"""Numerics of every HIP kernel against a plain fp32 PyTorch reference of the same op."""
+import numpy as np
+import pytest
+import torch
+
+from pytorch_r2d2_amd.config import get_config
+from pytorch_r2d2_amd.engine.layout import ParamLayout, UNITS
+from pytorch_r2d2_amd.models import QNet
+from pytorch_r2d2_amd.ops._lib import kernels, ptr, stream_handle
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _setup(B=8, H=256, seed=0):
+    cfg = get_config("atari57", **{"model.hidden": H})
+    torch.manual_seed(seed)
+    net = QNet("cpu", cfg.model, cfg.env)
+    L = ParamLayout(cfg.model, cfg.env)
+    flat = L.from_module(net, DEV)
+    bf = torch.zeros(L.bf_numel, dtype=torch.bfloat16, device=DEV)
+    f32 = torch.zeros(L.f_numel, device=DEV)
+    k = kernels()
+    k.r2_pack_bf16(ptr(flat), ptr(L.bf_index.to(DEV)), ptr(bf), L.bf_numel, stream_handle())
+    k.r2_gather_f32(ptr(flat), ptr(L.f_index.to(DEV)), ptr(f32), L.f_numel, stream_handle())
+    return cfg, net.to(DEV), L, flat, L.packed_views(bf, f32)
+
+
+@pytest.mark.parametrize("B,H", [(8, 256), (64, 256), (40, 128), (128, 256)])
+def test_lstm_forward_matches_lstmcell(B, H):
+    cfg, net, L, flat, pk = _setup(B, H)
+    T = 7
+    G = 4 * H
+    x = torch.randn(T, B, L.D, device=DEV) * 0.5
+    h0 = torch.randn(B, H, device=DEV) * 0.3
+    c0 = torch.randn(B, H, device=DEV) * 0.3
+    # reference in fp32 with bf16-rounded inputs/weights (the kernel's operand precision)
+    xb = x.bfloat16().float()
+    wih = net.lstm.weight_ih.bfloat16().float()
+    whh = net.lstm.weight_hh.bfloat16().float()
+    b = net.lstm.bias_ih + net.lstm.bias_hh
+    h, c = h0.bfloat16().float(), c0.clone()
+    ref_h, ref_c = [], []
+    for t in range(T):
+        g = xb[t] @ wih.t() + b + h.bfloat16().float() @ whh.t()
+        i, f, gg, o = g.chunk(4, 1)
+        c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
+        h = torch.sigmoid(o) * torch.tanh(c)
+        ref_h.append(h)
+        ref_c.append(c)
+    ref_h, ref_c = torch.stack(ref_h), torch.stack(ref_c)
+    perm = L.gate_perm.to(DEV)
+    xproj = (xb.view(T * B, -1) @ wih[perm].t() + b[perm]).contiguous()
+    hseq = torch.zeros(T, B, H, dtype=torch.bfloat16, device=DEV)
+    cseq = torch.zeros(T, B, H, device=DEV)
+    h32 = torch.zeros(T, B, H, device=DEV)
+    gates = torch.zeros(T, B, G, device=DEV)
+    h0b = h0.bfloat16()
+    chain = [ptr(xproj), ptr(pk["w_hh"]), ptr(h0b), ptr(c0), ptr(hseq), ptr(cseq), ptr(h32),
+             ptr(gates), 0]
+    arr = np.asarray(chain * 2, dtype=np.int64)  # two identical chains in one launch
+    hseq2 = torch.zeros_like(hseq)
+    cseq2 = torch.zeros_like(cseq)
+    arr[9 + 4] = ptr(hseq2)
+    arr[9 + 5] = ptr(cseq2)
+    arr[9 + 6] = 0
+    arr[9 + 7] = 0
+    rc = kernels().r2_lstm_fwd(arr.ctypes.data, 2, B, T, H, 0, stream_handle())
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert _rel(h32, ref_h) < 2e-2
+    assert _rel(cseq, ref_c) < 2e-2
+    assert torch.equal(cseq, cseq2)
+    # saved gates (packed) == activations of the reference gate pre-activations
+    g_last = (xb[-1] @ wih.t() + b + ref_h[-2].bfloat16().float() @ whh.t())
+    act = torch.cat([torch.sigmoid(g_last[:, :2 * H]), torch.tanh(g_last[:, 2 * H:3 * H]),
+                     torch.sigmoid(g_last[:, 3 * H:])], 1)
+    assert _rel(gates[-1], act[:, perm]) < 3e-2
+
+
+@pytest.mark.parametrize("B,H", [(8, 256), (64, 256), (96, 128)])
+def test_lstm_backward_matches_autograd(B, H):
+    cfg, net, L, flat, pk = _setup(B, H, seed=1)
+    T, t0 = 9, 3
+    G = 4 * H
+    x = (torch.randn(T, B, L.D, device=DEV) * 0.5).bfloat16().float()
+    h0 = (torch.randn(B, H, device=DEV) * 0.3).bfloat16().float()
+    c0 = torch.randn(B, H, device=DEV) * 0.3
+    perm = L.gate_perm.to(DEV)
+    wih = net.lstm.weight_ih.detach().bfloat16().float()
+    whh = net.lstm.weight_hh.detach().bfloat16().float()
+    b = (net.lstm.bias_ih + net.lstm.bias_hh).detach()
+    xproj = (x.view(T * B, -1) @ wih[perm].t() + b[perm]).contiguous()
+    hseq = torch.zeros(T, B, H, dtype=torch.bfloat16, device=DEV)
+    cseq = torch.zeros(T, B, H, device=DEV)
+    gates = torch.zeros(T - t0, B, G, device=DEV)
+    h0b = h0.bfloat16()
+    arr = np.asarray([ptr(xproj), ptr(pk["w_hh"]), ptr(h0b), ptr(c0), ptr(hseq), ptr(cseq), 0,
+                      ptr(gates), t0], dtype=np.int64)
+    k = kernels()
+    assert k.r2_lstm_fwd(arr.ctypes.data, 1, B, T, H, 0, stream_handle()) == 0
+    dh_ext = torch.randn(T - t0, B, H, device=DEV)
+    nwg = H // UNITS
+    s0 = torch.zeros(nwg, B, H, device=DEV)
+    s1 = torch.zeros_like(s0)
+    dc = torch.zeros(B, H, device=DEV)
+    dg = torch.zeros(T - t0, B, G, dtype=torch.bfloat16, device=DEV)
+    assert k.r2_lstm_bwd(ptr(dh_ext), ptr(gates), ptr(cseq), ptr(c0), ptr(pk["w_hhT"]), ptr(s0),
+                         ptr(s1), ptr(dc), ptr(dg), B, T, t0, H, stream_handle()) == 0
+    torch.cuda.synchronize()
+    # autograd reference: state after burn-in steps [0,t0) is a constant (detached)
+    h, c = h0, c0
+    with torch.no_grad():
+        for t in range(t0):
+            g = x[t] @ wih.t() + b + h @ whh.t()
+            i, f, gg, o = g.chunk(4, 1)
+            c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
+            h = torch.sigmoid(o) * torch.tanh(c)
+    pre, hs = [], []
+    for t in range(t0, T):
+        g = x[t] @ wih.t() + b + h @ whh.t()
+        if not g.requires_grad:
+            g.requires_grad_(True)
+        else:
+            g.retain_grad()
+        pre.append(g)
+        i, f, gg, o = g.chunk(4, 1)
+        c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
+        h = torch.sigmoid(o) * torch.tanh(c)
+        hs.append(h)
+    loss = sum((hh * dh_ext[i]).sum() for i, hh in enumerate(hs))
+    loss.backward()
+    ref = torch.stack([p.grad for p in pre])  # (T-t0, B, G) original gate order
+    got = dg.float()[..., L.gate_inv.to(DEV)]
+    assert _rel(got, ref) < 3e-2
+
+
+def test_torso_matches_conv_stack():
+    cfg, net, L, flat, pk = _setup()
+    n = 37
+    frames = torch.randint(0, 256, (50, 4 * 84 * 84), dtype=torch.uint8, device=DEV)
+    rows = torch.randint(0, 50, (n,), dtype=torch.int32, device=DEV)
+    out = torch.zeros(n, 1568, dtype=torch.bfloat16, device=DEV)
+    a1 = torch.zeros(n, 400, 32, dtype=torch.bfloat16, device=DEV)
+    a2 = torch.zeros(n, 81, 32, dtype=torch.bfloat16, device=DEV)
+    for grid in (256, 5):  # one frame per block, and grid-stride with prefetch
+        rc = kernels().r2_torso_fwd(ptr(frames), ptr(rows), n, ptr(pk["conv1"]), ptr(pk["b1"]),
+                                    ptr(pk["conv2"]), ptr(pk["b2"]), ptr(pk["conv3"]), ptr(pk["b3"]),
+                                    ptr(out), ptr(a1), ptr(a2), grid, stream_handle())
+        assert rc == 0
+        torch.cuda.synchronize()
+        x = frames[rows.long()].view(n, 4, 84, 84).float() / 255.0
+        with torch.no_grad():
+            v = net.vis_layers
+            r1 = torch.relu(v[0](x))
+            r2 = torch.relu(v[2](r1))
+            ref = torch.relu(v[4](r2)).reshape(n, -1)
+        assert _rel(out, ref) < 2e-2
+        assert _rel(a1.view(n, 20, 20, 32).permute(0, 3, 1, 2), r1) < 2e-2
+        assert _rel(a2.view(n, 9, 9, 32).permute(0, 3, 1, 2), r2) < 2e-2
+
+
+def test_dueling_head_fwd_bwd():
+    cfg, net, L, flat, pk = _setup()
+    N, H, HD, A = 77, 256, 256, 6
+    h = torch.randn(N, H, device=DEV).bfloat16()
+    z = torch.mm(h, pk["head1"].t())
+    q = torch.zeros(N, A, device=DEV)
+    zr = torch.zeros(N, 2 * HD, dtype=torch.bfloat16, device=DEV)
+    k = kernels()
+    assert k.r2_dueling_fwd(ptr(z), ptr(pk["head_b1"]), ptr(pk["head_w2"]), ptr(pk["head_b2"]),
+                            ptr(q), ptr(zr), N, A, HD, stream_handle()) == 0
+    hf = h.float().requires_grad_(True)
+    with torch.enable_grad():
+        ref = net.head(hf)
+    assert _rel(q, ref) < 2e-2
+    dq = torch.randn(N, A, device=DEV)
+    dz = torch.zeros(N, 2 * HD, dtype=torch.bfloat16, device=DEV)
+    dva = torch.zeros(N, 1 + A, device=DEV)
+    assert k.r2_dueling_bwd(ptr(dq), ptr(zr), ptr(pk["head_w2"]), ptr(dz), ptr(dva), N, A, HD,
+                            stream_handle()) == 0
+    dh = torch.mm(dz, pk["head1"]).float()
+    ref.backward(dq)
+    torch.cuda.synchronize()
+    assert _rel(dh, hf.grad) < 3e-2
+    g_v = torch.mm(dva.t(), zr.float())
+    assert _rel(g_v[0, :HD], net.val[2].weight.grad[0]) < 3e-2
+    assert _rel(g_v[1:, HD:], net.adv[2].weight.grad) < 3e-2
+
+
+def test_rmsprop_centered_matches_torch():
+    n = 100003
+    p = torch.randn(n + 1, device=DEV)[:n].clone()  # odd size exercises the tail loop
+    g = torch.randn(n, device=DEV)
+    sq = torch.zeros(n, device=DEV)
+    ga = torch.zeros(n, device=DEV)
+    ref = p.clone().requires_grad_(True)
+    opt = torch.optim.RMSprop([ref], lr=6.25e-5, alpha=0.95, eps=1.5e-7, centered=True)
+    k = kernels()
+    for _ in range(3):
+        assert k.r2_rmsprop_centered(ptr(p), ptr(g), ptr(sq), ptr(ga), n, 6.25e-5, 0.95, 1.5e-7,
+                                     1.0, 0, 0.0, stream_handle()) == 0
+        ref.grad = g.clone()
+        opt.step()
+    torch.cuda.synchronize()
+    assert torch.allclose(p, ref.detach(), atol=1e-6, rtol=1e-5)
+
+
+def test_adam_matches_torch():
+    n = 4099
+    p = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    step = torch.zeros(1, dtype=torch.int64, device=DEV)
+    ref = p.clone().requires_grad_(True)
+    opt = torch.optim.Adam([ref], lr=1e-4, eps=1e-3)
+    k = kernels()
+    for _ in range(3):
+        assert k.r2_adam(ptr(p), ptr(g), ptr(m), ptr(v), n, 1e-4, 0.9, 0.999, 1e-3, 1.0, ptr(step),
+                         0, 0.0, stream_handle()) == 0
+        step += 1
+        ref.grad = g.clone()
+        opt.step()
+    torch.cuda.synchronize()
+    assert torch.allclose(p, ref.detach(), atol=1e-6, rtol=1e-5)
+
+
+def test_sum_tree_sample_and_update():
+    from pytorch_r2d2_amd.engine.replay_hbm import HBMReplay
+    cfg = get_config("reference", **{"replay.capacity": 70000, "replay.n_subrings": 7})
+    rp = HBMReplay(cfg, DEV)
+    rp.fill_synthetic(episode_len=120, seed=3)
+    leaves = rp.tree[: rp.capacity].clone()
+    total = rp.total_priority()
+    assert abs(total - leaves.double().sum().item()) / total < 1e-4
+    B = 4096
+    idx = torch.zeros(B, dtype=torch.int32, device=DEV)
+    prob = torch.zeros(B, device=DEV)
+    rp.sample(B, idx, prob)
+    torch.cuda.synchronize()
+    il = idx.long()
+    assert bool((leaves[il] > 0).all()), "sampled a row that is not a sequence start"
+    assert torch.allclose(prob, leaves[il] / total, rtol=1e-4)
+    # proportionality: chi-square-ish check on coarse bins
+    bins = 14
+    edges = torch.linspace(0, rp.capacity, bins + 1, device=DEV).long()
+    exp = torch.stack([leaves[edges[i]:edges[i + 1]].sum() for i in range(bins)]) / total * B
+    got = torch.histc(il.float(), bins=bins, min=0, max=rp.capacity)
+    assert ((got - exp).abs() / exp.sqrt()).max() < 5.0
+    # incremental update == full rebuild
+    rp.priority[il[:100]] = 5.0
+    rp.refresh_sequences(idx[:100], 100, 0, cfg.replay.seq_len)
+    rp.update_tree()
+    inc = rp.tree.clone()
+    rp.rebuild_tree()
+    torch.cuda.synchronize()
+    assert torch.allclose(inc, rp.tree, rtol=1e-5, atol=1e-3)
