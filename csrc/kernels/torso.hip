@@ -219,6 +219,57 @@ __global__ void frames_to_bf16_kernel(const uint8_t* __restrict__ frames, const 
   }
 }
 
+// Same, channels-last (N, 84, 84, 4) so the library conv1 weight-gradient pass needs no transpose.
+__global__ void frames_to_bf16_nhwc_kernel(const uint8_t* __restrict__ frames,
+                                           const int* __restrict__ rows, int n_frames,
+                                           bf16* __restrict__ out) {
+  const int f = blockIdx.y;
+  const size_t row = rows ? (size_t)rows[f] : (size_t)f;
+  const uint8_t* src = frames + row * torso::IN_BYTES;
+  bf16x4* dst = (bf16x4*)(out + (size_t)f * torso::IN_BYTES);
+  constexpr int PIX = 84 * 84;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < PIX; p += gridDim.x * blockDim.x) {
+    bf16x4 o;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) o[c] = (bf16)((float)src[c * PIX + p] * (1.f / 255.f));
+    dst[p] = o;
+  }
+}
+
+// grad * (act > 0) on bf16 tensors with identical memory layout (ReLU backward from output)
+__global__ void relu_mask_bf16_kernel(const bf16* __restrict__ g, const bf16* __restrict__ act,
+                                      bf16* __restrict__ out, int64_t n8) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += stride) {
+    bf16x8 gv = ((const bf16x8*)g)[i];
+    const bf16x8 av = ((const bf16x8*)act)[i];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gv[e] = ((float)av[e] > 0.f) ? gv[e] : (bf16)0.f;
+    ((bf16x8*)out)[i] = gv;
+  }
+}
+
+extern "C" int r2_frames_to_bf16_nhwc(const uint8_t* frames, const int* rows, int n_frames,
+                                      bf16* out, void* stream) {
+  if (n_frames <= 0) return 0;
+  hipLaunchKernelGGL(frames_to_bf16_nhwc_kernel, dim3(7, n_frames), dim3(1024), 0,
+                     (hipStream_t)stream, frames, rows, n_frames, out);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int r2_relu_mask_bf16(const bf16* g, const bf16* act, bf16* out, int64_t n,
+                                 void* stream) {
+  if (n <= 0) return 0;
+  if ((n & 7) || (((uintptr_t)g | (uintptr_t)act | (uintptr_t)out) & 15)) return -1;
+  int64_t blocks = (n / 8 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(relu_mask_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                     (hipStream_t)stream, g, act, out, n / 8);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int r2_torso_fwd(const uint8_t* frames, const int* rows, int n_frames,
                             const bf16* w1, const float* b1, const bf16* w2, const float* b2,
                             const bf16* w3, const float* b3, bf16* out, bf16* save1, bf16* save2,

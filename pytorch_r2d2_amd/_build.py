@@ -45,7 +45,7 @@ CXX_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
 def _digest(paths) -> str:
     h = hashlib.sha256()
     for p in sorted(paths):
-        h.update(str(p).encode())
+        h.update(Path(p).name.encode())
         h.update(Path(p).read_bytes())
     h.update(" ".join(HIP_FLAGS + CXX_FLAGS).encode())
     return h.hexdigest()[:16]

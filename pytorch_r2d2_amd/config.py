@@ -88,6 +88,7 @@ class LearnerConfig:
     #            Q(s_{t+n}) is read at offset +n of the same chain.
     target_mode: str = "shifted"
     compute_dtype: str = "bf16"
+    lstm_impl: str = "persistent"     # persistent (one launch per sequence) | step (launch per t)
     use_graph: bool = True            # capture the whole step in a HIP graph
     save_dir: str = "save"
 

@@ -103,7 +103,11 @@ class ParamLayout:
             off += int(np.prod(shape))
         self.numel = off
         self.padded = (off + 3) // 4 * 4
-        self.ref_order = [n for n, _ in torso] + [n for n, _ in core]
+        # module registration order of QNet == reference state_dict order (model.py:12-36)
+        self.ref_order = [n for n, _ in torso] + [
+            "lstm.weight_ih", "lstm.weight_hh", "lstm.bias_ih", "lstm.bias_hh",
+            "val.0.weight", "val.0.bias", "val.2.weight", "val.2.bias",
+            "adv.0.weight", "adv.0.bias", "adv.2.weight", "adv.2.bias"]
         self._build_pack_maps()
 
     # ------------------------------------------------------------------ views

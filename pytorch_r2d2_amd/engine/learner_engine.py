@@ -175,8 +175,13 @@ class LearnerEngine:
         self.slab0 = z(nwg, B, H)
         self.slab1 = z(nwg, B, H)
         self.dc = z(B, H)
+        self.slab_p = z(2, nwg, B, H)
+        self.ctr = z(1024, dt=torch.int32)
+        self.err = z(1, dt=torch.int32)
         self.dgates = z(Ll * B, G, dt=bf16)
         self.gamma_n = float(lc.gamma ** n)
+        self.ones_bf = torch.ones(1, Tn * B, dtype=bf16, device=d)
+        self.ones_f32 = torch.ones(1, Tn * B, dtype=f32, device=d)
 
     # ------------------------------------------------------------------ weights
     def _pack(self, always: bool = False, stream=None):
@@ -225,8 +230,13 @@ class LearnerEngine:
     def _lstm(self, chains, T, t_begin=0):
         k = kernels()
         arr = np.asarray([v for c in chains for v in c], dtype=np.int64)
-        check(k.r2_lstm_fwd(arr.ctypes.data, len(chains), self.B, T, self.layout.H, t_begin,
-                            stream_handle()), "lstm_fwd")
+        if self.cfg.learner.lstm_impl == "persistent" and t_begin == 0:
+            check(k.r2_lstm_fwd_persist(arr.ctypes.data, len(chains), self.B, T, self.layout.H,
+                                        ptr(self.ctr), ptr(self.err), stream_handle()),
+                  "lstm_fwd_persist")
+        else:
+            check(k.r2_lstm_fwd(arr.ctypes.data, len(chains), self.B, T, self.layout.H, t_begin,
+                                stream_handle()), "lstm_fwd")
 
     def _head(self, pk, h: torch.Tensor, q: torch.Tensor, zr: Optional[torch.Tensor]):
         N = h.shape[0]
@@ -317,15 +327,22 @@ class LearnerEngine:
         gw2 = L.span(g, "val.2.weight", "adv.2.weight", (1 + A, HD))
         gw2[0].copy_(g2[0, :HD])
         gw2[1:].copy_(g2[1:, HD:])
-        torch.sum(self.dva, 0, out=L.span(g, "val.2.bias", "adv.2.bias", (1 + A,)))
+        # column sums as GEMVs against a ones row (torch's dim-0 reduce is ~300 us here)
+        torch.mm(self.ones_f32[:, :N], self.dva, out=L.span(g, "val.2.bias", "adv.2.bias", (1, 1 + A)))
         h_learn = self.hseq["on"][Lb:T].reshape(N, H)
         L.span(g, "val.0.weight", "adv.0.weight", (2 * HD, H)).copy_(mm_f32(self.dz.t(), h_learn))
-        torch.sum(self.dz, 0, dtype=torch.float32, out=L.span(g, "val.0.bias", "adv.0.bias", (2 * HD,)))
+        L.span(g, "val.0.bias", "adv.0.bias", (1, 2 * HD)).copy_(mm_f32(self.ones_bf[:, :N], self.dz))
         dh = mm_f32(self.dz, pk["head1"])                               # (N, H)
-        self.dc.zero_()
-        check(k.r2_lstm_bwd(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]), ptr(self.c0["on"]),
-                            ptr(pk["w_hhT"]), ptr(self.slab0), ptr(self.slab1), ptr(self.dc),
-                            ptr(self.dgates), B, T, Lb, H, s), "lstm_bwd")
+        if self.cfg.learner.lstm_impl == "persistent":
+            check(k.r2_lstm_bwd_persist(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]),
+                                        ptr(self.c0["on"]), ptr(pk["w_hhT"]), ptr(self.slab_p),
+                                        ptr(self.dgates), B, T, Lb, H, ptr(self.ctr), ptr(self.err),
+                                        s), "lstm_bwd_persist")
+        else:
+            self.dc.zero_()
+            check(k.r2_lstm_bwd(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]), ptr(self.c0["on"]),
+                                ptr(pk["w_hhT"]), ptr(self.slab0), ptr(self.slab1), ptr(self.dc),
+                                ptr(self.dgates), B, T, Lb, H, s), "lstm_bwd")
         dg_o = self.dgates.index_select(1, self.gate_inv)               # original gate order
         X = self.X_on[Lb * B: T * B]
         L.view(g, "lstm.weight_ih").copy_(mm_f32(dg_o.t(), X))
@@ -334,20 +351,34 @@ class LearnerEngine:
         else:
             h_prev = torch.cat([self.h0["on"][None], self.hseq["on"][: T - 1]]).reshape(N, H)
         L.view(g, "lstm.weight_hh").copy_(mm_f32(dg_o.t(), h_prev))
-        db = torch.sum(dg_o, 0, dtype=torch.float32)
+        db = mm_f32(self.ones_bf[:, :N], dg_o).view(-1)
         L.view(g, "lstm.bias_ih").copy_(db)
         L.view(g, "lstm.bias_hh").copy_(db)
         self._dX = torch.mm(self.dgates, pk["w_ih"])                   # (N, D) bf16
 
+    def _relu_mask(self, grad: torch.Tensor, act: torch.Tensor) -> torch.Tensor:
+        """grad * (act > 0) for two tensors with the same (channels-last) memory layout."""
+        cl = torch.channels_last
+        if grad.is_contiguous(memory_format=cl) and act.is_contiguous(memory_format=cl):
+            out = torch.empty_like(grad)
+            check(kernels().r2_relu_mask_bf16(ptr(grad), ptr(act), ptr(out), grad.numel(),
+                                              stream_handle()), "relu_mask")
+            return out
+        return grad * (act > 0)
+
     def _backward_torso(self):
-        """Conv backward from the activations saved by the torso kernel."""
+        """Conv backward (library kernels) from the activations saved by the torso kernel.
+        Everything is channels-last so the library picks its NHWC kernels with no transposes."""
         k = kernels()
         s = stream_handle()
         B, Lb, Ll, T = self.B, self.Lb, self.Ll, self.T
         L, g = self.layout, self.grad
         N = Ll * B
-        out3 = self.X_on[Lb * B: T * B].view(N, 32, 7, 7)
-        g3 = self._dX.view(N, 32, 7, 7) * (out3 > 0)
+        cl = torch.channels_last
+        out3 = self.X_on[Lb * B: T * B]
+        g3 = torch.empty_like(self._dX)
+        check(k.r2_relu_mask_bf16(ptr(self._dX), ptr(out3), ptr(g3), g3.numel(), s), "relu_mask")
+        g3 = g3.view(N, 32, 7, 7).contiguous(memory_format=cl)
         a2 = self.act2.view(N, 9, 9, 32).permute(0, 3, 1, 2)
         a1 = self.act1.view(N, 20, 20, 32).permute(0, 3, 1, 2)
         m = self.master
@@ -355,16 +386,17 @@ class LearnerEngine:
         w2 = L.view(m, "vis_layers.2.weight").to(torch.bfloat16)
         w1 = L.view(m, "vis_layers.0.weight").to(torch.bfloat16)
         cb = torch.ops.aten.convolution_backward
-        d2, dw3, db3 = cb(g3.contiguous(memory_format=torch.channels_last), a2, w3, [32], [1, 1],
-                          [0, 0], [1, 1], False, [0, 0], 1, [True, True, True])
-        g2 = d2 * (a2 > 0)
-        d1, dw2, db2 = cb(g2.contiguous(memory_format=torch.channels_last), a1, w2, [32], [2, 2],
-                          [0, 0], [1, 1], False, [0, 0], 1, [True, True, True])
-        g1 = d1 * (a1 > 0)
-        check(k.r2_frames_to_bf16(ptr(self.replay.frames), ptr(self.rows[Lb * B: T * B]), N,
-                                  ptr(self.frames_bf), s), "frames_to_bf16")
-        _, dw1, db1 = cb(g1.contiguous(), self.frames_bf, w1, [32],
-                         [4, 4], [0, 0], [1, 1], False, [0, 0], 1, [False, True, True])
+        d2, dw3, db3 = cb(g3, a2, w3, [32], [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                          [True, True, True])
+        g2 = self._relu_mask(d2, a2)
+        d1, dw2, db2 = cb(g2, a1, w2, [32], [2, 2], [0, 0], [1, 1], False, [0, 0], 1,
+                          [True, True, True])
+        g1 = self._relu_mask(d1, a1)
+        check(k.r2_frames_to_bf16_nhwc(ptr(self.replay.frames), ptr(self.rows[Lb * B: T * B]), N,
+                                       ptr(self.frames_bf), s), "frames_to_bf16_nhwc")
+        fr = self.frames_bf.view(N, 84, 84, 4).permute(0, 3, 1, 2)
+        _, dw1, db1 = cb(g1, fr, w1, [32], [4, 4], [0, 0], [1, 1], False, [0, 0], 1,
+                         [False, True, True])
         L.view(g, "vis_layers.4.weight").copy_(dw3)
         L.view(g, "vis_layers.4.bias").copy_(db3)
         L.view(g, "vis_layers.2.weight").copy_(dw2)
@@ -469,3 +501,8 @@ class LearnerEngine:
 
     def loss_value(self) -> float:
         return float(self.loss.item())
+
+    def check_errors(self) -> None:
+        """Raise if a persistent kernel's bounded spin timed out (hand-off failure)."""
+        if int(self.err.item()) != 0:
+            raise RuntimeError("persistent LSTM kernel reported a hand-off timeout")

@@ -1,0 +1,141 @@
+"""Synthetic Atari-shaped environments (no ROMs in this image).
+
+Dynamics ("cue-and-act"): every ``switch`` agent steps the env draws a target action and paints
+a bright vertical bar in the column band of that action on all stacked frames (on top of
+low-amplitude noise).  Reward is +1 when the agent's action equals the current target, else 0;
+episodes last ``episode_len`` agent steps.  With ``cue_only_first`` the bar is visible only on
+the first step after a switch, so acting well requires memory (exercises the LSTM / stored
+state / burn-in path).  A greedy agent on random weights scores ~1/A per step; a trained one
+approaches 1.
+
+``SyntheticAtariEnv`` is the numpy single-env version with the PongEnv API
+(step -> (state float32 (4,84,84)/255, reward, done, info), reset -> state).
+``VecSyntheticAtari`` runs E envs on a torch device and writes uint8 frames into a
+preallocated (E, 4*84*84) buffer -- the batched GPU actor's input.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+
+class SyntheticAtariEnv:
+    def __init__(self, seed: int = 0, episode_len: int = 400, n_actions: int = 6,
+                 action_repeat: int = 4, n_stacks: int = 4, switch: int = 8,
+                 cue_only_first: bool = False, shape=(84, 84)):
+        self.rng = np.random.default_rng(seed)
+        self.episode_len = episode_len
+        self.n_actions = n_actions
+        self.action_repeat = action_repeat
+        self.n_stacks = n_stacks
+        self.switch = switch
+        self.cue_only_first = cue_only_first
+        self.h, self.w = shape
+        self.t = 0
+        self.target = 0
+
+        class _Space:
+            def __init__(s, n, rng):
+                s.n, s._rng = n, rng
+
+            def sample(s):
+                return int(s._rng.integers(s.n))
+
+        self.action_space = _Space(n_actions, self.rng)
+
+    def _frame(self) -> np.ndarray:
+        f = self.rng.integers(0, 48, size=(self.n_stacks, self.h, self.w), dtype=np.uint8)
+        show = (not self.cue_only_first) or (self.t % self.switch == 0)
+        if show:
+            band = self.w // self.n_actions
+            f[:, :, self.target * band:(self.target + 1) * band] = 220
+        return f
+
+    def _obs(self) -> np.ndarray:
+        return self._frame().astype(np.float32) / 255.0
+
+    def step(self, action: int):
+        reward = 1.0 if int(action) == self.target else 0.0
+        self.t += 1
+        if self.t % self.switch == 0:
+            self.target = int(self.rng.integers(self.n_actions))
+        done = self.t >= self.episode_len
+        return self._obs(), reward, done, {}
+
+    def reset(self):
+        self.t = 0
+        self.target = int(self.rng.integers(self.n_actions))
+        return self._obs()
+
+
+class DMLabSynthEnv(SyntheticAtariEnv):
+    """96x72 RGB frames (DMLab-30 preset); obs (3*n_stacks, 72, 96)."""
+
+    def __init__(self, seed: int = 0, episode_len: int = 400, n_actions: int = 15, **kw):
+        super().__init__(seed=seed, episode_len=episode_len, n_actions=n_actions, n_stacks=3,
+                         shape=(72, 96), **kw)
+
+
+class VecSyntheticAtari:
+    """E synthetic envs on a torch device.  ``frames`` (E, C*H*W) uint8 is rewritten in place
+    by ``reset_all``/``step`` (the actor's torso kernel reads it directly)."""
+
+    def __init__(self, n_envs: int, device, seed: int = 0, episode_len: int = 400,
+                 n_actions: int = 6, n_stacks: int = 4, switch: int = 8,
+                 cue_only_first: bool = False, shape=(84, 84), randomize_start: bool = True):
+        self.E, self.A = n_envs, n_actions
+        self.device = torch.device(device)
+        self.episode_len, self.switch = episode_len, switch
+        self.cue_only_first = cue_only_first
+        self.C, (self.h, self.w) = n_stacks, shape
+        self.g = torch.Generator(device=self.device)
+        self.g.manual_seed(seed)
+        d = self.device
+        self.frames = torch.zeros((n_envs, self.C * self.h * self.w), dtype=torch.uint8, device=d)
+        self.t = torch.zeros(n_envs, dtype=torch.int64, device=d)
+        self.target = torch.zeros(n_envs, dtype=torch.int64, device=d)
+        self.ep_return = torch.zeros(n_envs, dtype=torch.float32, device=d)
+        self.randomize_start = randomize_start
+        band = self.w // n_actions
+        col = torch.arange(self.w, device=d)
+        # (A, W) mask of each action's column band
+        self._bands = (col[None, :] // band) == torch.arange(n_actions, device=d)[:, None]
+        self._bands &= col[None, :] < band * n_actions
+
+    def _render(self):
+        E = self.E
+        noise = torch.randint(0, 48, (E, self.C, self.h, self.w), dtype=torch.uint8,
+                              device=self.device, generator=self.g)
+        show = torch.ones(E, dtype=torch.bool, device=self.device)
+        if self.cue_only_first:
+            show = (self.t % self.switch) == 0
+        mask = self._bands[self.target] & show[:, None]                  # (E, W)
+        noise = torch.where(mask[:, None, None, :], torch.full_like(noise, 220), noise)
+        self.frames.copy_(noise.view(E, -1))
+
+    def reset_all(self):
+        self.t.zero_()
+        if self.randomize_start:  # de-synchronise episode boundaries across envs
+            self.t.copy_(torch.randint(0, self.episode_len, (self.E,), device=self.device,
+                                       generator=self.g))
+        self.target.copy_(torch.randint(0, self.A, (self.E,), device=self.device, generator=self.g))
+        self.ep_return.zero_()
+        self._render()
+        return self.frames
+
+    def step(self, actions: torch.Tensor):
+        """actions (E,) int on device -> (reward (E,) f32, done (E,) bool, finished_returns).
+
+        Envs whose episode ended are reset in place (their new first frame is rendered)."""
+        reward = (actions.long() == self.target).float()
+        self.ep_return += reward
+        self.t += 1
+        sw = (self.t % self.switch) == 0
+        new_t = torch.randint(0, self.A, (self.E,), device=self.device, generator=self.g)
+        self.target = torch.where(sw, new_t, self.target)
+        done = self.t >= self.episode_len
+        finished = torch.where(done, self.ep_return, torch.full_like(self.ep_return, float("nan")))
+        self.t = torch.where(done, torch.zeros_like(self.t), self.t)
+        self.ep_return = torch.where(done, torch.zeros_like(self.ep_return), self.ep_return)
+        self._render()
+        return reward, done, finished

@@ -104,7 +104,8 @@ def r2d2_loss(online: QNet, target: QNet, batch: SeqBatch, cfg: R2D2Config,
     delta = q_sa - y.detach()
     loss = (batch.weights[None, :] * 0.5 * delta ** 2).mean()
     prio = (delta.detach().abs() + rc.priority_eps) ** rc.alpha
-    return {"loss": loss, "delta": delta.detach(), "priority": prio, "q_sa": q_sa.detach()}
+    return {"loss": loss, "delta": delta.detach(), "priority": prio, "q_sa": q_sa.detach(),
+            "q_arg": q_arg.detach(), "q_tgt": q_tgt.detach()}
 
 
 def batch_from_hbm(replay, starts: torch.Tensor, probs: Optional[torch.Tensor], cfg: R2D2Config,

@@ -31,6 +31,8 @@ _SIGS = {
     "r2_lstm_bwd": [P, P, P, P, P, P, P, P, P, I, I, I, I, P],
     "r2_torso_fwd": [P, P, I, P, P, P, P, P, P, P, P, P, I, P],
     "r2_frames_to_bf16": [P, P, I, P, P],
+    "r2_frames_to_bf16_nhwc": [P, P, I, P, P],
+    "r2_relu_mask_bf16": [P, P, P, I64, P],
     "r2_dueling_fwd": [P, P, P, P, P, P, I, I, I, P],
     "r2_dueling_bwd": [P, P, P, P, P, I, I, I, P],
     "r2_td_loss": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, F, F, F, F, P],
@@ -48,6 +50,9 @@ _SIGS = {
     "r2_pack_bf16": [P, P, P, I64, P],
     "r2_gather_f32": [P, P, P, I64, P],
     "r2_copy_if_due": [P, P, I64, P, I64, P],
+    "r2_noop_chain": [P, I, I, P],
+    "r2_lstm_fwd_persist": [P, I, I, I, I, P, P, P],
+    "r2_lstm_bwd_persist": [P, P, P, P, P, P, P, I, I, I, I, P, P, P],
     "r2_actor_finalize": [P] * 21 + [I, I, I, I, I, I, F, F, F, F, U64, P],
 }
 

@@ -31,8 +31,9 @@ def _setup(B=8, H=256, seed=0):
     return cfg, net.to(DEV), L, flat, L.packed_views(bf, f32)
 
 
-@pytest.mark.parametrize("B,H", [(8, 256), (64, 256), (40, 128), (128, 256)])
-def test_lstm_forward_matches_lstmcell(B, H):
+@pytest.mark.parametrize("impl", ["step", "persistent"])
+@pytest.mark.parametrize("B,H", [(8, 256), (64, 256), (40, 128), (128, 256), (16, 512), (33, 64)])
+def test_lstm_forward_matches_lstmcell(B, H, impl):
     cfg, net, L, flat, pk = _setup(B, H)
     T = 7
     G = 4 * H
@@ -70,8 +71,17 @@ def test_lstm_forward_matches_lstmcell(B, H):
     arr[9 + 5] = ptr(cseq2)
     arr[9 + 6] = 0
     arr[9 + 7] = 0
-    rc = kernels().r2_lstm_fwd(arr.ctypes.data, 2, B, T, H, 0, stream_handle())
+    if impl == "step":
+        rc = kernels().r2_lstm_fwd(arr.ctypes.data, 2, B, T, H, 0, stream_handle())
+    else:
+        ctr = torch.zeros(1024, dtype=torch.int32, device=DEV)
+        err = torch.zeros(1, dtype=torch.int32, device=DEV)
+        rc = kernels().r2_lstm_fwd_persist(arr.ctypes.data, 2, B, T, H, ptr(ctr), ptr(err),
+                                           stream_handle())
     assert rc == 0
+    if impl == "persistent":
+        torch.cuda.synchronize()
+        assert err.item() == 0
     torch.cuda.synchronize()
     assert _rel(h32, ref_h) < 2e-2
     assert _rel(cseq, ref_c) < 2e-2
@@ -83,8 +93,9 @@ def test_lstm_forward_matches_lstmcell(B, H):
     assert _rel(gates[-1], act[:, perm]) < 3e-2
 
 
-@pytest.mark.parametrize("B,H", [(8, 256), (64, 256), (96, 128)])
-def test_lstm_backward_matches_autograd(B, H):
+@pytest.mark.parametrize("impl", ["step", "persistent"])
+@pytest.mark.parametrize("B,H", [(8, 256), (64, 256), (96, 128), (16, 512), (33, 64)])
+def test_lstm_backward_matches_autograd(B, H, impl):
     cfg, net, L, flat, pk = _setup(B, H, seed=1)
     T, t0 = 9, 3
     G = 4 * H
@@ -110,9 +121,19 @@ def test_lstm_backward_matches_autograd(B, H):
     s1 = torch.zeros_like(s0)
     dc = torch.zeros(B, H, device=DEV)
     dg = torch.zeros(T - t0, B, G, dtype=torch.bfloat16, device=DEV)
-    assert k.r2_lstm_bwd(ptr(dh_ext), ptr(gates), ptr(cseq), ptr(c0), ptr(pk["w_hhT"]), ptr(s0),
-                         ptr(s1), ptr(dc), ptr(dg), B, T, t0, H, stream_handle()) == 0
+    if impl == "step":
+        assert k.r2_lstm_bwd(ptr(dh_ext), ptr(gates), ptr(cseq), ptr(c0), ptr(pk["w_hhT"]), ptr(s0),
+                             ptr(s1), ptr(dc), ptr(dg), B, T, t0, H, stream_handle()) == 0
+    else:
+        slab = torch.zeros(2, nwg, B, H, device=DEV)
+        ctr = torch.zeros(1024, dtype=torch.int32, device=DEV)
+        err = torch.zeros(1, dtype=torch.int32, device=DEV)
+        assert k.r2_lstm_bwd_persist(ptr(dh_ext), ptr(gates), ptr(cseq), ptr(c0), ptr(pk["w_hhT"]),
+                                     ptr(slab), ptr(dg), B, T, t0, H, ptr(ctr), ptr(err),
+                                     stream_handle()) == 0
     torch.cuda.synchronize()
+    if impl == "persistent":
+        assert err.item() == 0
     # autograd reference: state after burn-in steps [0,t0) is a constant (detached)
     h, c = h0, c0
     with torch.no_grad():

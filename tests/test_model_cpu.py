@@ -1,0 +1,157 @@
+"""CPU tests: config presets, QNet reference API / state_dict parity, flat layout + packing,
+value rescaling, reference learner modes."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from pytorch_r2d2_amd.config import PRESETS, epsilon_ladder, get_config
+from pytorch_r2d2_amd.engine.layout import ParamLayout, gate_perm
+from pytorch_r2d2_amd.learner_ref import SeqBatch, r2d2_loss
+from pytorch_r2d2_amd.models import (QNet, REFERENCE_STATE_DICT_SHAPES, value_rescale,
+                                     value_rescale_inv)
+
+
+def test_presets_build_and_override():
+    for name in PRESETS:
+        cfg = get_config(name)
+        assert cfg.name == name
+        assert cfg.replay.seq_len == cfg.replay.burn_in + cfg.replay.learn
+    cfg = get_config("reference", **{"learner.batch_size": "32", "learner.value_rescale": "true"})
+    assert cfg.learner.batch_size == 32 and cfg.learner.value_rescale is True
+    ref = get_config("reference")
+    # SURVEY §2.6 values
+    assert (ref.learner.batch_size, ref.replay.burn_in, ref.replay.learn, ref.replay.n_step) == (8, 10, 10, 3)
+    assert ref.learner.gamma == 0.99 and ref.replay.eta == 0.9 and ref.replay.alpha == 0.6
+    assert ref.learner.lr == pytest.approx(6.25e-5) and ref.learner.rms_alpha == 0.95
+    a57 = get_config("atari57")
+    assert (a57.learner.batch_size, a57.replay.seq_len, a57.replay.n_step) == (64, 80, 5)
+
+
+def test_epsilon_ladder_matches_reference_and_fixes_n1():
+    # actor.py:22: 0.4 ** (1 + i*7/(N-1)); Q1: N==1 divides by zero in the reference
+    assert epsilon_ladder(0, 1) == pytest.approx(0.4)
+    assert epsilon_ladder(0, 8) == pytest.approx(0.4)
+    assert epsilon_ladder(7, 8) == pytest.approx(0.4 ** 8)
+    assert epsilon_ladder(3, 5) == pytest.approx(0.4 ** (1 + 3 * 7 / 4))
+
+
+def test_qnet_state_dict_matches_reference_shapes():
+    q = QNet()
+    sd = q.state_dict()
+    assert {k: tuple(v.shape) for k, v in sd.items()} == REFERENCE_STATE_DICT_SHAPES
+    assert sum(p.numel() for p in q.parameters()) == 2_037_095
+
+
+def test_qnet_stateful_forward_semantics():
+    torch.manual_seed(0)
+    q = QNet()
+    x = torch.rand(5, 3, 4, 84, 84)
+    q.reset()
+    out, hs, cs = q(x, True)
+    assert out.shape == (15, 6) and hs.shape == (15, 256) and isinstance(hs, np.ndarray)
+    # stepping one frame at a time with the carried state gives the same result
+    q.reset()
+    outs = [q(x[t]) for t in range(5)]
+    assert torch.allclose(torch.cat(outs), out, atol=1e-5)
+    # set_state/get_state round trip
+    h, c = q.get_state()
+    q.set_state(torch.from_numpy(h), torch.from_numpy(c))
+    o2 = q(x[0])
+    assert o2.shape == (3, 6)
+
+
+def test_value_rescale_inverse():
+    x = torch.linspace(-500, 500, 2001, dtype=torch.float64)
+    assert torch.allclose(value_rescale_inv(value_rescale(x)), x, rtol=1e-6, atol=1e-6)
+
+
+def test_layout_roundtrip_and_packing():
+    cfg = get_config("atari57")
+    torch.manual_seed(1)
+    q = QNet("cpu", cfg.model, cfg.env)
+    L = ParamLayout(cfg.model, cfg.env)
+    flat = L.from_module(q, "cpu")
+    sd = L.state_dict(flat)
+    assert list(sd) == list(q.state_dict())
+    for k, v in q.state_dict().items():
+        assert torch.equal(sd[k], v)
+    bf = torch.zeros(L.bf_numel, dtype=torch.bfloat16)
+    f32 = torch.zeros(L.f_numel)
+    L.pack_torch(flat, bf, f32)
+    pk = L.packed_views(bf, f32)
+    perm = gate_perm(256)
+    assert sorted(perm.tolist()) == list(range(1024))
+    assert torch.equal(pk["w_ih"], q.lstm.weight_ih.detach()[perm].bfloat16())
+    assert torch.equal(pk["w_hh"].view(1024, 256), q.lstm.weight_hh.detach()[perm].bfloat16())
+    assert torch.equal(pk["w_hhT"][5], q.lstm.weight_hh.detach()[perm].view(16, 64, 256)[5].t().bfloat16())
+    assert torch.equal(pk["conv2"], q.vis_layers[2].weight.detach().permute(0, 2, 3, 1).reshape(32, 512).bfloat16())
+    assert torch.equal(pk["conv3"], q.vis_layers[4].weight.detach().permute(0, 2, 3, 1).reshape(32, 288).bfloat16())
+    assert torch.equal(pk["head1"], torch.cat([q.val[0].weight, q.adv[0].weight]).detach().bfloat16())
+    assert torch.equal(pk["head_w2"], torch.cat([q.val[2].weight, q.adv[2].weight]).detach())
+    assert torch.equal(pk["b_ih"], q.lstm.bias_ih.detach()[perm])
+    # gradient bucket split: torso segment starts after the core (LSTM + head) bucket
+    assert L.torso_offset >= L.core_numel and L.torso_offset % 4 == 0
+
+
+def _toy_batch(cfg, B=3, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    rc = cfg.replay
+    T = rc.seq_len + rc.n_step
+    H = cfg.model.hidden
+    obs = torch.rand(T, B, 4, 84, 84, generator=g)
+    r = lambda *s: torch.randn(*s, generator=g) * 0.1  # noqa: E731
+    return SeqBatch(obs=obs, h0=r(B, H), c0=r(B, H), th0=r(B, H), tc0=r(B, H), nh0=r(B, H), nc0=r(B, H),
+                    action=torch.randint(0, 6, (rc.learn, B), generator=g),
+                    reward=torch.randn(rc.learn, B, generator=g),
+                    done=(torch.rand(rc.learn, B, generator=g) < 0.1).float(), weights=torch.ones(B))
+
+
+@pytest.mark.parametrize("mode", ["shifted", "fixed", "reference"])
+def test_reference_learner_modes(mode):
+    cfg = get_config("reference", **{"replay.burn_in": 3, "replay.learn": 4})
+    torch.manual_seed(0)
+    online, target = QNet(), QNet()
+    out = r2d2_loss(online, target, _toy_batch(cfg), cfg, mode)
+    out["loss"].backward()
+    assert out["loss"].item() > 0
+    assert out["priority"].shape == (4, 3)
+    # gradients reach every online parameter, none reach the target net
+    assert all(p.grad is not None for p in online.parameters())
+    assert all(p.grad is None for p in target.parameters())
+
+
+def test_reference_mode_reproduces_q7_continuation():
+    """In `reference` mode the online-on-next chain continues from the end of the learning
+    chain (learner.py:82-91); in `fixed` mode it starts from the stored state at s+n."""
+    cfg = get_config("reference", **{"replay.burn_in": 2, "replay.learn": 3})
+    torch.manual_seed(3)
+    online, target = QNet(), QNet()
+    b = _toy_batch(cfg, seed=4)
+    q_ref = r2d2_loss(online, target, b, cfg, "reference")["q_arg"]
+    q_fix = r2d2_loss(online, target, b, cfg, "fixed")["q_arg"]
+    assert q_ref.shape == q_fix.shape
+    assert not torch.allclose(q_ref, q_fix)
+    # the reference-mode chain does not depend on the stored state at s+n
+    b.nh0 = b.nh0 + 1.0
+    assert torch.allclose(r2d2_loss(online, target, b, cfg, "reference")["q_arg"], q_ref)
+    assert not torch.allclose(r2d2_loss(online, target, b, cfg, "fixed")["q_arg"], q_fix)
+
+
+def test_burn_in_blocks_gradient():
+    cfg = get_config("reference", **{"replay.burn_in": 3, "replay.learn": 2})
+    torch.manual_seed(0)
+    online, target = QNet(), QNet()
+    b = _toy_batch(cfg)
+    b2 = copy.deepcopy(b)
+    b2.obs[:3] += 0.0  # identical
+    l1 = r2d2_loss(online, target, b, cfg, "shifted")["loss"]
+    l1.backward()
+    g1 = online.vis_layers[0].weight.grad.clone()
+    online.zero_grad()
+    # perturbing only burn-in frames changes the loss (via the state) but the torso gradient
+    # only comes from learning frames, so zeroing learning-frame obs changes the grad
+    b2.obs[3:5] = 0
+    r2d2_loss(online, target, b2, cfg, "shifted")["loss"].backward()
+    assert not torch.allclose(g1, online.vis_layers[0].weight.grad)

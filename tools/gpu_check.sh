@@ -11,4 +11,10 @@ if [ -n "$BENCH_ARGS" ]; then
   timeout -k 10 ${BENCH_TIMEOUT:-600} python bench.py $BENCH_ARGS > gpurun_out/bench.log 2>&1; rc=$?
   echo "BENCH rc=$rc"; tail -15 gpurun_out/bench.log; stop_if_crash $rc
 fi
+if [ -n "$PROF_ARGS" ]; then
+  export TMPDIR=/tmp
+  rm -rf gpurun_out/prof
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -- python bench.py $PROF_ARGS > gpurun_out/prof.log 2>&1; rc=$?
+  echo "PROF rc=$rc"; grep metric gpurun_out/prof.log | tail -1; stop_if_crash $rc
+fi
 exit 0
