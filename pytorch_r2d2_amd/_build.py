@@ -80,6 +80,13 @@ def _build_so(srcs, out: Path, compiler, flags, link_extra, jobs: int, force: bo
     return True
 
 
+def build_runtime(force: bool = False, jobs: int = 0) -> bool:
+    """Host runtime only (g++; used on machines without a ROCm toolchain)."""
+    rt_srcs = sorted((CSRC / "runtime").glob("*.cpp"))
+    return _build_so(rt_srcs, RUNTIME_SO, CXX, CXX_FLAGS, ["-lpthread", "-lrt"],
+                     jobs or min(8, os.cpu_count() or 4), force)
+
+
 def build(force: bool = False, jobs: int = 0, verbose: bool = True) -> None:
     jobs = jobs or min(8, os.cpu_count() or 4)
     if not Path(HIPCC).exists() and shutil.which("hipcc") is None:

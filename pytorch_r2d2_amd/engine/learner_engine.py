@@ -435,38 +435,41 @@ class LearnerEngine:
         rp.update_tree()
         rp.step_end()
 
-    def _allreduce(self, lo: int, hi: int):
-        if self.world <= 1:
-            return
-        import torch.distributed as dist
-        buf = self.grad[lo:hi]
-        if self.cfg.dist.grad_dtype == "bf16":
-            tmp = buf.to(torch.bfloat16)
-            dist.all_reduce(tmp, group=self.pg)
-            buf.copy_(tmp)
-        else:
-            dist.all_reduce(buf, group=self.pg)
-
     # ------------------------------------------------------------------ public API
-    def _step_body(self):
+    def _sync(self):
+        if getattr(self, "_gsync", None) is None:
+            from ..parallel.grad_sync import GradSync
+            self._gsync = GradSync(self.grad, self.world, self.pg, self.cfg.dist.grad_dtype,
+                                   use_stream=self.cfg.dist.overlap_allreduce)
+        return self._gsync
+
+    def _seg_core(self):
         self._forward_loss()
         self._backward_core()
+
+    def _seg_torso(self):
         self._backward_torso()
 
-    def _step_tail(self):
+    def _seg_tail(self):
         self._update()
         self._priorities()
 
     def step_eager(self):
-        self._step_body()
+        L = self.layout
+        self._seg_core()
+        if self.world > 1:   # core bucket all-reduce overlaps the conv backward
+            self._sync().start(0, L.torso_offset)
+        self._seg_torso()
         if self.world > 1:
-            self._allreduce(0, self.layout.padded)
-        self._step_tail()
+            self._sync().start(L.torso_offset, L.padded)
+            self._sync().finish()
+        self._seg_tail()
         self.steps_done += 1
 
     def capture(self, warmup: int = 2):
-        """Capture the step into HIP graph(s).  With world > 1 the all-reduce runs between two
-        graphs (body, tail) on the same stream."""
+        """Capture the step into HIP graphs.  world == 1: one graph for the whole step.
+        world > 1: three graphs (core fwd/bwd | conv bwd | update) with the two bucket
+        all-reduces issued between them on the communication stream."""
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
@@ -474,30 +477,37 @@ class LearnerEngine:
                 self.step_eager()
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
-        self.g_body = torch.cuda.CUDAGraph()
-        self.g_tail = torch.cuda.CUDAGraph()
+        self.graphs = []
         if self.world > 1:
-            with torch.cuda.graph(self.g_body):
-                self._step_body()
-            with torch.cuda.graph(self.g_tail, pool=self.g_body.pool()):
-                self._step_tail()
+            segs = [self._seg_core, self._seg_torso, self._seg_tail]
         else:
-            with torch.cuda.graph(self.g_body):
-                self._step_body()
-                self._step_tail()
-            self.g_tail = None
+            segs = [lambda: (self._seg_core(), self._seg_torso(), self._seg_tail())]
+        pool = None
+        for fn in segs:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, pool=pool):
+                fn()
+            pool = g.pool()
+            self.graphs.append(g)
         torch.cuda.synchronize(self.device)
         self.graph = True
 
     def step(self):
-        if self.graph:
-            self.g_body.replay()
-            if self.g_tail is not None:
-                self._allreduce(0, self.layout.padded)
-                self.g_tail.replay()
-            self.steps_done += 1
-        else:
+        if not self.graph:
             self.step_eager()
+            return
+        if self.world <= 1:
+            self.graphs[0].replay()
+        else:
+            L = self.layout
+            g_core, g_torso, g_tail = self.graphs
+            g_core.replay()
+            self._sync().start(0, L.torso_offset)
+            g_torso.replay()
+            self._sync().start(L.torso_offset, L.padded)
+            self._sync().finish()
+            g_tail.replay()
+        self.steps_done += 1
 
     def loss_value(self) -> float:
         return float(self.loss.item())

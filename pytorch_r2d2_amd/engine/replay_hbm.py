@@ -203,3 +203,93 @@ class HBMReplay:
         self.heads[:] = 0
         self.rebuild_tree()
         torch.cuda.synchronize(d) if d.type == "cuda" else None
+
+    # ------------------------------------------------------------------ ingestion (host -> HBM)
+    @torch.no_grad()
+    def ingest_memory(self, mem, subring: Optional[int] = None) -> int:
+        """Write a ReplayMemory-schema dict (numpy / tensors, e.g. an actor transport file) as a
+        contiguous block into one sub-ring; sequence starts / priorities come with the block."""
+        n = int(mem["state"].shape[0])
+        if n == 0:
+            return 0
+        sub = (self.total_written // max(n, 1)) % self.n_sub if subring is None else subring % self.n_sub
+        keep = min(n, self.cap_e)
+        sl = slice(n - keep, n)
+        head = int(self.heads[sub])
+        base = sub * self.cap_e
+        rows = torch.as_tensor(base + (head + np.arange(keep)) % self.cap_e, device=self.device)
+        t = lambda k, dt=None: torch.as_tensor(np.asarray(mem[k])[sl]).to(self.device)  # noqa: E731
+        st = t("state")
+        if self.obs is not None:
+            self.obs[rows] = st.reshape(keep, -1).float()
+        else:
+            self.frames[rows] = st.reshape(keep, -1).to(torch.uint8)
+        self.hs_cs[rows] = t("hs_cs").float()
+        self.target_hs_cs[rows] = t("target_hs_cs").float()
+        self.action[rows] = t("action").reshape(-1).to(torch.uint8)
+        self.reward[rows] = t("reward").reshape(-1).float()
+        self.done[rows] = (t("done").reshape(-1) > 0).to(torch.uint8)
+        self.priority[rows] = t("priority").reshape(-1).float()
+        starts = t("is_seq_start").reshape(-1).to(torch.uint8)
+        self.is_start[rows] = starts
+        self.tree[rows] = t("sequence_priority").reshape(-1).float() * starts.float()
+        self.heads[sub] = (head + keep) % self.cap_e
+        self.total_written += keep
+        self.n_valid.fill_(int(self.is_start.sum().item()))
+        self.rebuild_tree()
+        return keep
+
+    def ingest_file(self, path: str, actor_id: int) -> int:
+        """Consume ``memory{actor_id}.pt`` written by a (compat) actor into HBM."""
+        import os
+        from ..replay.memory import ReplayMemory
+        from ..runtime import FileLock
+        fpath = os.path.join(path, f"memory{actor_id}.pt")
+        if not (os.path.isfile(fpath) and os.path.getsize(fpath) > 0):
+            return 0
+        lock = FileLock(fpath)
+        try:
+            if not lock.acquire(blocking=False):
+                return 0
+            mem = ReplayMemory.read_file(fpath)
+            n = self.ingest_memory(mem, subring=actor_id)
+            os.remove(fpath)
+            return n
+        finally:
+            lock.release()
+            lock.close()
+
+    # ------------------------------------------------------------------ device-side row writes
+    @torch.no_grad()
+    def clear_rows(self, rows: torch.Tensor) -> None:
+        """Rows about to be overwritten stop being sequence starts (leaf -> 0, n_valid--)."""
+        was = self.is_start[rows].to(torch.int32)
+        self.n_valid.sub_(was.sum().view(1))
+        self.is_start[rows] = 0
+        self.tree[rows] = 0.0
+        self._append_dirty(rows)
+
+    def _append_dirty(self, rows: torch.Tensor) -> None:
+        """Append rows to the dirty list (device-side, no host sync)."""
+        n = rows.numel()
+        if n == 0:
+            return
+        pos = self.dirty_count.long() + torch.arange(n, device=self.device)
+        ok = pos < self.max_dirty
+        self.dirty[pos.clamp_max(self.max_dirty - 1)] = torch.where(ok, rows.to(torch.int32),
+                                                                    self.dirty[pos.clamp_max(self.max_dirty - 1)])
+        self.dirty_count.add_(n)
+
+    def mark_starts(self, rows: torch.Tensor, n_rows: Optional[torch.Tensor] = None) -> None:
+        """Mark sequence starts (rows < 0 are ignored) and set their eta-mixed leaf priority."""
+        rc = self.cfg.replay
+        k = kernels()
+        check(k.r2_mark_starts(ptr(rows), ptr(n_rows), rows.numel(), ptr(self.is_start),
+                               ptr(self.priority), ptr(self.tree), rc.seq_len, self.cap_e,
+                               float(rc.eta), ptr(self.n_valid), ptr(self.dirty),
+                               ptr(self.dirty_count), self.max_dirty, stream_handle()), "mark_starts")
+
+    def flush_tree(self) -> None:
+        """Repair the tree for all dirty leaves and reset the dirty list."""
+        self.update_tree()
+        self.dirty_count.zero_()

@@ -1,0 +1,123 @@
+"""Actor -> learner trajectory push.
+
+Reference: actors pickle their whole 50k-row replay to ``./logs/memory/memory{id}.pt`` every 5
+episodes under a fasteners lock; the learner polls, unpickles, extends its ring and deletes the
+file (replay_memory.py:125-173) -- 233 MB per 5k rows, 1.5 s save / 1.2 s load.
+
+Two MI355X-native transports, both moving *packed rows* (uint8 frames + fp32 [h|c] x2 +
+scalars, the §2.5 schema) in fixed-size chunks:
+
+* ``RcclTrajectoryChannel`` -- GPU actor groups on one rank, learner replay shard on another:
+  a chunk is one ``dist.send`` of a header tensor + one of a packed byte tensor (device memory,
+  RCCL over xGMI), received with ``dist.recv`` directly into device memory and written into
+  the HBM replay with ``HBMReplay.ingest_memory``.
+* ``ShmTrajectoryWriter/Reader`` -- CPU actor processes on the same host: records go through
+  the native shared-memory SPSC ring (``runtime.ShmRing``) -- no files, no pickles, no locks.
+
+``pack_rows`` / ``unpack_rows`` define the wire format (a single uint8 buffer + header).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..runtime import ShmRing
+
+ORDER = ("state", "hs_cs", "target_hs_cs", "action", "reward", "done", "stack_count",
+         "priority", "sequence_priority", "is_seq_start")
+MAGIC = 0x52324454  # "R2DT"
+
+
+def pack_rows(mem: Dict[str, np.ndarray]) -> np.ndarray:
+    """Row-schema dict -> one contiguous uint8 buffer: [header int64 x (3 + 3*K)] + payloads."""
+    n = int(np.asarray(mem["state"]).shape[0])
+    parts, meta = [], []
+    for k in ORDER:
+        a = np.ascontiguousarray(np.asarray(mem[k]))
+        code = {np.dtype(np.uint8): 0, np.dtype(np.int8): 1, np.dtype(np.float32): 2}[a.dtype]
+        per_row = int(a.size // max(n, 1)) if n else int(np.prod(a.shape[1:]))
+        meta += [code, per_row, a.nbytes]
+        parts.append(a.view(np.uint8).reshape(-1))
+    hdr = np.asarray([MAGIC, n, len(ORDER)] + meta, dtype=np.int64).view(np.uint8)
+    return np.concatenate([hdr] + parts)
+
+
+def unpack_rows(buf: np.ndarray, state_shape=None) -> Dict[str, np.ndarray]:
+    buf = np.asarray(buf, dtype=np.uint8)
+    head = buf[:24].view(np.int64)
+    if int(head[0]) != MAGIC:
+        raise ValueError("bad trajectory record")
+    n, k = int(head[1]), int(head[2])
+    meta = buf[24:24 + 24 * k].view(np.int64).reshape(k, 3)
+    off = 24 + 24 * k
+    out = {}
+    dts = {0: np.uint8, 1: np.int8, 2: np.float32}
+    for name, (code, per_row, nbytes) in zip(ORDER, meta):
+        a = buf[off:off + int(nbytes)].view(dts[int(code)])
+        off += int(nbytes)
+        if name == "state" and state_shape is not None:
+            a = a.reshape(n, *state_shape)
+        elif per_row > 1:
+            a = a.reshape(n, int(per_row))
+        elif name in ("action", "reward", "done"):
+            a = a.reshape(n, 1)
+        out[name] = a
+    return out
+
+
+class ShmTrajectoryWriter:
+    def __init__(self, name: str, capacity: int = 256 << 20):
+        self.ring = ShmRing(name, capacity, create=False)
+        self.dropped = 0
+
+    def push(self, mem: Dict[str, np.ndarray], block: bool = True, spin_s: float = 0.001) -> bool:
+        import time
+        rec = pack_rows(mem)
+        while not self.ring.push(rec):
+            if not block:
+                self.dropped += 1
+                return False
+            time.sleep(spin_s)
+        return True
+
+
+class ShmTrajectoryReader:
+    def __init__(self, name: str, capacity: int = 256 << 20, state_shape=None):
+        self.ring = ShmRing(name, capacity, create=True)
+        self.state_shape = state_shape
+
+    def poll(self, max_records: int = 64) -> List[Dict[str, np.ndarray]]:
+        out = []
+        for _ in range(max_records):
+            rec = self.ring.pop()
+            if rec is None:
+                break
+            out.append(unpack_rows(np.frombuffer(rec, dtype=np.uint8), self.state_shape))
+        return out
+
+    def close(self):
+        self.ring.close(unlink=True)
+
+
+class RcclTrajectoryChannel:
+    """Point-to-point chunk transport between ranks (device tensors on RCCL, CPU on gloo)."""
+
+    def __init__(self, device, group=None):
+        self.device = torch.device(device)
+        self.group = group
+
+    def send(self, mem: Dict[str, np.ndarray], dst: int) -> None:
+        buf = torch.from_numpy(pack_rows(mem)).to(self.device)
+        size = torch.tensor([buf.numel()], dtype=torch.int64, device=self.device)
+        dist.send(size, dst, group=self.group)
+        dist.send(buf, dst, group=self.group)
+
+    def recv(self, src: int, state_shape=None) -> Dict[str, np.ndarray]:
+        size = torch.zeros(1, dtype=torch.int64, device=self.device)
+        dist.recv(size, src, group=self.group)
+        buf = torch.empty(int(size.item()), dtype=torch.uint8, device=self.device)
+        dist.recv(buf, src, group=self.group)
+        return unpack_rows(buf.cpu().numpy(), state_shape)

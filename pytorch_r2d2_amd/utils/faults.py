@@ -1,0 +1,72 @@
+"""Fault injection hooks (absent in the reference).
+
+Faults are declared with the ``R2D2_FAULTS`` environment variable (inherited by spawned
+processes) or programmatically, as ``;``-separated specs:
+
+    actor:<id>:crash_at=<step>        hard-exit (os._exit(17)) when that actor reaches step
+    actor:<id>:hang_at=<step>         stop beating (sleep forever) -> exercises the watchdog
+    learner:0:crash_at=<step>
+    push:<id>:drop=<prob>             drop a trajectory push with probability p
+    weights:<id>:stale=<n>            ignore the first n weight publications
+
+Roles call ``faults().check(role, id, step)`` / ``faults().drop(role, id)``; with no spec the
+calls are a dict lookup.
+"""
+from __future__ import annotations
+
+import os
+import random
+import time
+from typing import Dict, Tuple
+
+EXIT_CODE = 17
+
+
+class FaultPlan:
+    def __init__(self, spec: str = ""):
+        self.rules: Dict[Tuple[str, int], Dict[str, float]] = {}
+        self.rng = random.Random(1234)
+        for part in filter(None, (p.strip() for p in spec.split(";"))):
+            role, rid, kv = part.split(":", 2)
+            d = self.rules.setdefault((role, int(rid)), {})
+            for item in kv.split(","):
+                k, v = item.split("=")
+                d[k] = float(v)
+
+    def _r(self, role, rid):
+        return self.rules.get((role, int(rid)))
+
+    def check(self, role: str, rid: int, step: int) -> None:
+        r = self._r(role, rid)
+        if not r:
+            return
+        if "crash_at" in r and step >= r["crash_at"]:
+            os._exit(EXIT_CODE)
+        if "hang_at" in r and step >= r["hang_at"]:
+            while True:
+                time.sleep(3600)
+
+    def drop(self, role: str, rid: int) -> bool:
+        r = self._r(role, rid)
+        return bool(r and "drop" in r and self.rng.random() < r["drop"])
+
+    def stale(self, role: str, rid: int, n_seen: int) -> bool:
+        r = self._r(role, rid)
+        return bool(r and "stale" in r and n_seen < r["stale"])
+
+
+_plan = None
+
+
+def faults() -> FaultPlan:
+    global _plan
+    if _plan is None:
+        _plan = FaultPlan(os.environ.get("R2D2_FAULTS", ""))
+    return _plan
+
+
+def set_faults(spec: str) -> FaultPlan:
+    global _plan
+    os.environ["R2D2_FAULTS"] = spec
+    _plan = FaultPlan(spec)
+    return _plan
