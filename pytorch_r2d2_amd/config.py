@@ -89,6 +89,7 @@ class LearnerConfig:
     target_mode: str = "shifted"
     compute_dtype: str = "bf16"
     lstm_impl: str = "persistent"     # persistent (one launch per sequence) | step (launch per t)
+    torso_bwd: str = "fused"          # fused (HIP kernel) | library (MIOpen convolution_backward)
     use_graph: bool = True            # capture the whole step in a HIP graph
     save_dir: str = "save"
 

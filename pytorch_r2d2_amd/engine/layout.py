@@ -175,6 +175,19 @@ class ParamLayout:
                                          indexing="ij")
             add_bf("conv3", off("vis_layers.4.weight") + ((co * c2 + ci) * 3 + kh) * 3 + kw,
                    (c3, 9 * c2))
+            # backward (data-grad) layouts for the fused torso backward kernel:
+            # conv3_dg[ci][kh][kw][co] = W3[co][ci][kh][kw]     (B[k=(kh,kw,co)][ci])
+            ci, kh, kw, co = np.meshgrid(np.arange(c2), np.arange(3), np.arange(3), np.arange(c3),
+                                         indexing="ij")
+            add_bf("conv3_dg", off("vis_layers.4.weight") + ((co * c2 + ci) * 3 + kh) * 3 + kw,
+                   (c2, 9 * c3))
+            # conv2_dg[phase=(py,px)][ci][khi][kwi][co] = W2[co][ci][py+2khi][px+2kwi]
+            py, px, ci, khi, kwi, co = np.meshgrid(np.arange(2), np.arange(2), np.arange(c1),
+                                                   np.arange(2), np.arange(2), np.arange(c2),
+                                                   indexing="ij")
+            kh2, kw2 = py + 2 * khi, px + 2 * kwi
+            add_bf("conv2_dg", off("vis_layers.2.weight") + ((co * c1 + ci) * 4 + kh2) * 4 + kw2,
+                   (4, c1, 4 * c2))
         else:
             add_bf("mlp", off("vis_layers.0.weight") + np.arange(self.D * self.cin), (self.D, self.cin))
         add_bf("w_ih", off("lstm.weight_ih") + perm[:, None] * D + np.arange(D)[None, :], (G, D))
@@ -221,6 +234,27 @@ class ParamLayout:
         inv[perm] = np.arange(perm.size)
         self.gate_perm = torch.from_numpy(perm)
         self.gate_inv = torch.from_numpy(inv)
+
+    def torso_grad_map(self):
+        """(dst index into the flat grad buffer, scale) for every element of the fused torso
+        backward slab: [dW1 (co, ci*64) | dW2 (co, (kh,kw,ci)) | dW3 (co, (kh,kw,ci)) | db1 | db2 | db3]."""
+        c1, c2, c3 = self.model.conv_channels
+        off = lambda n: self.segs[n].offset  # noqa: E731
+        cin = self.cin
+        dst, scale = [], []
+        dst.append(off("vis_layers.0.weight") + np.arange(c1 * cin * 64))
+        scale.append(np.full(c1 * cin * 64, 1.0 / 255.0))
+        co, kh, kw, ci = np.meshgrid(np.arange(c2), np.arange(4), np.arange(4), np.arange(c1), indexing="ij")
+        dst.append((off("vis_layers.2.weight") + ((co * c1 + ci) * 4 + kh) * 4 + kw).reshape(-1))
+        scale.append(np.ones(c2 * 16 * c1))
+        co, kh, kw, ci = np.meshgrid(np.arange(c3), np.arange(3), np.arange(3), np.arange(c2), indexing="ij")
+        dst.append((off("vis_layers.4.weight") + ((co * c2 + ci) * 3 + kh) * 3 + kw).reshape(-1))
+        scale.append(np.ones(c3 * 9 * c2))
+        for name, c in (("vis_layers.0.bias", c1), ("vis_layers.2.bias", c2), ("vis_layers.4.bias", c3)):
+            dst.append(off(name) + np.arange(c))
+            scale.append(np.ones(c))
+        return (torch.from_numpy(np.concatenate(dst).astype(np.int32)),
+                torch.from_numpy(np.concatenate(scale).astype(np.float32)))
 
     def packed_views(self, bf: torch.Tensor, f32: torch.Tensor):
         out = {}

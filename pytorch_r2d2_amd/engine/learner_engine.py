@@ -180,6 +180,13 @@ class LearnerEngine:
         self.err = z(1, dt=torch.int32)
         self.dgates = z(Ll * B, G, dt=bf16)
         self.gamma_n = float(lc.gamma ** n)
+        # fused torso backward: per-workgroup gradient slabs + destination map (allocated here,
+        # never lazily: the step must be capturable without warm-up)
+        n_slab = int(kernels().r2_torso_bwd_slab_floats())
+        self._tb_grid = min(256, Ll * B)
+        self._tb_slab = z(self._tb_grid * n_slab)
+        dst, scale = L.torso_grad_map()
+        self._tb_dst, self._tb_scale = dst.to(d), scale.to(d)
         self.ones_bf = torch.ones(1, Tn * B, dtype=bf16, device=d)
         self.ones_f32 = torch.ones(1, Tn * B, dtype=f32, device=d)
 
@@ -367,6 +374,24 @@ class LearnerEngine:
         return grad * (act > 0)
 
     def _backward_torso(self):
+        if self.cfg.learner.torso_bwd == "fused":
+            self._backward_torso_fused()
+        else:
+            self._backward_torso_library()
+
+    def _backward_torso_fused(self):
+        """One fused HIP kernel (csrc/kernels/torso_bwd.hip) + slab reduction into self.grad."""
+        B, Lb, T = self.B, self.Lb, self.T
+        N = self.Ll * B
+        pk = self.pk
+        check(kernels().r2_torso_bwd(ptr(self.replay.frames), ptr(self.rows[Lb * B: T * B]), N,
+                                     ptr(self.act1), ptr(self.act2), ptr(self._dX),
+                                     ptr(self.X_on[Lb * B: T * B]), ptr(pk["conv3_dg"]),
+                                     ptr(pk["conv2_dg"]), ptr(self._tb_slab), self._tb_grid,
+                                     ptr(self._tb_dst), ptr(self._tb_scale), ptr(self.grad),
+                                     stream_handle()), "torso_bwd")
+
+    def _backward_torso_library(self):
         """Conv backward (library kernels) from the activations saved by the torso kernel.
         Everything is channels-last so the library picks its NHWC kernels with no transposes."""
         k = kernels()

@@ -51,6 +51,8 @@ _SIGS = {
     "r2_gather_f32": [P, P, P, I64, P],
     "r2_copy_if_due": [P, P, I64, P, I64, P],
     "r2_noop_chain": [P, I, I, P],
+    "r2_torso_bwd": [P, P, I, P, P, P, P, P, P, P, I, P, P, P, P],
+    "r2_torso_bwd_slab_floats": [],
     "r2_lstm_fwd_persist": [P, I, I, I, I, P, P, P],
     "r2_lstm_bwd_persist": [P, P, P, P, P, P, P, I, I, I, I, P, P, P],
     "r2_actor_finalize": [P] * 21 + [I, I, I, I, I, I, F, F, F, F, U64, P],

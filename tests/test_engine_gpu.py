@@ -91,3 +91,21 @@ def test_engine_training_reduces_loss_on_fixed_batch():
         eng.step_eager()
         losses.append(eng.loss.item())
     assert min(losses[-10:]) < losses[0]
+
+
+def test_fused_torso_backward_matches_library():
+    cfg, rp, eng, net, tgt = _make("shifted", B=16)
+    eng._forward_loss()
+    eng._backward_core()
+    eng.grad.zero_()
+    eng._backward_torso_library()
+    torch.cuda.synchronize()
+    ref = eng.grad.clone()
+    eng.grad.zero_()
+    eng._backward_torso_fused()
+    torch.cuda.synchronize()
+    L = eng.layout
+    for name in ("vis_layers.0.weight", "vis_layers.0.bias", "vis_layers.2.weight",
+                 "vis_layers.2.bias", "vis_layers.4.weight", "vis_layers.4.bias"):
+        r = _rel(L.view(eng.grad, name), L.view(ref, name))
+        assert r < 3e-2, f"{name}: rel err {r}"
