@@ -74,3 +74,45 @@ __device__ __forceinline__ float r2_uniform(uint64_t seed, uint64_t ctr, uint64_
   uint64_t z = r2_mix64(seed ^ r2_mix64(ctr * 0x100000001B3ull + idx));
   return (float)(z >> 40) * (1.0f / 16777216.0f);
 }
+
+// Workgroup barrier that orders LDS only.  __syncthreads() also emits s_waitcnt vmcnt(0), which
+// drains every outstanding global load -- including a next-frame register prefetch that is meant to
+// stay in flight across the barrier.  Use this where only LDS traffic must be ordered.
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Software-pipelined MFMA chain: acc += sum_s A(s) . B(s) for s < N with the operand loads of
+// step s+D issued before the MFMA of step s (register ring of depth D), so LDS latency overlaps
+// the matrix pipe instead of serialising every step on lgkmcnt(0).  `lda`/`ldb` are called with
+// compile-time step indices after unrolling (addresses fold to base + immediate).
+template <int N, int D, class FA, class FB>
+__device__ __forceinline__ void mfma_pipe(f32x16& acc, FA lda, FB ldb) {
+  bf16x8 ra[D], rb[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+    if (i < N) { ra[i] = lda(i); rb[i] = ldb(i); }
+#pragma unroll
+  for (int s = 0; s < N; ++s) {
+    const bf16x8 a = ra[s % D], b = rb[s % D];
+    if (s + D < N) { ra[s % D] = lda(s + D); rb[s % D] = ldb(s + D); }
+    __builtin_amdgcn_sched_barrier(0);
+    acc = mfma32(a, b, acc);
+  }
+}
+// Two accumulators sharing the A operand (two N tiles of one weight-gradient row block).
+template <int N, int D, class FA, class FB0, class FB1>
+__device__ __forceinline__ void mfma_pipe2(f32x16& acc0, f32x16& acc1, FA lda, FB0 ldb0, FB1 ldb1) {
+  bf16x8 ra[D], rb0[D], rb1[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+    if (i < N) { ra[i] = lda(i); rb0[i] = ldb0(i); rb1[i] = ldb1(i); }
+#pragma unroll
+  for (int s = 0; s < N; ++s) {
+    const bf16x8 a = ra[s % D], b0 = rb0[s % D], b1 = rb1[s % D];
+    if (s + D < N) { ra[s % D] = lda(s + D); rb0[s % D] = ldb0(s + D); rb1[s % D] = ldb1(s + D); }
+    __builtin_amdgcn_sched_barrier(0);
+    acc0 = mfma32(a, b0, acc0);
+    acc1 = mfma32(a, b1, acc1);
+  }
+}

@@ -13,13 +13,17 @@
 //    channels-last (HWC, 80-byte padded pixel rows -> 16-byte aligned, bank-spread
 //    ds_read_b128 fragment loads);
 //  * conv2/conv3 weights live in LDS (padded rows), conv1 weights in VGPRs (64 regs);
-//  * the next frame's 28 KB is prefetched into registers while the current frame computes and
-//    written to LDS after conv2 (async-stage split);
+//  * the frame is converted u8->bf16 once, when it is written to LDS (56 KB), so the conv1
+//    MFMA loop issues no conversion VALU; the next frame's 28 KB is prefetched into registers
+//    while the current frame computes;
+//  * two-phase software pipeline per frame: phase A = conv1(f) on all waves || conv3(f-1) on
+//    waves 2,3 (tiles dealt so every SIMD issues ~64 MFMAs); phase B = conv2(f) on waves 0..2
+//    || next frame -> LDS || conv1 activations saved; two barriers per frame;
 //  * output is bf16 in PyTorch's (C,H,W) flatten order, ready for the LSTM input GEMM.
 //  * optional: conv1/conv2 activations are written channels-last for the backward pass
 //    (torch channels_last NCHW tensors), so backward does not recompute the forward.
 //
-// One 512-thread workgroup per CU (118 KB LDS), grid-stride over frames.
+// One 512-thread workgroup per CU (147 KB LDS), grid-stride over frames.
 #include "../common.h"
 
 namespace torso {
@@ -31,23 +35,36 @@ constexpr int P1 = 400, P2 = 81, P3 = 49;
 constexpr int ACTS = 40;                 // bf16 per pixel row in LDS (32 + 8 pad) = 80 B
 constexpr int W2S = 512 + 8;             // bf16 per conv2 weight row (1040 B)
 constexpr int W3S = 288 + 8;             // bf16 per conv3 weight row (592 B)
-constexpr int OFF_IN = 0;
-constexpr int OFF_A1 = OFF_IN + IN_BYTES;            // 28224
-constexpr int OFF_A2 = OFF_A1 + P1 * ACTS * 2;       // 60224
-constexpr int OFF_W2 = OFF_A2 + P2 * ACTS * 2;       // 66704
-constexpr int OFF_W3 = OFF_W2 + 32 * W2S * 2;        // 99984
-constexpr int LDS_BYTES = OFF_W3 + 32 * W3S * 2;     // 118928
+constexpr int OFF_IN = 0;                            // frame as bf16 (converted once)
+constexpr int OFF_A1 = OFF_IN + IN_BYTES * 2;        // 56448
+constexpr int OFF_A2 = OFF_A1 + P1 * ACTS * 2;       // 88448
+constexpr int OFF_W2 = OFF_A2 + P2 * ACTS * 2;       // 94928
+constexpr int OFF_W3 = OFF_W2 + 32 * W2S * 2;        // 128208
+constexpr int LDS_BYTES = OFF_W3 + 32 * W3S * 2;     // 147152
 }  // namespace torso
+
+// 16 uint8 -> 16 bf16 written to LDS (the only u8->bf16 conversion of a frame)
+__device__ __forceinline__ void torso_store_chunk(bf16* dst, const u32x4& v) {
+  ((bf16x8*)dst)[0] = u8x8_to_bf16(v[0], v[1]);
+  ((bf16x8*)dst)[1] = u8x8_to_bf16(v[2], v[3]);
+}
+
+// Phase A of the frame pipeline: conv1 of frame f over 13 pixel tiles, while conv3 of frame
+// f-1 runs on waves 2 and 3.  Tiles are dealt so each SIMD (wave % 4) issues ~64 MFMAs:
+//   SIMD0 (w0,w4) 4 conv1 tiles, SIMD1 (w1,w5) 4, SIMD2 (w2,w6) 3 + conv3, SIMD3 (w3,w7) 2 + conv3.
+__constant__ int c_t1_begin[8] = {0, 2, 4, 5, 5, 7, 9, 11};
+__constant__ int c_t1_count[8] = {2, 2, 1, 0, 2, 2, 2, 2};
 
 __global__ __launch_bounds__(512) void torso_fwd_kernel(
     const uint8_t* __restrict__ frames, const int* __restrict__ rows, int n_frames,
     const bf16* __restrict__ w1, const float* __restrict__ b1,
     const bf16* __restrict__ w2, const float* __restrict__ b2,
     const bf16* __restrict__ w3, const float* __restrict__ b3,
-    bf16* __restrict__ out, bf16* __restrict__ save1, bf16* __restrict__ save2) {
+    bf16* __restrict__ out, bf16* __restrict__ save1, bf16* __restrict__ save2,
+    long long* __restrict__ dbg) {
   using namespace torso;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  uint8_t* in_u8 = lds + OFF_IN;
+  bf16* in_bf = (bf16*)(lds + OFF_IN);
   bf16* act1 = (bf16*)(lds + OFF_A1);
   bf16* act2 = (bf16*)(lds + OFF_A2);
   bf16* lw2 = (bf16*)(lds + OFF_W2);
@@ -67,138 +84,154 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(
   bf16x8 wf1[16];
 #pragma unroll
   for (int s = 0; s < 16; ++s) wf1[s] = *(const bf16x8*)(w1 + l32 * 256 + s * 16 + half * 8);
-  float bias1[16], bias2[16], bias3[16];
+  float bias1[16], bias23[16];
+  const bool conv3_wave = (wave == 2 || wave == 3), conv2_wave = wave < 3;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int co = (r & 3) + 8 * (r >> 2) + 4 * half;
-    bias1[r] = b1[co]; bias2[r] = b2[co]; bias3[r] = b3[co];
+    bias1[r] = b1[co];
+    // waves 0..2 run conv2 (phase B); waves 2,3 run conv3 (phase A); wave 2 does both and keeps
+    // conv3's bias, reading conv2's from global in its epilogue
+    bias23[r] = conv3_wave ? b3[co] : b2[co];
   }
+  const int t1b = c_t1_begin[wave], t1n = c_t1_count[wave];
 
   int f = blockIdx.x;
   if (f >= n_frames) return;
-  // ---- prologue: first frame -> LDS
+  // ---- prologue: first frame -> LDS (bf16)
   {
     const size_t row = rows ? (size_t)rows[f] : (size_t)f;
     const u32x4* src = (const u32x4*)(frames + row * IN_BYTES);
-    for (int c = tid; c < IN_CHUNKS; c += NT) ((u32x4*)in_u8)[c] = src[c];
+    for (int c = tid; c < IN_CHUNKS; c += NT) torso_store_chunk(in_bf + c * 16, src[c]);
   }
   __syncthreads();
 
-  for (; f < n_frames; f += gridDim.x) {
-    // ---- prefetch next frame into registers (lands while conv1/conv2 run)
+  int fprev = -1, it_dbg = 0;
+#define TF_TRACE(k) \
+  if (dbg && blockIdx.x == 0 && tid == 0 && it_dbg < 16) dbg[it_dbg * 4 + (k)] = clock64();
+  // replay row of the next frame, read one frame ahead so the prefetch never waits on its address
+  int row_nx = f + (int)gridDim.x < n_frames ? (rows ? rows[f + gridDim.x] : f + gridDim.x) : 0;
+  for (;;) {
+    const bool have = f < n_frames;
     const int fn = f + gridDim.x;
+    const int fnn = fn + gridDim.x;
+    const int row_nn = fnn < n_frames ? (rows ? rows[fnn] : fnn) : 0;
     u32x4 pf[PF];
-    if (fn < n_frames) {
-      const size_t row = rows ? (size_t)rows[fn] : (size_t)fn;
-      const u32x4* src = (const u32x4*)(frames + row * IN_BYTES);
+    TF_TRACE(0);
+    // =================== phase A: conv1(f) || conv3(f-1)
+    if (have) {
+      // prefetch frame f+grid into registers (lands while the convolutions run)
+      if (fn < n_frames) {
+        const u32x4* src = (const u32x4*)(frames + (size_t)row_nx * IN_BYTES);
 #pragma unroll
-      for (int q = 0; q < PF; ++q) {
-        const int c = tid + q * NT;
-        if (c < IN_CHUNKS) pf[q] = src[c];
+        for (int q = 0; q < PF; ++q) {
+          const int c = tid + q * NT;
+          if (c < IN_CHUNKS) pf[q] = src[c];
+        }
       }
-    }
-
-    // ---- conv1: 13 pixel tiles of 32 over 8 waves (waves 7..3 take two tiles)
-    for (int pt = 7 - wave; pt < 13; pt += 8) {
-      const int p = pt * 32 + l32;
-      const int pc = p < P1 ? p : P1 - 1;
-      const int oy = pc / 20, ox = pc % 20;
-      const uint32_t* base = (const uint32_t*)(in_u8 + (4 * oy) * 84 + 4 * ox);
-      f32x16 acc = {};
+      for (int i = 0; i < t1n; ++i) {
+        const int pt = t1b + i;
+        const int p = pt * 32 + l32;
+        const int pc = p < P1 ? p : P1 - 1;
+        const int oy = pc / 20, ox = pc % 20;
+        const bf16* base = in_bf + (4 * oy) * 84 + 4 * ox;
+        f32x16 acc = {};
+        mfma_pipe<16, 4>(acc, [&](int s) { return wf1[s]; }, [&](int s) {
+          const int ci = s >> 2, kh = (s & 3) * 2 + half;
+          const bf16x4* q = (const bf16x4*)(base + ci * 7056 + kh * 84);   // 8-byte aligned
+          const bf16x4 lo = q[0], hi = q[1];
+          return (bf16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        });
+        if (p < P1) {
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int ci = s >> 2, kh = (s & 3) * 2 + half;
-        const uint32_t* q = base + (ci * 7056 + kh * 84) / 4;
-        acc = mfma32(wf1[s], u8x8_to_bf16(q[0], q[1]), acc);
-      }
-      if (p < P1) {
+          for (int g = 0; g < 4; ++g) {
+            bf16x4 v;
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          bf16x4 v;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float x = acc[4 * g + e] * (1.f / 255.f) + bias1[4 * g + e];
-            v[e] = (bf16)fmaxf(x, 0.f);
+            for (int e = 0; e < 4; ++e) {
+              const float x = acc[4 * g + e] * (1.f / 255.f) + bias1[4 * g + e];
+              v[e] = (bf16)fmaxf(x, 0.f);
+            }
+            *(bf16x4*)(act1 + p * ACTS + 8 * g + 4 * half) = v;
           }
-          *(bf16x4*)(act1 + p * ACTS + 8 * g + 4 * half) = v;
         }
       }
     }
-    __syncthreads();
+    if (fprev >= 0 && conv3_wave) {
+      // conv3(f-1): 2 pixel tiles (49 px), K = 288 = (kh 3, kw 3, ci 32)
+      const int p = (wave - 2) * 32 + l32;
+      const int pc = p < P3 ? p : P3 - 1;
+      const int oy = pc / 7, ox = pc % 7;
+      const bf16* abase = lw3 + l32 * W3S + half * 8;
+      const bf16* bbase = act2 + (oy * 9 + ox) * ACTS + half * 8;
+      f32x16 acc = {};
+      mfma_pipe<18, 3>(acc, [&](int s) { return *(const bf16x8*)(abase + s * 16); }, [&](int s) {
+        const int khkw = s >> 1, kh = khkw / 3, kw = khkw % 3;
+        return *(const bf16x8*)(bbase + (kh * 9 + kw) * ACTS + (s & 1) * 16);
+      });
+      if (p < P3) {
+        bf16* o = out + (size_t)fprev * 1568 + p;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int co = (r & 3) + 8 * (r >> 2) + 4 * half;
+          o[co * 49] = (bf16)fmaxf(acc[r] + bias23[r], 0.f);
+        }
+      }
+    }
+    TF_TRACE(1);
+    lds_sync();
+    TF_TRACE(2);
+    if (!have) break;
 
-    // ---- conv2: 3 pixel tiles (81 px), K = 512 = (kh 4, kw 4, ci 32)
-    if (wave < 3) {
+    // =================== phase B: conv2(f) on waves 0..2; frame f+grid -> LDS; save act1(f)
+    if (conv2_wave) {
       const int p = wave * 32 + l32;
       const int pc = p < P2 ? p : P2 - 1;
       const int oy = pc / 9, ox = pc % 9;
       const bf16* abase = lw2 + l32 * W2S + half * 8;
       const bf16* bbase = act1 + ((2 * oy) * 20 + 2 * ox) * ACTS + half * 8;
       f32x16 acc = {};
-#pragma unroll 8
-      for (int s = 0; s < 32; ++s) {
+      mfma_pipe<32, 3>(acc, [&](int s) { return *(const bf16x8*)(abase + s * 16); }, [&](int s) {
         const int khkw = s >> 1, kh = khkw >> 2, kw = khkw & 3;
-        const bf16x8 av = *(const bf16x8*)(abase + s * 16);
-        const bf16x8 bv = *(const bf16x8*)(bbase + (kh * 20 + kw) * ACTS + (s & 1) * 16);
-        acc = mfma32(av, bv, acc);
-      }
+        return *(const bf16x8*)(bbase + (kh * 20 + kw) * ACTS + (s & 1) * 16);
+      });
       if (p < P2) {
+        bf16* d2 = save2 ? save2 + ((size_t)f * P2 + p) * 32 : nullptr;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           bf16x4 v;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = (bf16)fmaxf(acc[4 * g + e] + bias2[4 * g + e], 0.f);
+          for (int e = 0; e < 4; ++e) {
+            const int co = 4 * half + 8 * g + e;
+            const float bb = (wave == 2) ? b2[co] : bias23[4 * g + e];
+            v[e] = (bf16)fmaxf(acc[4 * g + e] + bb, 0.f);
+          }
           *(bf16x4*)(act2 + p * ACTS + 8 * g + 4 * half) = v;
+          if (d2) *(bf16x4*)(d2 + 8 * g + 4 * half) = v;
         }
       }
+    } else if (save1 != nullptr) {
+      // waves 3..7 copy the channels-last conv1 activations out for the backward pass
+      const int t5 = tid - 192;  // 0..319
+      bf16* d1 = save1 + (size_t)f * P1 * 32;
+      for (int c = t5; c < P1 * 4; c += 320) {   // 4 chunks of 8 channels per pixel
+        const int px = c >> 2, q = c & 3;
+        *(bf16x8*)(d1 + px * 32 + q * 8) = *(const bf16x8*)(act1 + px * ACTS + q * 8);
+      }
     }
-    // ---- next frame -> LDS (conv1 finished reading in_u8 before the barrier above)
+    // conv1(f) finished reading in_bf before the barrier above
     if (fn < n_frames) {
 #pragma unroll
       for (int q = 0; q < PF; ++q) {
         const int c = tid + q * NT;
-        if (c < IN_CHUNKS) ((u32x4*)in_u8)[c] = pf[q];
+        if (c < IN_CHUNKS) torso_store_chunk(in_bf + c * 16, pf[q]);
       }
     }
-    __syncthreads();
-
-    // ---- conv3: 2 pixel tiles (49 px), K = 288 = (kh 3, kw 3, ci 32)
-    if (wave < 2) {
-      const int p = wave * 32 + l32;
-      const int pc = p < P3 ? p : P3 - 1;
-      const int oy = pc / 7, ox = pc % 7;
-      const bf16* abase = lw3 + l32 * W3S + half * 8;
-      const bf16* bbase = act2 + (oy * 9 + ox) * ACTS + half * 8;
-      f32x16 acc = {};
-#pragma unroll 6
-      for (int s = 0; s < 18; ++s) {
-        const int khkw = s >> 1, kh = khkw / 3, kw = khkw % 3;
-        const bf16x8 av = *(const bf16x8*)(abase + s * 16);
-        const bf16x8 bv = *(const bf16x8*)(bbase + (kh * 9 + kw) * ACTS + (s & 1) * 16);
-        acc = mfma32(av, bv, acc);
-      }
-      if (p < P3) {
-        bf16* o = out + (size_t)f * 1568 + p;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int co = (r & 3) + 8 * (r >> 2) + 4 * half;
-          o[co * 49] = (bf16)fmaxf(acc[r] + bias3[r], 0.f);
-        }
-      }
-    } else if (save1 != nullptr) {
-      // waves 2..7 copy the channels-last activations out for the backward pass
-      const int t6 = tid - 128;  // 0..383
-      bf16* d1 = save1 + (size_t)f * P1 * 32;
-      for (int c = t6; c < P1 * 4; c += 384) {   // 4 chunks of 8 channels per pixel
-        const int px = c >> 2, q = c & 3;
-        *(bf16x8*)(d1 + px * 32 + q * 8) = *(const bf16x8*)(act1 + px * ACTS + q * 8);
-      }
-      bf16* d2 = save2 + (size_t)f * P2 * 32;
-      for (int c = t6; c < P2 * 4; c += 384) {
-        const int px = c >> 2, q = c & 3;
-        *(bf16x8*)(d2 + px * 32 + q * 8) = *(const bf16x8*)(act2 + px * ACTS + q * 8);
-      }
-    }
-    __syncthreads();
+    lds_sync();
+    TF_TRACE(3);
+    fprev = f;
+    f = fn;
+    row_nx = row_nn;
+    ++it_dbg;
   }
 }
 
@@ -270,6 +303,9 @@ extern "C" int r2_relu_mask_bf16(const bf16* g, const bf16* act, bf16* out, int6
   return 0;
 }
 
+static long long* g_tf_dbg = nullptr;
+extern "C" int r2_torso_fwd_set_debug(long long* p) { g_tf_dbg = p; return 0; }
+
 extern "C" int r2_torso_fwd(const uint8_t* frames, const int* rows, int n_frames,
                             const bf16* w1, const float* b1, const bf16* w2, const float* b2,
                             const bf16* w3, const float* b3, bf16* out, bf16* save1, bf16* save2,
@@ -285,7 +321,7 @@ extern "C" int r2_torso_fwd(const uint8_t* frames, const int* rows, int n_frames
   if (grid > n_frames) grid = n_frames;
   hipLaunchKernelGGL(torso_fwd_kernel, dim3(grid), dim3(torso::NT), torso::LDS_BYTES,
                      (hipStream_t)stream, frames, rows, n_frames, w1, b1, w2, b2, w3, b3, out,
-                     save1, save2);
+                     save1, save2, g_tf_dbg);
   R2_CHECK_LAUNCH();
   return 0;
 }

@@ -1,51 +1,57 @@
 // Fused Atari conv-torso BACKWARD for gfx950 (MI355X).
 //
 // Replaces the library path (3x convolution_backward on MIOpen + ReLU-mask elementwise kernels +
-// NCHW/NHWC transposes + bias reductions + a uint8->bf16 frame expansion: ~0.6 ms per learner
-// step at B=64 x 40 learning steps) with ONE kernel + one slab reduction.  Per learning frame,
-// entirely in LDS (150 KB, 512 threads, one workgroup per CU, grid-stride over frames):
+// NCHW/NHWC transposes + bias reductions + a uint8->bf16 frame expansion) with ONE kernel + one
+// slab reduction.  Reference semantics: model.py:12-22 (the conv stack) differentiated by
+// learner.py:118-120 (loss.backward()).  Per learning frame, entirely in LDS (151 KB, 512
+// threads, one workgroup per CU, grid-stride over frames, next frame prefetched in registers):
 //
-//   g3  = dX3 * (out3 > 0)                              (ReLU backward from the saved output)
-//   dW3 += g3 (co x px) . im2col^T(act2)                 MFMA, K = 49 px (padded 64)
-//   g2  = convT(g3, W3) * (act2 > 0)                      MFMA, M = 81 px, K = (kh,kw,co) = 288
-//   dW2 += g2 . im2col^T(act1)                            MFMA, K = 81 px in 3 chunks of 32
-//   g1  = convT_s2(g2, W2) * (act1 > 0)                   MFMA, stride-2 transposed conv split into
-//                                                         its 4 output phases: only the 4 (kh,kw)
-//                                                         taps that hit a phase are multiplied
-//                                                         (K = 128 instead of 512 with 3/4 zeros)
-//   dW1 += g1 . im2col^T(frame u8)                        MFMA, K = 400 px in 7 chunks of 64; the
-//                                                         uint8 pixels are exact in bf16, 1/255 is
-//                                                         applied once in the reduction
-//   db_l = sum over pixels of g_l                          (MFMA epilogues / one row pass)
+//   S0  frame u8 -> bf16 CHW image; act1/act2 (HWC) copied in; g3 = dX3 * (out3 > 0)
+//   S1  g2 = convT(g3, W3) * (act2>0) (waves 5-7, W3 from LDS)
+//       (dW3 += g3 . im2col(act2) and db3 run in the light torso_dw3_kernel straight from global
+//       dX3/out3/act2: keeping their 2 accumulator tiles here would push the fused kernel past 256
+//       VGPRs, and its spill reloads would wait (in-order vmcnt) on the next-frame prefetch)
+//   S2  dW2 += g2 . im2col(act1)      (2 N tiles per wave)
+//       g1 = convT_s2(g2, W2) * (act1>0): the stride-2 transposed conv split into its 4 output
+//            phases (only the 4 taps that hit a phase are multiplied; each wave keeps its phase's
+//            W2 slice in VGPRs)
+//   S3  dW1 += g1 . im2col(frame)     (1 N tile per wave, K = 400 pixels in 25 steps)
 //
-// Weight-gradient accumulators stay in MFMA registers across all frames of a workgroup
-// (dW1: 1, dW2: 2, dW3: <=2 32x32 tiles per wave); at the end each workgroup writes one fp32
-// slab and ``r2_torso_grad_reduce`` sums the slabs straight into the flat gradient buffer
-// (deterministic; torch layout via an index map).
-//
-// MFMA operands: A = g (rows = output channel co, 8 consecutive pixels per lane from a CHW tile),
-// B = im2col^T (rows = k, 8 consecutive pixels) built per frame in LDS with 16-byte source reads;
-// the transposed convs read g channels-last (8 consecutive co) and pre-packed data-grad weight
-// layouts conv3_dg[ci][kh][kw][co] / conv2_dg[phase][ci][khi][kwi][co] (engine/layout.py).
+// No im2col is ever materialised: the weight-gradient B operands (rows = pixels, columns =
+// (kh,kw,ci) or (ci,kh,kw)) are gathered straight from the HWC activation images / the CHW frame
+// image with ds_read_b64_tr_b16 -- each lane names one 4-element row piece of the im2col matrix
+// and the hardware transpose hands every lane its 8-pixel column fragment.  conv1's pixels run in
+// 4x4 blocks (K step s = block (s/5, s%5)), so every tr-read address is a per-lane base plus an
+// immediate; the A operand g1 is stored in that same K order.  Weight-gradient accumulators stay
+// in MFMA registers across all frames (dW1: 1, dW2: 2, dW3: <=2 32x32 tiles per wave); each
+// workgroup finally writes one fp32 slab and torso_grad_reduce_kernel sums the slabs straight
+// into the flat gradient buffer (deterministic; torch layout via an index map,
+// engine/layout.py torso_grad_map).
 #include "../common.h"
 
 namespace tb {
 constexpr int NT = 512;
 constexpr int P1 = 400, P2 = 81, P3 = 49;
 constexpr int IN_BYTES = 4 * 84 * 84;
-constexpr int G3C_S = 72, G2C_S = 104, G1C_S = 456;  // bf16 row strides (16-B aligned, bank-spread)
-constexpr int X3_S = 72, X2_S = 40, X1_S = 72;
-constexpr int FR = 0;
-constexpr int A1 = FR + IN_BYTES;        // act1 hwc [400][32] bf16
-constexpr int A2 = A1 + P1 * 32 * 2;     // act2 hwc [81][32]
-constexpr int G3H = A2 + P2 * 32 * 2;    // g3 hwc [49][32]
-constexpr int G3C = G3H + P3 * 32 * 2;   // g3 chw [32][72]
-constexpr int G2H = G3C + 32 * G3C_S * 2;  // g2 hwc [81][32]
-constexpr int G2C = G2H + P2 * 32 * 2;     // g2 chw [32][104]
-constexpr int G1C = G2C + 32 * G2C_S * 2;  // g1 chw [32][456]
-constexpr int XT = G1C + 32 * G1C_S * 2;   // im2col^T scratch
-constexpr int XT_BYTES = 288 * X3_S * 2;   // largest of the three builds
-constexpr int LDS = XT + XT_BYTES;         // 149248
+constexpr int IN_CHUNKS = IN_BYTES / 16;                 // 1764
+constexpr int G3C_S = 72;                                // g3 chw row stride (torso_dw3_kernel)
+constexpr int W3S = 288 + 8;                             // conv3_dg rows in LDS
+constexpr int FRB = 0;                                   // frame bf16 CHW [4][84][84]
+constexpr int A1 = FRB + IN_BYTES * 2;                   // act1 hwc [400][32] bf16
+constexpr int A2 = A1 + P1 * 32 * 2;                     // act2 hwc [81][32]
+constexpr int G3P = A2 + P2 * 32 * 2;                    // g3 hwc, zero border 2: [11*11][32]
+constexpr int G2P = G3P + 121 * 32 * 2;                  // g2 hwc, zero border 1: [11*11 + trash][32]
+constexpr int G1H = G2P + 122 * 32 * 2;                  // g1 [400 + trash][32], 4x4-block row order
+constexpr int W3L = G1H + 406 * 32 * 2;                  // conv3_dg [32][296]
+constexpr int TBL2 = W3L + 32 * W3S * 2;                 // dW2 gather offsets int2 [12][64]
+constexpr int TE1 = TBL2 + 12 * 64 * 8;                  // dact1 epilogue rows u32 [4 mt][2 h][16 r]
+constexpr int TE2 = TE1 + 128 * 4;                       // dact2 epilogue rows u32 [3 mt][2 h][16 r]
+constexpr int LDS = TE2 + 96 * 4;                        // 154752
+// trash rows absorb the padded accumulator rows (branch-free epilogues); g1's trash row also
+// takes the stride-2 phase offset 4*py + px (<= 5) added to it
+constexpr int G2_TRASH = 121, G1_TRASH = 400;
+constexpr int PF1 = (P1 * 4 + NT - 1) / NT;              // act1 prefetch chunks per thread (4)
+constexpr int PFF = (IN_CHUNKS + NT - 1) / NT;           // frame prefetch chunks per thread (4)
 constexpr int SLAB = 32 * 256 + 32 * 512 + 32 * 288 + 96;  // 33888 floats per workgroup
 constexpr int OFF_W2 = 32 * 256, OFF_W3 = OFF_W2 + 32 * 512, OFF_B = OFF_W3 + 32 * 288;
 }  // namespace tb
@@ -61,189 +67,273 @@ struct TBArgs {
   const bf16* w2dg;    // (4 phases, 32 ci, 128 = (khi,kwi,co))
   float* slab;         // (gridDim.x, SLAB)
   int n;
+  long long* dbg;      // optional phase clock trace of workgroup 0 (tools/torso_probe.py)
 };
 
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+
 __device__ __forceinline__ bf16x8 ld8(const bf16* p) { return *(const bf16x8*)p; }
+// two hardware-transposed LDS reads -> one 8-pixel B fragment (T10: ds_read_b64_tr_b16)
+__device__ __forceinline__ bf16x8 tr8(const bf16* p0, const bf16* p1) {
+  const i16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)p0);
+  const i16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)p1);
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+// im2col row address (pixel part, bf16 elements) of the tr-read lane for K step s, read r:
+// pixel P = 16s + 8*half + 4r + q (clamped: padded pixels meet zero g columns)
+__device__ __forceinline__ int im2col_off3(int s, int r, int half, int q, int colb) {
+  int P = 16 * s + 8 * half + 4 * r + q;
+  P = P < tb::P3 ? P : tb::P3 - 1;
+  return ((P / 7) * 9 + P % 7) * 32 + colb;
+}
 
 __global__ __launch_bounds__(512) void torso_bwd_kernel(const TBArgs a) {
   using namespace tb;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  uint8_t* fr = lds + FR;
-  bf16* a1 = (bf16*)(lds + A1);
-  bf16* a2 = (bf16*)(lds + A2);
-  bf16* g3h = (bf16*)(lds + G3H);
-  bf16* g3c = (bf16*)(lds + G3C);
-  bf16* g2h = (bf16*)(lds + G2H);
-  bf16* g2c = (bf16*)(lds + G2C);
-  bf16* g1c = (bf16*)(lds + G1C);
-  bf16* xt = (bf16*)(lds + XT);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int l32 = lane & 31, half = lane >> 5;
-  const bf16x8 zero8 = {};
 
-  // zero the CHW gradient tiles once: their pad columns stay zero for every frame
-  for (int i = tid; i < 32 * G3C_S * 2 / 16; i += NT) ((u32x4*)(lds + G3C))[i] = u32x4{0, 0, 0, 0};
-  for (int i = tid; i < 32 * G2C_S * 2 / 16; i += NT) ((u32x4*)(lds + G2C))[i] = u32x4{0, 0, 0, 0};
-  for (int i = tid; i < 32 * G1C_S * 2 / 16; i += NT) ((u32x4*)(lds + G1C))[i] = u32x4{0, 0, 0, 0};
-  f32x16 acc1 = {}, acc2a = {}, acc2b = {}, acc3a = {}, acc3b = {};
-  float db1p = 0.f, db2p = 0.f, db3p = 0.f;
-  __syncthreads();
-
-  for (int f = blockIdx.x; f < a.n; f += gridDim.x) {
-    // ---- stage 0: this frame's inputs -> LDS
-    {
-      const u32x4* src = (const u32x4*)(a.frames + (size_t)a.rows[f] * IN_BYTES);
-      for (int c = tid; c < IN_BYTES / 16; c += NT) ((u32x4*)fr)[c] = src[c];
-      const u32x4* s1 = (const u32x4*)(a.act1 + (size_t)f * P1 * 32);
-      for (int c = tid; c < P1 * 4; c += NT) ((u32x4*)a1)[c] = s1[c];
-      const u32x4* s2 = (const u32x4*)(a.act2 + (size_t)f * P2 * 32);
-      for (int c = tid; c < P2 * 4; c += NT) ((u32x4*)a2)[c] = s2[c];
-      for (int c = tid; c < 196; c += NT) {  // g3 = dx3 * (out3 > 0): 1568 = 196 x 8
-        const bf16x8 dx = ld8(a.dx3 + (size_t)f * 1568 + c * 8);
-        const bf16x8 o3 = ld8(a.out3 + (size_t)f * 1568 + c * 8);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int i = c * 8 + e, co = i / P3, p = i % P3;
-          const bf16 v = ((float)o3[e] > 0.f) ? dx[e] : (bf16)0.f;
-          g3c[co * G3C_S + p] = v;
-          g3h[p * 32 + co] = v;
-        }
-      }
+  // ---- once per workgroup: zero the bordered gradient images (borders stay zero), conv3_dg ->
+  // LDS, the dW2 gather-offset table, this wave's conv2_dg phase slice -> VGPRs
+  for (int i = tid; i < (121 + 122) * 4; i += NT) ((u32x4*)(lds + G3P))[i] = u32x4{0, 0, 0, 0};
+  for (int i = tid; i < 32 * 36; i += NT) {
+    const int r = i / 36, c = i % 36;
+    *(bf16x8*)((bf16*)(lds + W3L) + r * W3S + c * 8) = ld8(a.w3dg + r * 288 + c * 8);
+  }
+  for (int i = tid; i < 12 * 64; i += NT) {
+    // K step s, read r, lane l: pixel P = 16s + 8h + 4r + q of the 9x9 conv2 output (raster)
+    const int sr = i >> 6, l = i & 63, sS = sr >> 1, r = sr & 1;
+    const int h = l >> 5, qq = (l >> 2) & 3, cb = 16 * ((l >> 4) & 1) + 4 * (l & 3);
+    const int P = 16 * sS + 8 * h + 4 * r + qq, Pc = P < P2 ? P : P2 - 1;
+    const int arow = P < P2 ? (Pc / 9 + 1) * 11 + Pc % 9 + 1 : 0;   // row 0 = zero border
+    ((int2*)(lds + TBL2))[i] = make_int2(arow * 32 + cb, ((2 * (Pc / 9)) * 20 + 2 * (Pc % 9)) * 32 + cb);
+  }
+  // epilogue row tables: an accumulator row's pixel depends on (tile, lane half, register) only,
+  // so its index math is done once here; entry = mask pixel | dest row << 16 | valid << 31
+  for (int i = tid; i < 128 + 96; i += NT) {
+    const int j = i < 128 ? i : i - 128, mt = j >> 5, h = (j >> 4) & 1, r = j & 15;
+    const int m = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+    uint32_t e;
+    if (i < 128) {  // dact1: phase pixel (ay, bx) -> act1 pixel (2ay, 2bx) and 4x4-block g1 row
+      const int mv = m < 100 ? m : 99, ay = mv / 10, bx = mv % 10;
+      const int kb = 16 * (5 * (ay >> 1) + (bx >> 1)) + 8 * (ay & 1) + 2 * (bx & 1);
+      e = (uint32_t)((2 * ay) * 20 + 2 * bx) | (uint32_t)(m < 100 ? kb : G1_TRASH) << 16 |
+          (uint32_t)(m < 100) << 31;
+    } else {        // dact2: conv2 output pixel -> act2 pixel and bordered g2 row
+      const int qv = m < P2 ? m : P2 - 1;
+      e = (uint32_t)qv | (uint32_t)(m < P2 ? (qv / 9 + 1) * 11 + qv % 9 + 1 : G2_TRASH) << 16 |
+          (uint32_t)(m < P2) << 31;
     }
-    __syncthreads();
-    // ---- db3 (one row pass) and im2col^T of act2 for dW3: XT3[(kh,kw,ci)][p], p < 64
-    if (wave == 0 && lane < 32) {
-      float s = 0.f;
-      for (int p = 0; p < P3; ++p) s += (float)g3c[lane * G3C_S + p];
-      db3p += s;
-    }
-    for (int it = tid; it < 9 * 4 * 64; it += NT) {
-      const int p = it & 63, r = it >> 6, cg = r & 3, khkw = r >> 2;
-      const int kh = khkw / 3, kw = khkw % 3;
-      bf16x8 v = zero8;
-      if (p < P3) {
-        const int oy = p / 7, ox = p % 7;
-        v = ld8(a2 + ((oy + kh) * 9 + ox + kw) * 32 + cg * 8);
-      }
-      bf16* d = xt + (khkw * 32 + cg * 8) * X3_S + p;
+    ((uint32_t*)(lds + TE1))[i] = e;
+  }
+  bf16x8 w2f[8];
+  {
+    const int l32 = lane & 31, half = lane >> 5;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) d[e * X3_S] = v[e];
-    }
-    __syncthreads();
-    // ---- dW3 (waves 0-4, 9 N tiles) || dact2 -> g2 (waves 5-7, 3 M tiles)
-    if (wave < 5) {
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int nt = wave + q * 5;
-        if (nt < 9) {
-          f32x16 acc = q == 0 ? acc3a : acc3b;
-#pragma unroll
-          for (int s = 0; s < 4; ++s)
-            acc = mfma32(ld8(g3c + l32 * G3C_S + s * 16 + half * 8),
-                         ld8(xt + (nt * 32 + l32) * X3_S + s * 16 + half * 8), acc);
-          if (q == 0) acc3a = acc; else acc3b = acc;
-        }
-      }
-    } else {
-      const int mt = wave - 5;
-      const int q = mt * 32 + l32, qc = q < P2 ? q : P2 - 1;
-      const int qy = qc / 9, qx = qc % 9;
-      f32x16 acc = {};
-#pragma unroll 2
-      for (int s = 0; s < 18; ++s) {
-        const int k0 = s * 16 + half * 8, khkw = k0 >> 5, co0 = k0 & 31;
-        const int oy = qy - khkw / 3, ox = qx - khkw % 3;
-        const bool ok = q < P2 && oy >= 0 && oy < 7 && ox >= 0 && ox < 7;
-        const bf16x8 av = ok ? ld8(g3h + (oy * 7 + ox) * 32 + co0) : zero8;
-        acc = mfma32(av, ld8(a.w3dg + l32 * 288 + k0), acc);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int qq = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-        if (qq < P2) {
-          const bf16 v = ((float)a2[qq * 32 + l32] > 0.f) ? (bf16)acc[r] : (bf16)0.f;
-          g2h[qq * 32 + l32] = v;
-          g2c[l32 * G2C_S + qq] = v;
-          db2p += (float)v;
-        }
-      }
-    }
-    __syncthreads();
-    // ---- dW2 over 3 pixel chunks of 32 (wave w owns N tiles w and w+8)
-    for (int ch = 0; ch < 3; ++ch) {
-      for (int it = tid; it < 16 * 4 * 32; it += NT) {
-        const int pc = it & 31, r = it >> 5, cg = r & 3, khkw = r >> 2;
-        const int kh = khkw >> 2, kw = khkw & 3, p = ch * 32 + pc;
-        bf16x8 v = zero8;
-        if (p < P2) {
-          const int oy = p / 9, ox = p % 9;
-          v = ld8(a1 + ((2 * oy + kh) * 20 + 2 * ox + kw) * 32 + cg * 8);
-        }
-        bf16* d = xt + (khkw * 32 + cg * 8) * X2_S + pc;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) d[e * X2_S] = v[e];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 av = ld8(g2c + l32 * G2C_S + ch * 32 + s * 16 + half * 8);
-        acc2a = mfma32(av, ld8(xt + (wave * 32 + l32) * X2_S + s * 16 + half * 8), acc2a);
-        acc2b = mfma32(av, ld8(xt + ((wave + 8) * 32 + l32) * X2_S + s * 16 + half * 8), acc2b);
-      }
-      __syncthreads();
-    }
-    // ---- dact1 -> g1: stride-2 transposed conv by output phase (16 jobs, 2 per wave)
-#pragma unroll 1
-    for (int jj = 0; jj < 2; ++jj) {
-      const int job = wave * 2 + jj, phase = job >> 2, mt = job & 3;
-      const int py = phase >> 1, px = phase & 1;
-      const int m = mt * 32 + l32, mc = m < 100 ? m : 99;
-      const int ay = mc / 10, bx = mc % 10;
-      f32x16 acc = {};
-#pragma unroll 2
-      for (int s = 0; s < 8; ++s) {
-        const int k0 = s * 16 + half * 8, tap = k0 >> 5, co0 = k0 & 31;
-        const int oy = ay - (tap >> 1), ox = bx - (tap & 1);
-        const bool ok = m < 100 && oy >= 0 && oy < 9 && ox >= 0 && ox < 9;
-        const bf16x8 av = ok ? ld8(g2h + (oy * 9 + ox) * 32 + co0) : zero8;
-        acc = mfma32(av, ld8(a.w2dg + (phase * 32 + l32) * 128 + k0), acc);
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int mm = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-        if (mm < 100) {
-          const int qpix = (2 * (mm / 10) + py) * 20 + 2 * (mm % 10) + px;
-          const bf16 v = ((float)a1[qpix * 32 + l32] > 0.f) ? (bf16)acc[r] : (bf16)0.f;
-          g1c[l32 * G1C_S + qpix] = v;
-          db1p += (float)v;
-        }
-      }
-    }
-    __syncthreads();
-    // ---- dW1 over 7 pixel chunks of 64 from the uint8 frame (wave w owns N tile w)
-    for (int ch = 0; ch < 7; ++ch) {
-      for (int it = tid; it < 4 * 8 * 64; it += NT) {
-        const int pc = it & 63, r = it >> 6, kh = r & 7, ci = r >> 3, p = ch * 64 + pc;
-        bf16x8 v = zero8;
-        if (p < P1) {
-          const int oy = p / 20, ox = p % 20;
-          const uint32_t* q = (const uint32_t*)(fr + ci * 7056 + (4 * oy + kh) * 84 + 4 * ox);
-          v = u8x8_to_bf16(q[0], q[1]);
-        }
-        bf16* d = xt + ((ci * 8 + kh) * 8) * X1_S + pc;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) d[e * X1_S] = v[e];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-        acc1 = mfma32(ld8(g1c + l32 * G1C_S + ch * 64 + s * 16 + half * 8),
-                      ld8(xt + (wave * 32 + l32) * X1_S + s * 16 + half * 8), acc1);
-      __syncthreads();
-    }
+    for (int s = 0; s < 8; ++s) w2f[s] = ld8(a.w2dg + ((wave >> 1) * 32 + l32) * 128 + s * 16 + half * 8);
   }
 
-  // ---- epilogue: this workgroup's partial gradients -> slab
+  f32x16 acc1 = {}, acc2a = {}, acc2b = {};
+  float db1p = 0.f, db2p = 0.f;
+
+  // ---- register prefetch of one frame's inputs
+  u32x4 pfr[PFF], pa1[PF1], pa2, pdx, po3;
+  auto prefetch_frame = [&](int row) {
+    const u32x4* src = (const u32x4*)(a.frames + (size_t)row * IN_BYTES);
+#pragma unroll
+    for (int k = 0; k < PFF; ++k) {
+      const int c = tid + k * NT;
+      if (c < IN_CHUNKS) pfr[k] = src[c];
+    }
+  };
+  auto prefetch_acts = [&](int f) {
+    const u32x4* s1 = (const u32x4*)(a.act1 + (size_t)f * P1 * 32);
+#pragma unroll
+    for (int k = 0; k < PF1; ++k) {
+      const int c = tid + k * NT;
+      if (c < P1 * 4) pa1[k] = s1[c];
+    }
+    if (tid < P2 * 4) pa2 = ((const u32x4*)(a.act2 + (size_t)f * P2 * 32))[tid];
+    if (tid < 196) {
+      pdx = ((const u32x4*)(a.dx3 + (size_t)f * 1568))[tid];
+      po3 = ((const u32x4*)(a.out3 + (size_t)f * 1568))[tid];
+    }
+  };
+  if (blockIdx.x < a.n) {
+    prefetch_frame(a.rows[blockIdx.x]);
+    prefetch_acts(blockIdx.x);
+  }
+  // replay row of the frame after next is read one frame ahead, so issuing a prefetch never
+  // waits a memory round trip for its own address
+  int row_nx = blockIdx.x + gridDim.x < a.n ? a.rows[blockIdx.x + gridDim.x] : 0;
+  __syncthreads();
+
+  int it_dbg = 0;
+#define TB_TRACE(k)                                                                  \
+  if (a.dbg && blockIdx.x == 0 && tid == 0 && it_dbg < 16) a.dbg[it_dbg * 8 + (k)] = clock64();
+  for (int f = blockIdx.x; f < a.n; f += gridDim.x) {
+    TB_TRACE(0);
+    // Re-derive the LDS region pointers and lane roles from an opaque zero each frame: otherwise
+    // the compiler hoists every frame-invariant fragment address (dozens per lane) out of the
+    // frame loop and spills them.
+    int oz;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(oz));
+    bf16* frb = (bf16*)(lds + FRB + oz);
+    bf16* a1 = (bf16*)(lds + A1 + oz);
+    bf16* a2 = (bf16*)(lds + A2 + oz);
+    bf16* g3p = (bf16*)(lds + G3P + oz);
+    bf16* g2p = (bf16*)(lds + G2P + oz);
+    bf16* g1h = (bf16*)(lds + G1H + oz);
+    bf16* w3l = (bf16*)(lds + W3L + oz);
+    const int2* tbl2 = (const int2*)(lds + TBL2 + oz);
+    // transposed-read lane roles: group grp of 16 lanes, row q (pixel within a quad), column
+    // piece pp; colb = first of the lane's 4 im2col columns in a tile
+    const int lane_f = lane + oz;
+    const int l32 = lane_f & 31, half = lane_f >> 5;
+    const int grp = lane_f >> 4, q = (lane_f >> 2) & 3, pp = lane_f & 3;
+    const int colb = 16 * (grp & 1) + 4 * pp;
+    // dW1 (tile = wave): columns (ci, kh, kw) with ci = wave/2, kh = 4(wave&1) + 2(grp&1) + pp/2
+    const int kh1 = 4 * (wave & 1) + 2 * (grp & 1) + (pp >> 1);
+    const bf16* fb0 = frb + (wave >> 1) * 7056 + kh1 * 84 + 4 * (pp & 1) + (4 * (2 * half)) * 84 + 4 * q;
+    const bf16* fb1 = fb0 + 4 * 84;
+
+    // ======== S0: prefetched inputs -> LDS
+    const int row_nn = f + 2 * (int)gridDim.x < a.n ? a.rows[f + 2 * gridDim.x] : 0;
+#pragma unroll
+    for (int k = 0; k < PFF; ++k) {
+      const int c = tid + k * NT;
+      if (c < IN_CHUNKS) {
+        ((bf16x8*)(frb + c * 16))[0] = u8x8_to_bf16(pfr[k][0], pfr[k][1]);
+        ((bf16x8*)(frb + c * 16))[1] = u8x8_to_bf16(pfr[k][2], pfr[k][3]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < PF1; ++k) {
+      const int c = tid + k * NT;
+      if (c < P1 * 4) ((u32x4*)a1)[c] = pa1[k];
+    }
+    if (tid < P2 * 4) ((u32x4*)a2)[tid] = pa2;
+    if (tid < 196) {  // g3 = dx3 * (out3 > 0): 1568 = 196 x 8 (CHW) -> bordered HWC image
+      const bf16x8 dx = __builtin_bit_cast(bf16x8, pdx), o3 = __builtin_bit_cast(bf16x8, po3);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int i = tid * 8 + e, co = i / P3, p = i % P3;
+        const bf16 v = ((float)o3[e] > 0.f) ? dx[e] : (bf16)0.f;
+        g3p[((p / 7 + 2) * 11 + p % 7 + 2) * 32 + co] = v;
+      }
+    }
+    lds_sync();
+    TB_TRACE(1);
+
+    // ======== S1: dact2 -> g2 (waves 5-7); dW3/db3 run in torso_dw3_kernel
+    if (wave >= 5) {
+      const int mt = wave - 5;
+      const int qq0 = mt * 32 + l32, qc = qq0 < P2 ? qq0 : P2 - 1;
+      // A row of tap (kh,kw) = bordered pixel (qy-kh, qx-kw): lane base + per-step immediate
+      const bf16* ab = g3p + (((qc / 9) + 2) * 11 + qc % 9 + 2) * 32 + half * 8;
+      f32x16 acc = {};
+      mfma_pipe<18, 3>(acc, [&](int s) {
+        const int khkw = s >> 1;
+        return ld8(ab - ((khkw / 3) * 11 + khkw % 3) * 32 + (s & 1) * 16);
+      }, [&](int s) { return ld8(w3l + l32 * W3S + s * 16 + half * 8); });
+      // epilogue: all 16 ReLU-mask reads issued before any use; rows past the 81 pixels go to a
+      // trash row (branch-free)
+      const uint32_t* te = (const uint32_t*)(lds + TE2 + oz) + mt * 32 + half * 16;
+#pragma unroll
+      for (int r0 = 0; r0 < 16; r0 += 8) {
+        uint32_t e[8];
+        bf16 mk[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) e[r] = te[r0 + r];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) mk[r] = a2[(e[r] & 0xffff) * 32 + l32];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const bf16 v = ((float)mk[r] > 0.f) ? (bf16)acc[r0 + r] : (bf16)0.f;
+          g2p[((e[r] >> 16) & 0x7fff) * 32 + l32] = v;
+          db2p += (e[r] >> 31) ? (float)v : 0.f;
+        }
+      }
+    }
+    lds_sync();
+    TB_TRACE(2);
+
+    // ======== S2: dW2 (tiles wave, wave+8) and dact1 -> g1 (jobs 2w, 2w+1)
+    // the next frame's u8 frame starts loading here and its activations/gradients at the end of
+    // S2: S2+S3 cover the latency, and the 28 activation VGPRs are not live across dact1
+    const bool more = f + (int)gridDim.x < a.n;
+    if (more) prefetch_frame(row_nx);
+    row_nx = row_nn;
+    TB_TRACE(5);
+    {
+      const int nt = wave;  // (kh, kw) = (nt>>2, nt&3); tile nt+8 is kh+2
+      const bf16* b = a1 + ((nt >> 2) * 20 + (nt & 3)) * 32;
+      const int2* tl = tbl2 + lane_f;
+      // A = g2 (co x pixel) and B = im2col(act1) (pixel x ci), both by transposed reads
+      mfma_pipe2<6, 2>(acc2a, acc2b, [&](int s) {
+                         return tr8(g2p + tl[(2 * s) * 64].x, g2p + tl[(2 * s + 1) * 64].x);
+                       },
+                       [&](int s) { return tr8(b + tl[(2 * s) * 64].y, b + tl[(2 * s + 1) * 64].y); },
+                       [&](int s) {
+                         return tr8(b + 40 * 32 + tl[(2 * s) * 64].y, b + 40 * 32 + tl[(2 * s + 1) * 64].y);
+                       });
+    }
+    TB_TRACE(6);
+    {
+      const int phase = wave >> 1, py = phase >> 1, px = phase & 1;
+#pragma unroll 1
+      for (int jj = 0; jj < 2; ++jj) {
+        const int mt = (wave & 1) * 2 + jj;
+        const int m = mt * 32 + l32, mc = m < 100 ? m : 99;
+        // A row of tap t = bordered g2 pixel (ay - t/2, bx - t%2): lane base + immediate
+        const bf16* ab = g2p + ((mc / 10 + 1) * 11 + mc % 10 + 1) * 32 + half * 8;
+        f32x16 acc = {};
+        mfma_pipe<8, 3>(acc, [&](int s) {
+          const int tap = s >> 1;
+          return ld8(ab - ((tap >> 1) * 11 + (tap & 1)) * 32 + (s & 1) * 16);
+        }, [&](int s) { return w2f[s]; });
+        // epilogue: mask reads batched, destinations in the 4x4-block K order of the conv1
+        // weight-gradient pass, rows past the 100 phase pixels -> trash row (branch-free)
+        const uint32_t* te = (const uint32_t*)(lds + TE1 + oz) + mt * 32 + half * 16;
+        const int moff = (py * 20 + px) * 32 + l32, koff = (4 * py + px) * 32 + l32;
+#pragma unroll
+        for (int r0 = 0; r0 < 16; r0 += 8) {
+          uint32_t e[8];
+          bf16 mk[8];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) e[r] = te[r0 + r];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) mk[r] = a1[(e[r] & 0xffff) * 32 + moff];
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const bf16 v = ((float)mk[r] > 0.f) ? (bf16)acc[r0 + r] : (bf16)0.f;
+            g1h[((e[r] >> 16) & 0x7fff) * 32 + koff] = v;
+            db1p += (e[r] >> 31) ? (float)v : 0.f;
+          }
+        }
+      }
+    }
+    TB_TRACE(7);
+    if (more) prefetch_acts(f + gridDim.x);
+    lds_sync();
+    TB_TRACE(3);
+
+    // ======== S3: dW1, K = 25 steps of one 4x4 pixel block each (addresses = base + immediate)
+    mfma_pipe<25, 3>(acc1, [&](int s) {
+      const int r0 = (16 * s + 8 * half + q) * 32 + colb;
+      return tr8(g1h + r0, g1h + r0 + 4 * 32);
+    }, [&](int s) {
+      const int blk = (16 * (s / 5)) * 84 + 16 * (s % 5);
+      return tr8(fb0 + blk, fb1 + blk);
+    });
+    lds_sync();
+    TB_TRACE(4);
+    ++it_dbg;
+  }
+
+  // ---- epilogue: this workgroup's partial gradients -> slab (dW3/db3: torso_dw3_kernel)
+  const int l32 = lane & 31, half = lane >> 5;
   float* sl = a.slab + (size_t)blockIdx.x * SLAB;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -251,30 +341,117 @@ __global__ __launch_bounds__(512) void torso_bwd_kernel(const TBArgs a) {
     sl[co * 256 + wave * 32 + l32] = acc1[r];
     sl[OFF_W2 + co * 512 + wave * 32 + l32] = acc2a[r];
     sl[OFF_W2 + co * 512 + (wave + 8) * 32 + l32] = acc2b[r];
-    if (wave < 5) sl[OFF_W3 + co * 288 + wave * 32 + l32] = acc3a[r];
-    if (wave < 4) sl[OFF_W3 + co * 288 + (wave + 5) * 32 + l32] = acc3b[r];
   }
-  float* red = (float*)(lds + XT);
-  __syncthreads();
-  if (tid < 96) red[tid] = 0.f;
+  float* red = (float*)(lds + G1H);
+  if (tid < 64) red[tid] = 0.f;
   __syncthreads();
   atomicAdd(&red[l32], db1p);                       // conv1 bias (every wave ran dact1 jobs)
   if (wave >= 5) atomicAdd(&red[32 + l32], db2p);   // conv2 bias
-  if (wave == 0 && lane < 32) atomicAdd(&red[64 + lane], db3p);
   __syncthreads();
-  if (tid < 96) sl[OFF_B + tid] = red[tid];
+  if (tid < 64) sl[OFF_B + tid] = red[tid];
+}
+
+// dW3 += g3 . im2col(act2) and db3, straight from global dX3 / out3 / act2 (all written by
+// earlier kernels): 9 N tiles (wave w: tile w; wave 0 also tile 8), K = 49 pixels padded to 64,
+// B operand by transposed reads of the HWC act2 image.  Next frame prefetched in registers.
+// Writes the dW3 and db3 parts of each workgroup's slab (same grid as torso_bwd_kernel).
+__global__ __launch_bounds__(512) void torso_dw3_kernel(const TBArgs a) {
+  using namespace tb;
+  __shared__ __attribute__((aligned(16))) bf16 g3c[32 * G3C_S];
+  __shared__ __attribute__((aligned(16))) bf16 a2[P2 * 32];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int l32 = lane & 31, half = lane >> 5;
+  const int grp = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int colb = 16 * (grp & 1) + 4 * pp;
+  for (int i = tid; i < 32 * G3C_S * 2 / 16; i += NT) ((u32x4*)g3c)[i] = u32x4{0, 0, 0, 0};
+  f32x16 acc = {}, acc8 = {};
+  float db3p = 0.f;
+  u32x4 pa2, pdx, po3;
+  auto prefetch = [&](int f) {
+    if (tid < P2 * 4) pa2 = ((const u32x4*)(a.act2 + (size_t)f * P2 * 32))[tid];
+    if (tid < 196) {
+      pdx = ((const u32x4*)(a.dx3 + (size_t)f * 1568))[tid];
+      po3 = ((const u32x4*)(a.out3 + (size_t)f * 1568))[tid];
+    }
+  };
+  if (blockIdx.x < a.n) prefetch(blockIdx.x);
+  __syncthreads();
+  const bf16* b0 = a2 + ((wave / 3) * 9 + wave % 3) * 32;
+  const bf16* b8 = a2 + (2 * 9 + 2) * 32;
+  for (int f = blockIdx.x; f < a.n; f += gridDim.x) {
+    if (tid < P2 * 4) ((u32x4*)a2)[tid] = pa2;
+    if (tid < 196) {
+      const bf16x8 dx = __builtin_bit_cast(bf16x8, pdx), o3 = __builtin_bit_cast(bf16x8, po3);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int i = tid * 8 + e, co = i / P3, p = i % P3;
+        g3c[co * G3C_S + p] = ((float)o3[e] > 0.f) ? dx[e] : (bf16)0.f;
+      }
+    }
+    if (f + (int)gridDim.x < a.n) prefetch(f + gridDim.x);
+    lds_sync();
+    auto lda = [&](int s) { return ld8(g3c + l32 * G3C_S + s * 16 + half * 8); };
+    auto ldb = [&](const bf16* b, int s) {
+      return tr8(b + im2col_off3(s, 0, half, q, colb), b + im2col_off3(s, 1, half, q, colb));
+    };
+    if (wave == 0)
+      mfma_pipe2<4, 2>(acc, acc8, lda, [&](int s) { return ldb(b0, s); }, [&](int s) { return ldb(b8, s); });
+    else
+      mfma_pipe<4, 3>(acc, lda, [&](int s) { return ldb(b0, s); });
+    if (wave == 7) {  // db3[co] = sum_p g3[co][p] (pad columns are zero)
+      float sum = 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const bf16x8 v = ld8(g3c + l32 * G3C_S + half * 32 + c * 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sum += (float)v[e];
+      }
+      sum += __shfl_xor(sum, 32, 64);
+      db3p += sum;
+    }
+    lds_sync();
+  }
+  float* sl = a.slab + (size_t)blockIdx.x * SLAB;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int co = (r & 3) + 8 * (r >> 2) + 4 * half;
+    sl[OFF_W3 + co * 288 + wave * 32 + l32] = acc[r];
+    if (wave == 0) sl[OFF_W3 + co * 288 + 8 * 32 + l32] = acc8[r];
+  }
+  if (wave == 7 && lane < 32) sl[OFF_B + 64 + lane] = db3p;
 }
 
 // grad[dst[e]] = scale[e] * sum_g slab[g][e]
-__global__ void torso_grad_reduce_kernel(const float* __restrict__ slab, int G,
-                                         const int* __restrict__ dst, const float* __restrict__ scale,
-                                         float* __restrict__ grad) {
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < tb::SLAB; e += gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int g = 0; g < G; ++g) s += slab[(size_t)g * tb::SLAB + e];
-    grad[dst[e]] = s * scale[e];
+// grad[dst[e]] = scale[e] * sum_g slab[g][e].  Block = 64 columns x 4 row-groups (coalesced 256-B
+// row segments, 16 independent loads in flight per thread), partials combined through LDS;
+// 530 blocks fill the chip.
+__global__ __launch_bounds__(256) void torso_grad_reduce_kernel(
+    const float* __restrict__ slab, int G, const int* __restrict__ dst,
+    const float* __restrict__ scale, float* __restrict__ grad) {
+  __shared__ float part[4][64];
+  const int c = threadIdx.x & 63, gq = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + c;
+  float s = 0.f;
+  if (e < tb::SLAB) {
+    const float* p = slab + e;
+    int g = gq;
+    for (; g + 60 < G; g += 64) {
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = p[(size_t)(g + 4 * u) * tb::SLAB];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) s += v[u];
+    }
+    for (; g < G; g += 4) s += p[(size_t)g * tb::SLAB];
   }
+  part[gq][c] = s;
+  __syncthreads();
+  if (gq == 0 && e < tb::SLAB)
+    grad[dst[e]] = (part[0][c] + part[1][c] + part[2][c] + part[3][c]) * scale[e];
 }
+
+static long long* g_tb_dbg = nullptr;
+extern "C" int r2_torso_bwd_set_debug(long long* p) { g_tb_dbg = p; return 0; }
 
 extern "C" int r2_torso_bwd(const uint8_t* frames, const int* rows, int n, const bf16* act1,
                             const bf16* act2, const bf16* dx3, const bf16* out3, const bf16* w3dg,
@@ -288,10 +465,11 @@ extern "C" int r2_torso_bwd(const uint8_t* frames, const int* rows, int n, const
     attr = true;
   }
   if (grid <= 0 || grid > n) grid = n < 256 ? n : 256;
-  TBArgs a{frames, rows, act1, act2, dx3, out3, w3dg, w2dg, slab, n};
+  TBArgs a{frames, rows, act1, act2, dx3, out3, w3dg, w2dg, slab, n, g_tb_dbg};
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(torso_bwd_kernel, dim3(grid), dim3(tb::NT), tb::LDS, s, a);
-  hipLaunchKernelGGL(torso_grad_reduce_kernel, dim3((tb::SLAB + 255) / 256), dim3(256), 0, s, slab,
+  hipLaunchKernelGGL(torso_dw3_kernel, dim3(grid), dim3(tb::NT), 0, s, a);
+  hipLaunchKernelGGL(torso_grad_reduce_kernel, dim3((tb::SLAB + 63) / 64), dim3(256), 0, s, slab,
                      grid, dst, scale, grad);
   R2_CHECK_LAUNCH();
   return 0;

@@ -53,6 +53,8 @@ _SIGS = {
     "r2_noop_chain": [P, I, I, P],
     "r2_torso_bwd": [P, P, I, P, P, P, P, P, P, P, I, P, P, P, P],
     "r2_torso_bwd_slab_floats": [],
+    "r2_torso_bwd_set_debug": [P],
+    "r2_torso_fwd_set_debug": [P],
     "r2_lstm_fwd_persist": [P, I, I, I, I, P, P, P],
     "r2_lstm_bwd_persist": [P, P, P, P, P, P, P, I, I, I, I, P, P, P],
     "r2_actor_finalize": [P] * 21 + [I, I, I, I, I, I, F, F, F, F, U64, P],
