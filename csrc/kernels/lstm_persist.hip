@@ -17,8 +17,16 @@
 // stores its payload write-through (sc1), drains it (s_waitcnt vmcnt(0)), then ONE lane does a
 // relaxed agent-scope atomic add on the (chain, batch-tile) counter; the consumer polls that
 // counter with relaxed agent loads + s_sleep and reads every handed-off byte with sc1 loads.
-// No placement / dispatch-order assumption; counters are zeroed by a memset node before every
-// launch; every spin is bounded and reports through an error word instead of hanging.
+// No placement / dispatch-order assumption for correctness; counters are zeroed by a memset
+// node before every launch; every spin is bounded and reports through an error word.
+//
+// Same-XCD fast path (speed only): the grid deals the workgroups of one recurrence group
+// (chain, batch tile) to blocks b with equal b % 8, which the dispatcher places on one XCD.  At
+// launch every workgroup reports its HW_REG_XCC_ID; only if all members of its group really share
+// one XCD does the group publish h / dh partials with PLAIN stores, which keep the lines in that
+// XCD's L2 (sc1 stores drop them, so every consumer read would go to the memory side).  Consumers
+// always load with sc1 (L1 bypass, served by the shared L2).  Any other placement falls back to
+// sc1 write-through stores -- the placement-independent protocol above.
 // All (H/16)*ceil(B/32)*chains workgroups (<= 256 for the supported shapes) must be
 // co-resident: 256 threads, <= 40 KB LDS, one per CU is enough.
 #include "../common.h"
@@ -34,7 +42,11 @@
 // Each (chain, batch-tile) arrival counter sits on its own 128-byte line: several groups
 // polling / atomically adding on one line serialise at the memory-side atomic unit.
 #define PL_CTR_STRIDE 32
-#define PL_CTR_WORDS (PL_MAX_CHAINS * 8 * PL_CTR_STRIDE)
+#define PL_MAX_GROUPS 32
+// [0, 1024): per-group step counters; [1024, 2048): per-group XCC bitmask; [2048, 3072): arrivals
+#define PL_CTR_WORDS (3 * PL_MAX_GROUPS * PL_CTR_STRIDE)
+#define PL_OFF_XMASK (PL_MAX_GROUPS * PL_CTR_STRIDE)
+#define PL_OFF_ARRIVE (2 * PL_MAX_GROUPS * PL_CTR_STRIDE)
 
 struct PChain {
   const float* xproj;  // (T, B, G) packed, chain-local time
@@ -54,13 +66,58 @@ struct PFwdArgs {
   int B, T;
   unsigned* ctr;  // (n_chains, MB) arrival counters, zeroed before launch
   unsigned* err;  // error word (nonzero = a spin timed out)
+  long long* dbg; // optional per-step phase clock trace of group 0, slice 0 (tools/lstm_probe.py)
+  int MB, groups, xcd_map, force_slow;
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t pl_rsrc(const void* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, bytes, 0x00020000);
 }
 
-// one lane waits until *ctr >= target; result broadcast through LDS; bounded
+// Workgroup (g = recurrence group, j = unit slice) of this block; false for idle blocks.
+// xcd_map: block b -> (g = b % 8, j = b / 8), so a group's blocks share b % 8 (one XCD under the
+// dispatcher's round-robin placement); otherwise linear (g = b / nwg, j = b % nwg).
+__device__ __forceinline__ bool pl_decode(int xcd_map, int groups, int nwg, int& g, int& j) {
+  const int b = blockIdx.x;
+  if (xcd_map) { g = b & 7; j = b >> 3; }
+  else { g = b / nwg; j = b % nwg; }
+  return g < groups && j < nwg;
+}
+
+// One-time exchange: does every workgroup of group g run on the same XCD?  Each member ORs its
+// XCC bit into the group mask (returned atomic: completes before the arrival add), then arrives;
+// once all nwg have arrived the mask is final.  Bounded spin; on timeout reports err and says no.
+__device__ __forceinline__ int pl_same_xcd(unsigned* ctr, int g, int nwg, int force_slow,
+                                           unsigned* err, int* flag_lds) {
+  if (threadIdx.x == 0) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    unsigned* mask = ctr + PL_OFF_XMASK + g * PL_CTR_STRIDE;
+    unsigned* arrive = ctr + PL_OFF_ARRIVE + g * PL_CTR_STRIDE;
+    __hip_atomic_fetch_or(mask, 1u << (x & 15), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the OR must be performed before this member counts as arrived: a returning atomic
+    // decrements vmcnt only once performed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    int ok = 1;
+    while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nwg) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > PL_SPIN_LIMIT) {
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+    }
+    const unsigned m = __hip_atomic_load(mask, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag_lds = (ok && !force_slow && __builtin_popcount(m) == 1) ? 1 : (ok ? 0 : -1);
+  }
+  __syncthreads();
+  return *flag_lds;
+}
+
+// one lane waits until *ctr >= target; result broadcast through LDS; bounded.  The barrier is
+// LDS-only (lds_sync): loads/stores this wave issued earlier stay in flight across it.
 __device__ __forceinline__ bool pl_wait(unsigned* ctr, unsigned target, unsigned* err,
                                         int* flag_lds) {
   if (threadIdx.x == 0) {
@@ -76,27 +133,39 @@ __device__ __forceinline__ bool pl_wait(unsigned* ctr, unsigned target, unsigned
     }
     *flag_lds = ok;
   }
-  __syncthreads();
+  lds_sync();
   return *flag_lds != 0;
 }
 
 template <int H>
 __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const PFwdArgs a) {
   constexpr int G = 4 * H;
+  constexpr int NWG = H / PL_UNITS;
   constexpr int KS = H / 16;
   constexpr int KH = KS / 2;           // k-steps per wave (K split across wave pairs)
   constexpr int PW = PL_GCOLS + 4;     // fp32 row stride of the partial-gate tiles
+  constexpr int HS = H + 8;            // bf16 row stride of the staged h_{t-1} tile
   __shared__ float part[2][32 * PW];
   __shared__ __attribute__((aligned(16))) bf16 hst[32 * PL_UNITS];
+  __shared__ __attribute__((aligned(16))) bf16 hin[32 * HS];
   __shared__ int flag;
-  const PChain& cd = a.ch[blockIdx.z];
-  const int j = blockIdx.x, mb = blockIdx.y, MB = gridDim.y;
+  int g, j;
+  if (!pl_decode(a.xcd_map, a.groups, NWG, g, j)) return;
+  const int MB = a.MB, mb = g % MB;
+  const PChain& cd = a.ch[g / MB];
   const int B = a.B, T = a.T;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int nt = wave & 1, kq = wave >> 1;
-  unsigned* ctr = a.ctr + (blockIdx.z * MB + mb) * PL_CTR_STRIDE;
+  unsigned* ctr = a.ctr + g * PL_CTR_STRIDE;
   const uint32_t hbytes = (uint32_t)((size_t)T * B * H * sizeof(bf16));
   const __amdgpu_buffer_rsrc_t hrs = pl_rsrc(cd.h_seq, hbytes);
+  const int fast = pl_same_xcd(a.ctr, g, NWG, a.force_slow, a.err, &flag);
+  if (fast < 0) return;
+  if (a.dbg && tid == 0) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    a.dbg[256 + blockIdx.x] = (long long)(1000 + g * 100 + (x & 15) * 10 + fast);
+  }
 
   // ---- resident W_hh fragments: B[k][n] = Whh_pk[j][nt*32 + n][k], k-steps kq*KH .. +KH
   bf16x8 wf[KH];
@@ -119,32 +188,60 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const PFwdArgs a)
     const int bc = pv[q] ? pb[q] : B - 1;
     creg[q] = cd.c0[(size_t)bc * H + j * PL_UNITS + pu[q]];
   }
-  const int arow = min(mb * 32 + (lane & 31), B - 1);
   const int acol = kq * KH * 16 + (lane >> 5) * 8;
 
-  for (int t = 0; t < T; ++t) {
-    // x-projection of this step (plain loads: written by an earlier kernel)
-    float xv[2][4];
+  const bool trace = a.dbg && g == 0 && j == 0 && tid == 0;
+#define PL_TRACE(k) \
+  if (trace && t < 32) a.dbg[t * 8 + (k)] = clock64();
+  // x-projection rows (plain loads: written by an earlier kernel), one step ahead.  Issue order
+  // matters: vmcnt retires in order, so next step's rows are issued AFTER this step's h loads --
+  // waiting for h never waits for an HBM x-projection fetch.
+  float xv[2][4], xn[2][4];
+  auto load_x = [&](int t, float (&d)[2][4]) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int bc = pv[q] ? pb[q] : B - 1;
       const float* xr = cd.xproj + ((size_t)t * B + bc) * G + j * PL_GCOLS + pu[q];
-      xv[q][0] = xr[0]; xv[q][1] = xr[16]; xv[q][2] = xr[32]; xv[q][3] = xr[48];
+      d[q][0] = xr[0]; d[q][1] = xr[16]; d[q][2] = xr[32]; d[q][3] = xr[48];
     }
-    bf16x8 av[KH];
+  };
+  load_x(0, xv);
+  for (int t = 0; t < T; ++t) {
+    PL_TRACE(0);
+    // h_{t-1} tile (32 rows x H) staged ONCE per workgroup in LDS: each thread moves HL 16-B
+    // chunks (the MFMA fragments of the two N halves would otherwise fetch it twice)
+    constexpr int HC = H / 8;              // 16-B chunks per row
+    constexpr int HL = 32 * HC / 256;      // chunks per thread
+    u32x4 hv4[HL];
     if (t == 0) {
-      const bf16* hp = cd.h0 + (size_t)arow * H + acol;
 #pragma unroll
-      for (int s = 0; s < KH; ++s) av[s] = *(const bf16x8*)(hp + s * 16);
+      for (int i = 0; i < HL; ++i) {
+        const int c = tid + i * 256, r = c / HC, col = (c % HC) * 8;
+        hv4[i] = *(const u32x4*)(cd.h0 + (size_t)min(mb * 32 + r, B - 1) * H + col);
+      }
     } else {
-      if (!pl_wait(ctr, (unsigned)(H / PL_UNITS) * (unsigned)t, a.err, &flag)) return;
-      const uint32_t off = (uint32_t)((((size_t)(t - 1) * B + arow) * H + acol) * sizeof(bf16));
+      if (!pl_wait(ctr, (unsigned)NWG * (unsigned)t, a.err, &flag)) return;
+      PL_TRACE(1);
 #pragma unroll
-      for (int s = 0; s < KH; ++s) {
-        u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(hrs, off + s * 32, 0, 16);  // sc1
-        av[s] = __builtin_bit_cast(bf16x8, v);
+      for (int i = 0; i < HL; ++i) {
+        const int c = tid + i * 256, r = c / HC, col = (c % HC) * 8;
+        const uint32_t off = (uint32_t)((((size_t)(t - 1) * B + min(mb * 32 + r, B - 1)) * H + col) * sizeof(bf16));
+        hv4[i] = __builtin_amdgcn_raw_buffer_load_b128(hrs, off, 0, 16);  // sc1
       }
     }
+    __builtin_amdgcn_sched_barrier(0);
+    // unconditional (clamped): a conditional issue would make the compiler's vmcnt for the MFMA
+    // operands count these loads as possibly absent and wait for them
+    load_x(t + 1 < T ? t + 1 : t, xn);
+#pragma unroll
+    for (int i = 0; i < HL; ++i) {
+      const int c = tid + i * 256, r = c / HC, col = (c % HC) * 8;
+      *(u32x4*)(hin + r * HS + col) = hv4[i];
+    }
+    lds_sync();
+    bf16x8 av[KH];
+#pragma unroll
+    for (int s = 0; s < KH; ++s) av[s] = *(const bf16x8*)(hin + (lane & 31) * HS + acol + s * 16);
     __builtin_amdgcn_sched_barrier(0);
     f32x16 acc = {};
 #pragma unroll
@@ -154,43 +251,57 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const PFwdArgs a)
       const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       part[kq][row * PW + nt * 32 + (lane & 31)] = acc[r];
     }
-    __syncthreads();
-    const bool save = cd.gates != nullptr && t >= cd.save_from;
+    lds_sync();
+    PL_TRACE(2);
+    float hv[2], gsv[2][4];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int rl = (tid + q * 256) >> 4, u = pu[q];
       const float* p0 = part[0] + rl * PW;
       const float* p1 = part[1] + rl * PW;
-      const float gi = sigmoidf_(p0[u] + p1[u] + xv[q][0]);
-      const float gf = sigmoidf_(p0[16 + u] + p1[16 + u] + xv[q][1]);
-      const float gg = tanhf_(p0[32 + u] + p1[32 + u] + xv[q][2]);
-      const float go = sigmoidf_(p0[48 + u] + p1[48 + u] + xv[q][3]);
-      creg[q] = gf * creg[q] + gi * gg;
-      const float h = go * tanhf_(creg[q]);
-      hst[rl * PL_UNITS + u] = (bf16)h;
-      if (pv[q]) {
-        const size_t o = ((size_t)t * B + pb[q]) * H + j * PL_UNITS + u;
-        cd.c_seq[o] = creg[q];
-        if (cd.h32) cd.h32[o] = h;
-        if (save) {
-          float* gp = cd.gates + ((size_t)(t - cd.save_from) * B + pb[q]) * G + j * PL_GCOLS + u;
-          gp[0] = gi; gp[16] = gf; gp[32] = gg; gp[48] = go;
-        }
-      }
+      gsv[q][0] = sigmoidf_(p0[u] + p1[u] + xv[q][0]);
+      gsv[q][1] = sigmoidf_(p0[16 + u] + p1[16 + u] + xv[q][1]);
+      gsv[q][2] = tanhf_(p0[32 + u] + p1[32 + u] + xv[q][2]);
+      gsv[q][3] = sigmoidf_(p0[48 + u] + p1[48 + u] + xv[q][3]);
+      creg[q] = gsv[q][1] * creg[q] + gsv[q][0] * gsv[q][2];
+      hv[q] = gsv[q][3] * tanhf_(creg[q]);
+      hst[rl * PL_UNITS + u] = (bf16)hv[q];
     }
-    __syncthreads();
-    // ---- publish h_t slice: wave 0 stores 32 rows x 32 B write-through, drains, signals
+    lds_sync();
+    PL_TRACE(3);
+    // ---- publish h_t slice: wave 0 stores 32 rows x 32 B, drains, signals.  Bookkeeping
+    // stores (c, h32, gates) are issued after the signal, off the recurrence's critical path.
     if (wave == 0) {
       const int rl = lane >> 1, hf = lane & 1;
       const int b = mb * 32 + rl;
       if (b < B) {
         const u32x4 v = *(const u32x4*)(hst + rl * PL_UNITS + hf * 8);
         const uint32_t off = (uint32_t)((((size_t)t * B + b) * H + j * PL_UNITS + hf * 8) * sizeof(bf16));
-        __builtin_amdgcn_raw_buffer_store_b128(v, hrs, off, 0, 16);  // sc1
+        if (fast) __builtin_amdgcn_raw_buffer_store_b128(v, hrs, off, 0, 0);   // stays in this XCD's L2
+        else __builtin_amdgcn_raw_buffer_store_b128(v, hrs, off, 0, 16);       // sc1 write-through
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    PL_TRACE(4);
+    const bool save = cd.gates != nullptr && t >= cd.save_from;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (pv[q]) {
+        const int u = pu[q];
+        const size_t o = ((size_t)t * B + pb[q]) * H + j * PL_UNITS + u;
+        cd.c_seq[o] = creg[q];
+        if (cd.h32) cd.h32[o] = hv[q];
+        if (save) {
+          float* gp = cd.gates + ((size_t)(t - cd.save_from) * B + pb[q]) * G + j * PL_GCOLS + u;
+          gp[0] = gsv[q][0]; gp[16] = gsv[q][1]; gp[32] = gsv[q][2]; gp[48] = gsv[q][3];
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) xv[q][e] = xn[q][e];
   }
 }
 
@@ -203,8 +314,9 @@ struct PBwdArgs {
   float* slab;          // (2, NWG, B, H) partial dh ping-pong
   bf16* dgates;         // (Tl, B, G)
   int B, T, t0;
-  unsigned* ctr;        // (MB) zeroed before launch
+  unsigned* ctr;        // PL_CTR_WORDS, zeroed before launch
   unsigned* err;
+  int groups, xcd_map, force_slow;
 };
 
 template <int H>
@@ -219,12 +331,15 @@ __global__ __launch_bounds__(256) void lstm_bwd_persist_kernel(const PBwdArgs a)
   __shared__ __attribute__((aligned(16))) float pst[32 * PS];
   __shared__ float red[2][32 * PL_UNITS];
   __shared__ int flag;
-  const int j = blockIdx.x, mb = blockIdx.y;
+  int mb, j;
+  if (!pl_decode(a.xcd_map, a.groups, NWG, mb, j)) return;
   const int B = a.B, T = a.T, t0 = a.t0;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   unsigned* ctr = a.ctr + mb * PL_CTR_STRIDE;
   const uint32_t sbytes = (uint32_t)((size_t)2 * NWG * B * H * sizeof(float));
   const __amdgpu_buffer_rsrc_t srs = pl_rsrc(a.slab, sbytes);
+  const int fast = pl_same_xcd(a.ctr, mb, NWG, a.force_slow, a.err, &flag);
+  if (fast < 0) return;
 
   // ---- resident W_hh^T fragments for phase B: B[k][n] = Whh_pk[j][k][n] = whhT[j][n][k]
   bf16x8 wt[TPW][4];
@@ -249,35 +364,48 @@ __global__ __launch_bounds__(256) void lstm_bwd_persist_kernel(const PBwdArgs a)
   const int rr = (tid & 127) >> 2, u4 = tid & 3, hh = tid >> 7;
   const int rb = min(mb * 32 + rr, B - 1);
 
-  for (int t = T - 1, k = 0; t >= t0; --t, ++k) {
+  // per-step operands (plain loads of earlier kernels' outputs), one step ahead and issued after
+  // the step's slab loads: vmcnt retires in order, so waiting for the partials never waits for an
+  // HBM operand fetch
+  float dhv[2], gv[2][4], ctv[2], cpv[2], dhn[2], gn[2][4], ctn[2], cpn[2];
+  auto load_ops = [&](int t, float (&dh)[2], float (&gq)[2][4], float (&ct)[2], float (&cp)[2]) {
     const int tl = t - t0;
-    // independent operands first
-    float dhv[2], gv[2][4], ctv[2], cpv[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int bc = pv[q] ? pb[q] : B - 1;
       const size_t hidx = (size_t)bc * H + j * PL_UNITS + pu[q];
-      dhv[q] = a.dh_ext ? a.dh_ext[(size_t)tl * B * H + hidx] : 0.f;
+      dh[q] = a.dh_ext ? a.dh_ext[(size_t)tl * B * H + hidx] : 0.f;
       const float* gp = a.gates + ((size_t)tl * B + bc) * G + j * PL_GCOLS + pu[q];
-      gv[q][0] = gp[0]; gv[q][1] = gp[16]; gv[q][2] = gp[32]; gv[q][3] = gp[48];
-      ctv[q] = a.c_seq[(size_t)t * B * H + hidx];
-      cpv[q] = (t == 0) ? a.c0[hidx] : a.c_seq[(size_t)(t - 1) * B * H + hidx];
+      gq[q][0] = gp[0]; gq[q][1] = gp[16]; gq[q][2] = gp[32]; gq[q][3] = gp[48];
+      ct[q] = a.c_seq[(size_t)t * B * H + hidx];
+      cp[q] = (t == 0) ? a.c0[hidx] : a.c_seq[(size_t)(t - 1) * B * H + hidx];
     }
+  };
+  load_ops(T - 1, dhv, gv, ctv, cpv);
+  for (int t = T - 1, k = 0; t >= t0; --t, ++k) {
+    const int tl = t - t0;
     // recurrent partials from step t+1 (written by the NWG workgroups of this batch tile)
     if (k > 0) {
       if (!pl_wait(ctr, (unsigned)NWG * (unsigned)k, a.err, &flag)) return;
       const int slot = (k - 1) & 1;
+      // all NWG/2 partial loads in flight at once (compile-time trip count), then the sum
+      u32x4 pv4[NWG / 2];
+#pragma unroll
+      for (int ii = 0; ii < NWG / 2; ++ii) {
+        const int i = hh + 2 * ii;
+        const uint32_t off = (uint32_t)((((size_t)(slot * NWG + i) * B + rb) * H + j * PL_UNITS + u4 * 4) * sizeof(float));
+        pv4[ii] = __builtin_amdgcn_raw_buffer_load_b128(srs, off, 0, 16);  // sc1
+      }
       f32x4 sum = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int i = hh; i < NWG; i += 2) {
-        const uint32_t off = (uint32_t)((((size_t)(slot * NWG + i) * B + rb) * H + j * PL_UNITS + u4 * 4) * sizeof(float));
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(srs, off, 0, 16);  // sc1
-        sum += __builtin_bit_cast(f32x4, v);
-      }
+      for (int ii = 0; ii < NWG / 2; ++ii) sum += __builtin_bit_cast(f32x4, pv4[ii]);
 #pragma unroll
       for (int e = 0; e < 4; ++e) red[hh][rr * PL_UNITS + u4 * 4 + e] = sum[e];
     }
-    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+    load_ops(t > t0 ? t - 1 : t, dhn, gn, ctn, cpn);  // unconditional: see the forward kernel
+    lds_sync();
+    bf16 dgv[2][4];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const int rl = (tid + q * 256) >> 4, u = pu[q];
@@ -289,45 +417,38 @@ __global__ __launch_bounds__(256) void lstm_bwd_persist_kernel(const PBwdArgs a)
       const float d_o = dh * tc;
       const float d_i = dc * gg, d_g = dc * gi, d_f = dc * cpv[q];
       dcr[q] = dc * gf;
-      const bf16 bi = (bf16)(d_i * gi * (1.f - gi));
-      const bf16 bfv = (bf16)(d_f * gf * (1.f - gf));
-      const bf16 bg = (bf16)(d_g * (1.f - gg * gg));
-      const bf16 bo = (bf16)(d_o * go * (1.f - go));
+      dgv[q][0] = (bf16)(d_i * gi * (1.f - gi));
+      dgv[q][1] = (bf16)(d_f * gf * (1.f - gf));
+      dgv[q][2] = (bf16)(d_g * (1.f - gg * gg));
+      dgv[q][3] = (bf16)(d_o * go * (1.f - go));
       bf16* lrow = dg + rl * DW;
       const bool ok = pv[q];
-      lrow[u] = ok ? bi : (bf16)0.f;
-      lrow[16 + u] = ok ? bfv : (bf16)0.f;
-      lrow[32 + u] = ok ? bg : (bf16)0.f;
-      lrow[48 + u] = ok ? bo : (bf16)0.f;
-      if (ok) {
-        bf16* dgo = a.dgates + ((size_t)tl * B + pb[q]) * G + j * PL_GCOLS + u;
-        dgo[0] = bi; dgo[16] = bfv; dgo[32] = bg; dgo[48] = bo;
-      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) lrow[16 * e + u] = ok ? dgv[q][e] : (bf16)0.f;
     }
-    if (t == t0) break;  // dh into the stored initial state is not needed
-    __syncthreads();
-    // ---- phase B: partial dh_{t-1}[r][n] = sum_k dg[r][k] * Whh_pk[j][k][n]  (K = 64)
-    const bf16* arow = dg + (lane & 31) * DW + (lane >> 5) * 8;
-    bf16x8 afr[4];
+    if (t > t0) {
+      lds_sync();
+      // ---- phase B: partial dh_{t-1}[r][n] = sum_k dg[r][k] * Whh_pk[j][k][n]  (K = 64)
+      const bf16* arow = dg + (lane & 31) * DW + (lane >> 5) * 8;
+      bf16x8 afr[4];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) afr[s] = *(const bf16x8*)(arow + s * 16);
+      for (int s = 0; s < 4; ++s) afr[s] = *(const bf16x8*)(arow + s * 16);
 #pragma unroll
-    for (int q = 0; q < TPW; ++q) {
-      const int ntl = wave + q * 4;
-      if (ntl < NT32) {
-        f32x16 acc = {};
+      for (int q = 0; q < TPW; ++q) {
+        const int ntl = wave + q * 4;
+        if (ntl < NT32) {
+          f32x16 acc = {};
 #pragma unroll
-        for (int s = 0; s < 4; ++s) acc = mfma32(afr[s], wt[q][s], acc);
+          for (int s = 0; s < 4; ++s) acc = mfma32(afr[s], wt[q][s], acc);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-          pst[row * PS + ntl * 32 + (lane & 31)] = acc[r];
+          for (int r = 0; r < 16; ++r) {
+            const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            pst[row * PS + ntl * 32 + (lane & 31)] = acc[r];
+          }
         }
       }
-    }
-    __syncthreads();
-    // write-through store of the 32 x H fp32 slab (rows < B), 16 B per lane, then signal
-    {
+      lds_sync();
+      // store the 32 x H fp32 partial slab (rows < B), 16 B per lane, drain, then signal
       const int slot = k & 1;
       constexpr int C4 = H / 4;  // float4 per row
       for (int c = tid; c < 32 * C4; c += 256) {
@@ -336,15 +457,36 @@ __global__ __launch_bounds__(256) void lstm_bwd_persist_kernel(const PBwdArgs a)
         if (b < B) {
           const u32x4 v = *(const u32x4*)(pst + r * PS + col);
           const uint32_t off = (uint32_t)((((size_t)(slot * NWG + j) * B + b) * H + col) * sizeof(float));
-          __builtin_amdgcn_raw_buffer_store_b128(v, srs, off, 0, 16);  // sc1
+          if (fast) __builtin_amdgcn_raw_buffer_store_b128(v, srs, off, 0, 0);   // stays in L2
+          else __builtin_amdgcn_raw_buffer_store_b128(v, srs, off, 0, 16);       // sc1
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
+      lds_sync();
       if (tid == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // dgates output for the weight-gradient GEMMs, off the recurrence's critical path
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (pv[q]) {
+        bf16* dgo = a.dgates + ((size_t)tl * B + pb[q]) * G + j * PL_GCOLS + pu[q];
+        dgo[0] = dgv[q][0]; dgo[16] = dgv[q][1]; dgo[32] = dgv[q][2]; dgo[48] = dgv[q][3];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      dhv[q] = dhn[q]; ctv[q] = ctn[q]; cpv[q] = cpn[q];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gv[q][e] = gn[q][e];
     }
   }
 }
+
+static long long* g_pl_dbg = nullptr;
+static int g_pl_slow = 0;
+extern "C" int r2_lstm_persist_set_debug(long long* p) { g_pl_dbg = p; return 0; }
+// testing / diagnostics: 1 = always use the placement-independent sc1 protocol
+extern "C" int r2_lstm_persist_force_slow(int v) { g_pl_slow = v; return 0; }
 
 // chain_ptrs: n_chains x 9 int64 (same layout as r2_lstm_fwd).  ctr: >= PL_CTR_WORDS (1024) unsigned,
 // err: 1 unsigned.  Both are zeroed here with memset nodes (graph-capturable).
@@ -363,10 +505,12 @@ extern "C" int r2_lstm_fwd_persist(const int64_t* chain_ptrs, int n_chains, int 
     ch.c0 = (const float*)p[3]; ch.h_seq = (bf16*)p[4]; ch.c_seq = (float*)p[5];
     ch.h32 = (float*)p[6]; ch.gates = (float*)p[7]; ch.save_from = (int)p[8]; ch.pad_ = 0;
   }
-  args.B = B; args.T = T; args.ctr = ctr; args.err = err;
+  const int groups = n_chains * MB, nwg = H / PL_UNITS;
+  args.B = B; args.T = T; args.ctr = ctr; args.err = err; args.dbg = g_pl_dbg;
+  args.MB = MB; args.groups = groups; args.xcd_map = groups <= 8 && nwg <= 32; args.force_slow = g_pl_slow;
   hipStream_t s = (hipStream_t)stream;
   hipMemsetAsync(ctr, 0, PL_CTR_WORDS * sizeof(unsigned), s);
-  dim3 grid(H / PL_UNITS, MB, n_chains), block(256);
+  dim3 grid(args.xcd_map ? 8 * nwg : groups * nwg), block(256);
   const void* fn = H == 64 ? (const void*)lstm_fwd_persist_kernel<64>
                  : H == 128 ? (const void*)lstm_fwd_persist_kernel<128>
                  : H == 256 ? (const void*)lstm_fwd_persist_kernel<256>
@@ -392,10 +536,12 @@ extern "C" int r2_lstm_bwd_persist(const float* dh_ext, const float* gates, cons
   const int MB = (B + 31) / 32;
   if ((H / PL_UNITS) * MB > 256 || MB > 8) return -3;
   if ((size_t)2 * (H / PL_UNITS) * B * H * 4 >= (1ull << 32)) return -4;
-  PBwdArgs a{dh_ext, gates, c_seq, c0, whhT, slab, dgates, B, T, t0, ctr, err};
+  const int nwg = H / PL_UNITS;
+  const int xmap = MB <= 8 && nwg <= 32;
+  PBwdArgs a{dh_ext, gates, c_seq, c0, whhT, slab, dgates, B, T, t0, ctr, err, MB, xmap, g_pl_slow};
   hipStream_t s = (hipStream_t)stream;
   hipMemsetAsync(ctr, 0, PL_CTR_WORDS * sizeof(unsigned), s);
-  dim3 grid(H / PL_UNITS, MB), block(256);
+  dim3 grid(xmap ? 8 * nwg : MB * nwg), block(256);
   const void* fn = H == 64 ? (const void*)lstm_bwd_persist_kernel<64>
                  : H == 128 ? (const void*)lstm_bwd_persist_kernel<128>
                  : H == 256 ? (const void*)lstm_bwd_persist_kernel<256>

@@ -99,7 +99,7 @@ class BatchedActor:
         self.c_new = {k: z(E, H) for k in ("on", "tg")}
         self.q = {k: z(E, A) for k in ("on", "tg")}
         self.X = z(E, self.layout.D, dt=torch.bfloat16)
-        self.ctr = z(1024, dt=torch.int32)
+        self.ctr = z(int(kernels().r2_lstm_persist_ctr_words()), dt=torch.int32)
         self.err = z(1, dt=torch.int32)
         # n-step history ring (device)
         self.h_row = z(n, E, dt=torch.int64)

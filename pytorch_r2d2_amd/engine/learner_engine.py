@@ -176,7 +176,7 @@ class LearnerEngine:
         self.slab1 = z(nwg, B, H)
         self.dc = z(B, H)
         self.slab_p = z(2, nwg, B, H)
-        self.ctr = z(1024, dt=torch.int32)
+        self.ctr = z(int(kernels().r2_lstm_persist_ctr_words()), dt=torch.int32)
         self.err = z(1, dt=torch.int32)
         self.dgates = z(Ll * B, G, dt=bf16)
         self.gamma_n = float(lc.gamma ** n)

@@ -55,6 +55,8 @@ _SIGS = {
     "r2_torso_bwd_slab_floats": [],
     "r2_torso_bwd_set_debug": [P],
     "r2_torso_fwd_set_debug": [P],
+    "r2_lstm_persist_set_debug": [P],
+    "r2_lstm_persist_force_slow": [I],
     "r2_lstm_fwd_persist": [P, I, I, I, I, P, P, P],
     "r2_lstm_bwd_persist": [P, P, P, P, P, P, P, I, I, I, I, P, P, P],
     "r2_actor_finalize": [P] * 21 + [I, I, I, I, I, I, F, F, F, F, U64, P],

@@ -74,7 +74,7 @@ def test_lstm_forward_matches_lstmcell(B, H, impl):
     if impl == "step":
         rc = kernels().r2_lstm_fwd(arr.ctypes.data, 2, B, T, H, 0, stream_handle())
     else:
-        ctr = torch.zeros(1024, dtype=torch.int32, device=DEV)
+        ctr = torch.zeros(int(kernels().r2_lstm_persist_ctr_words()), dtype=torch.int32, device=DEV)
         err = torch.zeros(1, dtype=torch.int32, device=DEV)
         rc = kernels().r2_lstm_fwd_persist(arr.ctypes.data, 2, B, T, H, ptr(ctr), ptr(err),
                                            stream_handle())
@@ -126,7 +126,7 @@ def test_lstm_backward_matches_autograd(B, H, impl):
                              ptr(s1), ptr(dc), ptr(dg), B, T, t0, H, stream_handle()) == 0
     else:
         slab = torch.zeros(2, nwg, B, H, device=DEV)
-        ctr = torch.zeros(1024, dtype=torch.int32, device=DEV)
+        ctr = torch.zeros(int(kernels().r2_lstm_persist_ctr_words()), dtype=torch.int32, device=DEV)
         err = torch.zeros(1, dtype=torch.int32, device=DEV)
         assert k.r2_lstm_bwd_persist(ptr(dh_ext), ptr(gates), ptr(cseq), ptr(c0), ptr(pk["w_hhT"]),
                                      ptr(slab), ptr(dg), B, T, t0, H, ptr(ctr), ptr(err),
@@ -159,6 +159,42 @@ def test_lstm_backward_matches_autograd(B, H, impl):
     ref = torch.stack([p.grad for p in pre])  # (T-t0, B, G) original gate order
     got = dg.float()[..., L.gate_inv.to(DEV)]
     assert _rel(got, ref) < 3e-2
+
+
+@pytest.mark.parametrize("B", [64, 200])
+def test_lstm_persistent_same_xcd_path_matches_sc1_path(B):
+    """The same-XCD plain-store hand-off and the placement-independent sc1 hand-off must give
+    bit-identical results (only the store flavour of the published h / dh partials differs)."""
+    cfg, net, L, flat, pk = _setup(B, 256, seed=2)
+    H, G, T, t0 = 256, 1024, 12, 4
+    k = kernels()
+    xproj = torch.randn(T * B, G, device=DEV)
+    h0 = (torch.randn(B, H, device=DEV) * 0.3).bfloat16()
+    c0 = torch.randn(B, H, device=DEV) * 0.3
+    dh_ext = torch.randn(T - t0, B, H, device=DEV)
+    nw = int(k.r2_lstm_persist_ctr_words())
+    outs = []
+    for slow in (0, 1):
+        k.r2_lstm_persist_force_slow(slow)
+        hseq = torch.zeros(T, B, H, dtype=torch.bfloat16, device=DEV)
+        cseq = torch.zeros(T, B, H, device=DEV)
+        gates = torch.zeros(T - t0, B, G, device=DEV)
+        arr = np.asarray([ptr(xproj), ptr(pk["w_hh"]), ptr(h0), ptr(c0), ptr(hseq), ptr(cseq), 0,
+                          ptr(gates), t0] * 2, dtype=np.int64)
+        ctr = torch.zeros(nw, dtype=torch.int32, device=DEV)
+        err = torch.zeros(1, dtype=torch.int32, device=DEV)
+        assert k.r2_lstm_fwd_persist(arr.ctypes.data, 2, B, T, H, ptr(ctr), ptr(err), stream_handle()) == 0
+        slab = torch.zeros(2, H // UNITS, B, H, device=DEV)
+        dg = torch.zeros(T - t0, B, G, dtype=torch.bfloat16, device=DEV)
+        assert k.r2_lstm_bwd_persist(ptr(dh_ext), ptr(gates), ptr(cseq), ptr(c0), ptr(pk["w_hhT"]),
+                                     ptr(slab), ptr(dg), B, T, t0, H, ptr(ctr), ptr(err),
+                                     stream_handle()) == 0
+        torch.cuda.synchronize()
+        assert err.item() == 0
+        outs.append((hseq, cseq, dg))
+    k.r2_lstm_persist_force_slow(0)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
 
 
 def test_torso_matches_conv_stack():

@@ -71,7 +71,7 @@ for B in (8, 64):
         gt = torch.zeros(T, B, G, device=DEV)
         bufs += [hs, cs, gt]
         chains.append([ptr(xproj), ptr(pk["w_hh"]), ptr(h0), ptr(c0), ptr(hs), ptr(cs), 0, ptr(gt), 40])
-    ctr = torch.zeros(1024, dtype=torch.int32, device=DEV)
+    ctr = torch.zeros(int(k.r2_lstm_persist_ctr_words()), dtype=torch.int32, device=DEV)
     err = torch.zeros(1, dtype=torch.int32, device=DEV)
     for nch in (1, 2):
         arr = np.asarray([v for ch in chains[:nch] for v in ch], dtype=np.int64)
