@@ -169,16 +169,18 @@ def _hangs(i, beat=None):
 def test_supervisor_restarts_crashed_actor_and_kills_stalled(monkeypatch):
     from pytorch_r2d2_amd.utils.supervisor import RoleSpec, Supervisor
     monkeypatch.setenv("R2D2_FAULTS", "actor:0:crash_at=20;actor:1:hang_at=20")
-    roles = [RoleSpec("learner", _learner_like, (6.0,), restartable=False),
+    roles = [RoleSpec("learner", _learner_like, (60.0,), restartable=False),
              RoleSpec("actor0", _crashy, (0,), max_restarts=2),
-             RoleSpec("actor1", _hangs, (1,), max_restarts=1, stall_timeout_s=1.5)]
+             RoleSpec("actor1", _hangs, (1,), max_restarts=8, stall_timeout_s=1.5)]
     sup = Supervisor(roles, poll_s=0.05)
 
     def done():
-        p = sup.procs[0]
-        return p is None or not p.is_alive()
+        # finished once actor0 used up its restarts (3 exits seen) and actor1 was caught stalling;
+        # spawn start-up (a torch import per child) makes wall-clock budgets unreliable
+        r = sup.report
+        return len(r["actor0"]["exitcodes"]) >= 3 and r["actor1"]["stalls"] >= 1
 
-    rep = sup.run(until=done, timeout_s=40)
+    rep = sup.run(until=done, timeout_s=50)
     assert rep["actor0"]["restarts"] == 2
     assert 17 in rep["actor0"]["exitcodes"]
     assert rep["actor1"]["stalls"] >= 1
