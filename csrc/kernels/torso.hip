@@ -13,40 +13,62 @@
 //    channels-last (HWC, 80-byte padded pixel rows -> 16-byte aligned, bank-spread
 //    ds_read_b128 fragment loads);
 //  * conv2/conv3 weights live in LDS (padded rows), conv1 weights in VGPRs (64 regs);
-//  * the frame is converted u8->bf16 once, when it is written to LDS (56 KB), so the conv1
-//    MFMA loop issues no conversion VALU; the next frame's 28 KB is prefetched into registers
-//    while the current frame computes;
+//  * the frame is converted u8->bf16 once, when it is written to LDS, so the conv1 MFMA loop
+//    issues no conversion VALU; it is stored SPACE-TO-DEPTH: (21,21,64) with channel
+//    c = ci*16 + dy*4 + dx, which turns the 8x8/s4 conv1 into a 2x2/s1 conv whose B fragments
+//    (8 consecutive c) are single aligned ds_read_b128 (the plain CHW image needs two 8-byte
+//    reads per fragment, half the LDS rate); the next frame's 28 KB is prefetched into
+//    registers while the current frame computes;
 //  * two-phase software pipeline per frame: phase A = conv1(f) on all waves || conv3(f-1) on
 //    waves 2,3 (tiles dealt so every SIMD issues ~64 MFMAs); phase B = conv2(f) on waves 0..2
-//    || next frame -> LDS || conv1 activations saved; two barriers per frame;
+//    || next frame -> LDS and conv1 activations saved by waves 3..7; two barriers per frame;
 //  * output is bf16 in PyTorch's (C,H,W) flatten order, ready for the LSTM input GEMM.
 //  * optional: conv1/conv2 activations are written channels-last for the backward pass
 //    (torch channels_last NCHW tensors), so backward does not recompute the forward.
 //
-// One 512-thread workgroup per CU (147 KB LDS), grid-stride over frames.
+// One 512-thread workgroup per CU (151 KB LDS), grid-stride over frames.
 #include "../common.h"
 
 namespace torso {
 constexpr int IN_BYTES = 4 * 84 * 84;   // 28224
 constexpr int IN_CHUNKS = IN_BYTES / 16; // 1764
 constexpr int NT = 512;                  // threads
-constexpr int PF = (IN_CHUNKS + NT - 1) / NT;  // 4 prefetch chunks per thread
+constexpr int PF = (IN_CHUNKS + 319) / 320;   // 6 prefetch chunks per thread of waves 3..7
 constexpr int P1 = 400, P2 = 81, P3 = 49;
 constexpr int ACTS = 40;                 // bf16 per pixel row in LDS (32 + 8 pad) = 80 B
 constexpr int W2S = 512 + 8;             // bf16 per conv2 weight row (1040 B)
 constexpr int W3S = 288 + 8;             // bf16 per conv3 weight row (592 B)
-constexpr int OFF_IN = 0;                            // frame as bf16 (converted once)
-constexpr int OFF_A1 = OFF_IN + IN_BYTES * 2;        // 56448
+constexpr int S2DS = 72;                 // bf16 per space-to-depth pixel (64 + 8 pad) = 144 B
+constexpr int OFF_IN = 0;                            // frame, bf16 space-to-depth [441][72]
+constexpr int OFF_A1 = OFF_IN + 441 * S2DS * 2;      // 63504
 constexpr int OFF_A2 = OFF_A1 + P1 * ACTS * 2;       // 88448
 constexpr int OFF_W2 = OFF_A2 + P2 * ACTS * 2;       // 94928
 constexpr int OFF_W3 = OFF_W2 + 32 * W2S * 2;        // 128208
-constexpr int LDS_BYTES = OFF_W3 + 32 * W3S * 2;     // 147152
+constexpr int OFF_B23 = OFF_W3 + 32 * W3S * 2;      // conv2 / conv3 biases, fp32 [2][32]
+constexpr int LDS_BYTES = OFF_B23 + 64 * 4;          // 154464
 }  // namespace torso
 
-// 16 uint8 -> 16 bf16 written to LDS (the only u8->bf16 conversion of a frame)
-__device__ __forceinline__ void torso_store_chunk(bf16* dst, const u32x4& v) {
-  ((bf16x8*)dst)[0] = u8x8_to_bf16(v[0], v[1]);
-  ((bf16x8*)dst)[1] = u8x8_to_bf16(v[2], v[3]);
+// 16 uint8 of the CHW frame (chunk c) -> bf16 space-to-depth image (the only u8->bf16
+// conversion of a frame).  Rows are 84 B = 21 dwords, so every dword is 4 consecutive x of one
+// row: (ci, y, X) -> s2d pixel (y/4, X), channels ci*16 + (y%4)*4 + 0..3, one 8-byte store.
+__device__ __forceinline__ void torso_store_chunk(bf16* s2d, int c, const u32x4& v) {
+  int d = 4 * c;                 // first dword of the chunk
+  int ci = d / 1764, r = d - ci * 1764;
+  int y = r / 21, X = r - y * 21;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const uint32_t w = v[e];
+    bf16x4 o;
+    o[0] = (bf16)(float)(w & 0xff);
+    o[1] = (bf16)(float)((w >> 8) & 0xff);
+    o[2] = (bf16)(float)((w >> 16) & 0xff);
+    o[3] = (bf16)(float)(w >> 24);
+    *(bf16x4*)(s2d + ((y >> 2) * 21 + X) * torso::S2DS + ci * 16 + (y & 3) * 4) = o;
+    if (++X == 21) {
+      X = 0;
+      if (++y == 84) { y = 0; ++ci; }
+    }
+  }
 }
 
 // Phase A of the frame pipeline: conv1 of frame f over 13 pixel tiles, while conv3 of frame
@@ -84,16 +106,12 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(
   bf16x8 wf1[16];
 #pragma unroll
   for (int s = 0; s < 16; ++s) wf1[s] = *(const bf16x8*)(w1 + l32 * 256 + s * 16 + half * 8);
-  float bias1[16], bias23[16];
+  float bias1[16];
   const bool conv3_wave = (wave == 2 || wave == 3), conv2_wave = wave < 3;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int co = (r & 3) + 8 * (r >> 2) + 4 * half;
-    bias1[r] = b1[co];
-    // waves 0..2 run conv2 (phase B); waves 2,3 run conv3 (phase A); wave 2 does both and keeps
-    // conv3's bias, reading conv2's from global in its epilogue
-    bias23[r] = conv3_wave ? b3[co] : b2[co];
-  }
+  for (int r = 0; r < 16; ++r) bias1[r] = b1[(r & 3) + 8 * (r >> 2) + 4 * half];
+  float* lb23 = (float*)(lds + OFF_B23);   // epilogue biases of conv2 / conv3 (LDS broadcast)
+  if (tid < 64) lb23[tid] = tid < 32 ? b2[tid] : b3[tid - 32];
   const int t1b = c_t1_begin[wave], t1n = c_t1_count[wave];
 
   int f = blockIdx.x;
@@ -102,13 +120,13 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(
   {
     const size_t row = rows ? (size_t)rows[f] : (size_t)f;
     const u32x4* src = (const u32x4*)(frames + row * IN_BYTES);
-    for (int c = tid; c < IN_CHUNKS; c += NT) torso_store_chunk(in_bf + c * 16, src[c]);
+    for (int c = tid; c < IN_CHUNKS; c += NT) torso_store_chunk(in_bf, c, src[c]);
   }
   __syncthreads();
 
   int fprev = -1, it_dbg = 0;
 #define TF_TRACE(k) \
-  if (dbg && blockIdx.x == 0 && tid == 0 && it_dbg < 16) dbg[it_dbg * 4 + (k)] = clock64();
+  if (dbg && blockIdx.x == 0 && tid == 0 && it_dbg < 16) dbg[it_dbg * 8 + (k)] = clock64();
   // replay row of the next frame, read one frame ahead so the prefetch never waits on its address
   int row_nx = f + (int)gridDim.x < n_frames ? (rows ? rows[f + gridDim.x] : f + gridDim.x) : 0;
   for (;;) {
@@ -120,12 +138,13 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(
     TF_TRACE(0);
     // =================== phase A: conv1(f) || conv3(f-1)
     if (have) {
-      // prefetch frame f+grid into registers (lands while the convolutions run)
-      if (fn < n_frames) {
+      // waves 3..7 prefetch frame f+grid into registers (lands while the convolutions run);
+      // they convert it into LDS during phase B while waves 0..2 run conv2
+      if (fn < n_frames && wave >= 3) {
         const u32x4* src = (const u32x4*)(frames + (size_t)row_nx * IN_BYTES);
 #pragma unroll
         for (int q = 0; q < PF; ++q) {
-          const int c = tid + q * NT;
+          const int c = tid - 192 + q * 320;
           if (c < IN_CHUNKS) pf[q] = src[c];
         }
       }
@@ -134,13 +153,12 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(
         const int p = pt * 32 + l32;
         const int pc = p < P1 ? p : P1 - 1;
         const int oy = pc / 20, ox = pc % 20;
-        const bf16* base = in_bf + (4 * oy) * 84 + 4 * ox;
+        // K step s: s2d block (by, bx) = (s>>3, (s>>2)&1), channels (s&3)*16 + 8*half .. +8
+        const bf16* base = in_bf + (oy * 21 + ox) * S2DS + half * 8;
         f32x16 acc = {};
         mfma_pipe<16, 4>(acc, [&](int s) { return wf1[s]; }, [&](int s) {
-          const int ci = s >> 2, kh = (s & 3) * 2 + half;
-          const bf16x4* q = (const bf16x4*)(base + ci * 7056 + kh * 84);   // 8-byte aligned
-          const bf16x4 lo = q[0], hi = q[1];
-          return (bf16x8)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          const int by = s >> 3, bx = (s >> 2) & 1;
+          return *(const bf16x8*)(base + (by * 21 + bx) * S2DS + (s & 3) * 16);
         });
         if (p < P1) {
 #pragma unroll
@@ -173,7 +191,7 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int co = (r & 3) + 8 * (r >> 2) + 4 * half;
-          o[co * 49] = (bf16)fmaxf(acc[r] + bias23[r], 0.f);
+          o[co * 49] = (bf16)fmaxf(acc[r] + lb23[32 + co], 0.f);
         }
       }
     }
@@ -194,6 +212,7 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(
         const int khkw = s >> 1, kh = khkw >> 2, kw = khkw & 3;
         return *(const bf16x8*)(bbase + (kh * 20 + kw) * ACTS + (s & 1) * 16);
       });
+      TF_TRACE(4);
       if (p < P2) {
         bf16* d2 = save2 ? save2 + ((size_t)f * P2 + p) * 32 : nullptr;
 #pragma unroll
@@ -202,8 +221,7 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int co = 4 * half + 8 * g + e;
-            const float bb = (wave == 2) ? b2[co] : bias23[4 * g + e];
-            v[e] = (bf16)fmaxf(acc[4 * g + e] + bb, 0.f);
+            v[e] = (bf16)fmaxf(acc[4 * g + e] + lb23[co], 0.f);
           }
           *(bf16x4*)(act2 + p * ACTS + 8 * g + 4 * half) = v;
           if (d2) *(bf16x4*)(d2 + 8 * g + 4 * half) = v;
@@ -218,14 +236,16 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(
         *(bf16x8*)(d1 + px * 32 + q * 8) = *(const bf16x8*)(act1 + px * ACTS + q * 8);
       }
     }
+    TF_TRACE(5);
     // conv1(f) finished reading in_bf before the barrier above
-    if (fn < n_frames) {
+    if (fn < n_frames && wave >= 3) {
 #pragma unroll
       for (int q = 0; q < PF; ++q) {
-        const int c = tid + q * NT;
-        if (c < IN_CHUNKS) torso_store_chunk(in_bf + c * 16, pf[q]);
+        const int c = tid - 192 + q * 320;
+        if (c < IN_CHUNKS) torso_store_chunk(in_bf, c, pf[q]);
       }
     }
+    TF_TRACE(6);
     lds_sync();
     TF_TRACE(3);
     fprev = f;

@@ -22,7 +22,8 @@ are interchangeable with ``/root/reference``.
 The kernels read bf16 copies in their own layouts, produced every optimizer step by ONE
 ``pack_bf16`` gather launch through a precomputed int32 index map:
 
-    conv1  (C1, Cin*8*8)       k order (ci, kh, kw)   == torch order
+    conv1  (C1, Cin*8*8)       k order (by, bx, ci, dy, dx), kh = 4by+dy, kw = 4bx+dx
+                               (space-to-depth: 2x2 conv over a 21x21x64 image)
     conv2  (C2, 4*4*C1)        k order (kh, kw, ci)   channels-last implicit GEMM
     conv3  (C3, 3*3*C2)        k order (kh, kw, ci)
     w_ih   (G, D)  rows permuted to packed gate columns j*64 + g*16 + u  <- g*H + 16j + u
@@ -165,7 +166,12 @@ class ParamLayout:
         if self.model.torso == "atari":
             c1, c2, c3 = self.model.conv_channels
             cin = self.cin
-            w1 = off("vis_layers.0.weight") + np.arange(c1 * cin * 64)
+            # conv1 in space-to-depth order: the 8x8/s4 conv on (cin,84,84) is a 2x2/s1 conv on the
+            # (21,21,16*cin) image with channel c = ci*16 + dy*4 + dx; k = (by*2+bx)*16cin + c
+            co, by, bx, ci, dy, dx = np.meshgrid(np.arange(c1), np.arange(2), np.arange(2),
+                                                 np.arange(cin), np.arange(4), np.arange(4),
+                                                 indexing="ij")
+            w1 = off("vis_layers.0.weight") + ((co * cin + ci) * 8 + 4 * by + dy) * 8 + 4 * bx + dx
             add_bf("conv1", w1, (c1, cin * 64))
             co, kh, kw, ci = np.meshgrid(np.arange(c2), np.arange(4), np.arange(4), np.arange(c1),
                                          indexing="ij")

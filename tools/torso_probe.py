@@ -90,14 +90,15 @@ for i in range(10):
 print(json.dumps({"bwd_phase_cycles_S0_S1_S2_S3__S2split_pf_dw2_dact1_wait": phases}))
 
 # forward: phase A (conv1 || conv3) | barrier wait | phase B (conv2, frame -> LDS) for frames of WG 0
-dbg = torch.zeros(16 * 4, dtype=torch.int64, device=DEV)
+dbg = torch.zeros(16 * 8, dtype=torch.int64, device=DEV)
 k.r2_torso_fwd_set_debug(ptr(dbg))
 fwd(10880)
 k.r2_torso_fwd_set_debug(None)
-t = dbg.view(16, 4).cpu()
+t = dbg.view(16, 8).cpu()
 ph = []
 for i in range(15):
     if t[i + 1][0] == 0:
         break
-    ph.append([int(t[i][1] - t[i][0]), int(t[i][2] - t[i][1]), int(t[i][3] - t[i][2]), int(t[i + 1][0] - t[i][3])])
-print(json.dumps({"fwd_phase_cycles_A_waitA_B_waitB": ph}))
+    ph.append([int(t[i][1] - t[i][0]), int(t[i][2] - t[i][1]), int(t[i][4] - t[i][2]),
+               int(t[i][5] - t[i][4]), int(t[i][6] - t[i][5]), int(t[i][3] - t[i][6])])
+print(json.dumps({"fwd_phase_cycles_A_waitA_conv2mma_conv2epi_framewrite_waitB": ph}))
