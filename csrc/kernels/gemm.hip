@@ -1,0 +1,219 @@
+// Batched bf16 MFMA GEMM with fused epilogues for the learner's dense layers (gfx950).
+//
+// Replaces the library GEMMs of one learner step (reference math: learner.py:99-120 -- the
+// LSTM input projection, the dueling head's first layer and their backward products) and the
+// copies / gathers around them:
+//
+//   C[m][n] (=|+=) alpha * sum_k A[m][k] B[k][n]  (+ bias[n])      written fp32 or bf16,
+//   row m stored at crow[m] when a row map is given (the LSTM's packed gate order -> torch order)
+//
+// Each operand is either K-contiguous ("k-major": X[i][k] at X + i*ld + k) or M/N-contiguous
+// ("mn-major": X[i][k] at X + k*ld + i).  Up to 4 independent problems per launch (their tiles
+// enumerated linearly over blockIdx.x), so e.g. the online and target input projections run as
+// one grid.
+//
+// Tile 128x128x64, 256 threads = 4 waves in 2x2, each wave 64x64 = 2x2 v_mfma_f32_32x32x16_bf16
+// accumulators.  Global -> registers (tile t+1) overlaps the MFMAs of tile t; LDS double buffer,
+// one barrier per K tile.  LDS images: k-major operands as [row][64 k + 8 pad] read with
+// ds_read_b128; mn-major operands as [k][128 + 32 pad] read with ds_read_b64_tr_b16 (the hardware
+// transpose hands each lane its 8 consecutive k).  K must be a multiple of 8 (tails zero-filled); M and N are
+// arbitrary for k-major operands, multiples of 8 for mn-major ones.
+#include "../common.h"
+
+namespace gm {
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+constexpr int KS = BK + 8;        // k-major LDS row stride (bf16): 144 B rows (b128 reads conflict-free)
+constexpr int MS = BM + 32;       // mn-major LDS row stride (bf16): 320 B = 16 dwords mod 64 banks,
+                                  // so the 4 rows x 2 column groups of a tr read hit 8 distinct bank octets
+constexpr int LPT = BM * BK / 8 / NT;  // 16-B chunks per thread per operand tile (4)
+constexpr int TILE = BM * KS > BK * MS ? BM * KS : BK * MS;  // bf16 per operand tile
+constexpr int MAXP = 4;
+}  // namespace gm
+
+struct GemmProb {
+  const bf16* A;
+  const bf16* B;
+  void* C;
+  const float* bias;   // per output column, or null
+  const int* crow;     // output row map, or null
+  int M, N, K, lda, ldb, ldc;
+  int a_kmajor, b_kmajor, c_f32, accumulate;
+  float alpha;
+  int tiles_n, tile_base;  // tiles along N; first linear tile index of this problem
+};
+
+struct GemmArgs {
+  GemmProb p[gm::MAXP];
+  int nprob;
+};
+
+typedef short gi16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) gi16x4 glds_i16x4;
+
+__device__ __forceinline__ bf16x8 gm_tr8(const bf16* p0, const bf16* p1) {
+  const gi16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((glds_i16x4*)p0);
+  const gi16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((glds_i16x4*)p1);
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+// Global -> register staging of one 128 x 64 operand tile (256 threads, 4 x 16 B each).
+//   k-major: row r = c / 8, k chunk (c % 8) * 8;  mn-major: k row = c / 16, i chunk (c % 16) * 8
+template <bool KMAJ>
+__device__ __forceinline__ void gm_load(const bf16* X, int ld, int i0, int imax, int k0, int kmax,
+                                        int tid, u32x4 (&r)[gm::LPT]) {
+#pragma unroll
+  for (int q = 0; q < gm::LPT; ++q) {
+    const int c = tid + q * gm::NT;
+    if (KMAJ) {
+      const int row = min(i0 + (c >> 3), imax - 1), k = k0 + (c & 7) * 8;
+      r[q] = k < kmax ? *(const u32x4*)(X + (size_t)row * ld + k) : u32x4{0, 0, 0, 0};
+    } else {
+      const int k = k0 + (c >> 4), col = i0 + (c & 15) * 8;
+      // (imax % 8 == 0) chunks wholly past the edge read a valid chunk; never stored
+      const int cc = col < imax ? col : imax - 8;
+      r[q] = k < kmax ? *(const u32x4*)(X + (size_t)k * ld + cc) : u32x4{0, 0, 0, 0};
+    }
+  }
+}
+
+template <bool KMAJ>
+__device__ __forceinline__ void gm_store(bf16* L, int tid, const u32x4 (&r)[gm::LPT]) {
+#pragma unroll
+  for (int q = 0; q < gm::LPT; ++q) {
+    const int c = tid + q * gm::NT;
+    if (KMAJ) *(u32x4*)(L + (c >> 3) * gm::KS + (c & 7) * 8) = r[q];
+    else *(u32x4*)(L + (c >> 4) * gm::MS + (c & 15) * 8) = r[q];
+  }
+}
+
+// MFMA fragment (8 consecutive k of tile row i = i0 + lane&31) for K step ks (0..3) of the tile
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8 gm_frag(const bf16* L, int i0, int ks, int lane) {
+  const int l32 = lane & 31, h = lane >> 5;
+  if (KMAJ) return *(const bf16x8*)(L + (i0 + l32) * gm::KS + ks * 16 + h * 8);
+  // transposed read: 16-lane group g covers columns i0 + 16(g&1) .. +15; lane 4q+p names row
+  // (k) 16ks + 8h + 4r + q, columns 4p .. 4p+3
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const bf16* b = L + (ks * 16 + h * 8 + q) * gm::MS + i0 + 16 * (g & 1) + 4 * p;
+  return gm_tr8(b, b + 4 * gm::MS);
+}
+
+template <bool AK, bool BK_>
+__global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs args) {
+  using namespace gm;
+  __shared__ __attribute__((aligned(16))) bf16 la[2][TILE];
+  __shared__ __attribute__((aligned(16))) bf16 lb[2][TILE];
+  // problem of this block (tiles of all problems enumerated linearly)
+  int pi = 0;
+#pragma unroll
+  for (int i = 1; i < MAXP; ++i)
+    if (i < args.nprob && (int)blockIdx.x >= args.p[i].tile_base) pi = i;
+  const GemmProb& P = args.p[pi];
+  if (P.a_kmajor != (int)AK || P.b_kmajor != (int)BK_) return;  // launched per layout combo
+  const int t = blockIdx.x - P.tile_base;
+  const int tm = t / P.tiles_n, tn = t % P.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  if (m0 >= P.M) return;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+
+  f32x16 acc[2][2] = {};
+  u32x4 ra[LPT], rb[LPT];
+  const int nk = (P.K + BK - 1) / BK;   // the last tile's k >= K chunks are zero-filled
+  gm_load<AK>(P.A, P.lda, m0, P.M, 0, P.K, tid, ra);
+  gm_load<BK_>(P.B, P.ldb, n0, P.N, 0, P.K, tid, rb);
+  gm_store<AK>(la[0], tid, ra);
+  gm_store<BK_>(lb[0], tid, rb);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      gm_load<AK>(P.A, P.lda, m0, P.M, (kt + 1) * BK, P.K, tid, ra);
+      gm_load<BK_>(P.B, P.ldb, n0, P.N, (kt + 1) * BK, P.K, tid, rb);
+    }
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        fa[i] = gm_frag<AK>(la[cur], wm + 32 * i, ks, lane);
+        fb[i] = gm_frag<BK_>(lb[cur], wn + 32 * i, ks, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(fa[i], fb[j], acc[i][j]);
+    }
+    if (kt + 1 < nk) {
+      gm_store<AK>(la[cur ^ 1], tid, ra);
+      gm_store<BK_>(lb[cur ^ 1], tid, rb);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: C[row][col] with acc[i][j][r] = C[m0+wm+32i + (r&3)+8(r>>2)+4h][n0+wn+32j + l32]
+  const int l32 = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = n0 + wn + 32 * j + l32;
+    if (col >= P.N) continue;
+    const float bv = P.bias ? P.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row >= P.M) continue;
+        const int orow = P.crow ? P.crow[row] : row;
+        const float v = P.alpha * acc[i][j][r] + bv;
+        const size_t o = (size_t)orow * P.ldc + col;
+        if (P.c_f32) {
+          float* c = (float*)P.C + o;
+          *c = P.accumulate ? *c + v : v;
+        } else {
+          bf16* c = (bf16*)P.C + o;
+          *c = (bf16)(P.accumulate ? (float)*c + v : v);
+        }
+      }
+  }
+}
+
+// descs: nprob x 16 int64 {A, B, C, bias, crow, M, N, K, lda, ldb, ldc, a_kmajor, b_kmajor,
+// c_f32, accumulate, alpha_bits}.  All problems of one call must share (a_kmajor, b_kmajor).
+extern "C" int r2_gemm(const int64_t* descs, int nprob, void* stream) {
+  if (nprob < 1 || nprob > gm::MAXP) return -1;
+  GemmArgs a;
+  a.nprob = nprob;
+  int tiles = 0, ak = -1, bk = -1;
+  for (int i = 0; i < nprob; ++i) {
+    const int64_t* d = descs + 16 * i;
+    GemmProb& p = a.p[i];
+    p.A = (const bf16*)d[0]; p.B = (const bf16*)d[1]; p.C = (void*)d[2];
+    p.bias = (const float*)d[3]; p.crow = (const int*)d[4];
+    p.M = (int)d[5]; p.N = (int)d[6]; p.K = (int)d[7];
+    p.lda = (int)d[8]; p.ldb = (int)d[9]; p.ldc = (int)d[10];
+    p.a_kmajor = (int)d[11]; p.b_kmajor = (int)d[12]; p.c_f32 = (int)d[13];
+    p.accumulate = (int)d[14];
+    const uint32_t ab = (uint32_t)d[15];
+    p.alpha = __builtin_bit_cast(float, ab);
+    if (p.M < 1 || p.N < 1 || p.K < 8 || p.K % 8) return -2;
+    if (!p.b_kmajor && (p.N % 8)) return -3;   // mn-major loads move 8 columns at a time
+    if (!p.a_kmajor && (p.M % 8)) return -3;
+    if ((!p.a_kmajor && (p.lda % 8)) || (!p.b_kmajor && (p.ldb % 8)) ||
+        (p.a_kmajor && (p.lda % 8)) || (p.b_kmajor && (p.ldb % 8)))
+      return -4;  // 16-byte aligned rows
+    if (ak < 0) { ak = p.a_kmajor; bk = p.b_kmajor; }
+    if (ak != p.a_kmajor || bk != p.b_kmajor) return -5;
+    p.tiles_n = (p.N + gm::BN - 1) / gm::BN;
+    p.tile_base = tiles;
+    tiles += p.tiles_n * ((p.M + gm::BM - 1) / gm::BM);
+  }
+  for (int i = nprob; i < gm::MAXP; ++i) a.p[i] = a.p[0], a.p[i].tile_base = 1 << 30;
+  hipStream_t s = (hipStream_t)stream;
+  if (ak && bk) hipLaunchKernelGGL((gemm_kernel<true, true>), dim3(tiles), dim3(gm::NT), 0, s, a);
+  else if (ak) hipLaunchKernelGGL((gemm_kernel<true, false>), dim3(tiles), dim3(gm::NT), 0, s, a);
+  else if (bk) hipLaunchKernelGGL((gemm_kernel<false, true>), dim3(tiles), dim3(gm::NT), 0, s, a);
+  else hipLaunchKernelGGL((gemm_kernel<false, false>), dim3(tiles), dim3(gm::NT), 0, s, a);
+  R2_CHECK_LAUNCH();
+  return 0;
+}

@@ -53,6 +53,7 @@ _SIGS = {
     "r2_noop_chain": [P, I, I, P],
     "r2_torso_bwd": [P, P, I, P, P, P, P, P, P, P, I, P, P, P, P],
     "r2_torso_bwd_slab_floats": [],
+    "r2_gemm": [P, I, P],
     "r2_torso_bwd_set_debug": [P],
     "r2_torso_fwd_set_debug": [P],
     "r2_lstm_persist_set_debug": [P],

@@ -1,0 +1,63 @@
+"""Python front end of the batched MFMA GEMM (csrc/kernels/gemm.hip).
+
+A problem computes  C (=|+=) alpha * A @ B (+ bias)  with bf16 operands given as strided 2-D
+views; each operand may be K-contiguous or M/N-contiguous (the kernel stages the latter with
+hardware-transposed LDS reads), so transposed products such as ``dz.t() @ h`` need no copies.
+Output fp32 or bf16, optional per-column bias and an output row map (``crow[m]`` = row of C
+that receives row m of the product)."""
+from __future__ import annotations
+
+import struct
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from ._lib import check, kernels, stream_handle
+
+
+def _layout(x: torch.Tensor, rows_are_outer: bool):
+    """Classify a 2-D view X[i][k] (i = outer M/N index, k = reduction index).
+    Returns (kmajor, ld)."""
+    si, sk = x.stride()
+    if sk == 1:
+        return 1, si
+    if si == 1:
+        return 0, sk
+    raise ValueError("gemm operand must be contiguous in one dimension")
+
+
+@dataclass
+class Gemm:
+    a: torch.Tensor          # (M, K) view
+    b: torch.Tensor          # (K, N) view
+    c: torch.Tensor          # (M_out, N) fp32 or bf16, row stride ldc, unit column stride
+    bias: Optional[torch.Tensor] = None
+    crow: Optional[torch.Tensor] = None
+    accumulate: bool = False
+    alpha: float = 1.0
+
+    def desc(self) -> List[int]:
+        a, b, c = self.a, self.b, self.c
+        assert a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
+        M, K = a.shape
+        K2, N = b.shape
+        assert K == K2, (a.shape, b.shape)
+        ak, lda = _layout(a, True)                 # A[m][k]
+        bk, ldb = _layout(b.t(), True)             # B^T[n][k]
+        assert c.stride(1) == 1 and c.dtype in (torch.float32, torch.bfloat16)
+        if self.crow is None:
+            assert c.shape[0] >= M and c.shape[1] >= N
+        alpha_bits = struct.unpack("<I", struct.pack("<f", float(self.alpha)))[0]
+        return [a.data_ptr(), b.data_ptr(), c.data_ptr(),
+                0 if self.bias is None else self.bias.data_ptr(),
+                0 if self.crow is None else self.crow.data_ptr(),
+                M, N, K, lda, ldb, c.stride(0), ak, bk, int(c.dtype == torch.float32),
+                int(self.accumulate), alpha_bits]
+
+
+def gemm(*problems: Gemm, stream=None) -> None:
+    """Run up to 4 problems sharing one operand-layout combination in one launch."""
+    arr = np.asarray([v for p in problems for v in p.desc()], dtype=np.int64)
+    check(kernels().r2_gemm(arr.ctypes.data, len(problems), stream or stream_handle()), "gemm")

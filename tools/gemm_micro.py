@@ -1,0 +1,54 @@
+"""MFMA GEMM (csrc/kernels/gemm.hip) vs torch/hipBLASLt at the learner step's shapes."""
+import json
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from pytorch_r2d2_amd.ops.gemm import Gemm, gemm  # noqa: E402
+
+DEV = "cuda"
+torch.manual_seed(0)
+
+
+def timeit(fn, reps=50):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e3
+
+
+res = {}
+bf = torch.bfloat16
+# x-projection: (5440 x 1568) @ (1568 x 1024) + bias, fp32 out
+X = torch.randn(5440, 1568, device=DEV).to(bf)
+W = torch.randn(1024, 1568, device=DEV).to(bf)
+bias = torch.randn(1024, device=DEV)
+C = torch.empty(5440, 1024, device=DEV)
+fl = 2 * 5440 * 1568 * 1024
+us = timeit(lambda: gemm(Gemm(X, W.t(), C, bias=bias)))
+res["xp_mine_us"], res["xp_mine_tflops"] = us, fl / us / 1e6
+us = timeit(lambda: torch.addmm(bias, X, W.t(), out_dtype=torch.float32))
+res["xp_torch_us"], res["xp_torch_tflops"] = us, fl / us / 1e6
+# dW_ih: dgates^T (1024 x 2560) @ X (2560 x 1568), both mn-major
+dg = torch.randn(2560, 1024, device=DEV).to(bf)
+Xl = X[:2560]
+Cw = torch.empty(1024, 1568, device=DEV)
+fl = 2 * 1024 * 2560 * 1568
+us = timeit(lambda: gemm(Gemm(dg.t(), Xl, Cw)))
+res["dwih_mine_us"], res["dwih_mine_tflops"] = us, fl / us / 1e6
+us = timeit(lambda: torch.mm(dg.t(), Xl, out_dtype=torch.float32))
+res["dwih_torch_us"] = us
+# dX: dgates (2560 x 1024) @ W (1024 x 1568) bf16 out (k-major A, mn-major B)
+Cx = torch.empty(2560, 1568, dtype=bf, device=DEV)
+us = timeit(lambda: gemm(Gemm(dg, W, Cx)))
+res["dx_mine_us"], res["dx_mine_tflops"] = us, fl / us / 1e6
+us = timeit(lambda: torch.mm(dg, W))
+res["dx_torch_us"] = us
+print(json.dumps({k: round(v, 1) for k, v in res.items()}))
