@@ -45,6 +45,7 @@ import torch
 from ..config import R2D2Config
 from ..models.qnet import QNet
 from ..ops._lib import check, kernels, ptr, stream_handle
+from ..ops.gemm import Gemm, gemm
 from .layout import ParamLayout, UNITS
 from .replay_hbm import HBMReplay
 
@@ -189,6 +190,19 @@ class LearnerEngine:
         self._tb_dst, self._tb_scale = dst.to(d), scale.to(d)
         self.ones_bf = torch.ones(1, Tn * B, dtype=bf16, device=d)
         self.ones_f32 = torch.ones(1, Tn * B, dtype=f32, device=d)
+        # hand-written MFMA GEMM path (csrc/kernels/gemm.hip): K and the mn-major extents must be
+        # multiples of 8; otherwise the library GEMMs below are used
+        self.use_gemm = (d.type == "cuda" and (Ll * B) % 8 == 0 and D % 8 == 0 and H % 8 == 0
+                         and (2 * HD) % 8 == 0 and G % 8 == 0)
+        self.xp_on = z(Tn * B, G)
+        self.xp_tg = z(self.X_tg.shape[0], G)
+        self.z_on = z(self.Nh, 2 * HD, dt=bf16)
+        self.z_tg = z(Ntg, 2 * HD, dt=bf16)
+        if mode != "shifted":
+            self.z_nx = z(Nnx, 2 * HD, dt=bf16)
+        self.dh = z(Ll * B, H)
+        self.dX = z(Ll * B, D, dt=bf16)
+        self.gate_perm_i32 = L.gate_perm.to(d, torch.int32)
 
     # ------------------------------------------------------------------ weights
     def _pack(self, always: bool = False, stream=None):
@@ -245,12 +259,19 @@ class LearnerEngine:
             check(k.r2_lstm_fwd(arr.ctypes.data, len(chains), self.B, T, self.layout.H, t_begin,
                                 stream_handle()), "lstm_fwd")
 
-    def _head(self, pk, h: torch.Tensor, q: torch.Tensor, zr: Optional[torch.Tensor]):
-        N = h.shape[0]
-        z = torch.mm(h, pk["head1"].t())
-        check(kernels().r2_dueling_fwd(ptr(z), ptr(pk["head_b1"]), ptr(pk["head_w2"]),
-                                       ptr(pk["head_b2"]), ptr(q), ptr(zr), N, self.layout.A,
-                                       self.layout.HD, stream_handle()), "dueling_fwd")
+    def _heads(self, jobs):
+        """jobs: [(pk, h (N,H) bf16, z buffer, q out, zr out or None)].  Layer-1 GEMMs of all heads
+        in one launch, then one dueling kernel per head."""
+        if self.use_gemm:
+            gemm(*[Gemm(h, pk["head1"].t(), zb) for pk, h, zb, _, _ in jobs])
+            zs = [zb for _, _, zb, _, _ in jobs]
+        else:
+            zs = [torch.mm(h, pk["head1"].t()) for pk, h, _, _, _ in jobs]
+        for (pk, h, _, q, zr), z in zip(jobs, zs):
+            check(kernels().r2_dueling_fwd(ptr(z), ptr(pk["head_b1"]), ptr(pk["head_w2"]),
+                                           ptr(pk["head_b2"]), ptr(q), ptr(zr), h.shape[0],
+                                           self.layout.A, self.layout.HD, stream_handle()),
+                  "dueling_fwd")
 
     # ------------------------------------------------------------------ the step
     def _forward_loss(self):
@@ -269,8 +290,13 @@ class LearnerEngine:
         self._torso(pk, rows[T * B:], self.X_on[T * B:])
         self._torso(pt, rows[self.t_lo_tg * B:], self.X_tg)
         # input projections (one GEMM per net over every row)
-        xp_on = addmm_f32(self.lstm_b, self.X_on, pk["w_ih"].t())
-        xp_tg = addmm_f32(self.lstm_b_t, self.X_tg, pt["w_ih"].t())
+        if self.use_gemm:
+            xp_on, xp_tg = self.xp_on, self.xp_tg
+            gemm(Gemm(self.X_on, pk["w_ih"].t(), xp_on, bias=self.lstm_b),
+                 Gemm(self.X_tg, pt["w_ih"].t(), xp_tg, bias=self.lstm_b_t))
+        else:
+            xp_on = addmm_f32(self.lstm_b, self.X_on, pk["w_ih"].t())
+            xp_tg = addmm_f32(self.lstm_b_t, self.X_tg, pt["w_ih"].t())
         self._xp = (xp_on, xp_tg)
         # stored recurrent state
         st_off = {"on": 0, "tg": 0 if self.mode == "shifted" else n, "nx": n}
@@ -298,15 +324,17 @@ class LearnerEngine:
                                   self.hseq["nx"], self.cseq["nx"])
             self._lstm([nx], Ll)
         # heads (rows from the first learning step on)
-        self._head(pk, self.hseq["on"][Lb:].reshape(-1, H), self.q_on, self.zr_on)
-        self._head(pt, self.hseq["tg"][Lb:].reshape(-1, H), self.q_tg, None)
+        jobs = [(pk, self.hseq["on"][Lb:].reshape(-1, H), self.z_on, self.q_on, self.zr_on),
+                (pt, self.hseq["tg"][Lb:].reshape(-1, H), self.z_tg, self.q_tg, None)]
+        if self.mode != "shifted":
+            nx_from = Lb if self.mode == "fixed" else 0
+            jobs.append((pk, self.hseq["nx"][nx_from:].reshape(-1, H), self.z_nx, self.q_nx, None))
+        self._heads(jobs)
         if self.mode == "shifted":
             q_sa = self.q_on[: Ll * B]
             q_arg = self.q_on[n * B:(n + Ll) * B]
             q_tgt = self.q_tg[n * B:(n + Ll) * B]
         else:
-            nx_from = Lb if self.mode == "fixed" else 0
-            self._head(pk, self.hseq["nx"][nx_from:].reshape(-1, H), self.q_nx, None)
             q_sa = self.q_on[: Ll * B]
             q_arg = self.q_nx[: Ll * B]
             q_tgt = self.q_tg[: Ll * B]
@@ -337,9 +365,14 @@ class LearnerEngine:
         # column sums as GEMVs against a ones row (torch's dim-0 reduce is ~300 us here)
         torch.mm(self.ones_f32[:, :N], self.dva, out=L.span(g, "val.2.bias", "adv.2.bias", (1, 1 + A)))
         h_learn = self.hseq["on"][Lb:T].reshape(N, H)
-        L.span(g, "val.0.weight", "adv.0.weight", (2 * HD, H)).copy_(mm_f32(self.dz.t(), h_learn))
+        gw1 = L.span(g, "val.0.weight", "adv.0.weight", (2 * HD, H))
+        if self.use_gemm:
+            dh = self.dh
+            gemm(Gemm(self.dz, pk["head1"], dh))                          # (N, H) fp32
+        else:
+            gw1.copy_(mm_f32(self.dz.t(), h_learn))
+            dh = mm_f32(self.dz, pk["head1"])                           # (N, H)
         L.span(g, "val.0.bias", "adv.0.bias", (1, 2 * HD)).copy_(mm_f32(self.ones_bf[:, :N], self.dz))
-        dh = mm_f32(self.dz, pk["head1"])                               # (N, H)
         if self.cfg.learner.lstm_impl == "persistent":
             check(k.r2_lstm_bwd_persist(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]),
                                         ptr(self.c0["on"]), ptr(pk["w_hhT"]), ptr(self.slab_p),
@@ -350,18 +383,31 @@ class LearnerEngine:
             check(k.r2_lstm_bwd(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]), ptr(self.c0["on"]),
                                 ptr(pk["w_hhT"]), ptr(self.slab0), ptr(self.slab1), ptr(self.dc),
                                 ptr(self.dgates), B, T, Lb, H, s), "lstm_bwd")
-        dg_o = self.dgates.index_select(1, self.gate_inv)               # original gate order
         X = self.X_on[Lb * B: T * B]
-        L.view(g, "lstm.weight_ih").copy_(mm_f32(dg_o.t(), X))
         if Lb >= 1:
             h_prev = self.hseq["on"][Lb - 1: T - 1].reshape(N, H)
         else:
             h_prev = torch.cat([self.h0["on"][None], self.hseq["on"][: T - 1]]).reshape(N, H)
-        L.view(g, "lstm.weight_hh").copy_(mm_f32(dg_o.t(), h_prev))
-        db = mm_f32(self.ones_bf[:, :N], dg_o).view(-1)
-        L.view(g, "lstm.bias_ih").copy_(db)
-        L.view(g, "lstm.bias_hh").copy_(db)
-        self._dX = torch.mm(self.dgates, pk["w_ih"])                   # (N, D) bf16
+        if self.use_gemm:
+            # weight gradients straight into the flat buffer; the row map puts the packed gate
+            # order back into torch order (no gather of dgates, no copies)
+            dgT = self.dgates.t()
+            gemm(Gemm(dgT, X, L.view(g, "lstm.weight_ih"), crow=self.gate_perm_i32),
+                 Gemm(dgT, h_prev, L.view(g, "lstm.weight_hh"), crow=self.gate_perm_i32),
+                 Gemm(self.dz.t(), h_learn, gw1))
+            db = mm_f32(self.ones_bf[:, :N], self.dgates).view(-1)       # packed gate order
+            torch.index_select(db, 0, self.gate_inv, out=L.view(g, "lstm.bias_ih"))
+            L.view(g, "lstm.bias_hh").copy_(L.view(g, "lstm.bias_ih"))
+            gemm(Gemm(self.dgates, pk["w_ih"], self.dX))                  # (N, D) bf16
+            self._dX = self.dX
+        else:
+            dg_o = self.dgates.index_select(1, self.gate_inv)           # original gate order
+            L.view(g, "lstm.weight_ih").copy_(mm_f32(dg_o.t(), X))
+            L.view(g, "lstm.weight_hh").copy_(mm_f32(dg_o.t(), h_prev))
+            db = mm_f32(self.ones_bf[:, :N], dg_o).view(-1)
+            L.view(g, "lstm.bias_ih").copy_(db)
+            L.view(g, "lstm.bias_hh").copy_(db)
+            self._dX = torch.mm(self.dgates, pk["w_ih"])               # (N, D) bf16
 
     def _relu_mask(self, grad: torch.Tensor, act: torch.Tensor) -> torch.Tensor:
         """grad * (act > 0) for two tensors with the same (channels-last) memory layout."""
