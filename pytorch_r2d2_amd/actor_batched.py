@@ -31,6 +31,7 @@ from .engine.layout import ParamLayout
 from .engine.learner_engine import addmm_f32
 from .engine.replay_hbm import HBMReplay
 from .ops._lib import check, kernels, ptr, stream_handle
+from .ops.torso_lib import fused_torso_supported, torso_forward_library
 
 
 class PackedWeights:
@@ -82,6 +83,7 @@ class BatchedActor:
         self.gamma = cfg.learner.gamma
         self.gamma_n = self.gamma ** self.n
         self.layout = ParamLayout(m, cfg.env)
+        self.fused_torso = fused_torso_supported(cfg.env, m)
         total = total_envs or E
         eps = [epsilon_ladder(global_env_offset + i, total, cfg.actor.eps_base, cfg.actor.eps_alpha)
                for i in range(E)]
@@ -126,9 +128,13 @@ class BatchedActor:
         E, H, L = self.E, self.H, self.layout
         for key, w in (("on", self.online), ("tg", self.target)):
             pk = w.pk
-            check(k.r2_torso_fwd(ptr(self.env.frames), 0, E, ptr(pk["conv1"]), ptr(pk["b1"]),
-                                 ptr(pk["conv2"]), ptr(pk["b2"]), ptr(pk["conv3"]), ptr(pk["b3"]),
-                                 ptr(self.X), 0, 0, 256, s), "torso_fwd")
+            if self.fused_torso:
+                check(k.r2_torso_fwd(ptr(self.env.frames), 0, E, ptr(pk["conv1"]), ptr(pk["b1"]),
+                                     ptr(pk["conv2"]), ptr(pk["b2"]), ptr(pk["conv3"]), ptr(pk["b3"]),
+                                     ptr(self.X), 0, 0, 256, s), "torso_fwd")
+            else:
+                torso_forward_library(self.env.frames.reshape(E, -1), None, L, w.flat, self.cfg.env,
+                                      self.cfg.model, self.X)
             xp = addmm_f32(w.lstm_b, self.X, pk["w_ih"].t())
             chain = [ptr(xp), ptr(pk["w_hh"]), ptr(self.h_bf[key]), ptr(self.c[key]),
                      ptr(self.h_bf_new[key]), ptr(self.c_new[key]), ptr(self.h32_new[key]), 0, 0]
@@ -271,7 +277,8 @@ def engine_weights(engine):
     """Adapter exposing a LearnerEngine's live online / target packed weights to an actor."""
 
     class _W:
-        def __init__(self, pk, b):
-            self.pk, self.lstm_b = pk, b
+        def __init__(self, pk, b, flat):
+            self.pk, self.lstm_b, self.flat = pk, b, flat
 
-    return _W(engine.pk, engine.lstm_b), _W(engine.pk_t, engine.lstm_b_t)
+    return (_W(engine.pk, engine.lstm_b, engine.master),
+            _W(engine.pk_t, engine.lstm_b_t, engine.target))

@@ -46,6 +46,8 @@ from ..config import R2D2Config
 from ..models.qnet import QNet
 from ..ops._lib import check, kernels, ptr, stream_handle
 from ..ops.gemm import Gemm, gemm
+from ..models.qnet import torso_dims
+from ..ops.torso_lib import fused_torso_supported, torso_forward_library
 from .layout import ParamLayout, UNITS
 from .replay_hbm import HBMReplay
 
@@ -144,9 +146,17 @@ class LearnerEngine:
         t_lo = 0 if mode == "shifted" else n       # first frame the target net needs
         self.t_lo_tg = t_lo
         self.X_tg = z((Tn - t_lo) * B, D, dt=bf16)
-        self.act1 = z(Ll * B, 400, 32, dt=bf16)
-        self.act2 = z(Ll * B, 81, 32, dt=bf16)
-        self.frames_bf = z(Ll * B, 4, 84, 84, dt=bf16)
+        # conv activations of the learning frames, channels-last (N, h*w, c); the fused HIP torso
+        # kernels cover the Atari geometry (4x84x84 -> 32x20x20 -> 32x9x9 -> 32x7x7), every other
+        # geometry (e.g. DMLab RGB 3x72x96) runs the library conv path with the same buffers
+        self.fused_torso = fused_torso_supported(cfg.env, cfg.model)
+        if cfg.model.torso == "atari":
+            cin, dims, _ = torso_dims(cfg.env, cfg.model)
+            c1, c2, _c3 = cfg.model.conv_channels
+            self.tdims = (cin, dims)
+            self.act1 = z(Ll * B, dims[0][0] * dims[0][1], c1, dt=bf16)
+            self.act2 = z(Ll * B, dims[1][0] * dims[1][1], c2, dt=bf16)
+            self.frames_bf = z(Ll * B, cfg.env.frame_h * cfg.env.frame_w * cin, dt=bf16)
         self.h0 = {k: z(B, H, dt=bf16) for k in ("on", "tg", "nx")}
         self.c0 = {k: z(B, H) for k in ("on", "tg", "nx")}
         Tc = self.Tc
@@ -183,11 +193,12 @@ class LearnerEngine:
         self.gamma_n = float(lc.gamma ** n)
         # fused torso backward: per-workgroup gradient slabs + destination map (allocated here,
         # never lazily: the step must be capturable without warm-up)
-        n_slab = int(kernels().r2_torso_bwd_slab_floats())
-        self._tb_grid = min(256, Ll * B)
-        self._tb_slab = z(self._tb_grid * n_slab)
-        dst, scale = L.torso_grad_map()
-        self._tb_dst, self._tb_scale = dst.to(d), scale.to(d)
+        if self.fused_torso:
+            n_slab = int(kernels().r2_torso_bwd_slab_floats())
+            self._tb_grid = min(256, Ll * B)
+            self._tb_slab = z(self._tb_grid * n_slab)
+            dst, scale = L.torso_grad_map()
+            self._tb_dst, self._tb_scale = dst.to(d), scale.to(d)
         self.ones_bf = torch.ones(1, Tn * B, dtype=bf16, device=d)
         self.ones_f32 = torch.ones(1, Tn * B, dtype=f32, device=d)
         # hand-written MFMA GEMM path (csrc/kernels/gemm.hip): K and the mn-major extents must be
@@ -237,6 +248,12 @@ class LearnerEngine:
     def _torso(self, pk, rows: torch.Tensor, out: torch.Tensor, save=False):
         n = rows.numel()
         if n == 0:
+            return
+        if not self.fused_torso:
+            flat = self.master if pk is self.pk else self.target
+            torso_forward_library(self.replay.frames, rows, self.layout, flat, self.cfg.env,
+                                  self.cfg.model, out, self.act1 if save else None,
+                                  self.act2 if save else None)
             return
         k = kernels()
         check(k.r2_torso_fwd(ptr(self.replay.frames), ptr(rows), n, ptr(pk["conv1"]), ptr(pk["b1"]),
@@ -420,7 +437,7 @@ class LearnerEngine:
         return grad * (act > 0)
 
     def _backward_torso(self):
-        if self.cfg.learner.torso_bwd == "fused":
+        if self.cfg.learner.torso_bwd == "fused" and self.fused_torso:
             self._backward_torso_fused()
         else:
             self._backward_torso_library()
@@ -446,27 +463,36 @@ class LearnerEngine:
         L, g = self.layout, self.grad
         N = Ll * B
         cl = torch.channels_last
+        cin, dims = self.tdims
+        c1, c2, c3 = self.cfg.model.conv_channels
+        (h1, w1_), (h2, w2_), (h3, w3_) = dims
+        fh, fw = self.cfg.env.frame_h, self.cfg.env.frame_w
         out3 = self.X_on[Lb * B: T * B]
         g3 = torch.empty_like(self._dX)
         check(k.r2_relu_mask_bf16(ptr(self._dX), ptr(out3), ptr(g3), g3.numel(), s), "relu_mask")
-        g3 = g3.view(N, 32, 7, 7).contiguous(memory_format=cl)
-        a2 = self.act2.view(N, 9, 9, 32).permute(0, 3, 1, 2)
-        a1 = self.act1.view(N, 20, 20, 32).permute(0, 3, 1, 2)
+        g3 = g3.view(N, c3, h3, w3_).contiguous(memory_format=cl)
+        a2 = self.act2.view(N, h2, w2_, c2).permute(0, 3, 1, 2)
+        a1 = self.act1.view(N, h1, w1_, c1).permute(0, 3, 1, 2)
         m = self.master
         w3 = L.view(m, "vis_layers.4.weight").to(torch.bfloat16)
         w2 = L.view(m, "vis_layers.2.weight").to(torch.bfloat16)
         w1 = L.view(m, "vis_layers.0.weight").to(torch.bfloat16)
         cb = torch.ops.aten.convolution_backward
-        d2, dw3, db3 = cb(g3, a2, w3, [32], [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+        d2, dw3, db3 = cb(g3, a2, w3, [c3], [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
                           [True, True, True])
         g2 = self._relu_mask(d2, a2)
-        d1, dw2, db2 = cb(g2, a1, w2, [32], [2, 2], [0, 0], [1, 1], False, [0, 0], 1,
+        d1, dw2, db2 = cb(g2, a1, w2, [c2], [2, 2], [0, 0], [1, 1], False, [0, 0], 1,
                           [True, True, True])
         g1 = self._relu_mask(d1, a1)
-        check(k.r2_frames_to_bf16_nhwc(ptr(self.replay.frames), ptr(self.rows[Lb * B: T * B]), N,
-                                       ptr(self.frames_bf), s), "frames_to_bf16_nhwc")
-        fr = self.frames_bf.view(N, 84, 84, 4).permute(0, 3, 1, 2)
-        _, dw1, db1 = cb(g1, fr, w1, [32], [4, 4], [0, 0], [1, 1], False, [0, 0], 1,
+        rows = self.rows[Lb * B: T * B]
+        if self.fused_torso:
+            check(k.r2_frames_to_bf16_nhwc(ptr(self.replay.frames), ptr(rows), N,
+                                           ptr(self.frames_bf), s), "frames_to_bf16_nhwc")
+        else:
+            fr_nchw = self.replay.frames.index_select(0, rows.long()).view(N, cin, fh, fw)
+            self.frames_bf.view(N, fh, fw, cin).copy_(fr_nchw.permute(0, 2, 3, 1)).mul_(1.0 / 255)
+        fr = self.frames_bf.view(N, fh, fw, cin).permute(0, 3, 1, 2)
+        _, dw1, db1 = cb(g1, fr, w1, [c1], [4, 4], [0, 0], [1, 1], False, [0, 0], 1,
                          [False, True, True])
         L.view(g, "vis_layers.4.weight").copy_(dw3)
         L.view(g, "vis_layers.4.bias").copy_(db3)

@@ -44,7 +44,9 @@ def run_native(cfg: R2D2Config, steps: int = 1000, actor_steps_per_update: int =
     eng = LearnerEngine(cfg, replay, dev, rank=info.rank, world=info.world,
                         process_group=dist.group.WORLD if info.world > 1 else None)
     env = VecSyntheticAtari(E, dev, seed=cfg.seed + 101 * info.rank, episode_len=cfg.env.episode_len,
-                            n_actions=cfg.model.n_actions)
+                            n_actions=cfg.model.n_actions,
+                            n_stacks=cfg.env.channels_per_frame * cfg.env.n_stacks,
+                            shape=(cfg.env.frame_h, cfg.env.frame_w))
     on, tg = engine_weights(eng)
     actor = BatchedActor(cfg, replay, env, on, tg, global_env_offset=info.rank * E,
                          total_envs=info.world * E, seed=cfg.seed + info.rank)

@@ -115,6 +115,16 @@ def test_native_actor_learner_loop_runs():
     assert out["env_steps"] > 3000
 
 
+def test_native_loop_dmlab_rgb_runs():
+    """DMLab-30 geometry (3x72x96 RGB) through actor + learner (library conv torso path)."""
+    from pytorch_r2d2_amd.runner import run_native
+    cfg = get_config("dmlab30", **{"learner.batch_size": 8, "replay.burn_in": 4, "replay.learn": 8,
+                                   "replay.overlap": 6, "actor.envs_per_actor": 16,
+                                   "env.episode_len": 40, "learner.initial_exploration": 800})
+    out = run_native(cfg, steps=10, log_every=5, capacity=16 * 200)
+    assert len(out["losses"]) == 2 and all(np.isfinite(out["losses"]))
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

@@ -62,6 +62,26 @@ def test_engine_loss_and_grads_match_reference(mode):
     assert _rel(rp.priority[rows], out["priority"]) < 5e-2
 
 
+def test_engine_dmlab_rgb_library_torso_matches_reference():
+    """DMLab-30 preset (3x72x96 RGB): the generic library conv torso path of the engine."""
+    cfg, rp, eng, net, tgt = _make("shifted", B=8, preset="dmlab30",
+                                   **{"replay.burn_in": 4, "replay.learn": 8, "replay.overlap": 6})
+    assert not eng.fused_torso
+    eng._forward_loss()
+    eng._backward_core()
+    eng._backward_torso()
+    torch.cuda.synchronize()
+    online = copy.deepcopy(net).to(DEV)
+    target = copy.deepcopy(tgt).to(DEV)
+    batch = batch_from_hbm(rp, eng.starts, eng.probs, cfg, DEV)
+    out = r2d2_loss(online, target, batch, cfg, "shifted")
+    out["loss"].backward()
+    assert abs(eng.loss.item() - out["loss"].item()) / out["loss"].item() < 3e-2
+    got = eng.layout.views(eng.grad)
+    for name, p in online.named_parameters():
+        assert _rel(got[name], p.grad) < 8e-2, name
+
+
 def test_engine_graph_replay_matches_eager():
     cfg, rp, eng, net, tgt = _make("shifted", B=8)
     cfg2, rp2, eng2, _, _ = _make("shifted", B=8)
