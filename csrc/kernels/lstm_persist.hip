@@ -175,19 +175,13 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const PFwdArgs a)
 #pragma unroll
     for (int s = 0; s < KH; ++s) wf[s] = *(const bf16x8*)(brow + s * 16);
   }
-  // ---- pointwise ownership: 2 (row, unit) items per thread; c lives in registers
-  int pb[2], pu[2];
-  bool pv[2];
-  float creg[2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int idx = tid + q * 256;
-    pu[q] = idx & 15;
-    pb[q] = mb * 32 + (idx >> 4);
-    pv[q] = pb[q] < B;
-    const int bc = pv[q] ? pb[q] : B - 1;
-    creg[q] = cd.c0[(size_t)bc * H + j * PL_UNITS + pu[q]];
-  }
+  // ---- pointwise ownership: row prl, units pu0 and pu0+1 (8-byte LDS / global accesses);
+  // c lives in registers
+  const int prl = tid >> 3, pu0 = 2 * (tid & 7);
+  const int pb = mb * 32 + prl;
+  const bool pv = pb < B;
+  const int pbc = pv ? pb : B - 1;
+  float2 creg = *(const float2*)(cd.c0 + (size_t)pbc * H + j * PL_UNITS + pu0);
   const int acol = kq * KH * 16 + (lane >> 5) * 8;
 
   const bool trace = a.dbg && g == 0 && j == 0 && tid == 0;
@@ -196,14 +190,11 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const PFwdArgs a)
   // x-projection rows (plain loads: written by an earlier kernel), one step ahead.  Issue order
   // matters: vmcnt retires in order, so next step's rows are issued AFTER this step's h loads --
   // waiting for h never waits for an HBM x-projection fetch.
-  float xv[2][4], xn[2][4];
-  auto load_x = [&](int t, float (&d)[2][4]) {
+  float2 xv[4], xn[4];
+  auto load_x = [&](int t, float2 (&d)[4]) {
+    const float* xr = cd.xproj + ((size_t)t * B + pbc) * G + j * PL_GCOLS + pu0;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int bc = pv[q] ? pb[q] : B - 1;
-      const float* xr = cd.xproj + ((size_t)t * B + bc) * G + j * PL_GCOLS + pu[q];
-      d[q][0] = xr[0]; d[q][1] = xr[16]; d[q][2] = xr[32]; d[q][3] = xr[48];
-    }
+    for (int gi = 0; gi < 4; ++gi) d[gi] = *(const float2*)(xr + 16 * gi);
   };
   load_x(0, xv);
   for (int t = 0; t < T; ++t) {
@@ -253,19 +244,26 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const PFwdArgs a)
     }
     lds_sync();
     PL_TRACE(2);
-    float hv[2], gsv[2][4];
+    float2 hv, gsv[4];
+    {
+      float2 pre[4];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int rl = (tid + q * 256) >> 4, u = pu[q];
-      const float* p0 = part[0] + rl * PW;
-      const float* p1 = part[1] + rl * PW;
-      gsv[q][0] = sigmoidf_(p0[u] + p1[u] + xv[q][0]);
-      gsv[q][1] = sigmoidf_(p0[16 + u] + p1[16 + u] + xv[q][1]);
-      gsv[q][2] = tanhf_(p0[32 + u] + p1[32 + u] + xv[q][2]);
-      gsv[q][3] = sigmoidf_(p0[48 + u] + p1[48 + u] + xv[q][3]);
-      creg[q] = gsv[q][1] * creg[q] + gsv[q][0] * gsv[q][2];
-      hv[q] = gsv[q][3] * tanhf_(creg[q]);
-      hst[rl * PL_UNITS + u] = (bf16)hv[q];
+      for (int gi = 0; gi < 4; ++gi) {
+        const float2 a0 = *(const float2*)(part[0] + prl * PW + 16 * gi + pu0);
+        const float2 a1 = *(const float2*)(part[1] + prl * PW + 16 * gi + pu0);
+        pre[gi] = make_float2(a0.x + a1.x + xv[gi].x, a0.y + a1.y + xv[gi].y);
+      }
+      gsv[0] = make_float2(sigmoidf_(pre[0].x), sigmoidf_(pre[0].y));
+      gsv[1] = make_float2(sigmoidf_(pre[1].x), sigmoidf_(pre[1].y));
+      gsv[2] = make_float2(tanhf_(pre[2].x), tanhf_(pre[2].y));
+      gsv[3] = make_float2(sigmoidf_(pre[3].x), sigmoidf_(pre[3].y));
+      creg.x = gsv[1].x * creg.x + gsv[0].x * gsv[2].x;
+      creg.y = gsv[1].y * creg.y + gsv[0].y * gsv[2].y;
+      hv = make_float2(gsv[3].x * tanhf_(creg.x), gsv[3].y * tanhf_(creg.y));
+      bf16x2 hb;
+      hb[0] = (bf16)hv.x;
+      hb[1] = (bf16)hv.y;
+      *(bf16x2*)(hst + prl * PL_UNITS + pu0) = hb;
     }
     lds_sync();
     PL_TRACE(3);
@@ -285,23 +283,18 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist_kernel(const PFwdArgs a)
     }
     PL_TRACE(4);
     const bool save = cd.gates != nullptr && t >= cd.save_from;
+    if (pv) {
+      const size_t o = ((size_t)t * B + pb) * H + j * PL_UNITS + pu0;
+      *(float2*)(cd.c_seq + o) = creg;
+      if (cd.h32) *(float2*)(cd.h32 + o) = hv;
+      if (save) {
+        float* gp = cd.gates + ((size_t)(t - cd.save_from) * B + pb) * G + j * PL_GCOLS + pu0;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      if (pv[q]) {
-        const int u = pu[q];
-        const size_t o = ((size_t)t * B + pb[q]) * H + j * PL_UNITS + u;
-        cd.c_seq[o] = creg[q];
-        if (cd.h32) cd.h32[o] = hv[q];
-        if (save) {
-          float* gp = cd.gates + ((size_t)(t - cd.save_from) * B + pb[q]) * G + j * PL_GCOLS + u;
-          gp[0] = gsv[q][0]; gp[16] = gsv[q][1]; gp[32] = gsv[q][2]; gp[48] = gsv[q][3];
-        }
+        for (int gi = 0; gi < 4; ++gi) *(float2*)(gp + 16 * gi) = gsv[gi];
       }
     }
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) xv[q][e] = xn[q][e];
+    for (int gi = 0; gi < 4; ++gi) xv[gi] = xn[gi];
   }
 }
 
@@ -350,16 +343,12 @@ __global__ __launch_bounds__(256) void lstm_bwd_persist_kernel(const PBwdArgs a)
 #pragma unroll
     for (int s = 0; s < 4; ++s) wt[q][s] = *(const bf16x8*)(brow + s * 16);
   }
-  int pb[2], pu[2];
-  bool pv[2];
-  float dcr[2] = {0.f, 0.f};
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int idx = tid + q * 256;
-    pu[q] = idx & 15;
-    pb[q] = mb * 32 + (idx >> 4);
-    pv[q] = pb[q] < B;
-  }
+  // pointwise ownership: row prl, units pu0 and pu0+1 (8-byte accesses); dc carry in registers
+  const int prl = tid >> 3, pu0 = 2 * (tid & 7);
+  const int pb = mb * 32 + prl;
+  const bool pv = pb < B;
+  const int pbc = pv ? pb : B - 1;
+  float2 dcr = make_float2(0.f, 0.f);
   // slab-reduction ownership: (row, float4 group) pairs, two threads per pair split producers
   const int rr = (tid & 127) >> 2, u4 = tid & 3, hh = tid >> 7;
   const int rb = min(mb * 32 + rr, B - 1);
@@ -367,19 +356,16 @@ __global__ __launch_bounds__(256) void lstm_bwd_persist_kernel(const PBwdArgs a)
   // per-step operands (plain loads of earlier kernels' outputs), one step ahead and issued after
   // the step's slab loads: vmcnt retires in order, so waiting for the partials never waits for an
   // HBM operand fetch
-  float dhv[2], gv[2][4], ctv[2], cpv[2], dhn[2], gn[2][4], ctn[2], cpn[2];
-  auto load_ops = [&](int t, float (&dh)[2], float (&gq)[2][4], float (&ct)[2], float (&cp)[2]) {
+  float2 dhv, gv[4], ctv, cpv, dhn, gn[4], ctn, cpn;
+  auto load_ops = [&](int t, float2& dh, float2 (&gq)[4], float2& ct, float2& cp) {
     const int tl = t - t0;
+    const size_t hidx = (size_t)pbc * H + j * PL_UNITS + pu0;
+    dh = a.dh_ext ? *(const float2*)(a.dh_ext + (size_t)tl * B * H + hidx) : make_float2(0.f, 0.f);
+    const float* gp = a.gates + ((size_t)tl * B + pbc) * G + j * PL_GCOLS + pu0;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int bc = pv[q] ? pb[q] : B - 1;
-      const size_t hidx = (size_t)bc * H + j * PL_UNITS + pu[q];
-      dh[q] = a.dh_ext ? a.dh_ext[(size_t)tl * B * H + hidx] : 0.f;
-      const float* gp = a.gates + ((size_t)tl * B + bc) * G + j * PL_GCOLS + pu[q];
-      gq[q][0] = gp[0]; gq[q][1] = gp[16]; gq[q][2] = gp[32]; gq[q][3] = gp[48];
-      ct[q] = a.c_seq[(size_t)t * B * H + hidx];
-      cp[q] = (t == 0) ? a.c0[hidx] : a.c_seq[(size_t)(t - 1) * B * H + hidx];
-    }
+    for (int gi = 0; gi < 4; ++gi) gq[gi] = *(const float2*)(gp + 16 * gi);
+    ct = *(const float2*)(a.c_seq + (size_t)t * B * H + hidx);
+    cp = *(const float2*)((t == 0) ? a.c0 + hidx : a.c_seq + (size_t)(t - 1) * B * H + hidx);
   };
   load_ops(T - 1, dhv, gv, ctv, cpv);
   for (int t = T - 1, k = 0; t >= t0; --t, ++k) {
@@ -405,26 +391,41 @@ __global__ __launch_bounds__(256) void lstm_bwd_persist_kernel(const PBwdArgs a)
     __builtin_amdgcn_sched_barrier(0);
     load_ops(t > t0 ? t - 1 : t, dhn, gn, ctn, cpn);  // unconditional: see the forward kernel
     lds_sync();
-    bf16 dgv[2][4];
+    bf16x2 dgv[4];
+    {
+      float2 dh = dhv;
+      if (k > 0) {
+        const float2 r0 = *(const float2*)(red[0] + prl * PL_UNITS + pu0);
+        const float2 r1 = *(const float2*)(red[1] + prl * PL_UNITS + pu0);
+        dh.x += r0.x + r1.x;
+        dh.y += r0.y + r1.y;
+      }
+      float dgf[4][2];
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int rl = (tid + q * 256) >> 4, u = pu[q];
-      float dh = dhv[q];
-      if (k > 0) dh += red[0][rl * PL_UNITS + u] + red[1][rl * PL_UNITS + u];
-      const float gi = gv[q][0], gf = gv[q][1], gg = gv[q][2], go = gv[q][3];
-      const float tc = tanhf_(ctv[q]);
-      const float dc = dcr[q] + dh * go * (1.f - tc * tc);
-      const float d_o = dh * tc;
-      const float d_i = dc * gg, d_g = dc * gi, d_f = dc * cpv[q];
-      dcr[q] = dc * gf;
-      dgv[q][0] = (bf16)(d_i * gi * (1.f - gi));
-      dgv[q][1] = (bf16)(d_f * gf * (1.f - gf));
-      dgv[q][2] = (bf16)(d_g * (1.f - gg * gg));
-      dgv[q][3] = (bf16)(d_o * go * (1.f - go));
-      bf16* lrow = dg + rl * DW;
-      const bool ok = pv[q];
+      for (int e = 0; e < 2; ++e) {
+        const float gi = e ? gv[0].y : gv[0].x, gf = e ? gv[1].y : gv[1].x;
+        const float gg = e ? gv[2].y : gv[2].x, go = e ? gv[3].y : gv[3].x;
+        const float dhe = e ? dh.y : dh.x, cte = e ? ctv.y : ctv.x, cpe = e ? cpv.y : cpv.x;
+        const float tc = tanhf_(cte);
+        const float dc = (e ? dcr.y : dcr.x) + dhe * go * (1.f - tc * tc);
+        const float d_o = dhe * tc;
+        const float d_i = dc * gg, d_g = dc * gi, d_f = dc * cpe;
+        if (e) dcr.y = dc * gf; else dcr.x = dc * gf;
+        dgf[0][e] = d_i * gi * (1.f - gi);
+        dgf[1][e] = d_f * gf * (1.f - gf);
+        dgf[2][e] = d_g * (1.f - gg * gg);
+        dgf[3][e] = d_o * go * (1.f - go);
+      }
+      bf16* lrow = dg + prl * DW + pu0;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) lrow[16 * e + u] = ok ? dgv[q][e] : (bf16)0.f;
+      for (int gi = 0; gi < 4; ++gi) {
+        dgv[gi][0] = (bf16)dgf[gi][0];
+        dgv[gi][1] = (bf16)dgf[gi][1];
+        bf16x2 z;
+        z[0] = pv ? dgv[gi][0] : (bf16)0.f;
+        z[1] = pv ? dgv[gi][1] : (bf16)0.f;
+        *(bf16x2*)(lrow + 16 * gi) = z;
+      }
     }
     if (t > t0) {
       lds_sync();
@@ -466,19 +467,14 @@ __global__ __launch_bounds__(256) void lstm_bwd_persist_kernel(const PBwdArgs a)
       if (tid == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // dgates output for the weight-gradient GEMMs, off the recurrence's critical path
+    if (pv) {
+      bf16* dgo = a.dgates + ((size_t)tl * B + pb) * G + j * PL_GCOLS + pu0;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      if (pv[q]) {
-        bf16* dgo = a.dgates + ((size_t)tl * B + pb[q]) * G + j * PL_GCOLS + pu[q];
-        dgo[0] = dgv[q][0]; dgo[16] = dgv[q][1]; dgo[32] = dgv[q][2]; dgo[48] = dgv[q][3];
-      }
+      for (int gi = 0; gi < 4; ++gi) *(bf16x2*)(dgo + 16 * gi) = dgv[gi];
     }
+    dhv = dhn; ctv = ctn; cpv = cpn;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      dhv[q] = dhn[q]; ctv[q] = ctn[q]; cpv[q] = cpn[q];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) gv[q][e] = gn[q][e];
-    }
+    for (int gi = 0; gi < 4; ++gi) gv[gi] = gn[gi];
   }
 }
 

@@ -36,6 +36,7 @@ def build_parser():
     p.add_argument("--checkpoint-dir", default=None)
     p.add_argument("--capacity", type=int, default=None)
     p.add_argument("--set", nargs="*", default=[], help="dotted config overrides key=value")
+    p.add_argument("--resume", default=None, help="full-state checkpoint to continue from (native)")
     return p
 
 
@@ -50,7 +51,8 @@ def run(argv=None):
     if args.mode == "native":
         from pytorch_r2d2_amd.runner import run_native
         out = run_native(cfg, steps=args.steps or 1000, metrics_path=args.metrics,
-                         checkpoint_dir=args.checkpoint_dir, capacity=args.capacity)
+                         checkpoint_dir=args.checkpoint_dir, capacity=args.capacity,
+                         resume=args.resume)
     elif args.mode == "inproc":
         from pytorch_r2d2_amd.runner import run_inproc
         out = run_inproc(cfg, steps=args.steps or 1000, n_actors=args.n_actors,

@@ -240,6 +240,29 @@ class LearnerEngine:
         self.layout.load_state_dict(self.target, target_sd if target_sd is not None else sd)
         self._pack(always=True)
 
+    # ------------------------------------------------------------------ full state (resume)
+    def full_state_extra(self) -> Dict[str, torch.Tensor]:
+        """Optimizer moments + the device step counter (drives sampling RNG, Adam bias correction,
+        target-sync cadence); with the weights this resumes a run exactly."""
+        return {"opt_a": self.opt_a.detach().cpu().clone(), "opt_b": self.opt_b.detach().cpu().clone(),
+                "replay_step": self.replay.step.detach().cpu().clone(),
+                "steps_done": torch.tensor(self.steps_done)}
+
+    def load_full_state(self, obj) -> None:
+        """Restore from ``utils.checkpoint.load_full_checkpoint`` output (engine or Learner format)."""
+        self.layout.load_state_dict(self.master, obj["online"])
+        self.layout.load_state_dict(self.target, obj["target"])
+        ex = obj.get("extra") or {}
+        opt = obj.get("optimizer") or {}
+        for name, buf in (("opt_a", self.opt_a), ("opt_b", self.opt_b)):
+            v = ex.get(name, opt.get(name) if isinstance(opt, dict) else None)
+            if v is not None:
+                buf.copy_(v.to(buf.device))
+        if "replay_step" in ex:
+            self.replay.step.copy_(ex["replay_step"].to(self.replay.step.device))
+        self.steps_done = int(ex["steps_done"]) if "steps_done" in ex else int(obj.get("step", 0))
+        self._pack(always=True)
+
     def sync_target(self):
         self.target.copy_(self.master)
         self._pack(always=True)

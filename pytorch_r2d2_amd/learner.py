@@ -224,9 +224,28 @@ class Learner:
 
     def save_checkpoint(self, path: str):
         opt = None if self.backend == "hip" else self.optim.state_dict()
-        extra = {}
+        extra = {"version": torch.tensor(self.version)}
         if self.backend == "hip":
-            extra = {"opt_a": self.engine.opt_a.cpu(), "opt_b": self.engine.opt_b.cpu(),
-                     "replay_step": self.engine.replay.step.cpu()}
+            extra.update(self.engine.full_state_extra())
         save_full_checkpoint(path, self.state_dict(), self.target_state_dict(), opt, self.n_epochs,
                              self.cfg, extra)
+
+    def resume(self, path: str) -> int:
+        """Continue from a full-state checkpoint (weights, target, optimizer state, counters, RNG;
+        SURVEY §5.4).  The replay itself is not part of the checkpoint: actors refill it.
+        Returns the restored learner step."""
+        from .utils.checkpoint import load_full_checkpoint, restore_rng
+        obj = load_full_checkpoint(path)
+        restore_rng(obj)
+        if self.backend == "hip":
+            self.engine.load_full_state(obj)
+        else:
+            self.net.load_state_dict(obj["online"])
+            self.target_net.load_state_dict(obj["target"])
+            if obj.get("optimizer"):
+                self.optim.load_state_dict(obj["optimizer"])
+        self.n_epochs = int(obj["step"])
+        if "version" in (obj.get("extra") or {}):
+            self.version = int(obj["extra"]["version"])
+        self.save_model()
+        return self.n_epochs

@@ -26,7 +26,7 @@ from .config import R2D2Config
 def run_native(cfg: R2D2Config, steps: int = 1000, actor_steps_per_update: int = 1,
                warmup_rows: Optional[int] = None, metrics_path: Optional[str] = None,
                checkpoint_dir: Optional[str] = None, log_every: int = 100, use_graph: bool = True,
-               capacity: Optional[int] = None) -> Dict:
+               capacity: Optional[int] = None, resume: Optional[str] = None) -> Dict:
     from .actor_batched import BatchedActor, engine_weights
     from .engine.learner_engine import LearnerEngine
     from .engine.replay_hbm import HBMReplay
@@ -47,6 +47,13 @@ def run_native(cfg: R2D2Config, steps: int = 1000, actor_steps_per_update: int =
                             n_actions=cfg.model.n_actions,
                             n_stacks=cfg.env.channels_per_frame * cfg.env.n_stacks,
                             shape=(cfg.env.frame_h, cfg.env.frame_w))
+    start = 0
+    if resume:
+        from .utils.checkpoint import load_full_checkpoint, restore_rng
+        obj = load_full_checkpoint(resume)
+        restore_rng(obj)
+        eng.load_full_state(obj)
+        start = int(obj["step"])
     on, tg = engine_weights(eng)
     actor = BatchedActor(cfg, replay, env, on, tg, global_env_offset=info.rank * E,
                          total_envs=info.world * E, seed=cfg.seed + info.rank)
@@ -79,16 +86,15 @@ def run_native(cfg: R2D2Config, steps: int = 1000, actor_steps_per_update: int =
                 mlog.log("native", **rec)
             if info.is_main:
                 print("[native]", rec, flush=True)
-        if checkpoint_dir and info.is_main and (it + 1) % cfg.learner.checkpoint_interval == 0:
-            save_reference_checkpoint(eng.state_dict(), it + 1, checkpoint_dir)
+        if checkpoint_dir and info.is_main and (start + it + 1) % cfg.learner.checkpoint_interval == 0:
+            save_reference_checkpoint(eng.state_dict(), start + it + 1, checkpoint_dir)
     torch.cuda.synchronize(dev)
     eng.check_errors()
     out = {"steps": steps, "warmup_s": t_warm, "train_s": time.perf_counter() - t1,
            "losses": losses, "returns": list(actor.finished_returns), "env_steps": actor.env_steps}
     if checkpoint_dir and info.is_main:
         save_full_checkpoint(os.path.join(checkpoint_dir, "full_last.pt"), eng.state_dict(),
-                             eng.target_state_dict(), {"opt_a": eng.opt_a.cpu(), "opt_b": eng.opt_b.cpu()},
-                             steps, cfg)
+                             eng.target_state_dict(), None, start + steps, cfg, eng.full_state_extra())
     return out
 
 

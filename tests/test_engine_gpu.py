@@ -97,6 +97,29 @@ def test_engine_graph_replay_matches_eager():
     assert _rel(rp2.tree, rp.tree) < 1e-5
 
 
+def test_engine_resume_from_full_checkpoint(tmp_path):
+    from pytorch_r2d2_amd.utils.checkpoint import load_full_checkpoint, save_full_checkpoint
+    cfg, rp, eng, net, tgt = _make("shifted", B=8)
+    cfg2, rp2, eng2, _, _ = _make("shifted", B=8)
+    for _ in range(3):
+        eng.step_eager()
+    path = str(tmp_path / "full.pt")
+    save_full_checkpoint(path, eng.state_dict(), eng.target_state_dict(), None, 3, cfg,
+                         eng.full_state_extra())
+    for k, v in vars(rp).items():          # the replay is not part of the checkpoint
+        if torch.is_tensor(v):
+            getattr(rp2, k).copy_(v)
+    for _ in range(2):
+        eng.step_eager()
+    eng2.load_full_state(load_full_checkpoint(path))
+    for _ in range(2):
+        eng2.step_eager()
+    torch.cuda.synchronize()
+    assert eng2.steps_done == 5
+    assert _rel(eng2.master, eng.master) < 1e-6
+    assert _rel(eng2.opt_a, eng.opt_a) < 1e-6
+
+
 def test_engine_training_reduces_loss_on_fixed_batch():
     cfg, rp, eng, net, tgt = _make("shifted", B=16, **{"learner.lr": 3e-4})
     eng.step_eager()

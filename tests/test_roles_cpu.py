@@ -105,6 +105,33 @@ def test_learner_torch_backend_trains_and_publishes(tmp_path):
     assert a.load_model()
 
 
+def test_learner_resume_continues_identically(tmp_path):
+    """Full-state checkpoint -> resume reproduces the uninterrupted run bit for bit (weights,
+    target, centered-RMSprop moments, step counter and RNG streams restored; replay refilled)."""
+    import copy
+    cfg = _cfg(**{"learner.save_dir": str(tmp_path / "save"), "learner.checkpoint_interval": 10 ** 6})
+    L1 = Learner(1, {}, device="cpu", cfg=cfg, memory_path=str(tmp_path / "mem"), replay_capacity=500)
+    a = Actor(0, 1, {}, "cpu", cfg=cfg, env=ScriptEnv(12), memory_path=str(tmp_path / "mem"))
+    a.memory_save_interval = 2
+    for _ in range(60):
+        a.step()
+    assert L1.ingest() > 0
+    L1.run(max_steps=3)
+    ck = str(tmp_path / "full.pt")
+    L1.save_checkpoint(ck)
+    mem = copy.deepcopy(L1.replay_memory)
+    L1.run(max_steps=5)            # run() takes an absolute step target
+    L2 = Learner(1, {}, device="cpu", cfg=cfg, memory_path=str(tmp_path / "mem2"), replay_capacity=500)
+    L2.replay_memory = mem
+    assert L2.resume(ck) == 3
+    L2.run(max_steps=5)
+    assert L2.n_epochs == L1.n_epochs == 5
+    for (k, v1), v2 in zip(L1.net.state_dict().items(), L2.net.state_dict().values()):
+        assert torch.equal(v1, v2), k
+    for g1, g2 in zip(L1.optim.state_dict()["state"].values(), L2.optim.state_dict()["state"].values()):
+        assert torch.equal(g1["square_avg"], g2["square_avg"])
+
+
 def test_full_checkpoint_roundtrip(tmp_path):
     q = QNet()
     opt = torch.optim.RMSprop(q.parameters(), lr=1e-3, centered=True)
