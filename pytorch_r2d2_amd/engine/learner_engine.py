@@ -88,10 +88,9 @@ class LearnerEngine:
         self.replay = replay
         self.rank, self.world, self.pg = rank, world, process_group
         m, e, rc, lc = cfg.model, cfg.env, cfg.replay, cfg.learner
-        if m.torso != "atari" or tuple(m.conv_channels) != (32, 32, 32) or \
-                (e.frame_h, e.frame_w, e.channels_per_frame * e.n_stacks) != (84, 84, 4):
-            raise NotImplementedError("HIP engine torso kernel is specialised for the Atari "
-                                      "84x84x4 / 32-32-32 torso; use the torch learner otherwise")
+        if m.torso != "atari":
+            raise NotImplementedError("the HIP engine runs the conv torso (Atari / DMLab frames); "
+                                      "use the torch learner for vector observations")
         if m.hidden % UNITS != 0 or m.hidden not in (64, 128, 256, 512):
             raise NotImplementedError("LSTM kernels support hidden in {64,128,256,512}")
         self.layout = L = ParamLayout(m, e)
@@ -511,12 +510,14 @@ class LearnerEngine:
         if self.fused_torso:
             check(k.r2_frames_to_bf16_nhwc(ptr(self.replay.frames), ptr(rows), N,
                                            ptr(self.frames_bf), s), "frames_to_bf16_nhwc")
-        else:
+        else:   # exact 0..255 values; the 1/255 is applied to dW1 in fp32 below
             fr_nchw = self.replay.frames.index_select(0, rows.long()).view(N, cin, fh, fw)
-            self.frames_bf.view(N, fh, fw, cin).copy_(fr_nchw.permute(0, 2, 3, 1)).mul_(1.0 / 255)
+            self.frames_bf.view(N, fh, fw, cin).copy_(fr_nchw.permute(0, 2, 3, 1))
         fr = self.frames_bf.view(N, fh, fw, cin).permute(0, 3, 1, 2)
         _, dw1, db1 = cb(g1, fr, w1, [c1], [4, 4], [0, 0], [1, 1], False, [0, 0], 1,
                          [False, True, True])
+        if not self.fused_torso:
+            dw1 = dw1.float() * (1.0 / 255)
         L.view(g, "vis_layers.4.weight").copy_(dw3)
         L.view(g, "vis_layers.4.bias").copy_(db3)
         L.view(g, "vis_layers.2.weight").copy_(dw2)

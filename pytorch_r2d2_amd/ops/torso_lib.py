@@ -28,11 +28,14 @@ def torso_forward_library(frames: torch.Tensor, rows: Optional[torch.Tensor], la
     fh, fw = env.frame_h, env.frame_w
     x = frames if rows is None else frames.index_select(0, rows.long())
     n = x.shape[0]
-    x = x[:, : cin * fh * fw].view(n, cin, fh, fw).to(torch.bfloat16).mul_(1.0 / 255)
+    # uint8 0..255 is exact in bf16; the 1/255 of the reference's normalisation is folded into
+    # the fp32 conv1 weights before their bf16 rounding (as the fused kernel applies it in fp32)
+    x = x[:, : cin * fh * fw].view(n, cin, fh, fw).to(torch.bfloat16)
     x = x.contiguous(memory_format=torch.channels_last)
     w = {k: layout.view(flat, k).to(torch.bfloat16) for k in
-         ("vis_layers.0.weight", "vis_layers.0.bias", "vis_layers.2.weight", "vis_layers.2.bias",
+         ("vis_layers.0.bias", "vis_layers.2.weight", "vis_layers.2.bias",
           "vis_layers.4.weight", "vis_layers.4.bias")}
+    w["vis_layers.0.weight"] = (layout.view(flat, "vis_layers.0.weight") * (1.0 / 255)).to(torch.bfloat16)
     y1 = F.conv2d(x, w["vis_layers.0.weight"], w["vis_layers.0.bias"], stride=4).relu_()
     y2 = F.conv2d(y1, w["vis_layers.2.weight"], w["vis_layers.2.bias"], stride=2).relu_()
     y3 = F.conv2d(y2, w["vis_layers.4.weight"], w["vis_layers.4.bias"], stride=1).relu_()
