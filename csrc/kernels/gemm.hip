@@ -178,6 +178,139 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs args) {
   }
 }
 
+// ============================================================================================
+// v2: LDS-DMA staged (global_load_lds, 16 B/lane), used when every problem has K % 64 == 0.
+// 128x128x64 tiles, 2 LDS stages x (A 16 KB + B 16 KB), two raw barriers per K step with the
+// next-but-one tile's DMA in flight across them (counted vmcnt, never __syncthreads).
+// The DMA writes LDS linearly (wave base + 16 B x lane), so the bank-conflict swizzles are applied
+// to the per-lane GLOBAL source addresses and undone on the fragment reads:
+//   k-major tile  [128 rows][8 x 16-B chunks]: chunk c of row r stored at c ^ ((r >> 1) & 7)
+//   mn-major tile [64 k-rows][16 chunks]:      chunk c of k-row k stored at c ^ (4 (k & 3))
+namespace g2 {
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+constexpr int TILE_B = 16384;        // bytes per operand tile (both layouts)
+constexpr int GPW = 4;               // 1-KB DMA instructions per wave per operand tile
+}  // namespace g2
+
+template <bool KMAJ>
+__device__ __forceinline__ void g2_stage(const bf16* X, int ld, int i0, int imax, int k0,
+                                         uint8_t* lds_tile, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < g2::GPW; ++j) {
+    const int blk = wave * g2::GPW + j;          // 1-KB block of the tile
+    const bf16* src;
+    if (KMAJ) {
+      const int row = blk * 8 + (lane >> 3), cp = lane & 7;
+      const int c = cp ^ ((row >> 1) & 7);
+      src = X + (size_t)min(i0 + row, imax - 1) * ld + k0 + c * 8;
+    } else {
+      const int kr = blk * 4 + (lane >> 4), cp = lane & 15;
+      const int c = cp ^ (4 * (kr & 3));
+      const int col = i0 + c * 8;
+      src = X + (size_t)(k0 + kr) * ld + (col < imax ? col : imax - 8);
+    }
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(lds_tile + blk * 1024),
+                                     16, 0, 0);
+  }
+}
+
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8 g2_frag(const uint8_t* L, int i0, int ks, int lane) {
+  const int l32 = lane & 31, h = lane >> 5;
+  if (KMAJ) {
+    const int r = i0 + l32, c = 2 * ks + h;
+    return *(const bf16x8*)(L + r * 128 + ((c ^ ((r >> 1) & 7)) * 16));
+  }
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int c = (i0 >> 3) + 2 * (g & 1) + (p >> 1);
+  const int kr = 16 * ks + 8 * h + q;                      // + 4 for the second read
+  const uint8_t* b0 = L + kr * 256 + ((c ^ (4 * q)) * 16) + 8 * (p & 1);
+  return gm_tr8((const bf16*)b0, (const bf16*)(b0 + 4 * 256));
+}
+
+template <bool AK, bool BK_>
+__global__ __launch_bounds__(256) void gemm2_kernel(const GemmArgs args) {
+  using namespace g2;
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[2][2][TILE_B];   // [stage][A/B]
+  int pi = 0;
+#pragma unroll
+  for (int i = 1; i < gm::MAXP; ++i)
+    if (i < args.nprob && (int)blockIdx.x >= args.p[i].tile_base) pi = i;
+  const GemmProb& P = args.p[pi];
+  if (P.a_kmajor != (int)AK || P.b_kmajor != (int)BK_) return;
+  const int t = blockIdx.x - P.tile_base;
+  const int tm = t / P.tiles_n, tn = t % P.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  if (m0 >= P.M) return;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int nk = P.K / BK;
+
+  f32x16 acc[2][2] = {};
+  g2_stage<AK>(P.A, P.lda, m0, P.M, 0, lds[0][0], wave, lane);
+  g2_stage<BK_>(P.B, P.ldb, n0, P.N, 0, lds[0][1], wave, lane);
+  if (nk > 1) {
+    g2_stage<AK>(P.A, P.lda, m0, P.M, BK, lds[1][0], wave, lane);
+    g2_stage<BK_>(P.B, P.ldb, n0, P.N, BK, lds[1][1], wave, lane);
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    const int st = kt & 1;
+    // tile kt has landed once at most the next tile's 2*GPW DMA ops remain outstanding
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const uint8_t* la = lds[st][0];
+    const uint8_t* lb = lds[st][1];
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        fa[i] = g2_frag<AK>(la, wm + 32 * i, ks, lane);
+        fb[i] = g2_frag<BK_>(lb, wn + 32 * i, ks, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(fa[i], fb[j], acc[i][j]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();          // every wave is done reading stage st
+    if (kt + 2 < nk) {
+      g2_stage<AK>(P.A, P.lda, m0, P.M, (kt + 2) * BK, lds[st][0], wave, lane);
+      g2_stage<BK_>(P.B, P.ldb, n0, P.N, (kt + 2) * BK, lds[st][1], wave, lane);
+    }
+  }
+
+  const int l32 = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = n0 + wn + 32 * j + l32;
+    if (col >= P.N) continue;
+    const float bv = P.bias ? P.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row >= P.M) continue;
+        const int orow = P.crow ? P.crow[row] : row;
+        const float v = P.alpha * acc[i][j][r] + bv;
+        const size_t o = (size_t)orow * P.ldc + col;
+        if (P.c_f32) {
+          float* c = (float*)P.C + o;
+          *c = P.accumulate ? *c + v : v;
+        } else {
+          bf16* c = (bf16*)P.C + o;
+          *c = (bf16)(P.accumulate ? (float)*c + v : v);
+        }
+      }
+  }
+}
+
+static int g_gemm_version = 2;   // 1 = force the register-staged kernel (tests / A-B)
+extern "C" int r2_gemm_set_version(int v) { g_gemm_version = v; return 0; }
+
 // descs: nprob x 16 int64 {A, B, C, bias, crow, M, N, K, lda, ldb, ldc, a_kmajor, b_kmajor,
 // c_f32, accumulate, alpha_bits}.  All problems of one call must share (a_kmajor, b_kmajor).
 extern "C" int r2_gemm(const int64_t* descs, int nprob, void* stream) {
@@ -210,6 +343,16 @@ extern "C" int r2_gemm(const int64_t* descs, int nprob, void* stream) {
   }
   for (int i = nprob; i < gm::MAXP; ++i) a.p[i] = a.p[0], a.p[i].tile_base = 1 << 30;
   hipStream_t s = (hipStream_t)stream;
+  bool v2 = g_gemm_version >= 2;
+  for (int i = 0; i < nprob; ++i) v2 = v2 && a.p[i].K % g2::BK == 0;
+  if (v2) {
+    if (ak && bk) hipLaunchKernelGGL((gemm2_kernel<true, true>), dim3(tiles), dim3(g2::NT), 0, s, a);
+    else if (ak) hipLaunchKernelGGL((gemm2_kernel<true, false>), dim3(tiles), dim3(g2::NT), 0, s, a);
+    else if (bk) hipLaunchKernelGGL((gemm2_kernel<false, true>), dim3(tiles), dim3(g2::NT), 0, s, a);
+    else hipLaunchKernelGGL((gemm2_kernel<false, false>), dim3(tiles), dim3(g2::NT), 0, s, a);
+    R2_CHECK_LAUNCH();
+    return 0;
+  }
   if (ak && bk) hipLaunchKernelGGL((gemm_kernel<true, true>), dim3(tiles), dim3(gm::NT), 0, s, a);
   else if (ak) hipLaunchKernelGGL((gemm_kernel<true, false>), dim3(tiles), dim3(gm::NT), 0, s, a);
   else if (bk) hipLaunchKernelGGL((gemm_kernel<false, true>), dim3(tiles), dim3(gm::NT), 0, s, a);

@@ -157,4 +157,57 @@ extern "C" int r2_copy_if_due(float* dst, const float* src, int64_t n, const int
   return 0;
 }
 
+// One launch for everything between the optimizer and the next step's kernels (replaces
+// copy_if_due + 2 x {bf16 pack, fp32 gather, LSTM bias add}):
+//   * online: bf16 kernel-layout pack, fp32 small-vector gather, packed b_ih + b_hh
+//   * target, only when (step + 1) % interval == 0 (learner.py:107-108 target sync): target = master,
+//     and its packs are the online packs of the same master values (no read of the copy)
+__global__ void pack_step_kernel(const float* __restrict__ master, float* __restrict__ target,
+                                 int64_t n_master, const int* __restrict__ bf_idx,
+                                 bf16* __restrict__ bf, bf16* __restrict__ bf_t, int64_t n_bf,
+                                 const int* __restrict__ f_idx, float* __restrict__ f32,
+                                 float* __restrict__ f32_t, int64_t n_f, int64_t o_bih, int64_t o_bhh,
+                                 float* __restrict__ lstm_b, float* __restrict__ lstm_b_t, int64_t G,
+                                 const int64_t* __restrict__ step, int64_t interval) {
+  const bool due = interval <= 1 || ((*step) + 1) % interval == 0;
+  const int64_t total = (due ? n_master : 0) + n_bf + n_f + G;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += stride) {
+    int64_t j = i;
+    if (due) {
+      if (j < n_master) { target[j] = master[j]; continue; }
+      j -= n_master;
+    }
+    if (j < n_bf) {
+      const bf16 v = (bf16)master[bf_idx[j]];
+      bf[j] = v;
+      if (due) bf_t[j] = v;
+      continue;
+    }
+    j -= n_bf;
+    if (j < n_f) {
+      const float v = master[f_idx[j]];
+      f32[j] = v;
+      if (due) f32_t[j] = v;
+      continue;
+    }
+    j -= n_f;
+    const float b = master[f_idx[o_bih + j]] + master[f_idx[o_bhh + j]];
+    lstm_b[j] = b;
+    if (due) lstm_b_t[j] = b;
+  }
+}
+
+extern "C" int r2_pack_step(const float* master, float* target, int64_t n_master, const int* bf_idx,
+                            bf16* bf, bf16* bf_t, int64_t n_bf, const int* f_idx, float* f32,
+                            float* f32_t, int64_t n_f, int64_t o_bih, int64_t o_bhh, float* lstm_b,
+                            float* lstm_b_t, int64_t G, const int64_t* step, int64_t interval,
+                            void* stream) {
+  hipLaunchKernelGGL(pack_step_kernel, dim3(1024), dim3(256), 0, (hipStream_t)stream, master, target,
+                     n_master, bf_idx, bf, bf_t, n_bf, f_idx, f32, f32_t, n_f, o_bih, o_bhh, lstm_b,
+                     lstm_b_t, G, step, interval);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int r2_abi_version() { return 1; }

@@ -7,9 +7,12 @@
 //   y      = R_t + gamma^n * Q_target(s_{t+n})[a*] * (1 - d_t)  (learner.py:92-94)
 //   loss   = mean(0.5 (q - y)^2)                                (learner.py:98)
 //   p_row  = (|q - y| + 1e-6)^0.6  -> replay priority[index]    (learner.py:102-103)
-// Here it is ONE single-workgroup kernel that also gathers a_t / R_t / d_t from the HBM replay
-// by ring row, applies optional R2D2 value rescaling h / h^-1 and IS weights, writes dL/dQ
-// (the only gradient the head backward needs) and scatters the new row priorities.
+// Here it is ONE kernel (one thread per transition, ceil(Tl*B/256) workgroups) that also gathers
+// a_t / R_t / d_t from the HBM replay by ring row, applies optional R2D2 value rescaling h / h^-1
+// and IS weights, writes dL/dQ (the only gradient the head backward needs) and scatters the new
+// row priorities.  The loss is reduced deterministically: every workgroup publishes its partial
+// (sc1 store, drained), takes a ticket with an agent-scope atomic, and the last arriver sums the
+// partials in workgroup order with sc1 loads (MI355X_MICROARCH.md hand-off table, row 1).
 #include "../common.h"
 
 __device__ __forceinline__ float vr_h(float x, float eps) {
@@ -40,44 +43,39 @@ struct TdArgs {
   float* priority;      // (cap) row priorities, scatter out (may be null)
   float* is_w;          // (B) normalised IS weights out, may be null
   const int* n_valid;   // number of sampleable sequences (device), for IS weights
+  float* part;          // (gridDim.x) loss partials
+  unsigned* ticket;     // arrival counter, 0 between launches (reset by the last arriver)
   int Tl, B, A, burn_in, cap_e;
   float gamma_n, vr_eps, alpha, prio_eps, beta;
   int value_rescale;
 };
 
-__global__ __launch_bounds__(1024) void td_kernel(const TdArgs a) {
-  __shared__ float red[32];
+__global__ __launch_bounds__(256) void td_kernel(const TdArgs a) {
+  __shared__ float red[8];
   __shared__ float wsh[256];
+  __shared__ int last;
   const int tid = threadIdx.x;
-  // ---- IS weights w_b = (N * P_b)^-beta / max_b
-  if (tid < a.B) {
-    float w = 1.f;
-    if (a.probs != nullptr && a.beta > 0.f) {
-      const float nv = a.n_valid ? (float)max(*a.n_valid, 1) : 1.f;
-      w = powf(fmaxf(nv * a.probs[tid], 1e-30f), -a.beta);
-    }
-    wsh[tid] = w;
+  // ---- IS weights w_b = (N * P_b)^-beta / max_b  (B <= 256; recomputed per workgroup)
+  float w = 1.f;
+  if (tid < a.B && a.probs != nullptr && a.beta > 0.f) {
+    const float nv = a.n_valid ? (float)max(*a.n_valid, 1) : 1.f;
+    w = powf(fmaxf(nv * a.probs[tid], 1e-30f), -a.beta);
   }
+  float m = wave_max(tid < a.B ? w : 0.f);
+  if ((tid & 63) == 0) red[tid >> 6] = m;
   __syncthreads();
-  if (tid < 64) {
-    float m = 0.f;
-    for (int b = tid; b < a.B; b += 64) m = fmaxf(m, wsh[b]);
-    m = wave_max(m);
-    if (tid == 0) red[0] = m;
-  }
-  __syncthreads();
-  const float wmax = red[0];
-  __syncthreads();
+  const float wmax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   if (tid < a.B) {
-    wsh[tid] = wsh[tid] / wmax;
-    if (a.is_w) a.is_w[tid] = wsh[tid];
+    wsh[tid] = w / wmax;
+    if (a.is_w && blockIdx.x == 0) a.is_w[tid] = w / wmax;
   }
   __syncthreads();
 
   const int n = a.Tl * a.B;
   const float inv_n = 1.f / (float)n;
   float lsum = 0.f;
-  for (int i = tid; i < n; i += blockDim.x) {
+  const int i = blockIdx.x * 256 + tid;
+  if (i < n) {
     const int b = i % a.B, tl = i / a.B;
     const int row = ring_row(a.starts[b], a.burn_in + tl, a.cap_e);
     const int act = (int)a.action[row];
@@ -94,21 +92,32 @@ __global__ __launch_bounds__(1024) void td_kernel(const TdArgs a) {
     float y = a.reward[row] + (a.done[row] ? 0.f : a.gamma_n * boot);
     if (a.value_rescale) y = vr_h(y, a.vr_eps);
     const float delta = qs[act] - y;
-    const float w = wsh[b];
-    lsum += w * 0.5f * delta * delta;
+    const float wb = wsh[b];
+    lsum = wb * 0.5f * delta * delta;
     float* d = a.dq + (size_t)i * a.A;
-    for (int k = 0; k < a.A; ++k) d[k] = (k == act) ? w * delta * inv_n : 0.f;
+    for (int k = 0; k < a.A; ++k) d[k] = (k == act) ? wb * delta * inv_n : 0.f;
     const float ad = fabsf(delta);
     if (a.td_abs) a.td_abs[i] = ad;
     if (a.priority) a.priority[row] = powf(ad + a.prio_eps, a.alpha);
   }
   lsum = wave_sum(lsum);
+  __syncthreads();
   if ((tid & 63) == 0) red[tid >> 6] = lsum;
   __syncthreads();
-  if (tid < 64) {
-    float v = tid < (int)(blockDim.x >> 6) ? red[tid] : 0.f;
-    v = wave_sum(v);
-    if (tid == 0) *a.loss = v * inv_n;
+  if (tid == 0) {
+    const float v = red[0] + red[1] + red[2] + red[3];
+    __hip_atomic_store(a.part + blockIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (last && tid == 0) {
+    float tot = 0.f;
+    for (unsigned g = 0; g < gridDim.x; ++g)
+      tot += __hip_atomic_load(a.part + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *a.loss = tot * inv_n;
+    __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -118,12 +127,14 @@ extern "C" int r2_td_loss(const float* q_sa, const float* q_arg, const float* q_
                           float* td_abs, float* priority, float* is_w, const int* n_valid,
                           int Tl, int B, int A, int burn_in, int cap_e, float gamma_n,
                           int value_rescale, float vr_eps, float alpha, float prio_eps,
-                          float beta, void* stream) {
+                          float beta, float* part, unsigned* ticket, void* stream) {
   if (B > 256) return -1;
+  const int grid = (Tl * B + 255) / 256;
+  if (grid > 4096) return -2;   // part[] holds one float per workgroup (engine: 4096)
   TdArgs a{q_sa, q_arg, q_tgt, starts, probs, action, reward, done, dq, loss, td_abs, priority,
-           is_w, n_valid, Tl, B, A, burn_in, cap_e, gamma_n, vr_eps, alpha, prio_eps, beta,
-           value_rescale};
-  hipLaunchKernelGGL(td_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, a);
+           is_w, n_valid, part, ticket, Tl, B, A, burn_in, cap_e, gamma_n, vr_eps, alpha, prio_eps,
+           beta, value_rescale};
+  hipLaunchKernelGGL(td_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
   R2_CHECK_LAUNCH();
   return 0;
 }

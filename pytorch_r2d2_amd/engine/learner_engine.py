@@ -190,6 +190,8 @@ class LearnerEngine:
         self.err = z(1, dt=torch.int32)
         self.dgates = z(Ll * B, G, dt=bf16)
         self.gamma_n = float(lc.gamma ** n)
+        self.td_part = z(4096)                          # TD loss partials, one per workgroup
+        self.td_ticket = z(1, dt=torch.int32)           # reset by the kernel's last workgroup
         # fused torso backward: per-workgroup gradient slabs + destination map (allocated here,
         # never lazily: the step must be capturable without warm-up)
         if self.fused_torso:
@@ -227,6 +229,15 @@ class LearnerEngine:
             check(k.r2_pack_bf16(ptr(self.target), ptr(self.bf_index), ptr(self.bf_t), L.bf_numel, s), "pack_t")
             check(k.r2_gather_f32(ptr(self.target), ptr(self.f_index), ptr(self.f32_t), L.f_numel, s), "gather_t")
             torch.add(self.pk_t["b_ih"], self.pk_t["b_hh"], out=self.lstm_b_t)
+
+    def _pack_step(self, interval: int, s):
+        L = self.layout
+        check(kernels().r2_pack_step(ptr(self.master), ptr(self.target), L.padded, ptr(self.bf_index),
+                                     ptr(self.bf), ptr(self.bf_t), L.bf_numel, ptr(self.f_index),
+                                     ptr(self.f32), ptr(self.f32_t), L.f_numel,
+                                     L.f_offsets["b_ih"][0], L.f_offsets["b_hh"][0],
+                                     ptr(self.lstm_b), ptr(self.lstm_b_t), L.G, ptr(self.replay.step),
+                                     interval, s), "pack_step")
 
     def state_dict(self):
         return self.layout.state_dict(self.master)
@@ -383,7 +394,7 @@ class LearnerEngine:
                            ptr(self.td_abs), ptr(rp.priority), ptr(self.is_w), ptr(rp.n_valid),
                            Ll, B, A, Lb, rp.cap_e, self.gamma_n, int(lc.value_rescale),
                            float(lc.value_rescale_eps), float(rc.alpha), float(rc.priority_eps),
-                           float(rc.beta), s), "td_loss")
+                           float(rc.beta), ptr(self.td_part), ptr(self.td_ticket), s), "td_loss")
 
     def _backward_core(self):
         """Head backward, BPTT, LSTM/head weight gradients -> grad bucket 'core'."""
@@ -545,10 +556,9 @@ class LearnerEngine:
                                         ptr(self.opt_b), n, float(lc.lr), float(lc.rms_alpha),
                                         float(lc.eps), gscale, clip, float(lc.grad_clip), s),
                   "rmsprop")
-        # target sync on device when (step+1) % interval == 0 (learner.py:107-108), then repack
-        check(k.r2_copy_if_due(ptr(self.target), ptr(self.master), n, ptr(self.replay.step),
-                               int(lc.target_update_interval), s), "copy_if_due")
-        self._pack(always=True)
+        # one launch: online repack + target sync on device when (step+1) % interval == 0
+        # (learner.py:107-108) with the target packs written only then
+        self._pack_step(int(lc.target_update_interval), s)
 
     def _priorities(self):
         rp = self.replay

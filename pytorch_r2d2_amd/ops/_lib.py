@@ -35,7 +35,7 @@ _SIGS = {
     "r2_relu_mask_bf16": [P, P, P, I64, P],
     "r2_dueling_fwd": [P, P, P, P, P, P, I, I, I, P],
     "r2_dueling_bwd": [P, P, P, P, P, I, I, I, P],
-    "r2_td_loss": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, F, F, F, F, P],
+    "r2_td_loss": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, F, F, F, F, P, P, P],
     "r2_tree_sample": [P, P, P, I, I, U64, P, P, P, P],
     "r2_tree_rebuild": [P, P, P, I, P],
     "r2_tree_update": [P, P, P, I, P, P, I, P],
@@ -54,6 +54,8 @@ _SIGS = {
     "r2_torso_bwd": [P, P, I, P, P, P, P, P, P, P, I, P, P, P, P],
     "r2_torso_bwd_slab_floats": [],
     "r2_gemm": [P, I, P],
+    "r2_gemm_set_version": [I],
+    "r2_pack_step": [P, P, I64, P, P, P, I64, P, P, P, I64, I64, I64, P, P, I64, P, I64, P],
     "r2_torso_bwd_set_debug": [P],
     "r2_torso_fwd_set_debug": [P],
     "r2_lstm_persist_set_debug": [P],

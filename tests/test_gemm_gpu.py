@@ -21,8 +21,10 @@ def _op(rows, cols, kmajor, gen):
 
 
 @pytest.mark.parametrize("ak,bk", [(1, 1), (1, 0), (0, 1), (0, 0)])
-@pytest.mark.parametrize("M,N,K", [(296, 200, 64), (1024, 1568, 96), (136, 264, 1568), (64, 48, 40)])
+@pytest.mark.parametrize("M,N,K", [(296, 200, 64), (1024, 1568, 96), (136, 264, 1568), (64, 48, 40),
+                                   (520, 1568, 2560), (200, 136, 128)])
 def test_gemm_layouts(ak, bk, M, N, K):
+    """K % 64 == 0 runs the LDS-DMA kernel (v2), other K the register-staged one (v1)."""
     g = torch.Generator(device=DEV).manual_seed(M + N + K + 2 * ak + bk)
     a = _op(M, K, ak, g)
     b = _op(N, K, bk, g).t()          # (K, N) view; k-major means B^T rows contiguous
@@ -51,3 +53,21 @@ def test_gemm_row_map_accumulate_bf16_and_batch():
     ref[perm.long()] += a.float() @ b.float()
     assert _rel(c, ref) < 1e-5
     assert _rel(c2, a2.float() @ b2.float()) < 1e-2
+
+
+@pytest.mark.parametrize("ak,bk", [(1, 1), (0, 0), (1, 0)])
+def test_gemm_v1_v2_agree(ak, bk):
+    from pytorch_r2d2_amd.ops._lib import kernels
+    g = torch.Generator(device=DEV).manual_seed(11)
+    M, N, K = 384, 512, 640
+    a = _op(M, K, ak, g)
+    b = _op(N, K, bk, g).t()
+    outs = []
+    for v in (1, 2):
+        kernels().r2_gemm_set_version(v)
+        c = torch.empty(M, N, device=DEV)
+        gemm(Gemm(a, b, c))
+        outs.append(c)
+    kernels().r2_gemm_set_version(2)
+    torch.cuda.synchronize()
+    assert _rel(outs[0], outs[1]) < 1e-6

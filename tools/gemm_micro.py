@@ -51,4 +51,18 @@ us = timeit(lambda: gemm(Gemm(dg, W, Cx)))
 res["dx_mine_us"], res["dx_mine_tflops"] = us, fl / us / 1e6
 us = timeit(lambda: torch.mm(dg, W))
 res["dx_torch_us"] = us
+# v1 (register staged) vs v2 (LDS-DMA) on K % 64 shapes
+from pytorch_r2d2_amd.ops._lib import kernels  # noqa: E402
+Xp = torch.randn(5440, 1600, device=DEV).to(bf)
+Wp = torch.randn(1024, 1600, device=DEV).to(bf)
+fl = 2 * 5440 * 1600 * 1024
+for v in (1, 2):
+    kernels().r2_gemm_set_version(v)
+    us = timeit(lambda: gemm(Gemm(Xp, Wp.t(), C, bias=bias)))
+    res[f"xp1600_v{v}_us"], res[f"xp1600_v{v}_tflops"] = us, fl / us / 1e6
+    us = timeit(lambda: gemm(Gemm(dg.t(), Xl, Cw)))
+    res[f"dwih_v{v}_us"] = us
+    us = timeit(lambda: gemm(Gemm(dg, W, Cx)))
+    res[f"dx_v{v}_us"] = us
+kernels().r2_gemm_set_version(2)
 print(json.dumps({k: round(v, 1) for k, v in res.items()}))
