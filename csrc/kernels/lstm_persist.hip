@@ -554,3 +554,23 @@ extern "C" int r2_lstm_bwd_persist(const float* dh_ext, const float* gates, cons
 }
 
 extern "C" int r2_lstm_persist_ctr_words() { return PL_CTR_WORDS; }
+
+// ---- placement probe (tools / tests): XCC id of every block of a launch
+__global__ void xcc_probe_kernel(int* out, int spin) {
+  if (threadIdx.x == 0) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    out[blockIdx.x] = (int)(x & 15);
+  }
+  if (spin) __builtin_amdgcn_s_sleep(100);
+}
+
+extern "C" int r2_xcc_probe(int* out, int nblocks, int threads, int lds_bytes, void* stream) {
+  if (lds_bytes > 0)
+    hipFuncSetAttribute((const void*)xcc_probe_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        lds_bytes);
+  hipLaunchKernelGGL(xcc_probe_kernel, dim3(nblocks), dim3(threads), lds_bytes,
+                     (hipStream_t)stream, out, 1);
+  R2_CHECK_LAUNCH();
+  return 0;
+}

@@ -77,13 +77,37 @@ __device__ __forceinline__ void torso_store_chunk(bf16* s2d, int c, const u32x4&
 __constant__ int c_t1_begin[8] = {0, 2, 4, 5, 5, 7, 9, 11};
 __constant__ int c_t1_count[8] = {2, 2, 1, 0, 2, 2, 2, 2};
 
-__global__ __launch_bounds__(512) void torso_fwd_kernel(
-    const uint8_t* __restrict__ frames, const int* __restrict__ rows, int n_frames,
-    const bf16* __restrict__ w1, const float* __restrict__ b1,
-    const bf16* __restrict__ w2, const float* __restrict__ b2,
-    const bf16* __restrict__ w3, const float* __restrict__ b3,
-    bf16* __restrict__ out, bf16* __restrict__ save1, bf16* __restrict__ save2,
-    long long* __restrict__ dbg) {
+// One launch can run up to TF_MAX_JOBS frame lists (e.g. the online and the target net's frames
+// of one time chunk): the workers are split between the jobs in proportion to their frame
+// counts, so each workgroup loads ONE weight set.  With reserve_slots > 0 the blocks of the
+// last reserve_slots dispatch slots of XCDs 0..reserve_xcds-1 exit at once, leaving those CUs to a
+// concurrently running persistent LSTM chunk (blocks are dealt to XCDs round-robin: b % 8).
+#define TF_MAX_JOBS 4
+struct TFJob {
+  const int* rows;
+  const bf16* w1; const float* b1;
+  const bf16* w2; const float* b2;
+  const bf16* w3; const float* b3;
+  bf16* out; bf16* save1; bf16* save2;
+  int n, wbegin, wcount, pad_;
+};
+struct TFArgs {
+  const uint8_t* frames;
+  TFJob job[TF_MAX_JOBS];
+  int njobs, reserve_xcds, reserve_slots, pad_;
+  long long* dbg;
+};
+
+__device__ __forceinline__ int tf_worker(int reserve_xcds, int reserve_slots) {
+  const int b = blockIdx.x;
+  if (reserve_slots <= 0) return b;
+  const int x = b & 7, s = b >> 3, keep = 32 - reserve_slots;
+  if (s < keep) return b;
+  if (x < reserve_xcds) return -1;
+  return keep * 8 + (s - keep) * (8 - reserve_xcds) + (x - reserve_xcds);
+}
+
+__global__ __launch_bounds__(512) void torso_fwd_kernel(const TFArgs args) {
   using namespace torso;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   bf16* in_bf = (bf16*)(lds + OFF_IN);
@@ -93,6 +117,25 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(
   bf16* lw3 = (bf16*)(lds + OFF_W3);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int half = lane >> 5, l32 = lane & 31;
+  const int wk = tf_worker(args.reserve_xcds, args.reserve_slots);
+  if (wk < 0) return;
+  int ji = 0;
+#pragma unroll
+  for (int i = 1; i < TF_MAX_JOBS; ++i)
+    if (i < args.njobs && wk >= args.job[i].wbegin) ji = i;
+  const TFJob& J = args.job[ji];
+  const int stride = J.wcount;
+  if (wk - J.wbegin >= stride) return;
+  const uint8_t* __restrict__ frames = args.frames;
+  const int* __restrict__ rows = J.rows;
+  const int n_frames = J.n;
+  const bf16* __restrict__ w1 = J.w1; const float* __restrict__ b1 = J.b1;
+  const bf16* __restrict__ w2 = J.w2; const float* __restrict__ b2 = J.b2;
+  const bf16* __restrict__ w3 = J.w3; const float* __restrict__ b3 = J.b3;
+  bf16* __restrict__ out = J.out;
+  bf16* __restrict__ save1 = J.save1;
+  bf16* __restrict__ save2 = J.save2;
+  long long* __restrict__ dbg = args.dbg;
 
   // ---- weights -> LDS (conv2, conv3) with padded rows; conv1 fragments -> VGPRs
   for (int i = tid; i < 32 * 64; i += NT) {   // conv2: 32 rows x 64 chunks of 8 bf16
@@ -114,7 +157,7 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(
   if (tid < 64) lb23[tid] = tid < 32 ? b2[tid] : b3[tid - 32];
   const int t1b = c_t1_begin[wave], t1n = c_t1_count[wave];
 
-  int f = blockIdx.x;
+  int f = wk - J.wbegin;
   if (f >= n_frames) return;
   // ---- prologue: first frame -> LDS (bf16)
   {
@@ -126,19 +169,19 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(
 
   int fprev = -1, it_dbg = 0;
 #define TF_TRACE(k) \
-  if (dbg && blockIdx.x == 0 && tid == 0 && it_dbg < 16) dbg[it_dbg * 8 + (k)] = clock64();
+  if (dbg && wk == 0 && tid == 0 && it_dbg < 16) dbg[it_dbg * 8 + (k)] = clock64();
   // replay row of the next frame, read one frame ahead so the prefetch never waits on its address
-  int row_nx = f + (int)gridDim.x < n_frames ? (rows ? rows[f + gridDim.x] : f + gridDim.x) : 0;
+  int row_nx = f + stride < n_frames ? (rows ? rows[f + stride] : f + stride) : 0;
   for (;;) {
     const bool have = f < n_frames;
-    const int fn = f + gridDim.x;
-    const int fnn = fn + gridDim.x;
+    const int fn = f + stride;
+    const int fnn = fn + stride;
     const int row_nn = fnn < n_frames ? (rows ? rows[fnn] : fnn) : 0;
     u32x4 pf[PF];
     TF_TRACE(0);
     // =================== phase A: conv1(f) || conv3(f-1)
     if (have) {
-      // waves 3..7 prefetch frame f+grid into registers (lands while the convolutions run);
+      // waves 3..7 prefetch frame f+stride into registers (lands while the convolutions run);
       // they convert it into LDS during phase B while waves 0..2 run conv2
       if (fn < n_frames && wave >= 3) {
         const u32x4* src = (const u32x4*)(frames + (size_t)row_nx * IN_BYTES);
@@ -200,7 +243,7 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(
     TF_TRACE(2);
     if (!have) break;
 
-    // =================== phase B: conv2(f) on waves 0..2; frame f+grid -> LDS; save act1(f)
+    // =================== phase B: conv2(f) on waves 0..2; frame f+stride -> LDS; save act1(f)
     if (conv2_wave) {
       const int p = wave * 32 + l32;
       const int pc = p < P2 ? p : P2 - 1;
@@ -326,24 +369,70 @@ extern "C" int r2_relu_mask_bf16(const bf16* g, const bf16* act, bf16* out, int6
 static long long* g_tf_dbg = nullptr;
 extern "C" int r2_torso_fwd_set_debug(long long* p) { g_tf_dbg = p; return 0; }
 
-extern "C" int r2_torso_fwd(const uint8_t* frames, const int* rows, int n_frames,
-                            const bf16* w1, const float* b1, const bf16* w2, const float* b2,
-                            const bf16* w3, const float* b3, bf16* out, bf16* save1, bf16* save2,
-                            int max_blocks, void* stream) {
-  if (n_frames <= 0) return 0;
+// jobs: njobs x 12 int64 {rows, n, w1, b1, w2, b2, w3, b3, out, save1, save2, 0}.
+// grid 0 = one block per CU (256); reserve_slots > 0 (grid must then be 256) keeps the last
+// reserve_slots dispatch slots of XCDs 0..reserve_xcds-1 free (see tf_worker).
+extern "C" int r2_torso_fwd_multi(const uint8_t* frames, const int64_t* jobs, int njobs,
+                                  int grid, int reserve_xcds, int reserve_slots, void* stream) {
+  if (njobs < 1 || njobs > TF_MAX_JOBS) return -1;
+  if (reserve_slots < 0 || reserve_slots >= 32 || reserve_xcds < 0 || reserve_xcds > 8) return -2;
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute((const void*)torso_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                         torso::LDS_BYTES);
     attr_set = true;
   }
-  int grid = max_blocks > 0 ? max_blocks : 256;
-  if (grid > n_frames) grid = n_frames;
+  TFArgs a{};
+  a.frames = frames;
+  a.njobs = 0;
+  a.reserve_xcds = reserve_xcds;
+  a.reserve_slots = reserve_slots;
+  a.dbg = g_tf_dbg;
+  int64_t total = 0;
+  for (int i = 0; i < njobs; ++i) total += jobs[12 * i + 1] > 0 ? jobs[12 * i + 1] : 0;
+  if (total <= 0) return 0;
+  if (reserve_slots > 0) grid = 256;
+  if (grid <= 0) grid = 256;
+  const int nw = reserve_slots > 0 ? (32 - reserve_slots) * 8 + reserve_slots * (8 - reserve_xcds)
+                                   : grid;
+  // workers in proportion to frame counts (>= 1 each, never more than the job's frames)
+  int wb = 0;
+  int64_t seen = 0;
+  for (int i = 0; i < njobs; ++i) {
+    const int64_t* p = jobs + 12 * i;
+    if (p[1] <= 0) continue;
+    seen += p[1];
+    int end = (int)((seen * nw + total - 1) / total);
+    if (end > nw) end = nw;
+    int cnt = end - wb;
+    if (cnt < 1) cnt = 1;
+    if (cnt > p[1]) cnt = (int)p[1];
+    TFJob& J = a.job[a.njobs++];
+    J.rows = (const int*)p[0]; J.n = (int)p[1];
+    J.w1 = (const bf16*)p[2]; J.b1 = (const float*)p[3];
+    J.w2 = (const bf16*)p[4]; J.b2 = (const float*)p[5];
+    J.w3 = (const bf16*)p[6]; J.b3 = (const float*)p[7];
+    J.out = (bf16*)p[8]; J.save1 = (bf16*)p[9]; J.save2 = (bf16*)p[10];
+    J.wbegin = wb; J.wcount = cnt; J.pad_ = 0;
+    wb += cnt;
+  }
+  if (wb > nw) return -3;   // more jobs than workers
+  if (reserve_slots <= 0 && grid > wb) grid = wb;
   hipLaunchKernelGGL(torso_fwd_kernel, dim3(grid), dim3(torso::NT), torso::LDS_BYTES,
-                     (hipStream_t)stream, frames, rows, n_frames, w1, b1, w2, b2, w3, b3, out,
-                     save1, save2, g_tf_dbg);
+                     (hipStream_t)stream, a);
   R2_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int r2_torso_fwd(const uint8_t* frames, const int* rows, int n_frames,
+                            const bf16* w1, const float* b1, const bf16* w2, const float* b2,
+                            const bf16* w3, const float* b3, bf16* out, bf16* save1, bf16* save2,
+                            int max_blocks, void* stream) {
+  if (n_frames <= 0) return 0;
+  const int64_t job[12] = {(int64_t)rows, n_frames, (int64_t)w1, (int64_t)b1, (int64_t)w2,
+                           (int64_t)b2, (int64_t)w3, (int64_t)b3, (int64_t)out, (int64_t)save1,
+                           (int64_t)save2, 0};
+  return r2_torso_fwd_multi(frames, job, 1, max_blocks, 0, 0, stream);
 }
 
 extern "C" int r2_frames_to_bf16(const uint8_t* frames, const int* rows, int n_frames, bf16* out,

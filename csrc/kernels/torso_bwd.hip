@@ -342,13 +342,19 @@ __global__ __launch_bounds__(512) void torso_bwd_kernel(const TBArgs a) {
     sl[OFF_W2 + co * 512 + wave * 32 + l32] = acc2a[r];
     sl[OFF_W2 + co * 512 + (wave + 8) * 32 + l32] = acc2b[r];
   }
+  // bias partials: per-lane values -> LDS, summed in a fixed order (deterministic, unlike LDS
+  // float atomics): conv1 bias from every wave (all ran dact1 jobs), conv2 bias from waves 5..7
   float* red = (float*)(lds + G1H);
-  if (tid < 64) red[tid] = 0.f;
+  red[tid] = db1p;
+  red[512 + tid] = wave >= 5 ? db2p : 0.f;
   __syncthreads();
-  atomicAdd(&red[l32], db1p);                       // conv1 bias (every wave ran dact1 jobs)
-  if (wave >= 5) atomicAdd(&red[32 + l32], db2p);   // conv2 bias
-  __syncthreads();
-  if (tid < 64) sl[OFF_B + tid] = red[tid];
+  if (tid < 64) {
+    const int part = tid >> 5, c = tid & 31;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) v += red[part * 512 + w * 64 + c] + red[part * 512 + w * 64 + 32 + c];
+    sl[OFF_B + tid] = v;
+  }
 }
 
 // dW3 += g3 . im2col(act2) and db3, straight from global dX3 / out3 / act2 (all written by

@@ -89,6 +89,12 @@ class LearnerConfig:
     target_mode: str = "shifted"
     compute_dtype: str = "bf16"
     lstm_impl: str = "persistent"     # persistent (one launch per sequence) | step (launch per t)
+    # forward pipelining ("shifted" mode, persistent LSTM): the frames are processed in this many
+    # time chunks; the recurrence of chunk c runs on a side stream on CUs the torso leaves free
+    # while the torso + input projection of chunk c+1 run.  0/1 = serial forward (default:
+    # measured 1.146 ms/step at 5 chunks vs 0.993 serial -- each cross-stream graph edge costs
+    # ~15 us and a chunk's x-projection GEMM is tile-latency bound; profiles/r01_v9_pipelined.txt)
+    fwd_chunks: int = 0
     torso_bwd: str = "fused"          # fused (HIP kernel) | library (MIOpen convolution_backward)
     use_graph: bool = True            # capture the whole step in a HIP graph
     save_dir: str = "save"

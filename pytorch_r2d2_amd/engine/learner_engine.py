@@ -213,6 +213,8 @@ class LearnerEngine:
         if mode != "shifted":
             self.z_nx = z(Nnx, 2 * HD, dt=bf16)
         self.dh = z(Ll * B, H)
+        self._chunks = self._plan_chunks()
+        self._side = torch.cuda.Stream(device=d) if self._chunks is not None else None
         self.dX = z(Ll * B, D, dt=bf16)
         self.gate_perm_i32 = L.gate_perm.to(d, torch.int32)
 
@@ -323,6 +325,89 @@ class LearnerEngine:
                                            self.layout.A, self.layout.HD, stream_handle()),
                   "dueling_fwd")
 
+    # ------------------------------------------------------------------ pipelined forward
+    def _plan_chunks(self):
+        """Time-chunk boundaries of the pipelined forward, or None for the serial forward.
+
+        The pipeline: chunk c's torso (both nets, one launch) and input projection (one GEMM
+        launch) run on the main stream; its recurrence (both chains, one persistent launch) runs
+        on a side stream while the torso of chunk c+1 proceeds on the CUs the LSTM does not use
+        (``r2_torso_fwd_multi`` reserve).  Chunk 0 has no LSTM beside it and gets the whole chip,
+        so it is the longest; the last chunk is short because its recurrence is not overlapped.
+        """
+        lc = self.cfg.learner
+        k = int(getattr(lc, "fwd_chunks", 0) or 0)
+        H = self.layout.H
+        groups = 2 * ((self.B + 31) // 32)
+        if (k < 2 or self.mode != "shifted" or lc.lstm_impl != "persistent" or not self.fused_torso
+                or not self.use_gemm or self.device.type != "cuda" or groups > 8):
+            return None
+        Tc = self.Tc
+        first = max(1, int(round(0.42 * Tc)))
+        rest = Tc - first
+        w = [1.0] * (k - 2) + [0.6]
+        cuts, acc = [0, first], float(first)
+        for wi in w[:-1]:
+            acc += rest * wi / sum(w)
+            cuts.append(int(round(acc)))
+        cuts.append(Tc)
+        cuts = sorted(set(c for c in cuts if 0 <= c <= Tc))
+        if len(cuts) < 3:
+            return None
+        # LSTM placement (lstm_persist.hip): group g on XCD g, H/16 workgroups each
+        self._reserve = (groups, H // UNITS)
+        return cuts
+
+    def _torso_job(self, pk, rows, out, save_at=None):
+        B = self.B
+        s1 = s2 = 0
+        if save_at is not None:
+            P1 = self.act1.shape[1] * self.act1.shape[2]
+            P2 = self.act2.shape[1] * self.act2.shape[2]
+            s1 = self.act1.data_ptr() + save_at * B * P1 * 2
+            s2 = self.act2.data_ptr() + save_at * B * P2 * 2
+        return [ptr(rows), rows.numel(), ptr(pk["conv1"]), ptr(pk["b1"]), ptr(pk["conv2"]),
+                ptr(pk["b2"]), ptr(pk["conv3"]), ptr(pk["b3"]), ptr(out), s1, s2, 0]
+
+    def _forward_pipelined(self):
+        k = kernels()
+        B, Lb, T = self.B, self.Lb, self.T
+        pk, pt = self.pk, self.pk_t
+        rows, cuts = self.rows, self._chunks
+        main = torch.cuda.current_stream()
+        side = self._side
+        rx, rs = self._reserve
+        side.wait_stream(main)                      # stored states + row list are ready
+        for c, (t0, t1) in enumerate(zip(cuts[:-1], cuts[1:])):
+            jobs = []
+            # online frames, split where the saved-activation window [Lb, T) begins / ends
+            edges = sorted({t0, t1} | {e for e in (Lb, T) if t0 < e < t1})
+            for a, b in zip(edges[:-1], edges[1:]):
+                save = (a - Lb) if (Lb <= a and b <= T) else None
+                jobs.append(self._torso_job(pk, rows[a * B:b * B], self.X_on[a * B:b * B], save))
+            jobs.append(self._torso_job(pt, rows[t0 * B:t1 * B], self.X_tg[t0 * B:t1 * B]))
+            arr = np.asarray(jobs, dtype=np.int64)
+            check(k.r2_torso_fwd_multi(ptr(self.replay.frames), arr.ctypes.data, len(jobs), 256,
+                                       rx if c > 0 else 0, rs if c > 0 else 0, stream_handle(main)),
+                  "torso_fwd_multi")
+            r0, r1 = t0 * B, t1 * B
+            gemm(Gemm(self.X_on[r0:r1], pk["w_ih"].t(), self.xp_on[r0:r1], bias=self.lstm_b),
+                 Gemm(self.X_tg[r0:r1], pt["w_ih"].t(), self.xp_tg[r0:r1], bias=self.lstm_b_t))
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                chains = []
+                for key, p_, xp in (("on", pk, self.xp_on), ("tg", pt, self.xp_tg)):
+                    h0 = self.h0[key] if t0 == 0 else self.hseq[key][t0 - 1]
+                    c0 = self.c0[key] if t0 == 0 else self.cseq[key][t0 - 1]
+                    gates, save_from = None, 0
+                    if key == "on" and t1 > Lb:
+                        gates = self.gates[max(t0 - Lb, 0):]
+                        save_from = max(Lb - t0, 0)
+                    chains.append(self._chain_desc(xp[r0:], p_, h0, c0, self.hseq[key][t0:],
+                                                   self.cseq[key][t0:], gates, save_from))
+                self._lstm(chains, t1 - t0)
+        main.wait_stream(side)
+
     # ------------------------------------------------------------------ the step
     def _forward_loss(self):
         k = kernels()
@@ -334,6 +419,17 @@ class LearnerEngine:
         rp.sample(B, self.starts, self.probs)
         check(k.r2_make_rows(ptr(self.starts), B, Tn, 0, rp.cap_e, ptr(self.rows), s), "make_rows")
         rows = self.rows
+        # stored recurrent state
+        st_off = {"on": 0, "tg": 0 if self.mode == "shifted" else n, "nx": n}
+        check(k.r2_gather_state(ptr(rp.hs_cs), ptr(self.starts), B, 0, rp.cap_e, H,
+                                ptr(self.h0["on"]), ptr(self.c0["on"]), 0, s), "gather_state")
+        check(k.r2_gather_state(ptr(rp.target_hs_cs), ptr(self.starts), B, st_off["tg"], rp.cap_e,
+                                H, ptr(self.h0["tg"]), ptr(self.c0["tg"]), 0, s), "gather_state")
+        if self._chunks is not None:
+            self._forward_pipelined()
+            xp_on, xp_tg = self.xp_on, self.xp_tg
+            self._xp = (xp_on, xp_tg)
+            return self._forward_tail()
         # torso: online over all Tn frames (save activations of the learning frames)
         self._torso(pk, rows[: Lb * B], self.X_on[: Lb * B])
         self._torso(pk, rows[Lb * B: T * B], self.X_on[Lb * B: T * B], save=True)
@@ -348,12 +444,6 @@ class LearnerEngine:
             xp_on = addmm_f32(self.lstm_b, self.X_on, pk["w_ih"].t())
             xp_tg = addmm_f32(self.lstm_b_t, self.X_tg, pt["w_ih"].t())
         self._xp = (xp_on, xp_tg)
-        # stored recurrent state
-        st_off = {"on": 0, "tg": 0 if self.mode == "shifted" else n, "nx": n}
-        check(k.r2_gather_state(ptr(rp.hs_cs), ptr(self.starts), B, 0, rp.cap_e, H,
-                                ptr(self.h0["on"]), ptr(self.c0["on"]), 0, s), "gather_state")
-        check(k.r2_gather_state(ptr(rp.target_hs_cs), ptr(self.starts), B, st_off["tg"], rp.cap_e,
-                                H, ptr(self.h0["tg"]), ptr(self.c0["tg"]), 0, s), "gather_state")
         G = L.G
         on = self._chain_desc(xp_on, pk, self.h0["on"], self.c0["on"], self.hseq["on"],
                               self.cseq["on"], self.gates, Lb)
@@ -373,6 +463,16 @@ class LearnerEngine:
             nx = self._chain_desc(xp_on[(n + Lb) * B:], pk, self.h0["nx"], self.c0["nx"],
                                   self.hseq["nx"], self.cseq["nx"])
             self._lstm([nx], Ll)
+        self._forward_tail()
+
+    def _forward_tail(self):
+        """Heads, TD loss and priorities (after every recurrent chain has run)."""
+        k = kernels()
+        s = stream_handle()
+        B, Lb, Ll, n = self.B, self.Lb, self.Ll, self.n
+        L, rp, lc = self.layout, self.replay, self.cfg.learner
+        H, A = L.H, L.A
+        pk, pt = self.pk, self.pk_t
         # heads (rows from the first learning step on)
         jobs = [(pk, self.hseq["on"][Lb:].reshape(-1, H), self.z_on, self.q_on, self.zr_on),
                 (pt, self.hseq["tg"][Lb:].reshape(-1, H), self.z_tg, self.q_tg, None)]

@@ -30,6 +30,7 @@ _SIGS = {
     "r2_lstm_fwd": [P, I, I, I, I, I, P],
     "r2_lstm_bwd": [P, P, P, P, P, P, P, P, P, I, I, I, I, P],
     "r2_torso_fwd": [P, P, I, P, P, P, P, P, P, P, P, P, I, P],
+    "r2_torso_fwd_multi": [P, P, I, I, I, I, P],
     "r2_frames_to_bf16": [P, P, I, P, P],
     "r2_frames_to_bf16_nhwc": [P, P, I, P, P],
     "r2_relu_mask_bf16": [P, P, P, I64, P],
@@ -60,6 +61,7 @@ _SIGS = {
     "r2_torso_fwd_set_debug": [P],
     "r2_lstm_persist_set_debug": [P],
     "r2_lstm_persist_force_slow": [I],
+    "r2_xcc_probe": [P, I, I, I, P],
     "r2_lstm_fwd_persist": [P, I, I, I, I, P, P, P],
     "r2_lstm_bwd_persist": [P, P, P, P, P, P, P, I, I, I, I, P, P, P],
     "r2_actor_finalize": [P] * 21 + [I, I, I, I, I, I, F, F, F, F, U64, P],
