@@ -308,6 +308,215 @@ __global__ __launch_bounds__(256) void gemm2_kernel(const GemmArgs args) {
   }
 }
 
+// ============================================================================================
+// v4: 256 x BN x BK tiles (BN 256 or 128, BK 64 or 32), 8 waves (2 in M x 4 in N, two waves per
+// SIMD), each wave 128 x BN/4 as 8 x BN/64 v_mfma_f32_16x16x32_bf16 accumulators.  One LDS array
+// = NS buffers x {A, B}, filled by global_load_lds (16 B/lane) with the bank swizzle applied to
+// the per-lane SOURCE address and undone on the fragment read; per K tile: counted wait for own
+// DMA -> barrier -> DMA of tile k+NS-1 into the buffer everybody just finished -> fragment reads
+// -> MFMAs.  The two waves of a SIMD overlap each other's fragment reads and barrier waits with
+// MFMAs (cdna_hip_programming.md section 5.5, T3+T4 minimum form); blocks are remapped so
+// consecutive tiles (same A rows) share an XCD and its L2.
+//   k-major image   [rows][BK], 16-B chunk c of row r at c ^ ((r >> 1) & 7) (BK 64) or
+//                   c ^ 3 ((r >> 3) & 1) (BK 32): conflict-free 16x16x32 fragment reads
+//   mn-major image  per 128-column half: [BK][128], 256-B rows, chunk c of k-row k at
+//                   c ^ 2 ((k & 3) | ((k >> 3) & 1) << 2): conflict-free transposed reads
+// K % 8 == 0: 16-B chunks past K are DMA'd from a zero block, so a partial last K tile adds
+// zeros; mn-major extents % 8 == 0.
+// 16-B chunks past K are fetched from here
+__device__ __attribute__((aligned(16))) bf16 g4_zero[8];
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ int g4_mnswz(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }
+
+template <int BK>
+__device__ __forceinline__ int g4_kswz(int r) { return BK == 64 ? ((r >> 1) & 7) : 3 * ((r >> 3) & 1); }
+
+// Stage one R x BK operand tile (R*BK*2/1024 1-KB blocks dealt over the 8 waves).  Addresses are
+// rebuilt every K tile from 32-bit offsets (oz = opaque zero): hoisting 64-bit pointers out of the
+// K loop costs VGPRs the accumulators need.
+template <bool KMAJ, int R, int BK>
+__device__ __forceinline__ void g4_stage(const bf16* X, int ld, int i0, int imax, int k0, int kmax,
+                                         uint8_t* tile, int wave, int lane, int oz) {
+  constexpr int NBLK = R * BK * 2 / 1024, PW = NBLK / 8;
+#pragma unroll
+  for (int j = 0; j < PW; ++j) {
+    const int blk = wave * PW + j;
+    int off;
+    bool kin;
+    if (KMAJ) {
+      constexpr int CPR = BK / 8, RPB = 64 / CPR;            // chunks per row, rows per block
+      const int row = blk * RPB + lane / CPR, cp = lane % CPR;
+      const int c = cp ^ g4_kswz<BK>(row);
+      const int k = k0 + c * 8;
+      kin = k < kmax;
+      off = min(i0 + row, imax - 1) * ld + k;
+    } else {
+      constexpr int BPH = BK / 4;                            // blocks per 128-column half
+      const int h = blk / BPH, kr = (blk % BPH) * 4 + (lane >> 4), cp = lane & 15;
+      const int c = cp ^ g4_mnswz(kr);
+      const int col = i0 + h * 128 + c * 8;
+      kin = k0 + kr < kmax;
+      off = (k0 + kr) * ld + (col < imax ? col : imax - 8);
+    }
+    const bf16* src = kin ? X + (off + oz) : g4_zero;
+    __builtin_amdgcn_global_load_lds(src,
+                                     (__attribute__((address_space(3))) void*)(tile + blk * 1024),
+                                     16, 0, 0);
+  }
+}
+
+// 16x16x32 fragment (k-step ks of the tile): lane l holds X[i0 + (l & 15)][32 ks + 8 (l >> 4) .. +7]
+template <bool KMAJ, int R, int BK>
+__device__ __forceinline__ bf16x8 g4_frag(const uint8_t* tile, int i0, int ks, int lane) {
+  const int l16 = lane & 15, g = lane >> 4;
+  if (KMAJ) {
+    const int r = i0 + l16, c = 4 * ks + g;
+    return *(const bf16x8*)(tile + r * (BK * 2) + ((c ^ g4_kswz<BK>(r)) * 16));
+  }
+  // tr read: within the 16-lane group, lane 4q+p addresses k-row (32ks + 8g + q), columns
+  // i0 + 4p .. +3; the hardware hands lane i column i0+i's 4 k values (second read: k-rows +4)
+  const int q = (lane >> 2) & 3, p = lane & 3;
+  const uint8_t* half = tile + (i0 >> 7) * (BK * 256);
+  const int kr = 32 * ks + 8 * g + q;
+  const int c = ((i0 & 127) >> 3) + (p >> 1);
+  const uint8_t* b0 = half + kr * 256 + ((c ^ g4_mnswz(kr)) * 16) + 8 * (p & 1);
+  return gm_tr8((const bf16*)b0, (const bf16*)(b0 + 4 * 256));
+}
+
+template <int N>
+__device__ __forceinline__ void g4_vmwait() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
+}
+
+template <bool AK, bool BK_, int BN, int BK, int NS>
+__global__ __launch_bounds__(512) void gemm4_kernel(const GemmArgs args, int total_tiles) {
+  constexpr int BM = 256, TNW = BN / 64, KS = BK / 32;
+  constexpr int OPA = BM * BK * 2, OPB = BN * BK * 2, STB = OPA + OPB;
+  constexpr int NDMA = (BM + BN) * BK * 2 / (512 * 16);   // DMA instructions per thread per K tile
+  extern __shared__ __attribute__((aligned(1024))) uint8_t lds4[];
+  // XCD remap (bijective): blocks b with equal b % 8 share an XCD; give each XCD a contiguous
+  // range of tile ids so neighbouring tiles (same A rows) hit one L2
+  int bid;
+  {
+    const int b = blockIdx.x, x = b & 7, qn = total_tiles >> 3, r = total_tiles & 7;
+    bid = (x < r ? x * (qn + 1) : r * (qn + 1) + (x - r) * qn) + (b >> 3);
+  }
+  int pi = 0;
+#pragma unroll
+  for (int i = 1; i < gm::MAXP; ++i)
+    if (i < args.nprob && bid >= args.p[i].tile_base) pi = i;
+  const GemmProb& P = args.p[pi];
+  if (P.a_kmajor != (int)AK || P.b_kmajor != (int)BK_) return;
+  const int t = bid - P.tile_base;
+  const int tm = t / P.tiles_n, tn = t % P.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  if (m0 >= P.M) return;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int nk = (P.K + BK - 1) / BK;
+
+  f32x4 acc[8][TNW];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < TNW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto stage = [&](int kt) {
+    int oz;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(oz));
+    uint8_t* st = lds4 + (kt % NS) * STB;
+    g4_stage<AK, BM, BK>(P.A, P.lda, m0, P.M, kt * BK, P.K, st, wave, lane, oz);
+    g4_stage<BK_, BN, BK>(P.B, P.ldb, n0, P.N, kt * BK, P.K, st + OPA, wave, lane, oz);
+  };
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) stage(s);
+  for (int kt = 0; kt < nk; ++kt) {
+    // tile kt has landed once only the DMAs of tiles kt+1 .. kt+NS-2 (those issued) remain
+    const int ahead = nk - 1 - kt;
+    if (NS >= 4 && ahead >= 2) g4_vmwait<(NS >= 4 ? 2 : 0) * NDMA>();
+    else if (NS >= 3 && ahead >= 1) g4_vmwait<(NS >= 3 ? 1 : 0) * NDMA>();
+    else g4_vmwait<0>();
+    __builtin_amdgcn_s_barrier();     // tile kt visible; everyone finished reading tile kt-1
+    if (kt + NS - 1 < nk) stage(kt + NS - 1);
+    const uint8_t* la = lds4 + (kt % NS) * STB;
+    const uint8_t* lb = la + OPA;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf16x8 fa[8], fb[TNW];
+#pragma unroll
+      for (int j = 0; j < TNW; ++j) fb[j] = g4_frag<BK_, BN, BK>(lb, wc * (BN / 4) + 16 * j, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fa[i] = g4_frag<AK, BM, BK>(la, wr * 128 + 16 * i, ks, lane);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < TNW; ++j) acc[i][j] = mfma16(fa[i], fb[j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  // C[m0 + wr*128 + 16i + 4(l>>4) + e][n0 + wc*BN/4 + 16j + (l&15)] = acc[i][j][e]
+  const int l16 = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int j = 0; j < TNW; ++j) {
+    const int col = n0 + wc * (BN / 4) + 16 * j + l16;
+    if (col >= P.N) continue;
+    const float bv = P.bias ? P.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = m0 + wr * 128 + 16 * i + 4 * g + e;
+        if (row >= P.M) continue;
+        const int orow = P.crow ? P.crow[row] : row;
+        const float v = P.alpha * acc[i][j][e] + bv;
+        const size_t o = (size_t)orow * P.ldc + col;
+        if (P.c_f32) {
+          float* c = (float*)P.C + o;
+          *c = P.accumulate ? *c + v : v;
+        } else {
+          bf16* c = (bf16*)P.C + o;
+          *c = (bf16)(P.accumulate ? (float)*c + v : v);
+        }
+      }
+  }
+}
+
+template <int BN, int BK, int NS>
+static int g4_launch(GemmArgs& a, int ak, int bk, hipStream_t s) {
+  constexpr int LDS = NS * (256 + BN) * BK * 2;
+  static_assert(LDS <= 160 * 1024, "LDS");
+  int tiles = 0;
+  for (int i = 0; i < a.nprob; ++i) {
+    GemmProb& p = a.p[i];
+    p.tiles_n = (p.N + BN - 1) / BN;
+    p.tile_base = tiles;
+    tiles += p.tiles_n * ((p.M + 255) / 256);
+  }
+  for (int i = a.nprob; i < gm::MAXP; ++i) a.p[i] = a.p[0], a.p[i].tile_base = 1 << 30;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)gemm4_kernel<true, true, BN, BK, NS>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    hipFuncSetAttribute((const void*)gemm4_kernel<true, false, BN, BK, NS>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    hipFuncSetAttribute((const void*)gemm4_kernel<false, true, BN, BK, NS>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    hipFuncSetAttribute((const void*)gemm4_kernel<false, false, BN, BK, NS>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  if (ak && bk) hipLaunchKernelGGL((gemm4_kernel<true, true, BN, BK, NS>), dim3(tiles), dim3(512), LDS, s, a, tiles);
+  else if (ak) hipLaunchKernelGGL((gemm4_kernel<true, false, BN, BK, NS>), dim3(tiles), dim3(512), LDS, s, a, tiles);
+  else if (bk) hipLaunchKernelGGL((gemm4_kernel<false, true, BN, BK, NS>), dim3(tiles), dim3(512), LDS, s, a, tiles);
+  else hipLaunchKernelGGL((gemm4_kernel<false, false, BN, BK, NS>), dim3(tiles), dim3(512), LDS, s, a, tiles);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
 static int g_gemm_version = 2;   // 1 = force the register-staged kernel (tests / A-B)
 extern "C" int r2_gemm_set_version(int v) { g_gemm_version = v; return 0; }
 
@@ -343,6 +552,24 @@ extern "C" int r2_gemm(const int64_t* descs, int nprob, void* stream) {
   }
   for (int i = nprob; i < gm::MAXP; ++i) a.p[i] = a.p[0], a.p[i].tile_base = 1 << 30;
   hipStream_t s = (hipStream_t)stream;
+  bool k8 = true;
+  long t256 = 0;
+  for (int i = 0; i < nprob; ++i) {
+    k8 = k8 && a.p[i].K % 8 == 0;
+    t256 += (long)((a.p[i].M + 255) / 256) * ((a.p[i].N + 255) / 256);
+  }
+  if (g_gemm_version >= 5 && k8) {       // forced 8-wave variants (tests / micro-benchmarks)
+    switch (g_gemm_version) {
+      case 5: return g4_launch<256, 64, 2>(a, ak, bk, s);
+      case 6: return g4_launch<256, 32, 4>(a, ak, bk, s);
+      case 7: return g4_launch<128, 64, 3>(a, ak, bk, s);
+      default: return g4_launch<128, 32, 4>(a, ak, bk, s);
+    }
+  }
+  // auto: launches with enough 256x256 tiles to cover most CUs (the x-projection of both nets:
+  // 176) run the 8-wave kernel (70 vs 83 us there); fewer, larger-K tiles stay on 128x128, where
+  // per-CU operand traffic, not MFMA issue, bounds all of these shapes (tools/pmc_gemm.sh)
+  if (g_gemm_version == 2 && k8 && t256 >= 150) return g4_launch<256, 64, 2>(a, ak, bk, s);
   bool v2 = g_gemm_version >= 2;
   for (int i = 0; i < nprob; ++i) v2 = v2 && a.p[i].K % g2::BK == 0;
   if (v2) {

@@ -217,6 +217,8 @@ class LearnerEngine:
         self._side = torch.cuda.Stream(device=d) if self._chunks is not None else None
         self.dX = z(Ll * B, D, dt=bf16)
         self.gate_perm_i32 = L.gate_perm.to(d, torch.int32)
+        self.gs_ws = torch.zeros(int(kernels().r2_gradsum_ws_floats()), dtype=torch.float32, device=d)
+        self.gs_ticket = torch.zeros(64, dtype=torch.int32, device=d)
 
     # ------------------------------------------------------------------ weights
     def _pack(self, always: bool = False, stream=None):
@@ -508,12 +510,22 @@ class LearnerEngine:
         check(k.r2_dueling_bwd(ptr(self.dq), ptr(zr), ptr(pk["head_w2"]), ptr(self.dz),
                                ptr(self.dva), N, A, HD, s), "dueling_bwd")
         g = self.grad
-        g2 = torch.mm(self.dva.t(), zr.float())                      # (1+A, 2HD)
         gw2 = L.span(g, "val.2.weight", "adv.2.weight", (1 + A, HD))
-        gw2[0].copy_(g2[0, :HD])
-        gw2[1:].copy_(g2[1:, HD:])
-        # column sums as GEMVs against a ones row (torch's dim-0 reduce is ~300 us here)
-        torch.mm(self.ones_f32[:, :N], self.dva, out=L.span(g, "val.2.bias", "adv.2.bias", (1, 1 + A)))
+        gb2 = L.span(g, "val.2.bias", "adv.2.bias", (1, 1 + A))
+        gb1 = L.span(g, "val.0.bias", "adv.0.bias", (1, 2 * HD))
+        fused_hg = self.use_gemm and A + 1 <= 8 and HD % 64 == 0
+        if fused_hg:
+            # last-layer weight/bias grads and the layer-1 bias grads in one deterministic
+            # column-reduction launch (gradsum.hip), written in place into the flat buffer
+            check(k.r2_head_grads(ptr(self.dva), ptr(zr), ptr(self.dz), ptr(gw2), ptr(gb2),
+                                  ptr(gb1), N, A, HD, ptr(self.gs_ws), ptr(self.gs_ticket), s),
+                  "head_grads")
+        else:
+            g2 = torch.mm(self.dva.t(), zr.float())                      # (1+A, 2HD)
+            gw2[0].copy_(g2[0, :HD])
+            gw2[1:].copy_(g2[1:, HD:])
+            # column sums as GEMVs against a ones row (torch's dim-0 reduce is ~300 us here)
+            torch.mm(self.ones_f32[:, :N], self.dva, out=gb2)
         h_learn = self.hseq["on"][Lb:T].reshape(N, H)
         gw1 = L.span(g, "val.0.weight", "adv.0.weight", (2 * HD, H))
         if self.use_gemm:
@@ -522,7 +534,8 @@ class LearnerEngine:
         else:
             gw1.copy_(mm_f32(self.dz.t(), h_learn))
             dh = mm_f32(self.dz, pk["head1"])                           # (N, H)
-        L.span(g, "val.0.bias", "adv.0.bias", (1, 2 * HD)).copy_(mm_f32(self.ones_bf[:, :N], self.dz))
+        if not fused_hg:
+            gb1.copy_(mm_f32(self.ones_bf[:, :N], self.dz))
         if self.cfg.learner.lstm_impl == "persistent":
             check(k.r2_lstm_bwd_persist(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]),
                                         ptr(self.c0["on"]), ptr(pk["w_hhT"]), ptr(self.slab_p),
@@ -545,9 +558,10 @@ class LearnerEngine:
             gemm(Gemm(dgT, X, L.view(g, "lstm.weight_ih"), crow=self.gate_perm_i32),
                  Gemm(dgT, h_prev, L.view(g, "lstm.weight_hh"), crow=self.gate_perm_i32),
                  Gemm(self.dz.t(), h_learn, gw1))
-            db = mm_f32(self.ones_bf[:, :N], self.dgates).view(-1)       # packed gate order
-            torch.index_select(db, 0, self.gate_inv, out=L.view(g, "lstm.bias_ih"))
-            L.view(g, "lstm.bias_hh").copy_(L.view(g, "lstm.bias_ih"))
+            # bias grads: column sums of dgates, packed -> torch gate order, into both biases
+            check(k.r2_colsum_bf16(ptr(self.dgates), N, G, ptr(self.gate_perm_i32),
+                                   ptr(L.view(g, "lstm.bias_ih")), ptr(L.view(g, "lstm.bias_hh")),
+                                   ptr(self.gs_ws), ptr(self.gs_ticket[32:]), s), "colsum")
             gemm(Gemm(self.dgates, pk["w_ih"], self.dX))                  # (N, D) bf16
             self._dX = self.dX
         else:

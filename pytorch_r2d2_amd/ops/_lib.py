@@ -62,6 +62,9 @@ _SIGS = {
     "r2_lstm_persist_set_debug": [P],
     "r2_lstm_persist_force_slow": [I],
     "r2_xcc_probe": [P, I, I, I, P],
+    "r2_gradsum_ws_floats": [],
+    "r2_head_grads": [P, P, P, P, P, P, I, I, I, P, P, P],
+    "r2_colsum_bf16": [P, I, I, P, P, P, P, P, P],
     "r2_lstm_fwd_persist": [P, I, I, I, I, P, P, P],
     "r2_lstm_bwd_persist": [P, P, P, P, P, P, P, I, I, I, I, P, P, P],
     "r2_actor_finalize": [P] * 21 + [I, I, I, I, I, I, F, F, F, F, U64, P],

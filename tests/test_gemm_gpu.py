@@ -9,6 +9,15 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
 
 
+@pytest.fixture(params=[2, 5, 6, 7, 8], ids=["v1v2", "v4_256x64", "v4_256x32", "v4_128x64", "v4_128x32"])
+def gemm_version(request):
+    """2: 128x128 kernels (register-staged / LDS-DMA by K); 5..8: the 8-wave 256 x BN x BK kernels."""
+    from pytorch_r2d2_amd.ops._lib import kernels
+    kernels().r2_gemm_set_version(request.param)
+    yield request.param
+    kernels().r2_gemm_set_version(2)
+
+
 def _rel(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
@@ -22,9 +31,10 @@ def _op(rows, cols, kmajor, gen):
 
 @pytest.mark.parametrize("ak,bk", [(1, 1), (1, 0), (0, 1), (0, 0)])
 @pytest.mark.parametrize("M,N,K", [(296, 200, 64), (1024, 1568, 96), (136, 264, 1568), (64, 48, 40),
-                                   (520, 1568, 2560), (200, 136, 128)])
-def test_gemm_layouts(ak, bk, M, N, K):
-    """K % 64 == 0 runs the LDS-DMA kernel (v2), other K the register-staged one (v1)."""
+                                   (520, 1568, 2560), (200, 136, 128), (5440, 1024, 1568), (2560, 1568, 1024)])
+def test_gemm_layouts(ak, bk, M, N, K, gemm_version):
+    """K % 64 == 0 runs the LDS-DMA kernel (v2), other K the register-staged one (v1); version 5
+    runs every K % 8 == 0 shape on the 256x256 kernel (zero-block K tail)."""
     g = torch.Generator(device=DEV).manual_seed(M + N + K + 2 * ak + bk)
     a = _op(M, K, ak, g)
     b = _op(N, K, bk, g).t()          # (K, N) view; k-major means B^T rows contiguous
@@ -36,7 +46,7 @@ def test_gemm_layouts(ak, bk, M, N, K):
     assert _rel(c, ref) < 1e-5
 
 
-def test_gemm_row_map_accumulate_bf16_and_batch():
+def test_gemm_row_map_accumulate_bf16_and_batch(gemm_version):
     g = torch.Generator(device=DEV).manual_seed(3)
     M, N, K = 256, 1568, 128
     a = _op(K, M, 1, g).t()             # mn-major A (like dgates^T)

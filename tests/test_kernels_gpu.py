@@ -318,3 +318,44 @@ def test_sum_tree_sample_and_update():
     rp.rebuild_tree()
     torch.cuda.synchronize()
     assert torch.allclose(inc, rp.tree, rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("N", [2560, 333])
+def test_head_grads_and_colsum_match_torch(N):
+    """gradsum.hip: dueling last-layer weight/bias grads, layer-1 bias grads and the permuted
+    LSTM bias grads vs fp32 torch; bit-reproducible across launches (fixed-order reduction)."""
+    k = kernels()
+    g = torch.Generator(device=DEV).manual_seed(N)
+    A, HD, G = 6, 256, 1024
+    dva = torch.randn(N, 1 + A, generator=g, device=DEV)
+    zr = torch.relu(torch.randn(N, 2 * HD, generator=g, device=DEV)).bfloat16()
+    dz = torch.randn(N, 2 * HD, generator=g, device=DEV).bfloat16()
+    dgates = torch.randn(N, G, generator=g, device=DEV).bfloat16()
+    perm = torch.randperm(G, generator=torch.Generator().manual_seed(1)).to(DEV, torch.int32)
+    ws = torch.zeros(int(k.r2_gradsum_ws_floats()), device=DEV)
+    ticket = torch.zeros(64, dtype=torch.int32, device=DEV)
+    outs = []
+    for _ in range(2):
+        gw2 = torch.full((1 + A, HD), float("nan"), device=DEV)
+        gb2 = torch.full((1 + A,), float("nan"), device=DEV)
+        gb1 = torch.full((2 * HD,), float("nan"), device=DEV)
+        db = torch.full((G,), float("nan"), device=DEV)
+        db2 = torch.full((G,), float("nan"), device=DEV)
+        assert k.r2_head_grads(ptr(dva), ptr(zr), ptr(dz), ptr(gw2), ptr(gb2), ptr(gb1), N, A, HD,
+                               ptr(ws), ptr(ticket), stream_handle()) == 0
+        assert k.r2_colsum_bf16(ptr(dgates), N, G, ptr(perm), ptr(db), ptr(db2), ptr(ws),
+                                ptr(ticket[32:]), stream_handle()) == 0
+        torch.cuda.synchronize()
+        outs.append((gw2, gb2, gb1, db, db2))
+    gw2, gb2, gb1, db, db2 = outs[0]
+    g2 = dva.t() @ zr.float()
+    assert _rel(gw2[0], g2[0, :HD]) < 1e-5
+    assert _rel(gw2[1:], g2[1:, HD:]) < 1e-5
+    assert _rel(gb2, dva.sum(0)) < 1e-5
+    assert _rel(gb1, dz.float().sum(0)) < 1e-5
+    ref = torch.empty(G, device=DEV)
+    ref[perm.long()] = dgates.float().sum(0)
+    assert _rel(db, ref) < 1e-5 and torch.equal(db, db2)
+    assert int(ticket.abs().sum().item()) == 0          # last arrivers reset their tickets
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)

@@ -64,5 +64,22 @@ for v in (1, 2):
     res[f"dwih_v{v}_us"] = us
     us = timeit(lambda: gemm(Gemm(dg, W, Cx)))
     res[f"dx_v{v}_us"] = us
+# v3/v4 at the step's real K (1568: K % 16 path)
+for v in (2, 5, 7):
+    kernels().r2_gemm_set_version(v)
+    us = timeit(lambda: gemm(Gemm(X, W.t(), C, bias=bias)))
+    res[f"xp_v{v}_us"] = us
+    X2 = torch.randn(5440, 1568, device=DEV).to(bf)
+    C2 = torch.empty(5440, 1024, device=DEV)
+    us = timeit(lambda: gemm(Gemm(X, W.t(), C, bias=bias), Gemm(X2, W.t(), C2, bias=bias)))
+    res[f"xp2net_v{v}_us"] = us
+    err = (C - (X.float() @ W.float().t() + bias)).abs().max().item()
+    res[f"xp_v{v}_maxerr"] = err
+    us = timeit(lambda: gemm(Gemm(dg.t(), Xl, Cw)))
+    res[f"dwih_v{v}_us"] = us
+    err = (Cw - dg.float().t() @ Xl.float()).abs().max().item()
+    res[f"dwih_v{v}_maxerr"] = err
+    us = timeit(lambda: gemm(Gemm(dg, W, Cx)))
+    res[f"dx_v{v}_us"] = us
 kernels().r2_gemm_set_version(2)
 print(json.dumps({k: round(v, 1) for k, v in res.items()}))
