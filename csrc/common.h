@@ -30,12 +30,15 @@ __device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+// Activations on the hardware reciprocal (v_rcp_f32, 1 ulp) instead of an IEEE division: the
+// division expands to ~10 dependent VALU ops (div_scale / div_fmas / div_fixup) and sat on the
+// LSTM recurrence's critical path (10 of them per thread per step).
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float sigmoidf_(float x) { return fast_rcp(1.f + __expf(-x)); }
 __device__ __forceinline__ float tanhf_(float x) {
-  // tanh via exp; saturates cleanly for large |x|
-  float e = __expf(-2.f * fabsf(x));
-  float t = (1.f - e) / (1.f + e);
-  return copysignf(t, x);
+  // tanh via exp; saturates cleanly for large |x| (e -> 0)
+  const float e = __expf(-2.f * fabsf(x));
+  return copysignf((1.f - e) * fast_rcp(1.f + e), x);
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

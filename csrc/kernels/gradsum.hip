@@ -83,9 +83,13 @@ __device__ __forceinline__ void gs_gather(const float* ws_cb, int RS, int c, flo
     for (int q = 0; q < gs::QB; ++q) {
       if (q0 + q >= RS) break;
 #pragma unroll
-      for (int i = 0; i < gs::NV / 4; ++i)
+      for (int i = 0; i < gs::NV / 4; ++i) {
+        // whole-vector bit_cast: per-element bit_casts of the loaded u32x4 let the compiler
+        // shrink the b128 load to one dword and reuse it for all four elements (observed)
+        const f32x4 f = __builtin_bit_cast(f32x4, w[q][i]);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) t[4 * i + e] += __builtin_bit_cast(float, w[q][i][e]);
+        for (int e = 0; e < 4; ++e) t[4 * i + e] += f[e];
+      }
     }
   }
 }

@@ -16,5 +16,6 @@ if [ -n "$PROF_ARGS" ]; then
   rm -rf gpurun_out/prof
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -- python bench.py $PROF_ARGS > gpurun_out/prof.log 2>&1; rc=$?
   echo "PROF rc=$rc"; grep metric gpurun_out/prof.log | tail -1; stop_if_crash $rc
+  python tools/step_breakdown.py "gpurun_out/prof/*/*kernel_trace.csv" gpurun_out/breakdown.txt 5 | head -40
 fi
 exit 0
