@@ -47,6 +47,13 @@
 #define PL_CTR_WORDS (3 * PL_MAX_GROUPS * PL_CTR_STRIDE)
 #define PL_OFF_XMASK (PL_MAX_GROUPS * PL_CTR_STRIDE)
 #define PL_OFF_ARRIVE (2 * PL_MAX_GROUPS * PL_CTR_STRIDE)
+// tagged-hand-off kernels (below): finished-workgroup counter (zeroed with the counters) and the
+// launch epoch (never zeroed; advanced by the last workgroup of every launch)
+#define PT_DONE_OFF PL_CTR_WORDS
+#define PT_MEMSET_WORDS (PL_CTR_WORDS + 32)
+#define PT_EPOCH_FWD (PL_CTR_WORDS + 32)
+#define PT_EPOCH_BWD (PL_CTR_WORDS + 64)
+#define PT_CTR_WORDS (PL_CTR_WORDS + 96)
 
 struct PChain {
   const float* xproj;  // (T, B, G) packed, chain-local time
@@ -553,7 +560,339 @@ extern "C" int r2_lstm_bwd_persist(const float* dh_ext, const float* gates, cons
   return 0;
 }
 
-extern "C" int r2_lstm_persist_ctr_words() { return PL_CTR_WORDS; }
+// ============================================================================================
+// Forward v3: data-tagged granule hand-off (cdna_hip_programming / MI355X_MICROARCH price list,
+// "handoff-1to1": ~half the latency of a payload + flag / counter hand-off), 16-row batch tiles,
+// wave-owned gate columns.
+//
+//  * group = (chain, 16-row batch tile); its H/16 workgroups own 16 hidden units each; wave w of a
+//    workgroup owns units 4w..4w+3 of that slice, all four gates (16 MFMA columns), over the FULL
+//    K = H: no cross-wave K reduction, the gate exchange for the pointwise is wave-private LDS.
+//  * h_t is published as 8-byte granules {bf16 h[u], bf16 h[u+1], tag} (one store per granule,
+//    tag = epoch << 16 | t + 1) into a 2-slot ring; consumers poll the granules themselves with
+//    sc1 loads -- no counter, no drain, no ordering between granules.  Slot reuse is safe: a
+//    workgroup writes h_{t+1} only after every workgroup of its group has published h_t, i.e.
+//    finished loading h_{t-1} from that slot.  The epoch (advanced by the last workgroup of each
+//    launch) makes granules of earlier launches unmatchable, so the ring is never cleared.
+//  * same-XCD fast path as v2 (plain granule stores stay in the XCD's L2); sc1 stores otherwise.
+#define PT_ROWS 16
+
+struct PTArgs {
+  PChain ch[PL_MAX_CHAINS];
+  int B, T;
+  unsigned* ctr;
+  unsigned* err;
+  long long* dbg;
+  void* ring;     // (chains, 2, MB*16, H/2) granules
+  int MB, groups, xcd_map, force_slow;
+};
+
+__device__ __forceinline__ uint32_t pt_pack_bf16x2(float a, float b) {
+  bf16x2 v;
+  v[0] = (bf16)a;
+  v[1] = (bf16)b;
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+template <int H>
+__global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
+  constexpr int G = 4 * H;
+  constexpr int NWG = H / PL_UNITS;
+  constexpr int KS = H / 32;                  // 16x16x32 k-steps
+  constexpr int HS = H + 8;                   // bf16 stride of a staged h row (conflict-free b128)
+  constexpr int GR = H / 2;                   // granules per row
+  constexpr int CPR = H / 4;                  // 16-B chunks (2 granules) per row
+  constexpr int CH = PT_ROWS * CPR / 256;     // chunks per compute thread
+  constexpr int XS = 20;                      // fp32 stride of a gate-exchange row
+  static_assert(CH >= 1 && PT_ROWS * CPR % 256 == 0, "H");
+  // LDS: staged h (2 slots), wave-private gate exchange, x-projection ring (3 slots, filled by
+  // the I/O wave), per-step outputs (2 slots, drained by the I/O wave)
+  __shared__ __attribute__((aligned(16))) bf16 hin[2][PT_ROWS * HS];
+  __shared__ __attribute__((aligned(16))) float xch[4][PT_ROWS * XS];
+  __shared__ __attribute__((aligned(1024))) float xl[3][PT_ROWS * PL_GCOLS];
+  __shared__ __attribute__((aligned(16))) float oc[2][PT_ROWS * PL_UNITS];
+  __shared__ __attribute__((aligned(16))) float oh32[2][PT_ROWS * PL_UNITS];
+  __shared__ __attribute__((aligned(16))) bf16 ohs[2][PT_ROWS * PL_UNITS];
+  __shared__ __attribute__((aligned(16))) float og[2][PT_ROWS * PL_GCOLS];
+  __shared__ int flag;
+  int g, j;
+  if (!pl_decode(a.xcd_map, a.groups, NWG, g, j)) return;
+  const int MB = a.MB, mb = g % MB, chn = g / MB;
+  const PChain& cd = a.ch[chn];
+  const int B = a.B, T = a.T;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int rows_all = MB * PT_ROWS;
+  const uint32_t ring_bytes = (uint32_t)((size_t)a.groups / MB * 2 * rows_all * GR * 8);
+  const __amdgpu_buffer_rsrc_t rrs = pl_rsrc(a.ring, ring_bytes);
+  const unsigned ep = __hip_atomic_load(a.ctr + PT_EPOCH_FWD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int fast = pl_same_xcd(a.ctr, g, NWG, a.force_slow, a.err, &flag);
+  if (fast < 0) return;
+  if (a.dbg && tid == 0) {
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    a.dbg[256 + blockIdx.x] = (long long)(1000 + g * 100 + (x & 15) * 10 + fast);
+  }
+  const bool save_any = cd.gates != nullptr;
+
+  if (wave == 4) {
+    // ================= I/O wave: x-projection prefetch (2 steps ahead) + output drain.  Its
+    // loads and stores never sit in a compute wave's vmcnt queue in front of a granule poll.
+    auto io_load_x = [&](int t) {
+      float* dst = xl[t % 3];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int r = 4 * q + (lane >> 4);
+        const int b = min(mb * PT_ROWS + r, B - 1);
+        const float* src = cd.xproj + ((size_t)t * B + b) * G + j * PL_GCOLS + 4 * (lane & 15);
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(dst + q * 256),
+                                         16, 0, 0);
+      }
+    };
+    auto io_store = [&](int t) {
+      const int s = t & 1;
+      {
+        const int r = lane >> 2, q = lane & 3, b = mb * PT_ROWS + r;
+        if (b < B) {
+          const size_t o = ((size_t)t * B + b) * H + j * PL_UNITS + 4 * q;
+          *(f32x4*)(cd.c_seq + o) = *(const f32x4*)(oc[s] + r * PL_UNITS + 4 * q);
+          if (cd.h32) *(f32x4*)(cd.h32 + o) = *(const f32x4*)(oh32[s] + r * PL_UNITS + 4 * q);
+        }
+      }
+      if (lane < 32) {
+        const int r = lane >> 1, hf = lane & 1, b = mb * PT_ROWS + r;
+        if (b < B)
+          *(u32x4*)(cd.h_seq + ((size_t)t * B + b) * H + j * PL_UNITS + 8 * hf) =
+              *(const u32x4*)(ohs[s] + r * PL_UNITS + 8 * hf);
+      }
+      if (save_any && t >= cd.save_from) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = 4 * q + (lane >> 4), c4 = lane & 15, b = mb * PT_ROWS + r;
+          if (b < B)
+            *(f32x4*)(cd.gates + ((size_t)(t - cd.save_from) * B + b) * G + j * PL_GCOLS + 4 * c4) =
+                *(const f32x4*)(og[s] + r * PL_GCOLS + 4 * c4);
+        }
+      }
+    };
+    // x(t) must have landed by barrier t; the 4 DMA loads issued for x(t+2) in step t stay in
+    // flight across barrier t+1 (counted wait: vmcnt retires in order, the stores come first)
+    io_load_x(0);
+    if (T > 1) {
+      io_load_x(1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lds_sync();                                   // barrier 0
+    for (int t = 0; t < T; ++t) {
+      if (t >= 1) io_store(t - 1);
+      if (t + 2 < T) {
+        io_load_x(t + 2);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      if (a.dbg && g == 0 && j == 0 && lane == 0 && t + 1 < 32) a.dbg[(t + 1) * 8 + 6] = clock64();
+      lds_sync();                                 // barrier t + 1
+    }
+    io_store(T - 1);
+    return;
+  }
+
+  // ================= compute waves 0..3
+  auto goff = [&](int slot, int r, int p) -> uint32_t {
+    return (uint32_t)((((size_t)(chn * 2 + slot) * rows_all + mb * PT_ROWS + r) * GR + p) * 8);
+  };
+  // resident W_hh fragments: wave column c (0..15) = gate c>>2 of unit 4*wave + (c&3), i.e.
+  // packed row 16*(c>>2) + 4*wave + (c&3) of this workgroup's 64
+  bf16x8 wf[KS];
+  {
+    const int c = lane & 15;
+    const int n = 16 * (c >> 2) + 4 * wave + (c & 3);
+    const bf16* brow = cd.whh + ((size_t)j * PL_GCOLS + n) * H + 8 * (lane >> 4);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) wf[s] = *(const bf16x8*)(brow + 32 * s);
+  }
+  // pointwise ownership: lane = (row prow, unit 4*wave + pu); c lives in a register
+  const int prow = lane >> 2, pu = lane & 3;
+  const int ul = 4 * wave + pu, u = j * PL_UNITS + ul;
+  const int pb = mb * PT_ROWS + prow;
+  const bool pv = pb < B;
+  float creg = cd.c0[(size_t)(pv ? pb : B - 1) * H + u];
+  // compiler-visible drain of the one-time loads (W_hh fragments, c0): otherwise the waitcnt
+  // pass carries them as pending into the loop and waits on vmcnt inside every step -- behind
+  // that step's granule store
+  __builtin_amdgcn_s_waitcnt(0);
+  const bool trace = a.dbg && g == 0 && j == 0 && tid == 0;
+#define PT_TRACE(k) \
+  if (trace && t < 32) a.dbg[t * 8 + (k)] = clock64();
+
+  for (int t = 0; t < T; ++t) {
+    PT_TRACE(0);
+    bf16* hb = hin[t & 1];
+    if (t == 0) {
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const int c = tid + 256 * i, r = c / CPR, cc = c % CPR;
+        const int b = min(mb * PT_ROWS + r, B - 1);
+        *(u32x2*)(hb + r * HS + 4 * cc) = *(const u32x2*)(cd.h0 + (size_t)b * H + 4 * cc);
+      }
+    } else {
+      // h_{t-1}: poll the granules themselves (all CH loads in flight, then re-poll stragglers)
+      const unsigned want = (ep << 16) | (unsigned)t;
+      const int slot = (t - 1) & 1;
+      u32x4 v[CH];
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const int c = tid + 256 * i, r = c / CPR, cc = c % CPR;
+        v[i] = __builtin_amdgcn_raw_buffer_load_b128(rrs, goff(slot, r, 2 * cc), 0, 16);  // sc1
+      }
+      // re-poll every stale chunk at once: one round trip per retry round, not one per chunk
+      for (unsigned spins = 0;; ++spins) {
+        bool all = true;
+        bool ok[CH];
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          const int r = (tid + 256 * i) / CPR;
+          ok[i] = mb * PT_ROWS + r >= B || (v[i][1] == want && v[i][3] == want);
+          all = all && ok[i];
+        }
+        if (all) break;
+        if (spins > PL_SPIN_LIMIT) {
+          __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          const int c = tid + 256 * i, r = c / CPR, cc = c % CPR;
+          if (!ok[i]) v[i] = __builtin_amdgcn_raw_buffer_load_b128(rrs, goff(slot, r, 2 * cc), 0, 16);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < CH; ++i) {
+        const int c = tid + 256 * i, r = c / CPR, cc = c % CPR;
+        *(u32x2*)(hb + r * HS + 4 * cc) = u32x2{v[i][0], v[i][2]};
+      }
+    }
+    PT_TRACE(5);
+    lds_sync();                                   // barrier t (with the I/O wave)
+    PT_TRACE(1);
+    // gates of this wave's 16 columns for the 16 rows: acc[e] = C[4(l>>4)+e][l&15]
+    bf16x8 av[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) av[s] = *(const bf16x8*)(hb + (lane & 15) * HS + 32 * s + 8 * (lane >> 4));
+    float xv[4];
+    {
+      const float* xr = xl[t % 3] + prow * PL_GCOLS + ul;
+#pragma unroll
+      for (int gi = 0; gi < 4; ++gi) xv[gi] = xr[16 * gi];
+    }
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; s += 2) {
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[s], wf[s], acc0, 0, 0, 0);
+      if (s + 1 < KS) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[s + 1], wf[s + 1], acc1, 0, 0, 0);
+    }
+    // wave-private exchange: column c = (gate c>>2, unit c&3) -> xch[row][unit][gate]
+    {
+      float* xw = xch[wave];
+      const int c = lane & 15;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) xw[(4 * (lane >> 4) + e) * XS + (c & 3) * 4 + (c >> 2)] = acc0[e] + acc1[e];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const f32x4 gp = *(const f32x4*)(xch[wave] + prow * XS + pu * 4);
+    PT_TRACE(2);
+    const float si = sigmoidf_(gp[0] + xv[0]);
+    const float sf = sigmoidf_(gp[1] + xv[1]);
+    const float tg = tanhf_(gp[2] + xv[2]);
+    const float so = sigmoidf_(gp[3] + xv[3]);
+    creg = sf * creg + si * tg;
+    const float hv = so * tanhf_(creg);
+    const float hp = __shfl_xor(hv, 1, 64);      // partner unit of the granule
+    PT_TRACE(3);
+    // publish h_t: even units store {h[u], h[u+1], tag} (one 8-byte store per granule)
+    const uint32_t hpair = pt_pack_bf16x2(hv, hp);
+    if (pv && (pu & 1) == 0) {
+      const u32x2 gr = {hpair, (ep << 16) | (unsigned)(t + 1)};
+      const uint32_t off = goff(t & 1, prow, u >> 1);
+      if (fast) __builtin_amdgcn_raw_buffer_store_b64(gr, rrs, off, 0, 0);   // stays in the XCD's L2
+      else __builtin_amdgcn_raw_buffer_store_b64(gr, rrs, off, 0, 16);       // sc1 write-through
+    }
+    PT_TRACE(4);
+    // outputs of step t for the I/O wave (LDS; drained after barrier t + 1)
+    {
+      const int s = t & 1;
+      oc[s][prow * PL_UNITS + ul] = creg;
+      oh32[s][prow * PL_UNITS + ul] = hv;
+      ohs[s][prow * PL_UNITS + ul] = (bf16)hv;
+      if (save_any) {
+        float* gq = og[s] + prow * PL_GCOLS + ul;
+        gq[0] = si;
+        gq[16] = sf;
+        gq[32] = tg;
+        gq[48] = so;
+      }
+    }
+  }
+#undef PT_TRACE
+  lds_sync();                                     // barrier T: outputs of step T-1 complete
+  // the last workgroup to finish advances the epoch (every workgroup read it before any finished)
+  if (tid == 0) {
+    const unsigned done = __hip_atomic_fetch_add(a.ctr + PT_DONE_OFF, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (done == (unsigned)(a.groups * NWG) - 1)
+      __hip_atomic_fetch_add(a.ctr + PT_EPOCH_FWD, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+extern "C" int r2_lstm_tag_ring_bytes(int n_chains, int B, int H) {
+  const long long n = (long long)n_chains * 2 * ((B + PT_ROWS - 1) / PT_ROWS) * PT_ROWS * (H / 2) * 8;
+  return n < (1ll << 31) ? (int)n : -1;
+}
+
+// Same chain layout / ctr as r2_lstm_fwd_persist; ring: r2_lstm_tag_ring_bytes bytes, any content.
+// Returns -3 when the grid cannot be co-resident at one workgroup per CU (caller falls back).
+extern "C" int r2_lstm_fwd_tag(const int64_t* chain_ptrs, int n_chains, int B, int T, int H,
+                               unsigned* ctr, unsigned* err, void* ring, void* stream) {
+  if (n_chains < 1 || n_chains > PL_MAX_CHAINS || B < 1) return -1;
+  if (H != 64 && H != 128 && H != 256 && H != 512) return -2;
+  const int MB = (B + PT_ROWS - 1) / PT_ROWS, nwg = H / PL_UNITS;
+  const int groups = n_chains * MB;
+  if (groups * nwg > 256 || groups > PL_MAX_GROUPS) return -3;
+  if ((size_t)T * B * H * 4 >= (1ull << 32) || T >= 65535 ||
+      r2_lstm_tag_ring_bytes(n_chains, B, H) < 0) return -4;
+  PTArgs args;
+  for (int c = 0; c < n_chains; ++c) {
+    const int64_t* p = chain_ptrs + 9 * c;
+    PChain& ch = args.ch[c];
+    ch.xproj = (const float*)p[0]; ch.whh = (const bf16*)p[1]; ch.h0 = (const bf16*)p[2];
+    ch.c0 = (const float*)p[3]; ch.h_seq = (bf16*)p[4]; ch.c_seq = (float*)p[5];
+    ch.h32 = (float*)p[6]; ch.gates = (float*)p[7]; ch.save_from = (int)p[8]; ch.pad_ = 0;
+  }
+  args.B = B; args.T = T; args.ctr = ctr; args.err = err; args.dbg = g_pl_dbg; args.ring = ring;
+  args.MB = MB; args.groups = groups; args.xcd_map = groups <= 8 && nwg <= 32;
+  args.force_slow = g_pl_slow;
+  hipStream_t s = (hipStream_t)stream;
+  hipMemsetAsync(ctr, 0, PT_MEMSET_WORDS * sizeof(unsigned), s);
+  dim3 grid(args.xcd_map ? 8 * nwg : groups * nwg), block(320);   // 4 compute waves + 1 I/O wave
+  const void* fn = H == 64 ? (const void*)lstm_fwd_tag_kernel<64>
+                 : H == 128 ? (const void*)lstm_fwd_tag_kernel<128>
+                 : H == 256 ? (const void*)lstm_fwd_tag_kernel<256>
+                            : (const void*)lstm_fwd_tag_kernel<512>;
+  hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, PL_LDS_RESERVE);
+  switch (H) {
+    case 64: hipLaunchKernelGGL(lstm_fwd_tag_kernel<64>, grid, block, PL_LDS_RESERVE, s, args); break;
+    case 128: hipLaunchKernelGGL(lstm_fwd_tag_kernel<128>, grid, block, PL_LDS_RESERVE, s, args); break;
+    case 256: hipLaunchKernelGGL(lstm_fwd_tag_kernel<256>, grid, block, PL_LDS_RESERVE, s, args); break;
+    default: hipLaunchKernelGGL(lstm_fwd_tag_kernel<512>, grid, block, PL_LDS_RESERVE, s, args); break;
+  }
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int r2_lstm_persist_ctr_words() { return PT_CTR_WORDS; }
 
 // ---- placement probe (tools / tests): XCC id of every block of a launch
 __global__ void xcc_probe_kernel(int* out, int spin) {

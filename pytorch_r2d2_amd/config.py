@@ -89,6 +89,9 @@ class LearnerConfig:
     target_mode: str = "shifted"
     compute_dtype: str = "bf16"
     lstm_impl: str = "persistent"     # persistent (one launch per sequence) | step (launch per t)
+    # persistent forward hand-off: "tagged" (8-byte {h pair, tag} granules polled directly, 16-row
+    # batch tiles; falls back when the grid does not fit) | "counter" (payload + arrival counter)
+    lstm_handoff: str = "tagged"
     # forward pipelining ("shifted" mode, persistent LSTM): the frames are processed in this many
     # time chunks; the recurrence of chunk c runs on a side stream on CUs the torso leaves free
     # while the torso + input projection of chunk c+1 run.  0/1 = serial forward (default:

@@ -187,6 +187,8 @@ class LearnerEngine:
         self.dc = z(B, H)
         self.slab_p = z(2, nwg, B, H)
         self.ctr = z(int(kernels().r2_lstm_persist_ctr_words()), dt=torch.int32)
+        # granule ring of the tagged forward hand-off (up to 4 chains per launch)
+        self.ring = z(max(int(kernels().r2_lstm_tag_ring_bytes(4, B, H)), 16) // 4, dt=torch.int32)
         self.err = z(1, dt=torch.int32)
         self.dgates = z(Ll * B, G, dt=bf16)
         self.gamma_n = float(lc.gamma ** n)
@@ -306,6 +308,12 @@ class LearnerEngine:
         k = kernels()
         arr = np.asarray([v for c in chains for v in c], dtype=np.int64)
         if self.cfg.learner.lstm_impl == "persistent" and t_begin == 0:
+            if self.cfg.learner.lstm_handoff == "tagged":
+                rc = k.r2_lstm_fwd_tag(arr.ctypes.data, len(chains), self.B, T, self.layout.H,
+                                       ptr(self.ctr), ptr(self.err), ptr(self.ring), stream_handle())
+                if rc != -3:          # -3: grid too large for one workgroup per CU
+                    check(rc, "lstm_fwd_tag")
+                    return
             check(k.r2_lstm_fwd_persist(arr.ctypes.data, len(chains), self.B, T, self.layout.H,
                                         ptr(self.ctr), ptr(self.err), stream_handle()),
                   "lstm_fwd_persist")

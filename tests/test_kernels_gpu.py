@@ -31,7 +31,7 @@ def _setup(B=8, H=256, seed=0):
     return cfg, net.to(DEV), L, flat, L.packed_views(bf, f32)
 
 
-@pytest.mark.parametrize("impl", ["step", "persistent"])
+@pytest.mark.parametrize("impl", ["step", "persistent", "tagged"])
 @pytest.mark.parametrize("B,H", [(8, 256), (64, 256), (40, 128), (128, 256), (16, 512), (33, 64)])
 def test_lstm_forward_matches_lstmcell(B, H, impl):
     cfg, net, L, flat, pk = _setup(B, H)
@@ -76,10 +76,16 @@ def test_lstm_forward_matches_lstmcell(B, H, impl):
     else:
         ctr = torch.zeros(int(kernels().r2_lstm_persist_ctr_words()), dtype=torch.int32, device=DEV)
         err = torch.zeros(1, dtype=torch.int32, device=DEV)
-        rc = kernels().r2_lstm_fwd_persist(arr.ctypes.data, 2, B, T, H, ptr(ctr), ptr(err),
-                                           stream_handle())
+        if impl == "tagged":
+            ring = torch.full((kernels().r2_lstm_tag_ring_bytes(2, B, H) // 4,), -1,
+                              dtype=torch.int32, device=DEV)   # garbage content is fine
+            rc = kernels().r2_lstm_fwd_tag(arr.ctypes.data, 2, B, T, H, ptr(ctr), ptr(err),
+                                           ptr(ring), stream_handle())
+        else:
+            rc = kernels().r2_lstm_fwd_persist(arr.ctypes.data, 2, B, T, H, ptr(ctr), ptr(err),
+                                               stream_handle())
     assert rc == 0
-    if impl == "persistent":
+    if impl != "step":
         torch.cuda.synchronize()
         assert err.item() == 0
     torch.cuda.synchronize()
@@ -195,6 +201,51 @@ def test_lstm_persistent_same_xcd_path_matches_sc1_path(B):
     k.r2_lstm_persist_force_slow(0)
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B", [64, 24])
+def test_lstm_tagged_repeated_launches_and_placement(B):
+    """Tagged forward hand-off: (1) granules left in the ring by earlier launches are never
+    accepted (epoch tags): back-to-back launches with different inputs each match the counter
+    kernel; (2) the same-XCD plain-store path and the sc1 path are bit-identical."""
+    cfg, net, L, flat, pk = _setup(B, 256, seed=3)
+    H, G, T = 256, 1024, 10
+    k = kernels()
+    nw = int(k.r2_lstm_persist_ctr_words())
+    ctr = torch.zeros(nw, dtype=torch.int32, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ring = torch.zeros(k.r2_lstm_tag_ring_bytes(2, B, H) // 4, dtype=torch.int32, device=DEV)
+    h0 = (torch.randn(B, H, device=DEV) * 0.3).bfloat16()
+    c0 = torch.randn(B, H, device=DEV) * 0.3
+
+    def run(fn_name, xproj, slow=0):
+        k.r2_lstm_persist_force_slow(slow)
+        hseq = torch.zeros(T, B, H, dtype=torch.bfloat16, device=DEV)
+        cseq = torch.zeros(T, B, H, device=DEV)
+        arr = np.asarray([ptr(xproj), ptr(pk["w_hh"]), ptr(h0), ptr(c0), ptr(hseq), ptr(cseq), 0,
+                          0, 0] * 2, dtype=np.int64)
+        if fn_name == "tag":
+            rc = k.r2_lstm_fwd_tag(arr.ctypes.data, 2, B, T, H, ptr(ctr), ptr(err), ptr(ring),
+                                   stream_handle())
+        else:
+            rc = k.r2_lstm_fwd_persist(arr.ctypes.data, 2, B, T, H, ptr(ctr), ptr(err),
+                                       stream_handle())
+        assert rc == 0
+        torch.cuda.synchronize()
+        k.r2_lstm_persist_force_slow(0)
+        assert err.item() == 0
+        return hseq, cseq
+
+    for it in range(4):
+        xproj = torch.randn(T * B, G, device=DEV) * (0.5 + it)
+        h_t, c_t = run("tag", xproj, slow=it % 2)
+        h_p, c_p = run("persist", xproj)
+        assert _rel(c_t, c_p) < 1e-4, it
+        assert _rel(h_t.float(), h_p.float()) < 1e-2, it
+    xproj = torch.randn(T * B, G, device=DEV)
+    a = run("tag", xproj, slow=0)
+    b = run("tag", xproj, slow=1)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
 
 
 def test_torso_matches_conv_stack():

@@ -52,8 +52,13 @@ for c in range(2):
 ctr = torch.zeros(int(k.r2_lstm_persist_ctr_words()), dtype=torch.int32, device=DEV)
 err = torch.zeros(1, dtype=torch.int32, device=DEV)
 arr = np.asarray([v for ch in chains for v in ch], dtype=np.int64)
-fwd = lambda: k.r2_lstm_fwd_persist(arr.ctypes.data, 2, B, T, H, ptr(ctr), ptr(err), stream_handle())
-res["fwd_us_per_step"] = timeit(fwd) / T
+fwd_ctr = lambda: k.r2_lstm_fwd_persist(arr.ctypes.data, 2, B, T, H, ptr(ctr), ptr(err), stream_handle())
+ring = torch.zeros(k.r2_lstm_tag_ring_bytes(2, B, H) // 4, dtype=torch.int32, device=DEV)
+fwd_tag = lambda: k.r2_lstm_fwd_tag(arr.ctypes.data, 2, B, T, H, ptr(ctr), ptr(err), ptr(ring),
+                                    stream_handle())
+res["fwd_counter_us_per_step"] = timeit(fwd_ctr) / T
+res["fwd_us_per_step"] = timeit(fwd_tag) / T
+fwd = fwd_tag
 dh = torch.randn(40, B, H, device=DEV)
 slab = torch.zeros(2, 16, B, H, device=DEV)
 dg = torch.zeros(40, B, G, dtype=torch.bfloat16, device=DEV)
@@ -70,5 +75,7 @@ res['blocks_g_xcc_fast'] = [int(v) - 1000 for v in dbg[256:].cpu() if v > 0]
 res["fwd_trace_cycles_wait_mma_pointwise_publish_next"] = [
     [int(t[i][1] - t[i][0]), int(t[i][2] - t[i][1]), int(t[i][3] - t[i][2]), int(t[i][4] - t[i][3]),
      int(t[i + 1][0] - t[i][4])] for i in range(1, 12)]
+res["fwd_trace_poll_barrier_ioarrive_minus_poll"] = [
+    [int(t[i][5] - t[i][0]), int(t[i][1] - t[i][5]), int(t[i][6] - t[i][5])] for i in range(1, 12)]
 res["err"] = int(err.item())
 print(json.dumps(res))
