@@ -892,6 +892,259 @@ extern "C" int r2_lstm_fwd_tag(const int64_t* chain_ptrs, int n_chains, int B, i
   return 0;
 }
 
+// ============================================================================================
+// BPTT v3: tagged-granule reduce-scatter of the recurrent dh partials, 16-row batch tiles.
+//
+//  * group = 16-row batch tile; its H/16 workgroups own 16 units each (pointwise), and 64 packed
+//    gate columns each (the partial product dgates_t[:, own 64] @ W_hh[own 64, :] over ALL H
+//    units, 4 N tiles of 16 units per wave, K = 64, W_hh^T fragments resident in VGPRs).
+//  * partials are published as 8-byte granules {fp32 partial, tag} into a 2-slot ring
+//    [slot][source workgroup][row][unit]; a consumer gathers its 16 units from all sources with
+//    sc1 b128 loads (2 granules each), re-polls stale ones together, and sums them in source
+//    order (deterministic).  Slot reuse: a source publishes iteration k+2's partials only after
+//    consuming iteration k+1's from every source, i.e. after every consumer finished iteration k.
+//  * an I/O wave prefetches the per-step operands (saved gates, c_t, c_{t-1}, dh_ext) two steps
+//    ahead into an LDS ring and drains the dgates tiles; compute waves keep only granule traffic.
+struct PTBArgs {
+  const float* dh_ext;  // (Tl, B, H) or null
+  const float* gates;   // (Tl, B, G) packed post-activation
+  const float* c_seq;   // (T, B, H)
+  const float* c0;      // (B, H)
+  const bf16* whhT;     // packed (NWG, H, 64)
+  bf16* dgates;         // (Tl, B, G)
+  void* ring;           // (2, NWG, MB*16, H) granules
+  int B, T, t0;
+  unsigned* ctr;
+  unsigned* err;
+  int MB, xcd_map, force_slow, pad_;
+};
+
+template <int H>
+__global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
+  constexpr int G = 4 * H;
+  constexpr int NWG = H / PL_UNITS;
+  constexpr int NTW = H / 64;                 // 16-unit N tiles per wave (4 waves x 16 x NTW = H)
+  constexpr int DS = PL_GCOLS + 8;            // bf16 stride of the dgates tile rows (144 B)
+  constexpr int SRCH = NWG / 2;               // sources per consumer half
+  static_assert(NTW >= 1 && NWG % 2 == 0, "H");
+  __shared__ __attribute__((aligned(16))) bf16 dgl[2][PT_ROWS * DS];
+  __shared__ __attribute__((aligned(16))) float red[2][PT_ROWS * PL_UNITS];
+  __shared__ __attribute__((aligned(1024))) float gl[3][PT_ROWS * PL_GCOLS];  // saved gates
+  __shared__ __attribute__((aligned(1024))) float cl[3][PT_ROWS * PL_UNITS];  // c_t
+  __shared__ __attribute__((aligned(1024))) float cpl[3][PT_ROWS * PL_UNITS]; // c_{t-1}
+  __shared__ __attribute__((aligned(1024))) float dhl[3][PT_ROWS * PL_UNITS]; // dh_ext
+  __shared__ int flag;
+  int mb, j;
+  if (!pl_decode(a.xcd_map, a.MB, NWG, mb, j)) return;
+  const int B = a.B, T = a.T, t0 = a.t0, K = T - t0;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int rows_all = a.MB * PT_ROWS;
+  const uint32_t ring_bytes = (uint32_t)((size_t)2 * NWG * rows_all * H * 8);
+  const __amdgpu_buffer_rsrc_t rrs = pl_rsrc(a.ring, ring_bytes);
+  const unsigned ep = __hip_atomic_load(a.ctr + PT_EPOCH_BWD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int fast = pl_same_xcd(a.ctr, mb, NWG, a.force_slow, a.err, &flag);
+  if (fast < 0) return;
+  auto goff = [&](int slot, int src, int r, int unit) -> uint32_t {
+    return (uint32_t)((((size_t)(slot * NWG + src) * rows_all + mb * PT_ROWS + r) * H + unit) * 8);
+  };
+
+  if (wave == 4) {
+    // ================= I/O wave
+    auto io_load = [&](int k) {       // operands of iteration k (step t = T-1-k) into slot k % 3
+      const int t = T - 1 - k, tl = t - t0, s = k % 3;
+      typedef __attribute__((address_space(3))) void lds_t;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {   // gates: 16 rows x 64 fp32
+        const int r = 4 * q + (lane >> 4), b = min(mb * PT_ROWS + r, B - 1);
+        __builtin_amdgcn_global_load_lds(a.gates + ((size_t)tl * B + b) * G + j * PL_GCOLS + 4 * (lane & 15),
+                                         (lds_t*)(gl[s] + q * 256), 16, 0, 0);
+      }
+      const int r = lane >> 2, b = min(mb * PT_ROWS + r, B - 1);
+      const size_t hidx = (size_t)b * H + j * PL_UNITS + 4 * (lane & 3);
+      __builtin_amdgcn_global_load_lds(a.c_seq + (size_t)t * B * H + hidx, (lds_t*)cl[s], 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((t == 0 ? a.c0 : a.c_seq + (size_t)(t - 1) * B * H) + hidx,
+                                       (lds_t*)cpl[s], 16, 0, 0);
+      if (a.dh_ext)
+        __builtin_amdgcn_global_load_lds(a.dh_ext + (size_t)tl * B * H + hidx, (lds_t*)dhl[s], 16, 0, 0);
+    };
+    const int nload = a.dh_ext ? 7 : 6;     // DMA instructions per io_load
+    auto io_store = [&](int k) {      // dgates tile of iteration k
+      const int tl = T - 1 - k - t0, s = k & 1;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int c = lane + 64 * q, r = c >> 3, ch = c & 7, b = mb * PT_ROWS + r;
+        if (b < B)
+          *(u32x4*)(a.dgates + ((size_t)tl * B + b) * G + j * PL_GCOLS + 8 * ch) =
+              *(const u32x4*)(dgl[s] + r * DS + 8 * ch);
+      }
+    };
+    io_load(0);
+    if (K > 1) io_load(1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int k = 0; k < K; ++k) {
+      lds_sync();                         // barrier A_k: operands of k landed
+      if (k >= 1) io_store(k - 1);
+      const bool more = k + 2 < K;
+      if (more) io_load(k + 2);
+      lds_sync();                         // barrier B_k
+      // operands of k+1 (issued in iteration k-1) must land before barrier A_{k+1}
+      if (more) {
+        if (nload == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    lds_sync();                           // barrier E: dgates of the last iteration complete
+    io_store(K - 1);
+    return;
+  }
+
+  // ================= compute waves 0..3
+  // W_hh^T fragments: N tile q of this wave = units (H/4)*wave + 16*q + (l&15); B[k][n] = Whh_pk[j][k][n]
+  bf16x8 wt[NTW][2];
+#pragma unroll
+  for (int q = 0; q < NTW; ++q) {
+    const int n = (H / 4) * wave + 16 * q + (lane & 15);
+    const bf16* brow = a.whhT + ((size_t)j * H + n) * PL_GCOLS + 8 * (lane >> 4);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) wt[q][s] = *(const bf16x8*)(brow + 32 * s);
+  }
+  const int prow = lane >> 2, pu = lane & 3;
+  const int ul = 4 * wave + pu;
+  const bool pv = mb * PT_ROWS + prow < B;
+  float dcr = 0.f;
+  // consumer ownership of the partial gather: (row, unit pair) x source half
+  const int cmb = tid & 127, cr = cmb >> 3, cp2 = 2 * (cmb & 7), sh = tid >> 7;
+  const bool crow_ok = mb * PT_ROWS + cr < B;
+  __builtin_amdgcn_s_waitcnt(0);          // drain the one-time loads (see the forward kernel)
+
+  for (int k = 0; k < K; ++k) {
+    const int t = T - 1 - k;
+    if (k > 0) {
+      const unsigned want = (ep << 16) | (unsigned)k;
+      const int slot = (k - 1) & 1;
+      u32x4 v[SRCH];
+#pragma unroll
+      for (int i = 0; i < SRCH; ++i)
+        v[i] = __builtin_amdgcn_raw_buffer_load_b128(rrs, goff(slot, sh * SRCH + i, cr, j * PL_UNITS + cp2), 0, 16);
+      for (unsigned spins = 0;; ++spins) {
+        bool all = true;
+        bool ok[SRCH];
+#pragma unroll
+        for (int i = 0; i < SRCH; ++i) {
+          ok[i] = !crow_ok || (v[i][1] == want && v[i][3] == want);
+          all = all && ok[i];
+        }
+        if (all) break;
+        if (spins > PL_SPIN_LIMIT) {
+          __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < SRCH; ++i)
+          if (!ok[i]) v[i] = __builtin_amdgcn_raw_buffer_load_b128(rrs, goff(slot, sh * SRCH + i, cr, j * PL_UNITS + cp2), 0, 16);
+      }
+      // NOTE: __builtin_bit_cast of single vector ELEMENTS is miscompiled here (ROCm 7.2: every
+      // element read as element 0); cast whole vectors, then index
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int i = 0; i < SRCH; ++i) {
+        const f32x4 f = __builtin_bit_cast(f32x4, v[i]);
+        s0 += f[0];
+        s1 += f[2];
+      }
+      *(float2*)(red[sh] + cr * PL_UNITS + cp2) = make_float2(s0, s1);
+    }
+    lds_sync();                           // barrier A_k
+    // ---- pointwise (row prow, unit ul)
+    const int s3 = k % 3;
+    float dh = a.dh_ext ? dhl[s3][prow * PL_UNITS + ul] : 0.f;
+    if (k > 0) dh += red[0][prow * PL_UNITS + ul] + red[1][prow * PL_UNITS + ul];
+    const float* gq = gl[s3] + prow * PL_GCOLS + ul;
+    const float gi = gq[0], gf = gq[16], gg = gq[32], go = gq[48];
+    const float ct = cl[s3][prow * PL_UNITS + ul], cpv = cpl[s3][prow * PL_UNITS + ul];
+    const float tc = tanhf_(ct);
+    const float dc = dcr + dh * go * (1.f - tc * tc);
+    const float d_o = dh * tc;
+    dcr = dc * gf;
+    bf16* drow = dgl[k & 1] + prow * DS + ul;
+    drow[0] = (bf16)(pv ? dc * gg * gi * (1.f - gi) : 0.f);
+    drow[16] = (bf16)(pv ? dc * cpv * gf * (1.f - gf) : 0.f);
+    drow[32] = (bf16)(pv ? dc * gi * (1.f - gg * gg) : 0.f);
+    drow[48] = (bf16)(pv ? d_o * go * (1.f - go) : 0.f);
+    lds_sync();                           // barrier B_k: dgates tile complete
+    if (t > t0) {
+      // ---- partial dh_{t-1}[r][n] = sum_k dg[r][k] Whh_pk[j][k][n], published as granules
+      const bf16* arow = dgl[k & 1] + (lane & 15) * DS + 8 * (lane >> 4);
+      const bf16x8 a0 = *(const bf16x8*)arow, a1 = *(const bf16x8*)(arow + 32);
+      const unsigned tag = (ep << 16) | (unsigned)(k + 1);
+      const int slot = k & 1;
+#pragma unroll
+      for (int q = 0; q < NTW; ++q) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, wt[q][0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, wt[q][1], acc, 0, 0, 0);
+        const int n = (H / 4) * wave + 16 * q + (lane & 15);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * (lane >> 4) + e;
+          if (mb * PT_ROWS + r < B) {
+            const u32x2 gr = {__float_as_uint(acc[e]), tag};
+            const uint32_t off = goff(slot, j, r, n);
+            if (fast) __builtin_amdgcn_raw_buffer_store_b64(gr, rrs, off, 0, 0);
+            else __builtin_amdgcn_raw_buffer_store_b64(gr, rrs, off, 0, 16);
+          }
+        }
+      }
+    }
+  }
+  lds_sync();                             // barrier E
+  if (tid == 0) {
+    const unsigned done = __hip_atomic_fetch_add(a.ctr + PT_DONE_OFF, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (done == (unsigned)(a.MB * NWG) - 1)
+      __hip_atomic_fetch_add(a.ctr + PT_EPOCH_BWD, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+extern "C" int r2_lstm_bwd_tag_ring_bytes(int B, int H) {
+  const long long n = 2ll * (H / PL_UNITS) * ((B + PT_ROWS - 1) / PT_ROWS) * PT_ROWS * H * 8;
+  return n < (1ll << 31) ? (int)n : -1;
+}
+
+// Same operands as r2_lstm_bwd_persist minus the slab; ring: r2_lstm_bwd_tag_ring_bytes bytes,
+// any content.  -3: grid too large for one workgroup per CU (caller falls back).
+extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const float* c_seq,
+                               const float* c0, const bf16* whhT, bf16* dgates, int B, int T,
+                               int t0, int H, unsigned* ctr, unsigned* err, void* ring, void* stream) {
+  if (B < 1 || T < 1 || t0 < 0 || t0 >= T) return -1;
+  if (H != 64 && H != 128 && H != 256 && H != 512) return -2;
+  const int MB = (B + PT_ROWS - 1) / PT_ROWS, nwg = H / PL_UNITS;
+  if (MB * nwg > 256 || MB > PL_MAX_GROUPS) return -3;
+  if ((size_t)T * B * (size_t)(4 * H) * 4 >= (1ull << 32) || r2_lstm_bwd_tag_ring_bytes(B, H) < 0 ||
+      T - t0 >= 65535) return -4;
+  const int xmap = MB <= 8 && nwg <= 32;
+  PTBArgs args{dh_ext, gates, c_seq, c0, whhT, dgates, ring, B, T, t0, ctr, err, MB, xmap, g_pl_slow, 0};
+  hipStream_t s = (hipStream_t)stream;
+  hipMemsetAsync(ctr, 0, PT_MEMSET_WORDS * sizeof(unsigned), s);
+  dim3 grid(xmap ? 8 * nwg : MB * nwg), block(320);
+  const void* fn = H == 64 ? (const void*)lstm_bwd_tag_kernel<64>
+                 : H == 128 ? (const void*)lstm_bwd_tag_kernel<128>
+                 : H == 256 ? (const void*)lstm_bwd_tag_kernel<256>
+                            : (const void*)lstm_bwd_tag_kernel<512>;
+  hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, PL_LDS_RESERVE);
+  switch (H) {
+    case 64: hipLaunchKernelGGL(lstm_bwd_tag_kernel<64>, grid, block, PL_LDS_RESERVE, s, args); break;
+    case 128: hipLaunchKernelGGL(lstm_bwd_tag_kernel<128>, grid, block, PL_LDS_RESERVE, s, args); break;
+    case 256: hipLaunchKernelGGL(lstm_bwd_tag_kernel<256>, grid, block, PL_LDS_RESERVE, s, args); break;
+    default: hipLaunchKernelGGL(lstm_bwd_tag_kernel<512>, grid, block, PL_LDS_RESERVE, s, args); break;
+  }
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int r2_lstm_persist_ctr_words() { return PT_CTR_WORDS; }
 
 // ---- placement probe (tools / tests): XCC id of every block of a launch

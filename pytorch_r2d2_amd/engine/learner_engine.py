@@ -189,6 +189,7 @@ class LearnerEngine:
         self.ctr = z(int(kernels().r2_lstm_persist_ctr_words()), dt=torch.int32)
         # granule ring of the tagged forward hand-off (up to 4 chains per launch)
         self.ring = z(max(int(kernels().r2_lstm_tag_ring_bytes(4, B, H)), 16) // 4, dt=torch.int32)
+        self.ring_b = z(max(int(kernels().r2_lstm_bwd_tag_ring_bytes(B, H)), 16) // 4, dt=torch.int32)
         self.err = z(1, dt=torch.int32)
         self.dgates = z(Ll * B, G, dt=bf16)
         self.gamma_n = float(lc.gamma ** n)
@@ -544,16 +545,7 @@ class LearnerEngine:
             dh = mm_f32(self.dz, pk["head1"])                           # (N, H)
         if not fused_hg:
             gb1.copy_(mm_f32(self.ones_bf[:, :N], self.dz))
-        if self.cfg.learner.lstm_impl == "persistent":
-            check(k.r2_lstm_bwd_persist(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]),
-                                        ptr(self.c0["on"]), ptr(pk["w_hhT"]), ptr(self.slab_p),
-                                        ptr(self.dgates), B, T, Lb, H, ptr(self.ctr), ptr(self.err),
-                                        s), "lstm_bwd_persist")
-        else:
-            self.dc.zero_()
-            check(k.r2_lstm_bwd(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]), ptr(self.c0["on"]),
-                                ptr(pk["w_hhT"]), ptr(self.slab0), ptr(self.slab1), ptr(self.dc),
-                                ptr(self.dgates), B, T, Lb, H, s), "lstm_bwd")
+        self._lstm_bwd(dh)
         X = self.X_on[Lb * B: T * B]
         if Lb >= 1:
             h_prev = self.hseq["on"][Lb - 1: T - 1].reshape(N, H)
@@ -580,6 +572,30 @@ class LearnerEngine:
             L.view(g, "lstm.bias_ih").copy_(db)
             L.view(g, "lstm.bias_hh").copy_(db)
             self._dX = torch.mm(self.dgates, pk["w_ih"])               # (N, D) bf16
+
+    def _lstm_bwd(self, dh: torch.Tensor) -> None:
+        """BPTT over the learning window: dgates (Ll, B, G) from dh (Ll, B, H)."""
+        k = kernels()
+        s = stream_handle()
+        B, T, Lb, H, pk = self.B, self.T, self.Lb, self.layout.H, self.pk
+        lc = self.cfg.learner
+        if lc.lstm_impl == "persistent" and lc.lstm_handoff == "tagged":
+            rc = k.r2_lstm_bwd_tag(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]), ptr(self.c0["on"]),
+                                   ptr(pk["w_hhT"]), ptr(self.dgates), B, T, Lb, H, ptr(self.ctr),
+                                   ptr(self.err), ptr(self.ring_b), s)
+            if rc != -3:          # -3: grid too large for one workgroup per CU
+                check(rc, "lstm_bwd_tag")
+                return
+        if lc.lstm_impl == "persistent":
+            check(k.r2_lstm_bwd_persist(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]),
+                                        ptr(self.c0["on"]), ptr(pk["w_hhT"]), ptr(self.slab_p),
+                                        ptr(self.dgates), B, T, Lb, H, ptr(self.ctr), ptr(self.err),
+                                        s), "lstm_bwd_persist")
+        else:
+            self.dc.zero_()
+            check(k.r2_lstm_bwd(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]), ptr(self.c0["on"]),
+                                ptr(pk["w_hhT"]), ptr(self.slab0), ptr(self.slab1), ptr(self.dc),
+                                ptr(self.dgates), B, T, Lb, H, s), "lstm_bwd")
 
     def _relu_mask(self, grad: torch.Tensor, act: torch.Tensor) -> torch.Tensor:
         """grad * (act > 0) for two tensors with the same (channels-last) memory layout."""
