@@ -517,6 +517,115 @@ static int g4_launch(GemmArgs& a, int ak, int bk, hipStream_t s) {
   return 0;
 }
 
+// ============================================================================================
+// v3: the v2 tile (128x128x64, 4 waves, LDS-DMA, swizzled images) with an NS-stage ring: the
+// DMA of tile k+NS-1 is issued right after the barrier of tile k into the buffer every wave just
+// finished, so each tile has NS-1 tile-times to land (v2's 1-tile prefetch stalled on L2/HBM
+// latency at these K: dW_ih at K = 2560 ran at ~16 % of the CU's MFMA rate).  One barrier per K
+// tile, counted vmcnt, XCD-aware tile order (consecutive tiles share A rows and one L2).
+template <bool AK, bool BK_, int NS>
+__global__ __launch_bounds__(256) void gemm3_kernel(const GemmArgs args, int total_tiles) {
+  using namespace g2;
+  extern __shared__ __attribute__((aligned(1024))) uint8_t lds3[];
+  int bid;
+  {
+    const int b = blockIdx.x, x = b & 7, qn = total_tiles >> 3, r = total_tiles & 7;
+    bid = (x < r ? x * (qn + 1) : r * (qn + 1) + (x - r) * qn) + (b >> 3);
+  }
+  int pi = 0;
+#pragma unroll
+  for (int i = 1; i < gm::MAXP; ++i)
+    if (i < args.nprob && bid >= args.p[i].tile_base) pi = i;
+  const GemmProb& P = args.p[pi];
+  if (P.a_kmajor != (int)AK || P.b_kmajor != (int)BK_) return;
+  const int t = bid - P.tile_base;
+  const int tm = t / P.tiles_n, tn = t % P.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  if (m0 >= P.M) return;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int nk = P.K / BK;
+  auto stage = [&](int kt) {
+    uint8_t* st = lds3 + (kt % NS) * (2 * TILE_B);
+    g2_stage<AK>(P.A, P.lda, m0, P.M, kt * BK, st, wave, lane);
+    g2_stage<BK_>(P.B, P.ldb, n0, P.N, kt * BK, st + TILE_B, wave, lane);
+  };
+
+  f32x16 acc[2][2] = {};
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) stage(s);
+  for (int kt = 0; kt < nk; ++kt) {
+    // tile kt has landed once only the stages issued after it (at most NS-2) remain
+    const int ahead = min(NS - 2, nk - 1 - kt);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();       // tile kt visible; every wave done with tile kt-1
+    if (kt + NS - 1 < nk) stage(kt + NS - 1);
+    const uint8_t* la = lds3 + (kt % NS) * (2 * TILE_B);
+    const uint8_t* lb = la + TILE_B;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        fa[i] = g2_frag<AK>(la, wm + 32 * i, ks, lane);
+        fb[i] = g2_frag<BK_>(lb, wn + 32 * i, ks, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(fa[i], fb[j], acc[i][j]);
+    }
+  }
+
+  const int l32 = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = n0 + wn + 32 * j + l32;
+    if (col >= P.N) continue;
+    const float bv = P.bias ? P.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row >= P.M) continue;
+        const int orow = P.crow ? P.crow[row] : row;
+        const float v = P.alpha * acc[i][j][r] + bv;
+        const size_t o = (size_t)orow * P.ldc + col;
+        if (P.c_f32) {
+          float* c = (float*)P.C + o;
+          *c = P.accumulate ? *c + v : v;
+        } else {
+          bf16* c = (bf16*)P.C + o;
+          *c = (bf16)(P.accumulate ? (float)*c + v : v);
+        }
+      }
+  }
+}
+
+template <int NS>
+static int g3_launch(GemmArgs& a, int ak, int bk, int tiles, hipStream_t s) {
+  constexpr int LDS = NS * 2 * g2::TILE_B;
+  static_assert(LDS <= 160 * 1024, "LDS");
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)gemm3_kernel<true, true, NS>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    hipFuncSetAttribute((const void*)gemm3_kernel<true, false, NS>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    hipFuncSetAttribute((const void*)gemm3_kernel<false, true, NS>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    hipFuncSetAttribute((const void*)gemm3_kernel<false, false, NS>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  if (ak && bk) hipLaunchKernelGGL((gemm3_kernel<true, true, NS>), dim3(tiles), dim3(256), LDS, s, a, tiles);
+  else if (ak) hipLaunchKernelGGL((gemm3_kernel<true, false, NS>), dim3(tiles), dim3(256), LDS, s, a, tiles);
+  else if (bk) hipLaunchKernelGGL((gemm3_kernel<false, true, NS>), dim3(tiles), dim3(256), LDS, s, a, tiles);
+  else hipLaunchKernelGGL((gemm3_kernel<false, false, NS>), dim3(tiles), dim3(256), LDS, s, a, tiles);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
 static int g_gemm_version = 2;   // 1 = force the register-staged kernel (tests / A-B)
 extern "C" int r2_gemm_set_version(int v) { g_gemm_version = v; return 0; }
 
@@ -558,7 +667,7 @@ extern "C" int r2_gemm(const int64_t* descs, int nprob, void* stream) {
     k8 = k8 && a.p[i].K % 8 == 0;
     t256 += (long)((a.p[i].M + 255) / 256) * ((a.p[i].N + 255) / 256);
   }
-  if (g_gemm_version >= 5 && k8) {       // forced 8-wave variants (tests / micro-benchmarks)
+  if (g_gemm_version >= 5 && g_gemm_version <= 8 && k8) {   // forced 8-wave variants (tests / micro-benchmarks)
     switch (g_gemm_version) {
       case 5: return g4_launch<256, 64, 2>(a, ak, bk, s);
       case 6: return g4_launch<256, 32, 4>(a, ak, bk, s);
@@ -572,6 +681,8 @@ extern "C" int r2_gemm(const int64_t* descs, int nprob, void* stream) {
   if (g_gemm_version == 2 && k8 && t256 >= 150) return g4_launch<256, 64, 2>(a, ak, bk, s);
   bool v2 = g_gemm_version >= 2;
   for (int i = 0; i < nprob; ++i) v2 = v2 && a.p[i].K % g2::BK == 0;
+  if (v2 && g_gemm_version == 9) return g3_launch<3>(a, ak, bk, tiles, s);
+  if (v2 && g_gemm_version == 10) return g3_launch<4>(a, ak, bk, tiles, s);
   if (v2) {
     if (ak && bk) hipLaunchKernelGGL((gemm2_kernel<true, true>), dim3(tiles), dim3(g2::NT), 0, s, a);
     else if (ak) hipLaunchKernelGGL((gemm2_kernel<true, false>), dim3(tiles), dim3(g2::NT), 0, s, a);

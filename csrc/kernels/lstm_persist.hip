@@ -577,6 +577,22 @@ extern "C" int r2_lstm_bwd_persist(const float* dh_ext, const float* gates, cons
 //  * same-XCD fast path as v2 (plain granule stores stay in the XCD's L2); sc1 stores otherwise.
 #define PT_ROWS 16
 
+// Run by ONE lane of every workgroup at its very end: the last workgroup to finish (done ticket)
+// advances the launch epoch and returns the counter words (XCD masks / arrivals of `groups`
+// groups, the done ticket) to zero, so the next launch needs no memset node.  Returns true in the
+// last workgroup.
+__device__ __forceinline__ bool pt_finish(unsigned* ctr, int groups, int total_wgs, int epoch_off) {
+  const unsigned done = __hip_atomic_fetch_add(ctr + PT_DONE_OFF, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (done != (unsigned)total_wgs - 1) return false;
+  for (int g = 0; g < groups; ++g) {
+    __hip_atomic_store(ctr + PL_OFF_XMASK + g * PL_CTR_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(ctr + PL_OFF_ARRIVE + g * PL_CTR_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __hip_atomic_store(ctr + PT_DONE_OFF, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_add(ctr + epoch_off, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
 struct PTArgs {
   PChain ch[PL_MAX_CHAINS];
   int B, T;
@@ -839,12 +855,9 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
   }
 #undef PT_TRACE
   lds_sync();                                     // barrier T: outputs of step T-1 complete
-  // the last workgroup to finish advances the epoch (every workgroup read it before any finished)
-  if (tid == 0) {
-    const unsigned done = __hip_atomic_fetch_add(a.ctr + PT_DONE_OFF, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (done == (unsigned)(a.groups * NWG) - 1)
-      __hip_atomic_fetch_add(a.ctr + PT_EPOCH_FWD, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  // the last workgroup to finish advances the epoch (every workgroup read it before any
+  // finished) and clears the counters
+  if (tid == 0) pt_finish(a.ctr, a.groups, a.groups * NWG, PT_EPOCH_FWD);
 }
 
 extern "C" int r2_lstm_tag_ring_bytes(int n_chains, int B, int H) {
@@ -874,8 +887,7 @@ extern "C" int r2_lstm_fwd_tag(const int64_t* chain_ptrs, int n_chains, int B, i
   args.B = B; args.T = T; args.ctr = ctr; args.err = err; args.dbg = g_pl_dbg; args.ring = ring;
   args.MB = MB; args.groups = groups; args.xcd_map = groups <= 8 && nwg <= 32;
   args.force_slow = g_pl_slow;
-  hipStream_t s = (hipStream_t)stream;
-  hipMemsetAsync(ctr, 0, PT_MEMSET_WORDS * sizeof(unsigned), s);
+  hipStream_t s = (hipStream_t)stream;   // counters are left zeroed by the previous launch
   dim3 grid(args.xcd_map ? 8 * nwg : groups * nwg), block(320);   // 4 compute waves + 1 I/O wave
   const void* fn = H == 64 ? (const void*)lstm_fwd_tag_kernel<64>
                  : H == 128 ? (const void*)lstm_fwd_tag_kernel<128>
@@ -917,6 +929,12 @@ struct PTBArgs {
   unsigned* ctr;
   unsigned* err;
   int MB, xcd_map, force_slow, pad_;
+  // fused LSTM bias gradient (optional): per-tile column sums of dgates -> bias_ws (MB, G), summed
+  // in tile order by the last workgroup into db1[perm[c]] (and db2[perm[c]])
+  float* bias_ws;
+  const int* perm;
+  float* db1;
+  float* db2;
 };
 
 template <int H>
@@ -997,8 +1015,7 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
     }
     lds_sync();                           // barrier E: dgates of the last iteration complete
     io_store(K - 1);
-    return;
-  }
+  } else {
 
   // ================= compute waves 0..3
   // W_hh^T fragments: N tile q of this wave = units (H/4)*wave + 16*q + (l&15); B[k][n] = Whh_pk[j][k][n]
@@ -1014,6 +1031,7 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   const int ul = 4 * wave + pu;
   const bool pv = mb * PT_ROWS + prow < B;
   float dcr = 0.f;
+  float bsum[4] = {0.f, 0.f, 0.f, 0.f};      // this lane's dgates summed over time (bias grad)
   // consumer ownership of the partial gather: (row, unit pair) x source half
   const int cmb = tid & 127, cr = cmb >> 3, cp2 = 2 * (cmb & 7), sh = tid >> 7;
   const bool crow_ok = mb * PT_ROWS + cr < B;
@@ -1070,11 +1088,19 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
     const float dc = dcr + dh * go * (1.f - tc * tc);
     const float d_o = dh * tc;
     dcr = dc * gf;
+    const float dgi = pv ? dc * gg * gi * (1.f - gi) : 0.f;
+    const float dgf = pv ? dc * cpv * gf * (1.f - gf) : 0.f;
+    const float dgg = pv ? dc * gi * (1.f - gg * gg) : 0.f;
+    const float dgo = pv ? d_o * go * (1.f - go) : 0.f;
+    bsum[0] += dgi;
+    bsum[1] += dgf;
+    bsum[2] += dgg;
+    bsum[3] += dgo;
     bf16* drow = dgl[k & 1] + prow * DS + ul;
-    drow[0] = (bf16)(pv ? dc * gg * gi * (1.f - gi) : 0.f);
-    drow[16] = (bf16)(pv ? dc * cpv * gf * (1.f - gf) : 0.f);
-    drow[32] = (bf16)(pv ? dc * gi * (1.f - gg * gg) : 0.f);
-    drow[48] = (bf16)(pv ? d_o * go * (1.f - go) : 0.f);
+    drow[0] = (bf16)dgi;
+    drow[16] = (bf16)dgf;
+    drow[32] = (bf16)dgg;
+    drow[48] = (bf16)dgo;
     lds_sync();                           // barrier B_k: dgates tile complete
     if (t > t0) {
       // ---- partial dh_{t-1}[r][n] = sum_k dg[r][k] Whh_pk[j][k][n], published as granules
@@ -1101,11 +1127,41 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
       }
     }
   }
-  lds_sync();                             // barrier E
-  if (tid == 0) {
-    const unsigned done = __hip_atomic_fetch_add(a.ctr + PT_DONE_OFF, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (done == (unsigned)(a.MB * NWG) - 1)
-      __hip_atomic_fetch_add(a.ctr + PT_EPOCH_BWD, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.bias_ws) {
+      // column sums over the tile's 16 rows (lanes 4r + pu, fixed butterfly order), written
+      // write-through by the row-0 lanes and drained before the done ticket
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        float v = bsum[gq];
+        v += __shfl_xor(v, 4, 64);
+        v += __shfl_xor(v, 8, 64);
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        bsum[gq] = v;
+      }
+      if (prow == 0) {
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq)
+          __hip_atomic_store(a.bias_ws + (size_t)mb * G + j * PL_GCOLS + 16 * gq + ul, bsum[gq],
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lds_sync();                           // barrier E
+  }
+  // ---- every wave (compute and I/O): done ticket; the last workgroup sums the bias partials in
+  // tile order and clears the counters
+  if (tid == 0) flag = pt_finish(a.ctr, a.MB, a.MB * NWG, PT_EPOCH_BWD) ? 1 : 0;
+  lds_sync();                             // barrier F
+  if (flag && a.bias_ws) {
+    for (int c = tid; c < G; c += 320) {
+      float v = 0.f;
+      for (int m = 0; m < a.MB; ++m)
+        v += __hip_atomic_load(a.bias_ws + (size_t)m * G + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int o = a.perm[c];
+      a.db1[o] = v;
+      if (a.db2) a.db2[o] = v;
+    }
   }
 }
 
@@ -1118,7 +1174,9 @@ extern "C" int r2_lstm_bwd_tag_ring_bytes(int B, int H) {
 // any content.  -3: grid too large for one workgroup per CU (caller falls back).
 extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const float* c_seq,
                                const float* c0, const bf16* whhT, bf16* dgates, int B, int T,
-                               int t0, int H, unsigned* ctr, unsigned* err, void* ring, void* stream) {
+                               int t0, int H, unsigned* ctr, unsigned* err, void* ring,
+                               float* bias_ws, const int* perm, float* db1, float* db2,
+                               void* stream) {
   if (B < 1 || T < 1 || t0 < 0 || t0 >= T) return -1;
   if (H != 64 && H != 128 && H != 256 && H != 512) return -2;
   const int MB = (B + PT_ROWS - 1) / PT_ROWS, nwg = H / PL_UNITS;
@@ -1126,9 +1184,10 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
   if ((size_t)T * B * (size_t)(4 * H) * 4 >= (1ull << 32) || r2_lstm_bwd_tag_ring_bytes(B, H) < 0 ||
       T - t0 >= 65535) return -4;
   const int xmap = MB <= 8 && nwg <= 32;
-  PTBArgs args{dh_ext, gates, c_seq, c0, whhT, dgates, ring, B, T, t0, ctr, err, MB, xmap, g_pl_slow, 0};
-  hipStream_t s = (hipStream_t)stream;
-  hipMemsetAsync(ctr, 0, PT_MEMSET_WORDS * sizeof(unsigned), s);
+  if (bias_ws && (!perm || !db1)) return -1;
+  PTBArgs args{dh_ext, gates, c_seq, c0, whhT, dgates, ring, B, T, t0, ctr, err, MB, xmap, g_pl_slow, 0,
+               bias_ws, perm, db1, db2};
+  hipStream_t s = (hipStream_t)stream;   // counters are left zeroed by the previous launch
   dim3 grid(xmap ? 8 * nwg : MB * nwg), block(320);
   const void* fn = H == 64 ? (const void*)lstm_bwd_tag_kernel<64>
                  : H == 128 ? (const void*)lstm_bwd_tag_kernel<128>

@@ -190,6 +190,7 @@ class LearnerEngine:
         # granule ring of the tagged forward hand-off (up to 4 chains per launch)
         self.ring = z(max(int(kernels().r2_lstm_tag_ring_bytes(4, B, H)), 16) // 4, dt=torch.int32)
         self.ring_b = z(max(int(kernels().r2_lstm_bwd_tag_ring_bytes(B, H)), 16) // 4, dt=torch.int32)
+        self.bias_ws = z((B + 15) // 16, G)      # per-tile LSTM bias-gradient partials (tagged BPTT)
         self.err = z(1, dt=torch.int32)
         self.dgates = z(Ll * B, G, dt=bf16)
         self.gamma_n = float(lc.gamma ** n)
@@ -545,7 +546,7 @@ class LearnerEngine:
             dh = mm_f32(self.dz, pk["head1"])                           # (N, H)
         if not fused_hg:
             gb1.copy_(mm_f32(self.ones_bf[:, :N], self.dz))
-        self._lstm_bwd(dh)
+        bias_done = self._lstm_bwd(dh)
         X = self.X_on[Lb * B: T * B]
         if Lb >= 1:
             h_prev = self.hseq["on"][Lb - 1: T - 1].reshape(N, H)
@@ -559,9 +560,11 @@ class LearnerEngine:
                  Gemm(dgT, h_prev, L.view(g, "lstm.weight_hh"), crow=self.gate_perm_i32),
                  Gemm(self.dz.t(), h_learn, gw1))
             # bias grads: column sums of dgates, packed -> torch gate order, into both biases
-            check(k.r2_colsum_bf16(ptr(self.dgates), N, G, ptr(self.gate_perm_i32),
-                                   ptr(L.view(g, "lstm.bias_ih")), ptr(L.view(g, "lstm.bias_hh")),
-                                   ptr(self.gs_ws), ptr(self.gs_ticket[32:]), s), "colsum")
+            # (fused into the tagged BPTT kernel when it ran)
+            if not bias_done:
+                check(k.r2_colsum_bf16(ptr(self.dgates), N, G, ptr(self.gate_perm_i32),
+                                       ptr(L.view(g, "lstm.bias_ih")), ptr(L.view(g, "lstm.bias_hh")),
+                                       ptr(self.gs_ws), ptr(self.gs_ticket[32:]), s), "colsum")
             gemm(Gemm(self.dgates, pk["w_ih"], self.dX))                  # (N, D) bf16
             self._dX = self.dX
         else:
@@ -573,19 +576,22 @@ class LearnerEngine:
             L.view(g, "lstm.bias_hh").copy_(db)
             self._dX = torch.mm(self.dgates, pk["w_ih"])               # (N, D) bf16
 
-    def _lstm_bwd(self, dh: torch.Tensor) -> None:
-        """BPTT over the learning window: dgates (Ll, B, G) from dh (Ll, B, H)."""
+    def _lstm_bwd(self, dh: torch.Tensor) -> bool:
+        """BPTT over the learning window: dgates (Ll, B, G) from dh (Ll, B, H).  Returns True when
+        the kernel also produced the LSTM bias gradients (tagged BPTT, fused column sums)."""
         k = kernels()
         s = stream_handle()
         B, T, Lb, H, pk = self.B, self.T, self.Lb, self.layout.H, self.pk
-        lc = self.cfg.learner
+        lc, L, g = self.cfg.learner, self.layout, self.grad
         if lc.lstm_impl == "persistent" and lc.lstm_handoff == "tagged":
             rc = k.r2_lstm_bwd_tag(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]), ptr(self.c0["on"]),
                                    ptr(pk["w_hhT"]), ptr(self.dgates), B, T, Lb, H, ptr(self.ctr),
-                                   ptr(self.err), ptr(self.ring_b), s)
+                                   ptr(self.err), ptr(self.ring_b), ptr(self.bias_ws),
+                                   ptr(self.gate_perm_i32), ptr(L.view(g, "lstm.bias_ih")),
+                                   ptr(L.view(g, "lstm.bias_hh")), s)
             if rc != -3:          # -3: grid too large for one workgroup per CU
                 check(rc, "lstm_bwd_tag")
-                return
+                return True
         if lc.lstm_impl == "persistent":
             check(k.r2_lstm_bwd_persist(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]),
                                         ptr(self.c0["on"]), ptr(pk["w_hhT"]), ptr(self.slab_p),
@@ -596,6 +602,7 @@ class LearnerEngine:
             check(k.r2_lstm_bwd(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]), ptr(self.c0["on"]),
                                 ptr(pk["w_hhT"]), ptr(self.slab0), ptr(self.slab1), ptr(self.dc),
                                 ptr(self.dgates), B, T, Lb, H, s), "lstm_bwd")
+        return False
 
     def _relu_mask(self, grad: torch.Tensor, act: torch.Tensor) -> torch.Tensor:
         """grad * (act > 0) for two tensors with the same (channels-last) memory layout."""

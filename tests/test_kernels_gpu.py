@@ -135,10 +135,16 @@ def test_lstm_backward_matches_autograd(B, H, impl):
         err = torch.zeros(1, dtype=torch.int32, device=DEV)
         ring = torch.full((k.r2_lstm_bwd_tag_ring_bytes(B, H) // 4,), -1, dtype=torch.int32,
                           device=DEV)
+        bias_ws = torch.zeros((B + 15) // 16, G, device=DEV)
+        db1 = torch.full((G,), float("nan"), device=DEV)
+        db2 = torch.full((G,), float("nan"), device=DEV)
+        perm_i = L.gate_perm.to(DEV, torch.int32)
         for _ in range(2):      # second launch: stale granules of the first must be ignored
             assert k.r2_lstm_bwd_tag(ptr(dh_ext), ptr(gates), ptr(cseq), ptr(c0), ptr(pk["w_hhT"]),
                                      ptr(dg), B, T, t0, H, ptr(ctr), ptr(err), ptr(ring),
+                                     ptr(bias_ws), ptr(perm_i), ptr(db1), ptr(db2),
                                      stream_handle()) == 0
+        assert int(ctr[:int(k.r2_lstm_persist_ctr_words()) - 64].abs().sum().item()) == 0  # self-reset
     else:
         slab = torch.zeros(2, nwg, B, H, device=DEV)
         ctr = torch.zeros(int(kernels().r2_lstm_persist_ctr_words()), dtype=torch.int32, device=DEV)
@@ -174,6 +180,8 @@ def test_lstm_backward_matches_autograd(B, H, impl):
     ref = torch.stack([p.grad for p in pre])  # (T-t0, B, G) original gate order
     got = dg.float()[..., L.gate_inv.to(DEV)]
     assert _rel(got, ref) < 3e-2, [round(_rel(got[i], ref[i]), 4) for i in range(T - t0)]
+    if impl == "tagged":   # fused bias gradient (fp32 column sums of dgates, torch gate order)
+        assert _rel(db1, ref.sum((0, 1))) < 1e-2 and torch.equal(db1, db2)
 
 
 @pytest.mark.parametrize("B", [64, 200])
