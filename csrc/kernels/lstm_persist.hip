@@ -30,6 +30,7 @@
 // All (H/16)*ceil(B/32)*chains workgroups (<= 256 for the supported shapes) must be
 // co-resident: 256 threads, <= 40 KB LDS, one per CU is enough.
 #include "../common.h"
+#include "../gradsum.h"
 
 #define PL_UNITS 16
 #define PL_GCOLS 64
@@ -935,6 +936,10 @@ struct PTBArgs {
   const int* perm;
   float* db1;
   float* db2;
+  // optional side job for the idle workgroups (groups >= MB of the XCD map, i.e. XCDs the
+  // recurrence does not use): the dueling head's gradient reduction, (CB x 8) work items
+  HeadGradArgs hg;
+  int hg_on;
 };
 
 template <int H>
@@ -953,7 +958,14 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   __shared__ __attribute__((aligned(1024))) float dhl[3][PT_ROWS * PL_UNITS]; // dh_ext
   __shared__ int flag;
   int mb, j;
-  if (!pl_decode(a.xcd_map, a.MB, NWG, mb, j)) return;
+  if (!pl_decode(a.xcd_map, a.MB, NWG, mb, j)) {
+    if (a.hg_on) {          // helper: one head-gradient work item, beside the recurrence
+      const int b = blockIdx.x, g = b & 7, jj = b >> 3;
+      const int hid = (g - a.MB) * NWG + jj, cbn = (2 * a.hg.HD + 63) / 64;
+      if (g >= a.MB && jj < NWG && hid < cbn * a.hg.RS) head_grads_body(a.hg, hid % cbn, hid / cbn);
+    }
+    return;
+  }
   const int B = a.B, T = a.T, t0 = a.t0, K = T - t0;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int rows_all = a.MB * PT_ROWS;
@@ -1172,11 +1184,23 @@ extern "C" int r2_lstm_bwd_tag_ring_bytes(int B, int H) {
 
 // Same operands as r2_lstm_bwd_persist minus the slab; ring: r2_lstm_bwd_tag_ring_bytes bytes,
 // any content.  -3: grid too large for one workgroup per CU (caller falls back).
+// 1 when the launch's idle workgroups can take the dueling head's gradient reduction (head
+// width HD): the XCD map leaves (8 - MB) * H/16 workgroups free and the job needs (2HD/64) x 8.
+extern "C" int r2_lstm_bwd_tag_hg_ok(int B, int H, int HD) {
+  const int MB = (B + PT_ROWS - 1) / PT_ROWS, nwg = H / PL_UNITS;
+  const bool xmap = MB <= 8 && nwg <= 32;
+  return (xmap && HD % 64 == 0 && (8 - MB) * nwg >= ((2 * HD + 63) / 64) * 8) ? 1 : 0;
+}
+
+// hg_*: optional head-gradient job (gradsum.hip r2_head_grads operands); pass dva = null for none,
+// and only when r2_lstm_bwd_tag_hg_ok(B, H, HD).
 extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const float* c_seq,
                                const float* c0, const bf16* whhT, bf16* dgates, int B, int T,
                                int t0, int H, unsigned* ctr, unsigned* err, void* ring,
                                float* bias_ws, const int* perm, float* db1, float* db2,
-                               void* stream) {
+                               const float* hg_dva, const bf16* hg_zr, const bf16* hg_dz,
+                               float* hg_gw2, float* hg_gb2, float* hg_gb1, int hg_N, int hg_A,
+                               int hg_HD, float* hg_ws, unsigned* hg_ticket, void* stream) {
   if (B < 1 || T < 1 || t0 < 0 || t0 >= T) return -1;
   if (H != 64 && H != 128 && H != 256 && H != 512) return -2;
   const int MB = (B + PT_ROWS - 1) / PT_ROWS, nwg = H / PL_UNITS;
@@ -1186,7 +1210,14 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
   const int xmap = MB <= 8 && nwg <= 32;
   if (bias_ws && (!perm || !db1)) return -1;
   PTBArgs args{dh_ext, gates, c_seq, c0, whhT, dgates, ring, B, T, t0, ctr, err, MB, xmap, g_pl_slow, 0,
-               bias_ws, perm, db1, db2};
+               bias_ws, perm, db1, db2,
+               HeadGradArgs{hg_dva, hg_zr, hg_dz, hg_gw2, hg_gb2, hg_gb1, hg_ws, hg_ticket, hg_N, hg_A,
+                            hg_HD, 8},
+               0};
+  if (hg_dva) {
+    if (!r2_lstm_bwd_tag_hg_ok(B, H, hg_HD) || hg_A + 1 > gs::MAXW || hg_N < 1) return -5;
+    args.hg_on = 1;
+  }
   hipStream_t s = (hipStream_t)stream;   // counters are left zeroed by the previous launch
   dim3 grid(xmap ? 8 * nwg : MB * nwg), block(320);
   const void* fn = H == 64 ? (const void*)lstm_bwd_tag_kernel<64>

@@ -524,7 +524,15 @@ class LearnerEngine:
         gb2 = L.span(g, "val.2.bias", "adv.2.bias", (1, 1 + A))
         gb1 = L.span(g, "val.0.bias", "adv.0.bias", (1, 2 * HD))
         fused_hg = self.use_gemm and A + 1 <= 8 and HD % 64 == 0
-        if fused_hg:
+        lc = self.cfg.learner
+        # the tagged BPTT kernel's idle workgroups take the head-gradient reduction beside the
+        # recurrence when they are enough; otherwise it runs as its own launch here
+        self._hg_job = None
+        if (fused_hg and lc.lstm_impl == "persistent" and lc.lstm_handoff == "tagged"
+                and int(k.r2_lstm_bwd_tag_hg_ok(B, H, HD))):
+            self._hg_job = [ptr(self.dva), ptr(zr), ptr(self.dz), ptr(gw2), ptr(gb2), ptr(gb1),
+                            N, A, HD, ptr(self.gs_ws), ptr(self.gs_ticket)]
+        elif fused_hg:
             # last-layer weight/bias grads and the layer-1 bias grads in one deterministic
             # column-reduction launch (gradsum.hip), written in place into the flat buffer
             check(k.r2_head_grads(ptr(self.dva), ptr(zr), ptr(self.dz), ptr(gw2), ptr(gb2),
@@ -588,10 +596,13 @@ class LearnerEngine:
                                    ptr(pk["w_hhT"]), ptr(self.dgates), B, T, Lb, H, ptr(self.ctr),
                                    ptr(self.err), ptr(self.ring_b), ptr(self.bias_ws),
                                    ptr(self.gate_perm_i32), ptr(L.view(g, "lstm.bias_ih")),
-                                   ptr(L.view(g, "lstm.bias_hh")), s)
+                                   ptr(L.view(g, "lstm.bias_hh")),
+                                   *(self._hg_job or [0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0]), s)
             if rc != -3:          # -3: grid too large for one workgroup per CU
                 check(rc, "lstm_bwd_tag")
                 return True
+        if self._hg_job is not None:   # the side job did not run: its own launch
+            check(k.r2_head_grads(*self._hg_job, s), "head_grads")
         if lc.lstm_impl == "persistent":
             check(k.r2_lstm_bwd_persist(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]),
                                         ptr(self.c0["on"]), ptr(pk["w_hhT"]), ptr(self.slab_p),
