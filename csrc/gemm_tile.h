@@ -1,0 +1,188 @@
+// 128x128 MFMA GEMM tile machinery (gfx950) shared by gemm.hip and the kernels that run GEMM
+// tiles inside their own launch (lstm_persist.hip: BPTT helper workgroups).  See gemm.hip for
+// the operand conventions (k-major / mn-major operands, LDS-DMA staging with source swizzles).
+#pragma once
+#include "common.h"
+
+namespace gm {
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+constexpr int KS = BK + 8;        // k-major LDS row stride (bf16): 144 B rows (b128 reads conflict-free)
+constexpr int MS = BM + 32;       // mn-major LDS row stride (bf16): 320 B = 16 dwords mod 64 banks,
+                                  // so the 4 rows x 2 column groups of a tr read hit 8 distinct bank octets
+constexpr int LPT = BM * BK / 8 / NT;  // 16-B chunks per thread per operand tile (4)
+constexpr int TILE = BM * KS > BK * MS ? BM * KS : BK * MS;  // bf16 per operand tile
+constexpr int MAXP = 4;
+}  // namespace gm
+
+struct GemmProb {
+  const bf16* A;
+  const bf16* B;
+  void* C;
+  const float* bias;   // per output column, or null
+  const int* crow;     // output row map, or null
+  int M, N, K, lda, ldb, ldc;
+  int a_kmajor, b_kmajor, c_f32, accumulate;
+  float alpha;
+  int tiles_n, tile_base;  // tiles along N; first linear tile index of this problem
+};
+
+struct GemmArgs {
+  GemmProb p[gm::MAXP];
+  int nprob;
+};
+
+typedef short gi16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) gi16x4 glds_i16x4;
+
+__device__ __forceinline__ bf16x8 gm_tr8(const bf16* p0, const bf16* p1) {
+  const gi16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((glds_i16x4*)p0);
+  const gi16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((glds_i16x4*)p1);
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+
+namespace g2 {
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+constexpr int TILE_B = 16384;        // bytes per operand tile (both layouts)
+constexpr int GPW = 4;               // 1-KB DMA instructions per wave per operand tile
+}  // namespace g2
+
+// AUX: cache policy of the DMA loads (16 = sc1, for operands another CU of the SAME launch wrote
+// write-through: MI355X_MICROARCH.md hand-off table)
+template <bool KMAJ, int AUX = 0>
+__device__ __forceinline__ void g2_stage(const bf16* X, int ld, int i0, int imax, int k0,
+                                         uint8_t* lds_tile, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < g2::GPW; ++j) {
+    const int blk = wave * g2::GPW + j;          // 1-KB block of the tile
+    const bf16* src;
+    if (KMAJ) {
+      const int row = blk * 8 + (lane >> 3), cp = lane & 7;
+      const int c = cp ^ ((row >> 1) & 7);
+      src = X + (size_t)min(i0 + row, imax - 1) * ld + k0 + c * 8;
+    } else {
+      const int kr = blk * 4 + (lane >> 4), cp = lane & 15;
+      const int c = cp ^ (4 * (kr & 3));
+      const int col = i0 + c * 8;
+      src = X + (size_t)(k0 + kr) * ld + (col < imax ? col : imax - 8);
+    }
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(lds_tile + blk * 1024),
+                                     16, 0, AUX);
+  }
+}
+
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8 g2_frag(const uint8_t* L, int i0, int ks, int lane) {
+  const int l32 = lane & 31, h = lane >> 5;
+  if (KMAJ) {
+    const int r = i0 + l32, c = 2 * ks + h;
+    return *(const bf16x8*)(L + r * 128 + ((c ^ ((r >> 1) & 7)) * 16));
+  }
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int c = (i0 >> 3) + 2 * (g & 1) + (p >> 1);
+  const int kr = 16 * ks + 8 * h + q;                      // + 4 for the second read
+  const uint8_t* b0 = L + kr * 256 + ((c ^ (4 * q)) * 16) + 8 * (p & 1);
+  return gm_tr8((const bf16*)b0, (const bf16*)(b0 + 4 * 256));
+}
+
+
+// Epilogue of a 128x128 tile held as acc[2][2] (32x32x16 layout, wave (wm, wn) quadrant):
+// C[row][col] = alpha * acc + bias[col], row m stored at crow[m], fp32 or bf16, optional +=.
+__device__ __forceinline__ void g2_epilogue(const GemmProb& P, int m0, int n0, int wm, int wn,
+                                            int lane, const f32x16 (&acc)[2][2]) {
+  const int l32 = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = n0 + wn + 32 * j + l32;
+    if (col >= P.N) continue;
+    const float bv = P.bias ? P.bias[col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row >= P.M) continue;
+        const int orow = P.crow ? P.crow[row] : row;
+        const float v = P.alpha * acc[i][j][r] + bv;
+        const size_t o = (size_t)orow * P.ldc + col;
+        if (P.c_f32) {
+          float* c = (float*)P.C + o;
+          *c = P.accumulate ? *c + v : v;
+        } else {
+          bf16* c = (bf16*)P.C + o;
+          *c = (bf16)(P.accumulate ? (float)*c + v : v);
+        }
+      }
+  }
+}
+
+// One 128x128 output tile (tm, tn) of problem P by threads 0..255 (4 waves) of a workgroup,
+// usable inside other kernels: 2-stage LDS-DMA ring at `lds` (2 x 32 KB), K tiles visited in
+// ascending or descending order; ready(kt) is called by EVERY wave before it issues the DMA of K
+// tile kt (a per-wave poll when the operand is produced inside the same launch; then AUX = 16).
+// K % 64 == 0.  Raw barriers only (threads >= 256 of the workgroup must have exited).
+template <bool AK, bool BK_, int AUX, class Ready>
+__device__ __forceinline__ void g2_tile(const GemmProb& P, int tm, int tn, uint8_t* lds, bool desc,
+                                        Ready ready) {
+  using namespace g2;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int nk = P.K / BK;
+  auto stage = [&](int i) {
+    const int kt = desc ? nk - 1 - i : i;
+    ready(kt);
+    uint8_t* st = lds + (i & 1) * (2 * TILE_B);
+    g2_stage<AK, AUX>(P.A, P.lda, m0, P.M, kt * BK, st, wave, lane);
+    g2_stage<BK_, AUX>(P.B, P.ldb, n0, P.N, kt * BK, st + TILE_B, wave, lane);
+  };
+  f32x16 acc[2][2] = {};
+  stage(0);
+  if (nk > 1) stage(1);
+  for (int i = 0; i < nk; ++i) {
+    if (i + 1 < nk) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const uint8_t* la = lds + (i & 1) * (2 * TILE_B);
+    const uint8_t* lb = la + TILE_B;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        fa[q] = g2_frag<AK>(la, wm + 32 * q, ks, lane);
+        fb[q] = g2_frag<BK_>(lb, wn + 32 * q, ks, lane);
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int r = 0; r < 2; ++r) acc[q][r] = mfma32(fa[q], fb[r], acc[q][r]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();          // every wave is done reading this stage
+    if (i + 2 < nk) stage(i + 2);
+  }
+  g2_epilogue(P, m0, n0, wm, wn, lane, acc);
+}
+
+// Host: parse one 16 x int64 problem descriptor (ops/gemm.py Gemm.desc layout) and check the
+// shape rules of the 128x128 paths.  0 = ok.
+static inline int gemm_parse_desc(const int64_t* d, GemmProb& p) {
+  p.A = (const bf16*)d[0]; p.B = (const bf16*)d[1]; p.C = (void*)d[2];
+  p.bias = (const float*)d[3]; p.crow = (const int*)d[4];
+  p.M = (int)d[5]; p.N = (int)d[6]; p.K = (int)d[7];
+  p.lda = (int)d[8]; p.ldb = (int)d[9]; p.ldc = (int)d[10];
+  p.a_kmajor = (int)d[11]; p.b_kmajor = (int)d[12]; p.c_f32 = (int)d[13];
+  p.accumulate = (int)d[14];
+  const uint32_t ab = (uint32_t)d[15];
+  float al;
+  __builtin_memcpy(&al, &ab, 4);
+  p.alpha = al;
+  if (p.M < 1 || p.N < 1 || p.K < 8 || p.K % 8) return -2;
+  if (!p.b_kmajor && (p.N % 8)) return -3;
+  if (!p.a_kmajor && (p.M % 8)) return -3;
+  if (p.lda % 8 || p.ldb % 8) return -4;
+  p.tiles_n = (p.N + gm::BN - 1) / gm::BN;
+  p.tile_base = 0;
+  return 0;
+}

@@ -20,41 +20,7 @@
 // arbitrary for k-major operands, multiples of 8 for mn-major ones.
 #include "../common.h"
 
-namespace gm {
-constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
-constexpr int KS = BK + 8;        // k-major LDS row stride (bf16): 144 B rows (b128 reads conflict-free)
-constexpr int MS = BM + 32;       // mn-major LDS row stride (bf16): 320 B = 16 dwords mod 64 banks,
-                                  // so the 4 rows x 2 column groups of a tr read hit 8 distinct bank octets
-constexpr int LPT = BM * BK / 8 / NT;  // 16-B chunks per thread per operand tile (4)
-constexpr int TILE = BM * KS > BK * MS ? BM * KS : BK * MS;  // bf16 per operand tile
-constexpr int MAXP = 4;
-}  // namespace gm
-
-struct GemmProb {
-  const bf16* A;
-  const bf16* B;
-  void* C;
-  const float* bias;   // per output column, or null
-  const int* crow;     // output row map, or null
-  int M, N, K, lda, ldb, ldc;
-  int a_kmajor, b_kmajor, c_f32, accumulate;
-  float alpha;
-  int tiles_n, tile_base;  // tiles along N; first linear tile index of this problem
-};
-
-struct GemmArgs {
-  GemmProb p[gm::MAXP];
-  int nprob;
-};
-
-typedef short gi16x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) gi16x4 glds_i16x4;
-
-__device__ __forceinline__ bf16x8 gm_tr8(const bf16* p0, const bf16* p1) {
-  const gi16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((glds_i16x4*)p0);
-  const gi16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((glds_i16x4*)p1);
-  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
-}
+#include "../gemm_tile.h"
 
 // Global -> register staging of one 128 x 64 operand tile (256 threads, 4 x 16 B each).
 //   k-major: row r = c / 8, k chunk (c % 8) * 8;  mn-major: k row = c / 16, i chunk (c % 16) * 8
@@ -186,48 +152,6 @@ __global__ __launch_bounds__(256) void gemm_kernel(const GemmArgs args) {
 // to the per-lane GLOBAL source addresses and undone on the fragment reads:
 //   k-major tile  [128 rows][8 x 16-B chunks]: chunk c of row r stored at c ^ ((r >> 1) & 7)
 //   mn-major tile [64 k-rows][16 chunks]:      chunk c of k-row k stored at c ^ (4 (k & 3))
-namespace g2 {
-constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
-constexpr int TILE_B = 16384;        // bytes per operand tile (both layouts)
-constexpr int GPW = 4;               // 1-KB DMA instructions per wave per operand tile
-}  // namespace g2
-
-template <bool KMAJ>
-__device__ __forceinline__ void g2_stage(const bf16* X, int ld, int i0, int imax, int k0,
-                                         uint8_t* lds_tile, int wave, int lane) {
-#pragma unroll
-  for (int j = 0; j < g2::GPW; ++j) {
-    const int blk = wave * g2::GPW + j;          // 1-KB block of the tile
-    const bf16* src;
-    if (KMAJ) {
-      const int row = blk * 8 + (lane >> 3), cp = lane & 7;
-      const int c = cp ^ ((row >> 1) & 7);
-      src = X + (size_t)min(i0 + row, imax - 1) * ld + k0 + c * 8;
-    } else {
-      const int kr = blk * 4 + (lane >> 4), cp = lane & 15;
-      const int c = cp ^ (4 * (kr & 3));
-      const int col = i0 + c * 8;
-      src = X + (size_t)(k0 + kr) * ld + (col < imax ? col : imax - 8);
-    }
-    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(lds_tile + blk * 1024),
-                                     16, 0, 0);
-  }
-}
-
-template <bool KMAJ>
-__device__ __forceinline__ bf16x8 g2_frag(const uint8_t* L, int i0, int ks, int lane) {
-  const int l32 = lane & 31, h = lane >> 5;
-  if (KMAJ) {
-    const int r = i0 + l32, c = 2 * ks + h;
-    return *(const bf16x8*)(L + r * 128 + ((c ^ ((r >> 1) & 7)) * 16));
-  }
-  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const int c = (i0 >> 3) + 2 * (g & 1) + (p >> 1);
-  const int kr = 16 * ks + 8 * h + q;                      // + 4 for the second read
-  const uint8_t* b0 = L + kr * 256 + ((c ^ (4 * q)) * 16) + 8 * (p & 1);
-  return gm_tr8((const bf16*)b0, (const bf16*)(b0 + 4 * 256));
-}
-
 template <bool AK, bool BK_>
 __global__ __launch_bounds__(256) void gemm2_kernel(const GemmArgs args) {
   using namespace g2;

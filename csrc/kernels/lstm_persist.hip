@@ -31,6 +31,7 @@
 // co-resident: 256 threads, <= 40 KB LDS, one per CU is enough.
 #include "../common.h"
 #include "../gradsum.h"
+#include "../gemm_tile.h"
 
 #define PL_UNITS 16
 #define PL_GCOLS 64
@@ -54,7 +55,12 @@
 #define PT_MEMSET_WORDS (PL_CTR_WORDS + 32)
 #define PT_EPOCH_FWD (PL_CTR_WORDS + 32)
 #define PT_EPOCH_BWD (PL_CTR_WORDS + 64)
-#define PT_CTR_WORDS (PL_CTR_WORDS + 96)
+// BPTT progress for helper workgroups: word k counts the recurrence workgroups whose dgates of
+// iteration k are stored (exact per-iteration counts: a sum over iterations would let a fast
+// group hide a slow one); reset by the last workgroup
+#define PT_ITER_OFF (PL_CTR_WORDS + 128)
+#define PT_ITER_MAX 512
+#define PT_CTR_WORDS (PL_CTR_WORDS + 128 + PT_ITER_MAX)
 
 struct PChain {
   const float* xproj;  // (T, B, G) packed, chain-local time
@@ -582,7 +588,8 @@ extern "C" int r2_lstm_bwd_persist(const float* dh_ext, const float* gates, cons
 // advances the launch epoch and returns the counter words (XCD masks / arrivals of `groups`
 // groups, the done ticket) to zero, so the next launch needs no memset node.  Returns true in the
 // last workgroup.
-__device__ __forceinline__ bool pt_finish(unsigned* ctr, int groups, int total_wgs, int epoch_off) {
+__device__ __forceinline__ bool pt_finish(unsigned* ctr, int groups, int total_wgs, int epoch_off,
+                                          int n_iter = 0) {
   const unsigned done = __hip_atomic_fetch_add(ctr + PT_DONE_OFF, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (done != (unsigned)total_wgs - 1) return false;
   for (int g = 0; g < groups; ++g) {
@@ -590,6 +597,8 @@ __device__ __forceinline__ bool pt_finish(unsigned* ctr, int groups, int total_w
     __hip_atomic_store(ctr + PL_OFF_ARRIVE + g * PL_CTR_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __hip_atomic_store(ctr + PT_DONE_OFF, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int k = 0; k < n_iter; ++k)
+    __hip_atomic_store(ctr + PT_ITER_OFF + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_fetch_add(ctr + epoch_off, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
 }
@@ -940,6 +949,13 @@ struct PTBArgs {
   // recurrence does not use): the dueling head's gradient reduction, (CB x 8) work items
   HeadGradArgs hg;
   int hg_on;
+  // optional GEMMs beside the recurrence, on helper workgroups (the grid grows to 8 x 32):
+  // gw[0..n_gw) weight-gradient problems (mn-major A and B, K = the time-major learning rows;
+  // bit i of gw_wait: problem i reads dgates and waits for the BPTT per 64-row K tile),
+  // gx = dX (rows = time-major learning rows, waits per 128-row tile), when gx_on.
+  GemmProb gw[3];
+  int n_gw, gw_wait, gx_on, n_wtiles;
+  GemmProb gx;
 };
 
 template <int H>
@@ -957,17 +973,77 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   __shared__ __attribute__((aligned(1024))) float cpl[3][PT_ROWS * PL_UNITS]; // c_{t-1}
   __shared__ __attribute__((aligned(1024))) float dhl[3][PT_ROWS * PL_UNITS]; // dh_ext
   __shared__ int flag;
+  extern __shared__ __attribute__((aligned(1024))) uint8_t pt_dyn[];   // helper GEMM LDS ring
   int mb, j;
+  const int B = a.B, T = a.T, t0 = a.t0, K = T - t0;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   if (!pl_decode(a.xcd_map, a.MB, NWG, mb, j)) {
-    if (a.hg_on) {          // helper: one head-gradient work item, beside the recurrence
-      const int b = blockIdx.x, g = b & 7, jj = b >> 3;
-      const int hid = (g - a.MB) * NWG + jj, cbn = (2 * a.hg.HD + 63) / 64;
-      if (g >= a.MB && jj < NWG && hid < cbn * a.hg.RS) head_grads_body(a.hg, hid % cbn, hid / cbn);
+    // ================= helper workgroup (4 waves): work beside the recurrence
+    if (wave == 4) return;                 // helpers run 256 threads (barriers: surviving waves)
+    const int b = blockIdx.x, g = b & 7, jj = b >> 3;
+    const int h = b - (min(jj, NWG) * a.MB + (jj < NWG ? min(g, a.MB) : 0));   // helper ordinal
+    const int nh = (int)gridDim.x - a.MB * NWG;
+    const unsigned nbptt = (unsigned)(a.MB * NWG);
+    // rows [row_lo, row_hi) (time-major: row = tl * B + b) are stored once BPTT iterations
+    // K-1-tl are complete on every recurrence workgroup, for every tl they touch
+    auto wait_rows = [&](int row_lo, int row_hi) {
+      const int tl_hi = (min(row_hi, K * B) - 1) / B;
+      for (int tl = row_lo / B; tl <= tl_hi; ++tl) {
+        unsigned* w = a.ctr + PT_ITER_OFF + (K - 1 - tl);
+        unsigned spins = 0;
+        while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nbptt) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++spins > PL_SPIN_LIMIT) {
+            __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
+    };
+    if (h < a.n_wtiles) {
+      // one weight-gradient tile, K tiles in BPTT order (latest time step first)
+      int item = h, pi = 0;
+      while (pi + 1 < a.n_gw) {
+        const int nt = a.gw[pi].tiles_n * ((a.gw[pi].M + 127) / 128);
+        if (item < nt) break;
+        item -= nt;
+        ++pi;
+      }
+      const GemmProb& P = a.gw[pi];
+      const bool wt = (a.gw_wait >> pi) & 1;
+      g2_tile<false, false, 16>(P, item / P.tiles_n, item % P.tiles_n, pt_dyn, true,
+                                [&](int kt) { if (wt) wait_rows(64 * kt, 64 * kt + 64); });
+    } else {
+      const int hx = h - a.n_wtiles, nx = nh - a.n_wtiles;
+      if (a.hg_on) {
+        const int cbn = (2 * a.hg.HD + 63) / 64;
+        for (int it = hx; it < cbn * a.hg.RS; it += nx) head_grads_body(a.hg, it % cbn, it / cbn);
+      }
+      if (a.gx_on) {
+        // dX tiles, latest rows (first produced) first
+        const GemmProb& P = a.gx;
+        const int tmn = (P.M + 127) / 128, total = tmn * P.tiles_n;
+        for (int it = hx; it < total; it += nx) {
+          const int tm = tmn - 1 - it / P.tiles_n, tn = it % P.tiles_n;
+          g2_tile<true, false, 16>(P, tm, tn, pt_dyn, false,
+                                   [&](int) { wait_rows(128 * tm, 128 * tm + 128); });
+        }
+      }
+    }
+    if (tid == 0) flag = pt_finish(a.ctr, a.MB, (int)gridDim.x, PT_EPOCH_BWD, K) ? 1 : 0;
+    __syncthreads();
+    if (flag && a.bias_ws) {
+      for (int c = tid; c < G; c += 256) {
+        float v = 0.f;
+        for (int m = 0; m < a.MB; ++m)
+          v += __hip_atomic_load(a.bias_ws + (size_t)m * G + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int o = a.perm[c];
+        a.db1[o] = v;
+        if (a.db2) a.db2[o] = v;
+      }
     }
     return;
   }
-  const int B = a.B, T = a.T, t0 = a.t0, K = T - t0;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int rows_all = a.MB * PT_ROWS;
   const uint32_t ring_bytes = (uint32_t)((size_t)2 * NWG * rows_all * H * 8);
   const __amdgpu_buffer_rsrc_t rrs = pl_rsrc(a.ring, ring_bytes);
@@ -998,15 +1074,21 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
         __builtin_amdgcn_global_load_lds(a.dh_ext + (size_t)tl * B * H + hidx, (lds_t*)dhl[s], 16, 0, 0);
     };
     const int nload = a.dh_ext ? 7 : 6;     // DMA instructions per io_load
-    auto io_store = [&](int k) {      // dgates tile of iteration k
+    const __amdgpu_buffer_rsrc_t drs = pl_rsrc(a.dgates, (uint32_t)((size_t)K * B * G * 2));
+    auto io_store = [&](int k) {      // dgates tile of iteration k (write-through: helpers read it)
       const int tl = T - 1 - k - t0, s = k & 1;
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int c = lane + 64 * q, r = c >> 3, ch = c & 7, b = mb * PT_ROWS + r;
         if (b < B)
-          *(u32x4*)(a.dgates + ((size_t)tl * B + b) * G + j * PL_GCOLS + 8 * ch) =
-              *(const u32x4*)(dgl[s] + r * DS + 8 * ch);
+          __builtin_amdgcn_raw_buffer_store_b128(*(const u32x4*)(dgl[s] + r * DS + 8 * ch), drs,
+                                                 (uint32_t)((((size_t)tl * B + b) * G + j * PL_GCOLS + 8 * ch) * 2),
+                                                 0, 16);
       }
+    };
+    auto io_progress = [&](int k) {    // after this wave's dgates stores of iteration k completed
+      if (lane == 0 && K <= PT_ITER_MAX)
+        __hip_atomic_fetch_add(a.ctr + PT_ITER_OFF + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     io_load(0);
     if (K > 1) io_load(1);
@@ -1024,9 +1106,12 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+      if (k >= 1) io_progress(k - 1);    // the stores of iteration k-1 are complete
     }
     lds_sync();                           // barrier E: dgates of the last iteration complete
     io_store(K - 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    io_progress(K - 1);
   } else {
 
   // ================= compute waves 0..3
@@ -1163,10 +1248,11 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   }
   // ---- every wave (compute and I/O): done ticket; the last workgroup sums the bias partials in
   // tile order and clears the counters
-  if (tid == 0) flag = pt_finish(a.ctr, a.MB, a.MB * NWG, PT_EPOCH_BWD) ? 1 : 0;
-  lds_sync();                             // barrier F
-  if (flag && a.bias_ws) {
-    for (int c = tid; c < G; c += 320) {
+  lds_sync();                             // barrier F: the I/O wave's last stores + progress done
+  if (tid == 0) flag = pt_finish(a.ctr, a.MB, (int)gridDim.x, PT_EPOCH_BWD, K) ? 1 : 0;
+  lds_sync();                             // barrier G
+  if (flag && a.bias_ws && tid < 256) {
+    for (int c = tid; c < G; c += 256) {
       float v = 0.f;
       for (int m = 0; m < a.MB; ++m)
         v += __hip_atomic_load(a.bias_ws + (size_t)m * G + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1200,7 +1286,9 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
                                float* bias_ws, const int* perm, float* db1, float* db2,
                                const float* hg_dva, const bf16* hg_zr, const bf16* hg_dz,
                                float* hg_gw2, float* hg_gb2, float* hg_gb1, int hg_N, int hg_A,
-                               int hg_HD, float* hg_ws, unsigned* hg_ticket, void* stream) {
+                               int hg_HD, float* hg_ws, unsigned* hg_ticket,
+                               const int64_t* gemm_descs, int n_gw, int gw_wait, int gx_on,
+                               void* stream) {
   if (B < 1 || T < 1 || t0 < 0 || t0 >= T) return -1;
   if (H != 64 && H != 128 && H != 256 && H != 512) return -2;
   const int MB = (B + PT_ROWS - 1) / PT_ROWS, nwg = H / PL_UNITS;
@@ -1214,12 +1302,37 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
                HeadGradArgs{hg_dva, hg_zr, hg_dz, hg_gw2, hg_gb2, hg_gb1, hg_ws, hg_ticket, hg_N, hg_A,
                             hg_HD, 8},
                0};
-  if (hg_dva) {
-    if (!r2_lstm_bwd_tag_hg_ok(B, H, hg_HD) || hg_A + 1 > gs::MAXW || hg_N < 1) return -5;
-    args.hg_on = 1;
+  args.n_gw = 0; args.gw_wait = 0; args.gx_on = 0; args.n_wtiles = 0;
+  int taken = 0, nh = 0;
+  if (hg_dva || n_gw > 0 || gx_on) {
+    // helpers: every block of the 8 x 32 grid outside the recurrence's groups
+    if (!xmap || nwg > 32 || T - t0 > PT_ITER_MAX) return -6;
+    nh = 8 * 32 - MB * nwg;
+    int nw = 0, nx = 0;
+    if (n_gw < 0 || n_gw > 3) return -7;
+    for (int i = 0; i < n_gw + (gx_on ? 1 : 0); ++i) {
+      GemmProb& p = i < n_gw ? args.gw[i] : args.gx;
+      const int rc = gemm_parse_desc(gemm_descs + 16 * i, p);
+      if (rc) return -20 + rc;
+      if (p.K % 64) return -8;
+      const bool is_x = i == n_gw;
+      if (is_x ? (!p.a_kmajor || p.b_kmajor) : (p.a_kmajor || p.b_kmajor)) return -9;
+      const int tiles = p.tiles_n * ((p.M + 127) / 128);
+      if (is_x) nx = tiles; else nw += tiles;
+    }
+    const int hgi = hg_dva ? ((2 * hg_HD + 63) / 64) * 8 : 0;
+    if (nw >= nh || (hgi + nx > 0 && nh - nw < 16)) return -10;   // too few helpers
+    if (hg_dva) {
+      if (hg_A + 1 > gs::MAXW || hg_N < 1 || hg_HD % 64) return -5;
+      args.hg_on = 1;
+      taken |= 1;
+    }
+    args.n_gw = n_gw; args.gw_wait = gw_wait; args.n_wtiles = nw; args.gx_on = gx_on;
+    if (n_gw) taken |= 2;
+    if (gx_on) taken |= 4;
   }
   hipStream_t s = (hipStream_t)stream;   // counters are left zeroed by the previous launch
-  dim3 grid(xmap ? 8 * nwg : MB * nwg), block(320);
+  dim3 grid(nh ? 256 : (xmap ? 8 * nwg : MB * nwg)), block(320);
   const void* fn = H == 64 ? (const void*)lstm_bwd_tag_kernel<64>
                  : H == 128 ? (const void*)lstm_bwd_tag_kernel<128>
                  : H == 256 ? (const void*)lstm_bwd_tag_kernel<256>
@@ -1232,7 +1345,7 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
     default: hipLaunchKernelGGL(lstm_bwd_tag_kernel<512>, grid, block, PL_LDS_RESERVE, s, args); break;
   }
   R2_CHECK_LAUNCH();
-  return 0;
+  return taken;   // bit 0: head grads, 1: weight grads, 2: dX done here
 }
 
 extern "C" int r2_lstm_persist_ctr_words() { return PT_CTR_WORDS; }

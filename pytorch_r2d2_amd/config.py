@@ -92,6 +92,11 @@ class LearnerConfig:
     # persistent forward hand-off: "tagged" (8-byte {h pair, tag} granules polled directly, 16-row
     # batch tiles; falls back when the grid does not fit) | "counter" (payload + arrival counter)
     lstm_handoff: str = "tagged"
+    # tagged BPTT: GEMMs run beside the recurrence on the launch's helper workgroups
+    # ("w" = weight gradients, "x" = dX; comma-separated, "" = none).  Off by default: measured
+    # 0.799 ms/step without, 0.860 with "w", 0.987 with "x", 0.942 with both (atari57, 1 GPU) --
+    # a helper's K tiles are paced by the recurrence and each costs more than a BPTT step
+    bptt_helpers: str = ""
     # forward pipelining ("shifted" mode, persistent LSTM): the frames are processed in this many
     # time chunks; the recurrence of chunk c runs on a side stream on CUs the torso leaves free
     # while the torso + input projection of chunk c+1 run.  0/1 = serial forward (default:

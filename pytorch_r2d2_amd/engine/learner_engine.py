@@ -39,6 +39,8 @@ import math
 import time
 from typing import Dict, Optional
 
+import os
+
 import numpy as np
 import torch
 
@@ -527,9 +529,9 @@ class LearnerEngine:
         lc = self.cfg.learner
         # the tagged BPTT kernel's idle workgroups take the head-gradient reduction beside the
         # recurrence when they are enough; otherwise it runs as its own launch here
+        tagged = lc.lstm_impl == "persistent" and lc.lstm_handoff == "tagged"
         self._hg_job = None
-        if (fused_hg and lc.lstm_impl == "persistent" and lc.lstm_handoff == "tagged"
-                and int(k.r2_lstm_bwd_tag_hg_ok(B, H, HD))):
+        if fused_hg and tagged:
             self._hg_job = [ptr(self.dva), ptr(zr), ptr(self.dz), ptr(gw2), ptr(gb2), ptr(gb1),
                             N, A, HD, ptr(self.gs_ws), ptr(self.gs_ticket)]
         elif fused_hg:
@@ -554,26 +556,37 @@ class LearnerEngine:
             dh = mm_f32(self.dz, pk["head1"])                           # (N, H)
         if not fused_hg:
             gb1.copy_(mm_f32(self.ones_bf[:, :N], self.dz))
-        bias_done = self._lstm_bwd(dh)
         X = self.X_on[Lb * B: T * B]
         if Lb >= 1:
             h_prev = self.hseq["on"][Lb - 1: T - 1].reshape(N, H)
         else:
             h_prev = torch.cat([self.h0["on"][None], self.hseq["on"][: T - 1]]).reshape(N, H)
+        w_jobs = x_job = None
         if self.use_gemm:
             # weight gradients straight into the flat buffer; the row map puts the packed gate
             # order back into torch order (no gather of dgates, no copies)
             dgT = self.dgates.t()
-            gemm(Gemm(dgT, X, L.view(g, "lstm.weight_ih"), crow=self.gate_perm_i32),
-                 Gemm(dgT, h_prev, L.view(g, "lstm.weight_hh"), crow=self.gate_perm_i32),
-                 Gemm(self.dz.t(), h_learn, gw1))
+            w_jobs = [Gemm(self.dz.t(), h_learn, gw1),
+                      Gemm(dgT, h_prev, L.view(g, "lstm.weight_hh"), crow=self.gate_perm_i32),
+                      Gemm(dgT, X, L.view(g, "lstm.weight_ih"), crow=self.gate_perm_i32)]
+            x_job = Gemm(self.dgates, pk["w_ih"], self.dX)                # (N, D) bf16
+        # tagged BPTT: these GEMMs run on helper workgroups of the same launch, each K / row
+        # tile as soon as the recurrence has stored the dgates it reads
+        helpers = os.environ.get("R2D2_BPTT_HELPERS", lc.bptt_helpers).split(",")
+        ok = tagged and N % 64 == 0
+        bias_done, taken = self._lstm_bwd(dh, w_jobs if ok and "w" in helpers else None,
+                                          x_job if ok and "x" in helpers else None)
+        if self.use_gemm:
+            if not taken & 2:
+                gemm(w_jobs[2], w_jobs[1], w_jobs[0])
             # bias grads: column sums of dgates, packed -> torch gate order, into both biases
             # (fused into the tagged BPTT kernel when it ran)
             if not bias_done:
                 check(k.r2_colsum_bf16(ptr(self.dgates), N, G, ptr(self.gate_perm_i32),
                                        ptr(L.view(g, "lstm.bias_ih")), ptr(L.view(g, "lstm.bias_hh")),
                                        ptr(self.gs_ws), ptr(self.gs_ticket[32:]), s), "colsum")
-            gemm(Gemm(self.dgates, pk["w_ih"], self.dX))                  # (N, D) bf16
+            if not taken & 4:
+                gemm(x_job)
             self._dX = self.dX
         else:
             dg_o = self.dgates.index_select(1, self.gate_inv)           # original gate order
@@ -584,23 +597,35 @@ class LearnerEngine:
             L.view(g, "lstm.bias_hh").copy_(db)
             self._dX = torch.mm(self.dgates, pk["w_ih"])               # (N, D) bf16
 
-    def _lstm_bwd(self, dh: torch.Tensor) -> bool:
-        """BPTT over the learning window: dgates (Ll, B, G) from dh (Ll, B, H).  Returns True when
-        the kernel also produced the LSTM bias gradients (tagged BPTT, fused column sums)."""
+    def _lstm_bwd(self, dh: torch.Tensor, w_jobs=None, x_job=None):
+        """BPTT over the learning window: dgates (Ll, B, G) from dh (Ll, B, H).
+
+        Returns (bias_done, taken): bias_done when the kernel also produced the LSTM bias
+        gradients (tagged BPTT, fused column sums); taken = bitmask of the side jobs its helper
+        workgroups ran (1 head grads, 2 the weight-gradient GEMMs ``w_jobs`` =
+        [gw1, dW_hh, dW_ih], 4 the dX GEMM ``x_job``)."""
         k = kernels()
         s = stream_handle()
         B, T, Lb, H, pk = self.B, self.T, self.Lb, self.layout.H, self.pk
         lc, L, g = self.cfg.learner, self.layout, self.grad
         if lc.lstm_impl == "persistent" and lc.lstm_handoff == "tagged":
-            rc = k.r2_lstm_bwd_tag(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]), ptr(self.c0["on"]),
-                                   ptr(pk["w_hhT"]), ptr(self.dgates), B, T, Lb, H, ptr(self.ctr),
-                                   ptr(self.err), ptr(self.ring_b), ptr(self.bias_ws),
-                                   ptr(self.gate_perm_i32), ptr(L.view(g, "lstm.bias_ih")),
-                                   ptr(L.view(g, "lstm.bias_hh")),
-                                   *(self._hg_job or [0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0]), s)
+            base = [ptr(dh), ptr(self.gates), ptr(self.cseq["on"]), ptr(self.c0["on"]),
+                    ptr(pk["w_hhT"]), ptr(self.dgates), B, T, Lb, H, ptr(self.ctr), ptr(self.err),
+                    ptr(self.ring_b), ptr(self.bias_ws), ptr(self.gate_perm_i32),
+                    ptr(L.view(g, "lstm.bias_ih")), ptr(L.view(g, "lstm.bias_hh"))]
+            hg = self._hg_job or [0] * 11
+            descs = [d for j in (w_jobs or []) + ([x_job] if x_job is not None else []) for d in j.desc()]
+            self._gdesc = np.asarray(descs or [0], dtype=np.int64)   # kept alive for capture
+            rc = k.r2_lstm_bwd_tag(*base, *hg, self._gdesc.ctypes.data, len(w_jobs or []),
+                                   0b110 if w_jobs else 0, int(x_job is not None), s)
+            if rc in (-6, -10):   # not enough helper workgroups: recurrence alone
+                rc = k.r2_lstm_bwd_tag(*base, *([0] * 11), 0, 0, 0, 0, s)
             if rc != -3:          # -3: grid too large for one workgroup per CU
-                check(rc, "lstm_bwd_tag")
-                return True
+                if rc < 0:
+                    check(rc, "lstm_bwd_tag")
+                if self._hg_job is not None and not rc & 1:
+                    check(k.r2_head_grads(*self._hg_job, s), "head_grads")
+                return True, rc
         if self._hg_job is not None:   # the side job did not run: its own launch
             check(k.r2_head_grads(*self._hg_job, s), "head_grads")
         if lc.lstm_impl == "persistent":
@@ -613,7 +638,7 @@ class LearnerEngine:
             check(k.r2_lstm_bwd(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]), ptr(self.c0["on"]),
                                 ptr(pk["w_hhT"]), ptr(self.slab0), ptr(self.slab1), ptr(self.dc),
                                 ptr(self.dgates), B, T, Lb, H, s), "lstm_bwd")
-        return False
+        return False, 0
 
     def _relu_mask(self, grad: torch.Tensor, act: torch.Tensor) -> torch.Tensor:
         """grad * (act > 0) for two tensors with the same (channels-last) memory layout."""

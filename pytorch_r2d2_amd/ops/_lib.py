@@ -69,7 +69,7 @@ _SIGS = {
     "r2_lstm_fwd_tag": [P, I, I, I, I, P, P, P, P],
     "r2_lstm_tag_ring_bytes": [I, I, I],
     "r2_lstm_bwd_tag": [P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P, P,
-                        P, P, P, P, P, P, I, I, I, P, P, P],
+                        P, P, P, P, P, P, I, I, I, P, P, P, I, I, I, P],
     "r2_lstm_bwd_tag_hg_ok": [I, I, I],
     "r2_lstm_bwd_tag_ring_bytes": [I, I],
     "r2_lstm_bwd_persist": [P, P, P, P, P, P, P, I, I, I, I, P, P, P],

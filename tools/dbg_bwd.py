@@ -26,7 +26,7 @@ for B, H in ((8, 256), (64, 256)):
         k.r2_lstm_persist_force_slow(slow)
         dg = torch.zeros_like(dg_ref)
         k.r2_lstm_bwd_tag(ptr(dh_ext), ptr(gates), ptr(cseq), ptr(c0), ptr(pk["w_hhT"]), ptr(dg),
-                          B, T, t0, H, ptr(ctr), ptr(err), ptr(ring), 0, 0, 0, 0, *([0] * 11), stream_handle())
+                          B, T, t0, H, ptr(ctr), ptr(err), ptr(ring), 0, 0, 0, 0, *([0] * 15), stream_handle())
         torch.cuda.synchronize()
         print(B, H, "slow", slow, "err", err.item(), [round(_rel(dg[i].float(), dg_ref[i].float()), 4) for i in range(T - t0)])
         # per gate block error at tl = T - t0 - 2
