@@ -121,22 +121,24 @@ __device__ __forceinline__ void g2_epilogue(const GemmProb& P, int m0, int n0, i
 // ascending or descending order; ready(kt) is called by EVERY wave before it issues the DMA of K
 // tile kt (a per-wave poll when the operand is produced inside the same launch; then AUX = 16).
 // K % 64 == 0.  Raw barriers only (threads >= 256 of the workgroup must have exited).
+// acc += the tile's product over K tiles [kt0, kt1) (visited ascending, or descending if desc).
 template <bool AK, bool BK_, int AUX, class Ready>
-__device__ __forceinline__ void g2_tile(const GemmProb& P, int tm, int tn, uint8_t* lds, bool desc,
-                                        Ready ready) {
+__device__ __forceinline__ void g2_tile_acc(const GemmProb& P, int tm, int tn, uint8_t* lds,
+                                            int kt0, int kt1, bool desc, Ready ready,
+                                            f32x16 (&acc)[2][2]) {
   using namespace g2;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int m0 = tm * BM, n0 = tn * BN;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  const int nk = P.K / BK;
+  const int nk = kt1 - kt0;
   auto stage = [&](int i) {
-    const int kt = desc ? nk - 1 - i : i;
+    const int kt = desc ? kt1 - 1 - i : kt0 + i;
     ready(kt);
     uint8_t* st = lds + (i & 1) * (2 * TILE_B);
     g2_stage<AK, AUX>(P.A, P.lda, m0, P.M, kt * BK, st, wave, lane);
     g2_stage<BK_, AUX>(P.B, P.ldb, n0, P.N, kt * BK, st + TILE_B, wave, lane);
   };
-  f32x16 acc[2][2] = {};
+  if (nk <= 0) return;
   stage(0);
   if (nk > 1) stage(1);
   for (int i = 0; i < nk; ++i) {
@@ -162,7 +164,15 @@ __device__ __forceinline__ void g2_tile(const GemmProb& P, int tm, int tn, uint8
     __builtin_amdgcn_s_barrier();          // every wave is done reading this stage
     if (i + 2 < nk) stage(i + 2);
   }
-  g2_epilogue(P, m0, n0, wm, wn, lane, acc);
+}
+
+template <bool AK, bool BK_, int AUX, class Ready>
+__device__ __forceinline__ void g2_tile(const GemmProb& P, int tm, int tn, uint8_t* lds, bool desc,
+                                        Ready ready) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  f32x16 acc[2][2] = {};
+  g2_tile_acc<AK, BK_, AUX>(P, tm, tn, lds, 0, P.K / g2::BK, desc, ready, acc);
+  g2_epilogue(P, tm * g2::BM, tn * g2::BN, (wave >> 1) * 64, (wave & 1) * 64, lane, acc);
 }
 
 // Host: parse one 16 x int64 problem descriptor (ops/gemm.py Gemm.desc layout) and check the

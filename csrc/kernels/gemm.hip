@@ -550,6 +550,131 @@ static int g3_launch(GemmArgs& a, int ak, int bk, int tiles, hipStream_t s) {
   return 0;
 }
 
+// ============================================================================================
+// Grouped split-K launch: up to 4 problems with their own A layout (B mn-major) and K split
+// in ONE grid, items ordered as given (put the longest first).  A split item computes its K
+// range, publishes the fp32 partial tile write-through, takes the tile's ticket; the last
+// arriver sums ALL partials in split order (bit-reproducible) and runs the epilogue.  Two
+// 64-KB-LDS workgroups fit per CU, so e.g. the learner's weight-gradient products (K = 2560,
+// 128 tiles) and dX (260 tiles) share the chip instead of running one after the other.
+struct GroupArgs {
+  GemmProb p[gm::MAXP];
+  int split[gm::MAXP];
+  int item_base[gm::MAXP + 1];
+  int slab_base[gm::MAXP];     // first partial slab (64 KB) of each problem
+  int ticket_base[gm::MAXP];
+  int np, total;
+  float* ws;
+  unsigned* tickets;
+};
+
+__global__ __launch_bounds__(256) void gemm_group_kernel(const GroupArgs a) {
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[2 * 2 * g2::TILE_B];
+  __shared__ int last;
+  int bid;
+  {
+    const int b = blockIdx.x, x = b & 7, qn = a.total >> 3, r = a.total & 7;
+    bid = (x < r ? x * (qn + 1) : r * (qn + 1) + (x - r) * qn) + (b >> 3);
+  }
+  int pi = 0;
+#pragma unroll
+  for (int i = 1; i < gm::MAXP; ++i)
+    if (i < a.np && bid >= a.item_base[i]) pi = i;
+  const GemmProb& P = a.p[pi];
+  const int S = a.split[pi];
+  const int item = bid - a.item_base[pi];
+  const int tile = item / S, ks = item % S;
+  const int tm = tile / P.tiles_n, tn = tile % P.tiles_n;
+  const int nk = P.K / g2::BK, per = (nk + S - 1) / S;
+  const int kt0 = min(nk, ks * per), kt1 = min(nk, kt0 + per);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  f32x16 acc[2][2] = {};
+  auto none = [](int) {};
+  if (P.a_kmajor) g2_tile_acc<true, false, 0>(P, tm, tn, lds, kt0, kt1, false, none, acc);
+  else g2_tile_acc<false, false, 0>(P, tm, tn, lds, kt0, kt1, false, none, acc);
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  if (S > 1) {
+    // partial slab: 16 x (256 threads x 16 B), lane-major so each b128 store / load of a wave
+    // covers 1 KB of whole cache lines (thread-major rows made every write-through store touch
+    // 64 lines for 16 B each: 0.1 us per split item)
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(a.ws, 0, 0x7fffffff, 0x00020000);
+    const int slab0 = a.slab_base[pi] + tile * S;
+    auto off = [&](int s, int q) { return (uint32_t)((((size_t)(slab0 + s) * 16 + q) * 256 + tid) * 16); };
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const f32x4 v = {acc[q >> 3][(q >> 2) & 1][4 * (q & 3)], acc[q >> 3][(q >> 2) & 1][4 * (q & 3) + 1],
+                       acc[q >> 3][(q >> 2) & 1][4 * (q & 3) + 2], acc[q >> 3][(q >> 2) & 1][4 * (q & 3) + 3]};
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off(ks, q), 0, 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned* tk = a.tickets + a.ticket_base[pi] + tile;
+    if (tid == 0) last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(S - 1);
+    __syncthreads();
+    if (!last) return;
+    f32x16 sum[2][2] = {};
+    for (int s = 0; s < S; ++s) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        f32x4 v;
+        if (s == ks) {
+          v = f32x4{acc[q >> 3][(q >> 2) & 1][4 * (q & 3)], acc[q >> 3][(q >> 2) & 1][4 * (q & 3) + 1],
+                    acc[q >> 3][(q >> 2) & 1][4 * (q & 3) + 2], acc[q >> 3][(q >> 2) & 1][4 * (q & 3) + 3]};
+        } else {
+          v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off(s, q), 0, 16));
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sum[q >> 3][(q >> 2) & 1][4 * (q & 3) + e] += v[e];
+      }
+    }
+    if (tid == 0) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    g2_epilogue(P, tm * g2::BM, tn * g2::BN, wm, wn, lane, sum);
+    return;
+  }
+  g2_epilogue(P, tm * g2::BM, tn * g2::BN, wm, wn, lane, acc);
+}
+
+// descs: np x 16 int64 (ops/gemm.py layout); split[i] >= 1; ws: sum over split problems of
+// tiles * split * 64 KB; tickets: one per tile of split problems, zero at first use.
+extern "C" long long r2_gemm_group_ws_bytes(const int64_t* descs, const int* split, int np) {
+  long long b = 0;
+  for (int i = 0; i < np; ++i) {
+    GemmProb p;
+    if (gemm_parse_desc(descs + 16 * i, p)) return -1;
+    if (split[i] > 1) b += (long long)p.tiles_n * ((p.M + 127) / 128) * split[i] * 65536;
+  }
+  return b;
+}
+
+extern "C" int r2_gemm_group(const int64_t* descs, const int* split, int np, float* ws,
+                             long long ws_bytes, unsigned* tickets, int n_tickets, void* stream) {
+  if (np < 1 || np > gm::MAXP) return -1;
+  GroupArgs a;
+  a.np = np; a.ws = ws; a.tickets = tickets;
+  int items = 0, slabs = 0, tks = 0;
+  for (int i = 0; i < np; ++i) {
+    GemmProb& p = a.p[i];
+    const int rc = gemm_parse_desc(descs + 16 * i, p);
+    if (rc) return rc;
+    if (p.K % 64 || p.b_kmajor || (!p.a_kmajor && p.M % 8)) return -6;
+    const int tiles = p.tiles_n * ((p.M + 127) / 128);
+    const int S = split[i] < 1 ? 1 : split[i];
+    a.split[i] = S;
+    a.item_base[i] = items;
+    a.slab_base[i] = slabs;
+    a.ticket_base[i] = tks;
+    items += tiles * S;
+    if (S > 1) { slabs += tiles * S; tks += tiles; }
+  }
+  for (int i = np; i < gm::MAXP; ++i) { a.p[i] = a.p[0]; a.split[i] = 1; a.item_base[i] = 1 << 30; }
+  a.item_base[gm::MAXP] = items;
+  a.total = items;
+  if ((long long)slabs * 65536 > ws_bytes || tks > n_tickets) return -7;
+  hipLaunchKernelGGL(gemm_group_kernel, dim3(items), dim3(256), 0, (hipStream_t)stream, a);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
 static int g_gemm_version = 2;   // 1 = force the register-staged kernel (tests / A-B)
 extern "C" int r2_gemm_set_version(int v) { g_gemm_version = v; return 0; }
 

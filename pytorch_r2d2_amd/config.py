@@ -97,6 +97,9 @@ class LearnerConfig:
     # 0.799 ms/step without, 0.860 with "w", 0.987 with "x", 0.942 with both (atari57, 1 GPU) --
     # a helper's K tiles are paced by the recurrence and each costs more than a BPTT step
     bptt_helpers: str = ""
+    # post-BPTT GEMMs: "group" = weight gradients + dX in one grid (58 us vs 85 separate),
+    # "group:a,b,c,d" = with K splits, "separate"
+    bwd_gemm: str = "group"
     # forward pipelining ("shifted" mode, persistent LSTM): the frames are processed in this many
     # time chunks; the recurrence of chunk c runs on a side stream on CUs the torso leaves free
     # while the torso + input projection of chunk c+1 run.  0/1 = serial forward (default:

@@ -47,7 +47,7 @@ import torch
 from ..config import R2D2Config
 from ..models.qnet import QNet
 from ..ops._lib import check, kernels, ptr, stream_handle
-from ..ops.gemm import Gemm, gemm
+from ..ops.gemm import Gemm, gemm, gemm_group, group_ws_bytes
 from ..models.qnet import torso_dims
 from ..ops.torso_lib import fused_torso_supported, torso_forward_library
 from .layout import ParamLayout, UNITS
@@ -577,6 +577,12 @@ class LearnerEngine:
         bias_done, taken = self._lstm_bwd(dh, w_jobs if ok and "w" in helpers else None,
                                           x_job if ok and "x" in helpers else None)
         if self.use_gemm:
+            splits = self._group_splits(w_jobs, x_job) if not taken & 6 else None
+            if splits:
+                # weight gradients and dX share one grid (gemm_group_kernel), longest K first
+                gemm_group([w_jobs[2], w_jobs[1], w_jobs[0], x_job], splits,
+                           self.gg_ws, self.gg_tickets)
+                taken |= 6
             if not taken & 2:
                 gemm(w_jobs[2], w_jobs[1], w_jobs[0])
             # bias grads: column sums of dgates, packed -> torch gate order, into both biases
@@ -596,6 +602,25 @@ class LearnerEngine:
             L.view(g, "lstm.bias_ih").copy_(db)
             L.view(g, "lstm.bias_hh").copy_(db)
             self._dX = torch.mm(self.dgates, pk["w_ih"])               # (N, D) bf16
+
+    def _group_splits(self, w_jobs, x_job):
+        """K splits of the grouped post-BPTT launch ([dW_ih, dW_hh, dW_head1, dX]) or None for
+        separate launches.  ``learner.bwd_gemm`` (env R2D2_BWD_GEMM): "group" = no split,
+        "group:a,b,c,d" = explicit splits, "separate".  Needs every K % 64 == 0."""
+        mode = os.environ.get("R2D2_BWD_GEMM", self.cfg.learner.bwd_gemm)
+        if not mode.startswith("group"):
+            return None
+        splits = [int(v) for v in mode.split(":")[1].split(",")] if ":" in mode else [1, 1, 1, 1]
+        probs = [w_jobs[2], w_jobs[1], w_jobs[0], x_job]
+        if len(splits) != 4 or any(p.a.shape[1] % 64 for p in probs):
+            return None
+        need = group_ws_bytes(probs, splits)
+        if getattr(self, "gg_ws", None) is None or self.gg_ws.numel() * 4 < need:
+            if torch.cuda.is_current_stream_capturing():
+                return None
+            self.gg_ws = torch.zeros(need // 4 + 1, dtype=torch.float32, device=self.device)
+            self.gg_tickets = torch.zeros(1024, dtype=torch.int32, device=self.device)
+        return splits
 
     def _lstm_bwd(self, dh: torch.Tensor, w_jobs=None, x_job=None):
         """BPTT over the learning window: dgates (Ll, B, G) from dh (Ll, B, H).

@@ -61,3 +61,25 @@ def gemm(*problems: Gemm, stream=None) -> None:
     """Run up to 4 problems sharing one operand-layout combination in one launch."""
     arr = np.asarray([v for p in problems for v in p.desc()], dtype=np.int64)
     check(kernels().r2_gemm(arr.ctypes.data, len(problems), stream or stream_handle()), "gemm")
+
+
+def group_ws_bytes(problems: List[Gemm], splits: List[int]) -> int:
+    """Workspace of :func:`gemm_group` (64 KB fp32 partial per split item)."""
+    total = 0
+    for p, sp in zip(problems, splits):
+        M, N = p.a.shape[0], p.b.shape[1]
+        if sp > 1:
+            total += ((M + 127) // 128) * ((N + 127) // 128) * sp * 65536
+    return total
+
+
+def gemm_group(problems: List[Gemm], splits: List[int], ws: torch.Tensor, tickets: torch.Tensor,
+               stream=None) -> None:
+    """Up to 4 problems (any A layout, mn-major B, K % 64 == 0) in ONE launch, problem i's K
+    split ``splits[i]`` ways with a deterministic last-arriver reduction (gemm.hip
+    gemm_group_kernel).  ``tickets`` int32 zeros, >= total tiles of the split problems."""
+    arr = np.asarray([v for p in problems for v in p.desc()], dtype=np.int64)
+    sp = np.asarray(splits, dtype=np.int32)
+    check(kernels().r2_gemm_group(arr.ctypes.data, sp.ctypes.data, len(problems), ws.data_ptr(),
+                                  ws.numel() * ws.element_size(), tickets.data_ptr(), tickets.numel(),
+                                  stream or stream_handle()), "gemm_group")

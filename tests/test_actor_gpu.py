@@ -133,7 +133,7 @@ def _free_port():
     return p
 
 
-def _dp_worker(rank, world, port, outdir):
+def _dp_worker(rank, world, port, outdir, graph=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK="0")
     import torch.distributed as dist
@@ -146,17 +146,23 @@ def _dp_worker(rank, world, port, outdir):
     torch.manual_seed(5)
     eng = LearnerEngine(cfg, rp, DEV, rank=rank, world=world, process_group=dist.group.WORLD,
                         init_module=QNet("cpu", cfg.model, cfg.env))
-    for _ in range(3):
-        eng.step_eager()
+    if graph:   # 3 graph segments with the bucket all-reduces issued between them
+        eng.capture(warmup=1)
+        for _ in range(2):
+            eng.step()
+    else:
+        for _ in range(3):
+            eng.step_eager()
     torch.cuda.synchronize()
     torch.save({"master": eng.master.cpu(), "loss": eng.loss_value()}, os.path.join(outdir, f"dp{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_dp_engine_ranks_stay_identical(tmp_path):
+@pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
+def test_dp_engine_ranks_stay_identical(tmp_path, graph):
     import torch.multiprocessing as tmp
-    tmp.spawn(_dp_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    tmp.spawn(_dp_worker, args=(2, _free_port(), str(tmp_path), graph), nprocs=2, join=True)
     a = torch.load(tmp_path / "dp0.pt", weights_only=True)
     b = torch.load(tmp_path / "dp1.pt", weights_only=True)
     assert torch.equal(a["master"], b["master"])       # synchronous DP: identical replicas

@@ -81,3 +81,32 @@ def test_gemm_v1_v2_agree(ak, bk):
     kernels().r2_gemm_set_version(2)
     torch.cuda.synchronize()
     assert _rel(outs[0], outs[1]) < 1e-6
+
+
+def test_gemm_group_split_k_deterministic():
+    """gemm_group_kernel: k-major and mn-major A in one grid, K split 1/2/3 ways with the
+    last-arriver reduction; bit-identical across runs (tickets self-reset) and vs fp32 torch."""
+    from pytorch_r2d2_amd.ops.gemm import gemm_group, group_ws_bytes
+    g = torch.Generator(device=DEV).manual_seed(21)
+    probs, refs = [], []
+    shapes = [(1024, 1568, 2560, 0, 2), (1024, 256, 2560, 0, 3), (520, 1568, 1024, 1, 1)]
+    for M, N, K, ak, _ in shapes:
+        a = _op(M, K, ak, g) if ak else _op(K, M, 1, g).t()
+        b = _op(N, K, 0, g).t()
+        c = torch.randn(M, N, generator=g, device=DEV)
+        refs.append((c.clone(), a, b))
+        probs.append(Gemm(a, b, c, accumulate=True))
+    splits = [s[4] for s in shapes]
+    ws = torch.zeros(group_ws_bytes(probs, splits) // 4 + 1, device=DEV)
+    tickets = torch.zeros(1024, dtype=torch.int32, device=DEV)
+    outs = []
+    for _ in range(2):
+        for p, (c0, _, _) in zip(probs, refs):
+            p.c.copy_(c0)
+        gemm_group(probs, splits, ws, tickets)
+        torch.cuda.synchronize()
+        outs.append([p.c.clone() for p in probs])
+    assert int(tickets.abs().sum()) == 0
+    for i, (c0, a, b) in enumerate(refs):
+        assert torch.equal(outs[0][i], outs[1][i])
+        assert _rel(outs[0][i], c0 + a.float() @ b.float()) < 1e-5
