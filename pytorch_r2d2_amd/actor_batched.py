@@ -17,10 +17,12 @@ GPU context with 4 blocking D2H copies per env step (actor.py:96-106, model.py:6
 * weights are read from the co-located learner's packed bf16 buffers (zero-copy "broadcast"
   when actor and learner share a GPU), or from a versioned ``WeightPublisher`` slot.
 
-No host synchronisation per step except the optional episode-return logging.
+No host synchronisation per step: the whole env step is device-only and replays as a HIP graph
+(``capture``); finished-episode returns land in a device ring drained when read.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Dict, Optional
 
 import numpy as np
@@ -32,6 +34,24 @@ from .engine.learner_engine import addmm_f32
 from .engine.replay_hbm import HBMReplay
 from .ops._lib import check, kernels, ptr, stream_handle
 from .ops.torso_lib import fused_torso_supported, torso_forward_library
+
+
+_VP = ctypes.c_void_p
+
+
+class ActArgs(ctypes.Structure):
+    """Mirror of ``struct ActArgs`` (csrc/kernels/actor.hip); size checked against the .so."""
+    _fields_ = [(name, _VP) for name in (
+        "frames", "obs", "hs_cs", "ths_cs", "action", "reward", "done", "priority", "is_start",
+        "leaves", "n_valid", "dirty", "dcount", "q_on", "q_tg")] + [
+        (name, _VP * 2) for name in ("st_h", "st_c", "h_new", "c_new", "h32", "c", "h_bf")] + [
+        (name, _VP) for name in (
+            "h_row", "h_q", "h_a", "h_r", "h_step", "h_valid", "ep_start", "t", "head", "eps", "act",
+            "env_reward", "env_done", "env_finished", "ret_ring", "ret_cnt", "marks")] + [
+        ("FB", ctypes.c_longlong), ("seed", ctypes.c_ulonglong)] + [
+        (name, ctypes.c_int) for name in ("E", "A", "H", "n", "T", "stride", "cap_e", "W", "wrap",
+                                          "max_dirty", "R", "value_rescale")] + [
+        (name, ctypes.c_float) for name in ("gamma", "gamma_n", "prio_eps", "alpha", "vr_eps")]
 
 
 class PackedWeights:
@@ -88,8 +108,8 @@ class BatchedActor:
         eps = [epsilon_ladder(global_env_offset + i, total, cfg.actor.eps_base, cfg.actor.eps_alpha)
                for i in range(E)]
         self.eps = torch.tensor(eps, dtype=torch.float32, device=d)
-        self.g = torch.Generator(device=d)
-        self.g.manual_seed(seed + 7919 * global_env_offset)
+        # epsilon-greedy draws: counter-based hash of (seed, step, env) inside actor_pre_kernel
+        self.seed = ((seed + 7919 * global_env_offset) * 0x9E3779B97F4A7C15 + 1) & ((1 << 64) - 1)
         H, A, n = self.H, self.A, self.n
         z = lambda *s, dt=torch.float32: torch.zeros(s, dtype=dt, device=d)  # noqa: E731
         # recurrent state of both nets: bf16 h (MFMA operand), fp32 h (stored state), fp32 c
@@ -104,21 +124,51 @@ class BatchedActor:
         self.ctr = z(int(kernels().r2_lstm_persist_ctr_words()), dt=torch.int32)
         self.err = z(1, dt=torch.int32)
         # n-step history ring (device)
-        self.h_row = z(n, E, dt=torch.int64)
+        # each env's history rows point into its own sub-ring (initially its first row), so the
+        # masked scatters below never see two envs on one row
+        self.h_row = (torch.arange(E, device=d, dtype=torch.int64) * replay.cap_e).repeat(n, 1)
         self.h_q = z(n, E, A)
         self.h_a = z(n, E, dt=torch.int64)
         self.h_r = z(n, E)
         self.h_step = torch.full((n, E), -1, dtype=torch.int64, device=d)
         self.h_valid = z(n, E, dt=torch.bool)
-        # episode bookkeeping
+        # episode bookkeeping.  The step counter and the common sub-ring write position live on
+        # the device (t_d, head_d) so one captured graph serves every step; host mirrors (t, head)
+        # only pick the graph variant (the sub-ring wrap step also invalidates the old windows).
         self.t = 0                                  # actor step counter (all envs in lockstep)
         self.head = 0                               # common sub-ring write position
+        self.t_d = z(1, dt=torch.int64)
+        self.head_d = z(1, dt=torch.int64)
         self.ep_start = z(E, dt=torch.int64)        # actor step at which each episode started
         self.base = torch.arange(E, device=d, dtype=torch.int64) * replay.cap_e
-        self.finished_returns = []
+        W = self.T + n
+        self.tail_off = torch.arange(replay.cap_e - W + 1, replay.cap_e, device=d)
+        # finished-episode returns: device ring + count, drained into a host list on read
+        self.R = max(int(cfg.actor.return_ring), E)
+        if ctypes.sizeof(ActArgs) != kernels().r2_actor_args_bytes():
+            raise RuntimeError("ActArgs layout differs from csrc/kernels/actor.hip")
+        self.act = z(E, dt=torch.int64)
+        self.marks = z(E * (n + 2), dt=torch.int32)
+        self.ret_ring = z(self.R + 1)
+        self.ret_cnt = z(1, dt=torch.int64)
+        self._ret_read = 0
+        self._returns = []
         self.env_steps = 0
+        self.graphs = None
         if hasattr(env, "reset_all"):
             env.reset_all()
+
+    @property
+    def finished_returns(self):
+        """Returns of the episodes finished so far (host list; syncs to drain the device ring,
+        keeping at most ``actor.return_ring`` returns per drain)."""
+        cnt = int(self.ret_cnt.item())
+        lo = max(self._ret_read, cnt - self.R)
+        if cnt > lo:
+            ring = self.ret_ring[: self.R].cpu()
+            self._returns.extend(float(ring[i % self.R]) for i in range(lo, cnt))
+        self._ret_read = cnt
+        return self._returns
 
     # ------------------------------------------------------------------ inference
     def _infer(self):
@@ -146,127 +196,86 @@ class BatchedActor:
                                    ptr(self.q[key]), 0, E, self.A, L.HD, s), "dueling_fwd")
 
     # ------------------------------------------------------------------ one env step
+    @property
+    def can_capture(self) -> bool:
+        return (self.device.type == "cuda" and self.fused_torso
+                and getattr(self.env, "capture_safe", False))
+
+    def capture(self, warmup: int = 1):
+        """Capture the env step into two HIP graphs (plain step / sub-ring wrap step).  The
+        warmup steps are real steps; capture itself executes nothing."""
+        for _ in range(warmup):
+            self.step()
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        gens = [self.env.g] if hasattr(self.env, "g") else []
+        graphs, pool = [], None
+        for wrap in (False, True):
+            g = torch.cuda.CUDAGraph()
+            for gen in gens:
+                g.register_generator_state(gen)
+            with torch.cuda.graph(g, pool=pool, stream=side):
+                self._body(wrap)
+            pool = g.pool()
+            graphs.append(g)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        self.graphs = graphs
+
     @torch.no_grad()
     def step(self):
-        E, n, d = self.E, self.n, self.device
-        rp, rc = self.replay, self.cfg.replay
-        rows = self.base + self.head                                    # (E,) this step's rows
-        # the rows we are about to write stop being sequence starts; at a sub-ring wrap also the
-        # old sequences whose window wraps into the rows we start overwriting
-        clear = rows
-        if self.head == 0 and rp.total_written > 0:
-            W = self.T + n
-            tail = torch.arange(rp.cap_e - W + 1, rp.cap_e, device=d)
-            clear = torch.cat([rows, (self.base[:, None] + tail[None, :]).reshape(-1)])
-        rp.clear_rows(clear)
-        # observation frames of this step -> replay rows (state uint8, like state*255)
-        rp.frames[rows] = self.env.frames
-        pre = rc.stored_state == "pre"
-        self._infer()
-        q_on, q_tg = self.q["on"], self.q["tg"]
-        for key, buf in (("on", rp.hs_cs), ("tg", rp.target_hs_cs)):
-            h = self.h32[key] if pre else self.h32_new[key]
-            c = self.c[key] if pre else self.c_new[key]
-            buf[rows] = torch.cat([h, c], 1)
-        # ---- finalise the transition of step t-n (its n rewards are known; bootstrap Q(s_t))
-        slot = self.t % n
-        a_star = q_on.argmax(1, keepdim=True)
-        boot = q_tg.gather(1, a_star).squeeze(1)
-        self._finalize_slot(slot, boot)
-        # ---- act (epsilon-greedy) and step the envs
-        rand = torch.rand(E, device=d, generator=self.g)
-        ra = torch.randint(0, self.A, (E,), device=d, generator=self.g)
-        action = torch.where(rand < self.eps, ra, q_on.argmax(1))
-        rp.action[rows] = action.to(torch.uint8)
-        reward, done, finished = self.env.step(action)
-        self.h_row[slot], self.h_q[slot], self.h_a[slot] = rows, q_on, action
-        self.h_r[slot] = reward
-        self.h_step[slot] = self.t
-        self.h_valid[slot] = True
-        # ---- mark the start whose window just became complete (rows finalised through t-n)
-        newest = (self.t - n) - self.ep_start                           # newest finalised offset
-        o = newest - self.T + 1
-        ok = (o >= 0) & (o % self.stride == 0)
-        srow = self.base + (self.head - (self.t - self.ep_start) + o) % rp.cap_e
-        cand = [torch.where(ok, srow, torch.full_like(srow, -1))]
-        # ---- episode ends: flush pending transitions (truncated returns, done=1), final starts
-        if bool(done.any()):
-            cand.append(self._flush_done(done))
-            fin = finished[done]
-            self.finished_returns.extend(fin.tolist())
-        marks = torch.cat(cand).to(torch.int32)
-        rp.mark_starts(marks)
-        # recurrent state advances; episodes that ended restart from zero state
-        keep = (~done).float()[:, None]
-        for key in ("on", "tg"):
-            self.h32[key] = self.h32_new[key] * keep
-            self.c[key] = self.c_new[key] * keep
-            self.h_bf[key] = self.h32[key].to(torch.bfloat16)
-        self.ep_start = torch.where(done, torch.full_like(self.ep_start, self.t + 1), self.ep_start)
-        rp.flush_tree()
+        wrap = self.head == 0
+        if self.graphs is not None:
+            self.graphs[int(wrap)].replay()
+        else:
+            self._body(wrap)
+        rp = self.replay
         self.t += 1
         self.head = (self.head + 1) % rp.cap_e
-        rp.total_written += E
-        self.env_steps += E
+        rp.total_written += self.E
+        self.env_steps += self.E
 
-    def _write_final(self, rows, q_sel, ret, done_flag, valid):
-        rp, rc = self.replay, self.cfg.replay
-        y = ret
-        delta = q_sel - y
-        prio = (delta.abs() + rc.priority_eps) ** rc.alpha
-        r_idx = torch.where(valid, rows, torch.zeros_like(rows))
-        rp.reward[r_idx] = torch.where(valid, ret, rp.reward[r_idx])
-        rp.done[r_idx] = torch.where(valid, torch.full_like(rp.done[r_idx], done_flag), rp.done[r_idx])
-        rp.priority[r_idx] = torch.where(valid, prio, rp.priority[r_idx])
+    def _args(self, wrap: bool) -> ActArgs:
+        rp, rc, lc = self.replay, self.cfg.replay, self.cfg.learner
+        pre = rc.stored_state == "pre"
+        a = ActArgs()
+        for name, t in (("frames", rp.frames), ("obs", self.env.frames), ("hs_cs", rp.hs_cs),
+                        ("ths_cs", rp.target_hs_cs), ("action", rp.action), ("reward", rp.reward),
+                        ("done", rp.done), ("priority", rp.priority), ("is_start", rp.is_start),
+                        ("leaves", rp.tree), ("n_valid", rp.n_valid), ("dirty", rp.dirty),
+                        ("dcount", rp.dirty_count), ("q_on", self.q["on"]), ("q_tg", self.q["tg"]),
+                        ("h_row", self.h_row), ("h_q", self.h_q), ("h_a", self.h_a), ("h_r", self.h_r),
+                        ("h_step", self.h_step), ("h_valid", self.h_valid), ("ep_start", self.ep_start),
+                        ("t", self.t_d), ("head", self.head_d), ("eps", self.eps), ("act", self.act),
+                        ("ret_ring", self.ret_ring), ("ret_cnt", self.ret_cnt), ("marks", self.marks)):
+            setattr(a, name, ptr(t))
+        for i, key in enumerate(("on", "tg")):
+            a.st_h[i] = ptr(self.h32[key] if pre else self.h32_new[key])
+            a.st_c[i] = ptr(self.c[key] if pre else self.c_new[key])
+            a.h_new[i], a.c_new[i] = ptr(self.h32_new[key]), ptr(self.c_new[key])
+            a.h32[i], a.c[i], a.h_bf[i] = ptr(self.h32[key]), ptr(self.c[key]), ptr(self.h_bf[key])
+        a.FB, a.seed = rp.frames.shape[1] if rp.frame_bytes else 0, self.seed
+        a.E, a.A, a.H, a.n, a.T, a.stride = self.E, self.A, self.H, self.n, self.T, self.stride
+        a.cap_e, a.W, a.wrap = rp.cap_e, self.T + self.n, int(wrap)
+        a.max_dirty, a.R, a.value_rescale = rp.max_dirty, self.R, int(lc.value_rescale)
+        a.gamma, a.gamma_n = self.gamma, self.gamma_n
+        a.prio_eps, a.alpha, a.vr_eps = rc.priority_eps, rc.alpha, lc.value_rescale_eps
+        return a
 
-    def _returns_from(self, step_from: torch.Tensor, upto: int) -> torch.Tensor:
-        """sum_k gamma^(s_k - step_from) r_k over buffered steps s_k in [step_from, upto]."""
-        st = self.h_step                                               # (n, E)
-        inside = (st >= step_from[None, :]) & (st <= upto) & (st >= 0)
-        pw = torch.pow(torch.tensor(self.gamma, device=self.device),
-                       (st - step_from[None, :]).clamp_min(0).float())
-        return (self.h_r * pw * inside.float()).sum(0)
-
-    def _finalize_slot(self, slot: int, boot: torch.Tensor):
-        valid = self.h_valid[slot]
-        s0 = self.h_step[slot]
-        R = self._returns_from(s0, self.t - 1)
-        if self.cfg.learner.value_rescale:
-            from .models.qnet import value_rescale, value_rescale_inv
-            eps = self.cfg.learner.value_rescale_eps
-            y = value_rescale(R + self.gamma_n * value_rescale_inv(boot, eps), eps)
-        else:
-            y = R + self.gamma_n * boot
-        q_sel = self.h_q[slot].gather(1, self.h_a[slot][:, None]).squeeze(1)
-        rp, rc = self.replay, self.cfg.replay
-        prio = ((q_sel - y).abs() + rc.priority_eps) ** rc.alpha
-        rows = torch.where(valid, self.h_row[slot], torch.zeros_like(self.h_row[slot]))
-        rp.reward[rows] = torch.where(valid, R, rp.reward[rows])
-        rp.done[rows] = torch.where(valid, torch.zeros_like(rp.done[rows]), rp.done[rows])
-        rp.priority[rows] = torch.where(valid, prio, rp.priority[rows])
-        self.h_valid[slot] = False
-
-    def _flush_done(self, done: torch.Tensor) -> torch.Tensor:
-        """Episode end for envs in `done`: every pending transition gets its truncated return,
-        done=1 (no bootstrap).  Returns the start rows to mark (or -1)."""
-        n, t = self.n, self.t
-        rp = self.replay
-        for j in range(n):
-            valid = self.h_valid[j] & done
-            R = self._returns_from(self.h_step[j], t)
-            q_sel = self.h_q[j].gather(1, self.h_a[j][:, None]).squeeze(1)
-            self._write_final(self.h_row[j], q_sel, R, 1, valid)
-            self.h_valid[j] = self.h_valid[j] & ~done
-        # starts whose windows end inside the just-finalised tail, plus the final start L-T
-        L = (t - self.ep_start) + 1                                    # episode length (rows)
-        prev_newest = (t - n) - self.ep_start                          # handled by per-step marks
-        out = []
-        for jj in range(n + 1):
-            o = L - self.T - jj
-            ok = done & (o >= 0) & (o > prev_newest - self.T + 1) & ((o % self.stride == 0) | (jj == 0))
-            srow = self.base + (self.head - (t - self.ep_start) + o) % rp.cap_e
-            out.append(torch.where(ok, srow, torch.full_like(srow, -1)))
-        return torch.cat(out)
+    def _body(self, wrap: bool):
+        """One env step for all E envs, device-only (no host sync, capture-safe): inference of
+        both nets, then actor.hip's fused bookkeeping around the device env step."""
+        k = kernels()
+        s = stream_handle()
+        self._infer()
+        a = self._args(wrap)
+        check(k.r2_actor_pre(ctypes.byref(a), s), "actor_pre")
+        reward, done, finished = self.env.step(self.act)
+        a.env_reward, a.env_finished = ptr(reward.float().contiguous()), ptr(finished.contiguous())
+        a.env_done = ptr(done.to(torch.bool).contiguous())
+        check(k.r2_actor_post(ctypes.byref(a), s), "actor_post")
+        self.replay.mark_starts(self.marks)
+        self.replay.update_tree()
+        check(k.r2_actor_tail(ctypes.byref(a), s), "actor_tail")
 
     def run(self, n_steps: int):
         for _ in range(n_steps):

@@ -120,6 +120,10 @@ class ActorConfig:
     net_load_interval: int = 5        # actor.py:51 (episodes)
     memory_save_interval: int = 5     # actor.py:44 (episodes)
     local_capacity: int = 50_000      # actor.py:34
+    # batched GPU actor: replay each env step as a HIP graph (two variants: plain / sub-ring
+    # wrap); needs a device env whose step() is capture-safe (VecSyntheticAtari)
+    use_graph: bool = True
+    return_ring: int = 4096           # device ring of finished-episode returns (drained lazily)
 
 
 @dataclass

@@ -265,8 +265,8 @@ class HBMReplay:
         """Rows about to be overwritten stop being sequence starts (leaf -> 0, n_valid--)."""
         was = self.is_start[rows].to(torch.int32)
         self.n_valid.sub_(was.sum().view(1))
-        self.is_start[rows] = 0
-        self.tree[rows] = 0.0
+        self.is_start.index_fill_(0, rows, 0)      # (index_fill_: no host scalar copy, capturable)
+        self.tree.index_fill_(0, rows, 0.0)
         self._append_dirty(rows)
 
     def _append_dirty(self, rows: torch.Tensor) -> None:

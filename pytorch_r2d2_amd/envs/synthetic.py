@@ -80,6 +80,8 @@ class VecSyntheticAtari:
     """E synthetic envs on a torch device.  ``frames`` (E, C*H*W) uint8 is rewritten in place
     by ``reset_all``/``step`` (the actor's torso kernel reads it directly)."""
 
+    capture_safe = True   # step() is device-only and in place (BatchedActor.capture)
+
     def __init__(self, n_envs: int, device, seed: int = 0, episode_len: int = 400,
                  n_actions: int = 6, n_stacks: int = 4, switch: int = 8,
                  cue_only_first: bool = False, shape=(84, 84), randomize_start: bool = True):
@@ -132,10 +134,11 @@ class VecSyntheticAtari:
         self.t += 1
         sw = (self.t % self.switch) == 0
         new_t = torch.randint(0, self.A, (self.E,), device=self.device, generator=self.g)
-        self.target = torch.where(sw, new_t, self.target)
+        # in place throughout: the batched actor replays this step inside a HIP graph
+        self.target.copy_(torch.where(sw, new_t, self.target))
         done = self.t >= self.episode_len
         finished = torch.where(done, self.ep_return, torch.full_like(self.ep_return, float("nan")))
-        self.t = torch.where(done, torch.zeros_like(self.t), self.t)
-        self.ep_return = torch.where(done, torch.zeros_like(self.ep_return), self.ep_return)
+        self.t.masked_fill_(done, 0)
+        self.ep_return.masked_fill_(done, 0.0)
         self._render()
         return reward, done, finished

@@ -57,6 +57,10 @@ _SIGS = {
     "r2_gemm": [P, I, P],
     "r2_gemm_set_version": [I],
     "r2_gemm_group": [P, P, I, P, I64, P, I, P],
+    "r2_actor_pre": [P, P],
+    "r2_actor_post": [P, P],
+    "r2_actor_tail": [P, P],
+    "r2_actor_args_bytes": [],
     "r2_pack_step": [P, P, I64, P, P, P, I64, P, P, P, I64, I64, I64, P, P, I64, P, I64, P],
     "r2_torso_bwd_set_debug": [P],
     "r2_torso_fwd_set_debug": [P],

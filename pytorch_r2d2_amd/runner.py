@@ -68,6 +68,8 @@ def run_native(cfg: R2D2Config, steps: int = 1000, actor_steps_per_update: int =
     t_warm = time.perf_counter() - t0
     if use_graph and cfg.learner.use_graph:
         eng.capture(warmup=1)
+    if use_graph and cfg.actor.use_graph and actor.can_capture:
+        actor.capture(warmup=1)
     losses = []
     t1 = time.perf_counter()
     for it in range(steps):

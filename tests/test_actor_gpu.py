@@ -19,17 +19,30 @@ DEV = torch.device("cuda")
 
 
 class RecEnv(VecSyntheticAtari):
-    def __init__(self, *a, **k):
+    """Records every step's rewards / dones into device logs (in place, so it also works when
+    the actor replays its step as a HIP graph)."""
+
+    def __init__(self, *a, max_steps=512, **k):
         super().__init__(*a, **k)
-        self.log = []
+        self._r = torch.zeros(max_steps, self.E, device=self.device)
+        self._d = torch.zeros(max_steps, self.E, dtype=torch.bool, device=self.device)
+        self._i = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.steps = 0
 
     def step(self, actions):
         r, d, f = super().step(actions)
-        self.log.append((r.cpu().numpy().copy(), d.cpu().numpy().copy()))
+        self._r.index_copy_(0, self._i, r[None])
+        self._d.index_copy_(0, self._i, d[None])
+        self._i.add_(1)
         return r, d, f
 
+    @property
+    def log(self):
+        n = int(self._i.item())
+        return list(zip(self._r[:n].cpu().numpy(), self._d[:n].cpu().numpy()))
 
-def _actor(E=8, cap_e=400, ep=37, **over):
+
+def _actor(E=8, cap_e=400, ep=37, graph=False, **over):
     kw = {"replay.burn_in": 4, "replay.learn": 6, "replay.overlap": 5, "replay.n_step": 3}
     kw.update(over)
     cfg = get_config("atari57", **kw)
@@ -39,11 +52,16 @@ def _actor(E=8, cap_e=400, ep=37, **over):
     w = PackedWeights(L, DEV)
     w.load(QNet("cpu", cfg.model, cfg.env).state_dict())
     env = RecEnv(E, DEV, seed=3, episode_len=ep, randomize_start=True)
-    return cfg, rp, env, BatchedActor(cfg, rp, env, w, w, seed=1)
+    actor = BatchedActor(cfg, rp, env, w, w, seed=1)
+    if graph:   # HIP-graph replay of the env step (the same checks must hold)
+        assert actor.can_capture
+        actor.capture(warmup=0)
+    return cfg, rp, env, actor
 
 
-def test_actor_nstep_returns_dones_and_starts():
-    cfg, rp, env, actor = _actor()
+@pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
+def test_actor_nstep_returns_dones_and_starts(graph):
+    cfg, rp, env, actor = _actor(graph=graph)
     steps = 150
     actor.run(steps)
     torch.cuda.synchronize()
@@ -74,6 +92,10 @@ def test_actor_nstep_returns_dones_and_starts():
             assert reward[row] == pytest.approx(R, rel=1e-5, abs=1e-5), (e, t)
             checked += 1
     assert checked > 500
+    # every finished episode's return reached the (device) return ring
+    rets = actor.finished_returns
+    assert len(rets) == int(dn.sum()) > 0
+    assert all(r == r and 0 <= r <= ep_len for r in rets for ep_len in [37])
     # starts: inside one episode, on the stride grid or the final start; window complete
     for e in range(E):
         ends = [-1] + list(np.nonzero(dn[:, e])[0])
@@ -90,8 +112,9 @@ def test_actor_nstep_returns_dones_and_starts():
     assert rp.total_priority() == pytest.approx(float(leaves.double().sum()), rel=1e-4)
 
 
-def test_actor_ring_wrap_invalidates_overwritten_sequences():
-    cfg, rp, env, actor = _actor(E=4, cap_e=60, ep=25)
+@pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
+def test_actor_ring_wrap_invalidates_overwritten_sequences(graph):
+    cfg, rp, env, actor = _actor(E=4, cap_e=60, ep=25, graph=graph)
     actor.run(200)   # > 3 passes over each sub-ring
     torch.cuda.synchronize()
     T, n = cfg.replay.seq_len, cfg.replay.n_step

@@ -5,12 +5,12 @@ import glob
 import sys
 
 
-def main(path_glob, out=None, last=1):
+def main(path_glob, out=None, last=1, marker='step_end'):
     import os
     paths = sorted(glob.glob(path_glob), key=os.path.getmtime, reverse=True)
     rows = list(csv.DictReader(open(paths[0])))
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
-    ends = [i for i, r in enumerate(rows) if 'step_end' in r['Kernel_Name']]
+    ends = [i for i, r in enumerate(rows) if marker in r['Kernel_Name']]
     a, b = ends[-1 - last] + 1, ends[-1] + 1
     st = rows[a:b]
     t0 = int(st[0]['Start_Timestamp'])
@@ -32,4 +32,5 @@ def main(path_glob, out=None, last=1):
 
 if __name__ == "__main__":
     main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None,
-         int(sys.argv[3]) if len(sys.argv) > 3 else 1)
+         int(sys.argv[3]) if len(sys.argv) > 3 else 1,
+         sys.argv[4] if len(sys.argv) > 4 else 'step_end')
