@@ -42,6 +42,8 @@ def main(argv=None):
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--target-mode", default="")
     ap.add_argument("--profile-phases", action="store_true")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="config override, e.g. --set learner.fwd_chunks=2 (A/B experiments)")
     args = ap.parse_args(argv)
 
     import torch
@@ -62,6 +64,9 @@ def main(argv=None):
     overrides = {"seed": 1234 + rank}
     if args.target_mode:
         overrides["learner.target_mode"] = args.target_mode
+    for kv in args.set:
+        key, _, val = kv.partition("=")
+        overrides[key] = val
     cfg = get_config(args.config, **overrides)
     cap = args.capacity or cfg.replay.capacity
     replay = HBMReplay(cfg, device, capacity=cap)

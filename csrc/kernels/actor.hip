@@ -76,13 +76,6 @@ __device__ __forceinline__ long long pymod(long long a, long long m) {
   return r < 0 ? r + m : r;
 }
 
-__device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
-  x += 0x9E3779B97F4A7C15ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  return x ^ (x >> 31);
-}
-
 __device__ __forceinline__ float vr_h(float x, float e) {
   return copysignf(sqrtf(fabsf(x) + 1.f) - 1.f, x) * (x != 0.f) + e * x;
 }
@@ -170,10 +163,8 @@ __global__ __launch_bounds__(256) void actor_pre_kernel(const ActArgs a) {
   }
   a.h_valid[hs] = 0;
   // 5. epsilon-greedy over the per-env ladder (counter-based RNG: seed, step, env)
-  const unsigned long long k0 = a.seed ^ ((unsigned long long)t * 0xD1B54A32D192ED03ull) ^
-                                ((unsigned long long)e << 40);
-  const float u = (float)(mix64(k0) >> 40) * (1.f / 16777216.f);
-  const int ra = (int)((mix64(k0 ^ 0x5851F42D4C957F2Dull) >> 32) % (unsigned long long)a.A);
+  const float u = r2_uniform(a.seed, (uint64_t)t, 2 * (uint64_t)e);
+  const int ra = min((int)(r2_uniform(a.seed, (uint64_t)t, 2 * (uint64_t)e + 1) * a.A), a.A - 1);
   const int act = u < a.eps[e] ? ra : greedy;
   a.act[e] = act;
   a.action[row] = (uint8_t)act;

@@ -42,13 +42,12 @@ __device__ __forceinline__ float wave_incl_scan(float v, int lane) {
   return v;
 }
 
-// ---- sampling: one wave per sample, stratified over [0, total)
-__global__ void tree_sample_kernel(const float* __restrict__ tree, TreeGeom g, int B,
-                                   uint64_t seed, const int64_t* __restrict__ step,
-                                   int* __restrict__ out_idx, float* __restrict__ out_prob) {
-  const int lane = threadIdx.x & 63;
-  const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (b >= B) return;
+// ---- sampling: one wave per sample, stratified over [0, total).  Returns the leaf (row) and
+// sets *prob = leaf / total (lane 0's value is the one to use).
+__device__ __forceinline__ int tree_descend(const float* __restrict__ tree, const TreeGeom& g,
+                                            int B, int b, uint64_t seed,
+                                            const int64_t* __restrict__ step, int lane,
+                                            float* prob) {
   const float total = tree[g.off[g.levels - 1]];
   const uint64_t ctr = step ? (uint64_t)(*step) : 0ull;
   float u = ((float)b + r2_uniform(seed, ctr, (uint64_t)b)) / (float)B * total;
@@ -71,9 +70,64 @@ __global__ void tree_sample_kernel(const float* __restrict__ tree, TreeGeom g, i
     u = fminf(fmaxf(u - ex, 0.f), pv * 0.99999f);
     node = node * 64 + pick;
   }
+  *prob = total > 0.f ? tree[node] / total : 0.f;
+  return (int)node;
+}
+
+__global__ void tree_sample_kernel(const float* __restrict__ tree, TreeGeom g, int B,
+                                   uint64_t seed, const int64_t* __restrict__ step,
+                                   int* __restrict__ out_idx, float* __restrict__ out_prob) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (b >= B) return;
+  float prob;
+  const int node = tree_descend(tree, g, B, b, seed, step, lane, &prob);
   if (lane == 0) {
-    out_idx[b] = (int)node;
-    if (out_prob) out_prob[b] = total > 0.f ? tree[node] / total : 0.f;
+    out_idx[b] = node;
+    if (out_prob) out_prob[b] = prob;
+  }
+}
+
+// ---- the learner's batch head in one launch, one workgroup per sampled sequence b: tree
+// descent (wave 0) -> time-major row list rows[t*B + b] = row(s_b, t) for t < Tn -> stored
+// recurrent states of up to 3 chains (row(s_b, off_j): h as bf16, c fp32).  Replaces
+// tree_sample + make_rows + one gather_state per chain (4-5 dependent launches).
+struct SampleBatchArgs {
+  const float* tree;
+  TreeGeom g;
+  uint64_t seed;
+  const int64_t* step;
+  int* starts;
+  float* probs;
+  int* rows;
+  const float* hs[3];
+  bf16* h[3];
+  float* c[3];
+  int off[3];
+  int B, Tn, cap_e, H, nstate;
+};
+
+__global__ __launch_bounds__(256) void sample_batch_kernel(const SampleBatchArgs a) {
+  __shared__ int s_start;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (tid < 64) {
+    float prob;
+    const int node = tree_descend(a.tree, a.g, a.B, b, a.seed, a.step, tid, &prob);
+    if (tid == 0) {
+      a.starts[b] = node;
+      a.probs[b] = prob;
+      s_start = node;
+    }
+  }
+  __syncthreads();
+  const int s = s_start;
+  for (int t = tid; t < a.Tn; t += blockDim.x) a.rows[t * a.B + b] = ring_row_s(s, t, a.cap_e);
+  for (int j = 0; j < a.nstate; ++j) {
+    const float* src = a.hs[j] + (size_t)ring_row_s(s, a.off[j], a.cap_e) * 2 * a.H;
+    for (int k = tid; k < a.H; k += blockDim.x) {
+      a.h[j][(size_t)b * a.H + k] = (bf16)src[k];
+      a.c[j][(size_t)b * a.H + k] = src[a.H + k];
+    }
   }
 }
 
@@ -230,6 +284,28 @@ extern "C" int r2_tree_sample(const float* tree, const int64_t* offs, const int6
   TreeGeom g = make_geom(offs, sizes, levels);
   hipLaunchKernelGGL(tree_sample_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream,
                      tree, g, B, seed, step, out_idx, out_prob);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
+// hs/h/c: nstate pointers each (host arrays, int64); off: nstate row offsets
+extern "C" int r2_sample_batch(const float* tree, const int64_t* offs, const int64_t* sizes,
+                               int levels, int B, uint64_t seed, const int64_t* step, int* starts,
+                               float* probs, int* rows, int Tn, int cap_e, int H, int nstate,
+                               const int64_t* hs, const int* off, const int64_t* h,
+                               const int64_t* c, void* stream) {
+  if (levels < 2 || levels > TREE_MAX_LEVELS || nstate < 0 || nstate > 3 || B < 1) return -1;
+  SampleBatchArgs a;
+  a.tree = tree; a.g = make_geom(offs, sizes, levels); a.seed = seed; a.step = step;
+  a.starts = starts; a.probs = probs; a.rows = rows;
+  for (int j = 0; j < 3; ++j) {
+    a.hs[j] = j < nstate ? (const float*)hs[j] : nullptr;
+    a.h[j] = j < nstate ? (bf16*)h[j] : nullptr;
+    a.c[j] = j < nstate ? (float*)c[j] : nullptr;
+    a.off[j] = j < nstate ? off[j] : 0;
+  }
+  a.B = B; a.Tn = Tn; a.cap_e = cap_e; a.H = H; a.nstate = nstate;
+  hipLaunchKernelGGL(sample_batch_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, a);
   R2_CHECK_LAUNCH();
   return 0;
 }

@@ -430,15 +430,15 @@ class LearnerEngine:
         L, rp, lc = self.layout, self.replay, self.cfg.learner
         H, A = L.H, L.A
         pk, pt = self.pk, self.pk_t
-        rp.sample(B, self.starts, self.probs)
-        check(k.r2_make_rows(ptr(self.starts), B, Tn, 0, rp.cap_e, ptr(self.rows), s), "make_rows")
-        rows = self.rows
-        # stored recurrent state
+        # sample -> time-major row list -> stored recurrent states, one launch
+        # (replay_memory.py:224-262: multinomial over a host scan + per-row Python gathers)
         st_off = {"on": 0, "tg": 0 if self.mode == "shifted" else n, "nx": n}
-        check(k.r2_gather_state(ptr(rp.hs_cs), ptr(self.starts), B, 0, rp.cap_e, H,
-                                ptr(self.h0["on"]), ptr(self.c0["on"]), 0, s), "gather_state")
-        check(k.r2_gather_state(ptr(rp.target_hs_cs), ptr(self.starts), B, st_off["tg"], rp.cap_e,
-                                H, ptr(self.h0["tg"]), ptr(self.c0["tg"]), 0, s), "gather_state")
+        states = [(rp.hs_cs, 0, self.h0["on"], self.c0["on"]),
+                  (rp.target_hs_cs, st_off["tg"], self.h0["tg"], self.c0["tg"])]
+        if self.mode == "fixed":
+            states.append((rp.hs_cs, n, self.h0["nx"], self.c0["nx"]))
+        rp.sample_batch(B, self.starts, self.probs, self.rows, Tn, states)
+        rows = self.rows
         if self._chunks is not None:
             self._forward_pipelined()
             xp_on, xp_tg = self.xp_on, self.xp_tg
@@ -465,8 +465,6 @@ class LearnerEngine:
         if self.mode == "shifted":
             self._lstm([on, tg], self.Tc)
         elif self.mode == "fixed":
-            check(k.r2_gather_state(ptr(rp.hs_cs), ptr(self.starts), B, n, rp.cap_e, H,
-                                    ptr(self.h0["nx"]), ptr(self.c0["nx"]), 0, s), "gather_state")
             nx = self._chain_desc(xp_on[n * B:], pk, self.h0["nx"], self.c0["nx"], self.hseq["nx"],
                                   self.cseq["nx"])
             self._lstm([on, tg, nx], T)

@@ -43,6 +43,7 @@ _SIGS = {
     "r2_seqprio_refresh": [P, I, P, P, P, I, I, I, I, F, P, P, I, P],
     "r2_mark_starts": [P, P, I, P, P, P, I, I, F, P, P, P, I, P],
     "r2_make_rows": [P, I, I, I, I, P, P],
+    "r2_sample_batch": [P, P, P, I, I, U64, P, P, P, P, I, I, I, I, P, P, P, P, P],
     "r2_gather_state": [P, P, I, I, I, I, P, P, P, P],
     "r2_step_end": [P, P, P],
     "r2_rmsprop_centered": [P, P, P, P, I64, F, F, F, F, P, F, P],
@@ -78,7 +79,6 @@ _SIGS = {
     "r2_lstm_bwd_tag_hg_ok": [I, I, I],
     "r2_lstm_bwd_tag_ring_bytes": [I, I],
     "r2_lstm_bwd_persist": [P, P, P, P, P, P, P, I, I, I, I, P, P, P],
-    "r2_actor_finalize": [P] * 21 + [I, I, I, I, I, I, F, F, F, F, U64, P],
 }
 
 
