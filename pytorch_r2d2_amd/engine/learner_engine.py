@@ -444,11 +444,24 @@ class LearnerEngine:
             xp_on, xp_tg = self.xp_on, self.xp_tg
             self._xp = (xp_on, xp_tg)
             return self._forward_tail()
-        # torso: online over all Tn frames (save activations of the learning frames)
-        self._torso(pk, rows[: Lb * B], self.X_on[: Lb * B])
-        self._torso(pk, rows[Lb * B: T * B], self.X_on[Lb * B: T * B], save=True)
-        self._torso(pk, rows[T * B:], self.X_on[T * B:])
-        self._torso(pt, rows[self.t_lo_tg * B:], self.X_tg)
+        # torso: online over all Tn frames (save activations of the learning frames) and target
+        if self.fused_torso:
+            # one launch, workers dealt to the 4 jobs in proportion to their frames: separate
+            # launches each ended in a partly idle last round of frames (18.6 us for the 320
+            # tail frames alone)
+            jobs = [self._torso_job(pk, rows[: Lb * B], self.X_on[: Lb * B]),
+                    self._torso_job(pk, rows[Lb * B: T * B], self.X_on[Lb * B: T * B], save_at=0),
+                    self._torso_job(pk, rows[T * B:], self.X_on[T * B:]),
+                    self._torso_job(pt, rows[self.t_lo_tg * B:], self.X_tg)]
+            jobs = [j for j in jobs if j[1] > 0]
+            self._tjobs = np.asarray(jobs, dtype=np.int64)          # kept alive for capture
+            check(k.r2_torso_fwd_multi(ptr(rp.frames), self._tjobs.ctypes.data, len(jobs), 256,
+                                       0, 0, s), "torso_fwd_multi")
+        else:
+            self._torso(pk, rows[: Lb * B], self.X_on[: Lb * B])
+            self._torso(pk, rows[Lb * B: T * B], self.X_on[Lb * B: T * B], save=True)
+            self._torso(pk, rows[T * B:], self.X_on[T * B:])
+            self._torso(pt, rows[self.t_lo_tg * B:], self.X_tg)
         # input projections (one GEMM per net over every row)
         if self.use_gemm:
             xp_on, xp_tg = self.xp_on, self.xp_tg
