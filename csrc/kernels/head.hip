@@ -16,14 +16,36 @@
 // z: (N, 2*HD) bf16 pre-activation of [val.0 ; adv.0] WITHOUT bias; b1: (2*HD) fp32
 // w2: (1 + A, HD) fp32 rows [val.2.weight ; adv.2.weight]; b2: (1 + A)
 // q: (N, A) fp32 out.  zr (optional): (N, 2*HD) bf16 relu(z + b1) out (for weight grads)
+// Up to 3 heads (online / target / online-on-next) per launch: wave w takes row w - row0[j] of
+// the head j whose row range holds it.
+#define HEAD_MAXJ 3
+struct DuelJob {
+  const bf16* z; const float* b1; const float* w2; const float* b2; float* q; bf16* zr;
+  int N, row0;
+};
+struct DuelArgs {
+  DuelJob j[HEAD_MAXJ];
+  int nj, A;
+};
+
 template <int HD>
-__global__ __launch_bounds__(256) void dueling_fwd_kernel(
-    const bf16* __restrict__ z, const float* __restrict__ b1, const float* __restrict__ w2,
-    const float* __restrict__ b2, float* __restrict__ q, bf16* __restrict__ zr, int N, int A) {
+__global__ __launch_bounds__(256) void dueling_fwd_kernel(const DuelArgs args) {
   constexpr int PER = HD / 64;
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  int ji = 0;
+#pragma unroll
+  for (int i = 1; i < HEAD_MAXJ; ++i)
+    if (i < args.nj && w >= args.j[i].row0) ji = i;
+  const DuelJob& J = args.j[ji];
+  const int row = w - J.row0, N = J.N, A = args.A;
   if (row >= N) return;
+  const bf16* __restrict__ z = J.z;
+  const float* __restrict__ b1 = J.b1;
+  const float* __restrict__ w2 = J.w2;
+  const float* __restrict__ b2 = J.b2;
+  float* __restrict__ q = J.q;
+  bf16* __restrict__ zr = J.zr;
   const bf16* zrow = z + (size_t)row * 2 * HD;
   float hv[PER], ha[PER];
 #pragma unroll
@@ -86,21 +108,42 @@ __global__ __launch_bounds__(256) void dueling_bwd_kernel(
   }
 }
 
-extern "C" int r2_dueling_fwd(const bf16* z, const float* b1, const float* w2, const float* b2,
-                              float* q, bf16* zr, int N, int A, int HD, void* stream) {
-  if (N <= 0) return 0;
+// jobs: nj x 7 int64 {z, b1, w2, b2, q, zr, N}
+extern "C" int r2_dueling_fwd_multi(const int64_t* jobs, int nj, int A, int HD, void* stream) {
+  if (nj < 1 || nj > HEAD_MAXJ) return -3;
   if (A < 1 || A > HEAD_MAXA) return -1;
-  dim3 grid((N + 3) / 4), block(256);
+  DuelArgs a{};
+  a.nj = nj;
+  a.A = A;
+  int rows = 0;
+  for (int i = 0; i < nj; ++i) {
+    const int64_t* p = jobs + 7 * i;
+    DuelJob& J = a.j[i];
+    J.z = (const bf16*)p[0]; J.b1 = (const float*)p[1]; J.w2 = (const float*)p[2];
+    J.b2 = (const float*)p[3]; J.q = (float*)p[4]; J.zr = (bf16*)p[5];
+    J.N = (int)(p[6] > 0 ? p[6] : 0); J.row0 = rows;
+    rows += J.N;
+  }
+  for (int i = nj; i < HEAD_MAXJ; ++i) a.j[i].row0 = 1 << 30;
+  if (rows <= 0) return 0;
+  dim3 grid((rows + 3) / 4), block(256);
   hipStream_t s = (hipStream_t)stream;
   switch (HD) {
-    case 64: hipLaunchKernelGGL(dueling_fwd_kernel<64>, grid, block, 0, s, z, b1, w2, b2, q, zr, N, A); break;
-    case 128: hipLaunchKernelGGL(dueling_fwd_kernel<128>, grid, block, 0, s, z, b1, w2, b2, q, zr, N, A); break;
-    case 256: hipLaunchKernelGGL(dueling_fwd_kernel<256>, grid, block, 0, s, z, b1, w2, b2, q, zr, N, A); break;
-    case 512: hipLaunchKernelGGL(dueling_fwd_kernel<512>, grid, block, 0, s, z, b1, w2, b2, q, zr, N, A); break;
+    case 64: hipLaunchKernelGGL(dueling_fwd_kernel<64>, grid, block, 0, s, a); break;
+    case 128: hipLaunchKernelGGL(dueling_fwd_kernel<128>, grid, block, 0, s, a); break;
+    case 256: hipLaunchKernelGGL(dueling_fwd_kernel<256>, grid, block, 0, s, a); break;
+    case 512: hipLaunchKernelGGL(dueling_fwd_kernel<512>, grid, block, 0, s, a); break;
     default: return -2;
   }
   R2_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int r2_dueling_fwd(const bf16* z, const float* b1, const float* w2, const float* b2,
+                              float* q, bf16* zr, int N, int A, int HD, void* stream) {
+  const int64_t job[7] = {(int64_t)z, (int64_t)b1, (int64_t)w2, (int64_t)b2, (int64_t)q,
+                          (int64_t)zr, N};
+  return r2_dueling_fwd_multi(job, 1, A, HD, stream);
 }
 
 extern "C" int r2_dueling_bwd(const float* dq, const bf16* zr, const float* w2, bf16* dz,

@@ -333,11 +333,12 @@ class LearnerEngine:
             zs = [zb for _, _, zb, _, _ in jobs]
         else:
             zs = [torch.mm(h, pk["head1"].t()) for pk, h, _, _, _ in jobs]
-        for (pk, h, _, q, zr), z in zip(jobs, zs):
-            check(kernels().r2_dueling_fwd(ptr(z), ptr(pk["head_b1"]), ptr(pk["head_w2"]),
-                                           ptr(pk["head_b2"]), ptr(q), ptr(zr), h.shape[0],
-                                           self.layout.A, self.layout.HD, stream_handle()),
-                  "dueling_fwd")
+        # bias + ReLU + 512 -> 1+A + dueling combine of every head in one launch
+        self._djobs = np.asarray([[ptr(z), ptr(pk["head_b1"]), ptr(pk["head_w2"]), ptr(pk["head_b2"]),
+                                   ptr(q), ptr(zr), h.shape[0]]
+                                  for (pk, h, _, q, zr), z in zip(jobs, zs)], dtype=np.int64)
+        check(kernels().r2_dueling_fwd_multi(self._djobs.ctypes.data, len(jobs), self.layout.A,
+                                             self.layout.HD, stream_handle()), "dueling_fwd")
 
     # ------------------------------------------------------------------ pipelined forward
     def _plan_chunks(self):
@@ -561,6 +562,7 @@ class LearnerEngine:
         gw1 = L.span(g, "val.0.weight", "adv.0.weight", (2 * HD, H))
         if self.use_gemm:
             dh = self.dh
+            # (a K split of this 40-tile GEMM through gemm_group measured no faster)
             gemm(Gemm(self.dz, pk["head1"], dh))                          # (N, H) fp32
         else:
             gw1.copy_(mm_f32(self.dz.t(), h_learn))

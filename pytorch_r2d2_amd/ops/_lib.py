@@ -58,6 +58,7 @@ _SIGS = {
     "r2_gemm": [P, I, P],
     "r2_gemm_set_version": [I],
     "r2_gemm_group": [P, P, I, P, I64, P, I, P],
+    "r2_dueling_fwd_multi": [P, I, I, I, P],
     "r2_actor_pre": [P, P],
     "r2_actor_post": [P, P],
     "r2_actor_tail": [P, P],
