@@ -55,9 +55,18 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the multi-rank path on a box with fewer GPUs than ranks (R2D2_BENCH_SHARED=1):
+    # ranks share GPUs round-robin and reduce over gloo (RCCL refuses two ranks on one GPU).
+    # Never used for reported numbers: the JSON line says so in "parallelism".
+    shared = os.environ.get("R2D2_BENCH_SHARED") == "1"
+    if shared:
+        local = local % torch.cuda.device_count()
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
@@ -122,7 +131,7 @@ def main(argv=None):
                 "n_step": rc.n_step,
                 "target_mode": lc.target_mode,
                 "replay_rows_per_gpu": replay.capacity,
-                "parallelism": "dp%d" % world,
+                "parallelism": "dp%d" % world + ("-shared-gpu-gloo-rehearsal" if shared else ""),
                 "hip_graph": bool(use_graph),
             },
             "optimizer_steps_per_sec": round(opt_steps, 3),
