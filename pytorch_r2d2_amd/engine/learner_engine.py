@@ -5,16 +5,18 @@ Parity target: ``/root/reference/learner.py:68-120`` (train + interval).  The re
 36 MB H2D batch upload, autograd, torch.optim.RMSprop, a D2H of the TD errors and numpy
 priority scatters.  Here a step is:
 
-    sample    tree_sample (64-ary sum tree, device RNG keyed by the device step counter)
-    rows      make_rows: time-major ring rows of the T+n frames of every sampled sequence
-    torso     fused uint8->conv1->conv2->conv3 MFMA kernel, online + target nets
-    proj      ONE library GEMM per net: x . W_ih^T + (b_ih + b_hh), all T*B rows at once
-    state     gather stored (h, c) from the replay
-    lstm      recurrence kernels, all chains in one launch per step (grid.y = chain)
-    head      [val.0;adv.0] GEMM + fused dueling epilogue kernel
+    sample    sample_batch: 64-ary sum-tree descent (device RNG keyed by the device step
+              counter) -> time-major ring rows of the T+n frames -> stored (h, c) of every
+              chain, one launch
+    torso     fused uint8->conv1->conv2->conv3 MFMA kernel, every frame list of both nets in
+              one multi-job launch
+    proj      ONE MFMA GEMM launch for both nets: x . W_ih^T + (b_ih + b_hh), all T*B rows
+    lstm      persistent recurrence kernel, all chains in one launch
+    head      [val.0;adv.0] GEMM + fused dueling epilogue kernel (every head in one launch)
     td        fused double-Q n-step target / loss / dL/dQ / IS weights / row priorities
-    backward  dueling backward kernel + 3 small GEMMs, BPTT kernels, weight-grad GEMMs,
-              conv backward (library) from activations saved by the torso kernel
+    backward  dueling backward kernel, dh GEMM, persistent BPTT (fused bias-gradient column
+              sums; head-gradient reduction on its idle workgroups), weight-gradient + dX
+              GEMMs in one grouped launch, fused conv backward from the saved activations
     allreduce (DP) bucket "core" overlapped with the conv backward, then bucket "torso"
     update    fused centered RMSprop (or Adam) over the flat master buffer, one pack launch
               producing every bf16 kernel layout, target sync as a device-side
