@@ -104,3 +104,20 @@ def test_gloo_world2_collectives_and_dp_equivalence(tmp_path):
     assert r0["bcast_ok"] and r1["bcast_ok"]
     assert r1["push_ok"]
     assert r0["shards"] == ([1.0, 2.0], [10.0, 20.0])
+
+
+def test_collectives_bench_gloo_world2():
+    """tools/bench_collectives.py rehearsal: 2 gloo ranks, every learner message size."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "tools", "bench_collectives.py"),
+                          "--backend", "gloo", "--world", "2", "--iters", "3", "--warmup", "1"],
+                         capture_output=True, text=True, timeout=300, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["world"] == 2 and res["backend"] == "gloo"
+    assert res["all_reduce_all_fp32"]["bytes"] == 2_037_095 * 4
+    assert all(res[k]["us"] > 0 for k in res if isinstance(res[k], dict))
