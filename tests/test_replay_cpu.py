@@ -90,6 +90,23 @@ def test_neighbour_refresh_q8():
     assert changed(False) == [40, 50, 60]
 
 
+def test_indexing_sample_contiguous_one_step_batches():
+    """replay_memory.py:264-277 (unused by the reference, kept for API parity): 1-step batches
+    over [start, last) with next_state n rows ahead, ring-wrapped."""
+    m = _mem(10)
+    for k in range(10):
+        x = np.full((4, 84, 84), k * 20, dtype=np.uint8)
+        m.add(x.astype(np.float32) / 255.0, np.zeros(256), np.zeros(256), np.zeros(256),
+              np.zeros(256), k % 6, float(k), k == 9, 1, 0.1)
+    batch, index = m.indexing_sample(6, 9)
+    assert index.tolist() == [6, 7, 8]
+    assert batch["state"].shape == (3, 1, 4, 84, 84)
+    assert batch["state"][0, 0, 0, 0, 0] == pytest.approx(120 / 255)
+    nxt = (index + m.n_step) % 10
+    assert np.allclose(batch["next_state"][:, 0, 0, 0, 0], nxt * 20 / 255)
+    assert batch["reward"][:, 0].tolist() == [6.0, 7.0, 8.0]
+
+
 def test_extend_fit_and_wrap():
     m = _mem(10)
     src = {k: v[:7].copy() for k, v in _mem(7).memory.items()}
