@@ -30,9 +30,9 @@ import torch
 
 from .config import R2D2Config, epsilon_ladder
 from .engine.layout import ParamLayout
-from .engine.learner_engine import addmm_f32
 from .engine.replay_hbm import HBMReplay
 from .ops._lib import check, kernels, ptr, stream_handle
+from .ops.gemm import Gemm, gemm
 from .ops.torso_lib import fused_torso_supported, torso_forward_library
 
 
@@ -120,7 +120,9 @@ class BatchedActor:
         self.h32_new = {k: z(E, H) for k in ("on", "tg")}
         self.c_new = {k: z(E, H) for k in ("on", "tg")}
         self.q = {k: z(E, A) for k in ("on", "tg")}
-        self.X = z(E, self.layout.D, dt=torch.bfloat16)
+        self.Xn = {k: z(E, self.layout.D, dt=torch.bfloat16) for k in ("on", "tg")}
+        self.xp = {k: z(E, self.layout.G) for k in ("on", "tg")}
+        self.zh = {k: z(E, 2 * self.layout.HD, dt=torch.bfloat16) for k in ("on", "tg")}
         self.ctr = z(int(kernels().r2_lstm_persist_ctr_words()), dt=torch.int32)
         self.err = z(1, dt=torch.int32)
         # n-step history ring (device)
@@ -172,28 +174,36 @@ class BatchedActor:
 
     # ------------------------------------------------------------------ inference
     def _infer(self):
-        """Q values + next recurrent state of both nets for the current observations."""
+        """Q values + next recurrent state of both nets for the current observations: one launch
+        per stage for BOTH nets (torso multi-job, x-projection GEMM, 2-chain LSTM step, head
+        GEMM, dueling epilogue) -- the actor step is launch-bound at these batch sizes."""
         k = kernels()
         s = stream_handle()
         E, H, L = self.E, self.H, self.layout
-        for key, w in (("on", self.online), ("tg", self.target)):
-            pk = w.pk
-            if self.fused_torso:
-                check(k.r2_torso_fwd(ptr(self.env.frames), 0, E, ptr(pk["conv1"]), ptr(pk["b1"]),
-                                     ptr(pk["conv2"]), ptr(pk["b2"]), ptr(pk["conv3"]), ptr(pk["b3"]),
-                                     ptr(self.X), 0, 0, 256, s), "torso_fwd")
-            else:
+        nets = (("on", self.online), ("tg", self.target))
+        if self.fused_torso:
+            self._tjobs = np.asarray(
+                [[0, E, ptr(w.pk["conv1"]), ptr(w.pk["b1"]), ptr(w.pk["conv2"]), ptr(w.pk["b2"]),
+                  ptr(w.pk["conv3"]), ptr(w.pk["b3"]), ptr(self.Xn[key]), 0, 0, 0] for key, w in nets],
+                dtype=np.int64)
+            check(k.r2_torso_fwd_multi(ptr(self.env.frames), self._tjobs.ctypes.data, 2, 256, 0, 0, s),
+                  "torso_fwd_multi")
+        else:
+            for key, w in nets:
                 torso_forward_library(self.env.frames.reshape(E, -1), None, L, w.flat, self.cfg.env,
-                                      self.cfg.model, self.X)
-            xp = addmm_f32(w.lstm_b, self.X, pk["w_ih"].t())
-            chain = [ptr(xp), ptr(pk["w_hh"]), ptr(self.h_bf[key]), ptr(self.c[key]),
-                     ptr(self.h_bf_new[key]), ptr(self.c_new[key]), ptr(self.h32_new[key]), 0, 0]
-            arr = np.asarray(chain, dtype=np.int64)
-            check(k.r2_lstm_fwd_persist(arr.ctypes.data, 1, E, 1, H, ptr(self.ctr), ptr(self.err), s),
-                  "lstm_step")
-            zz = torch.mm(self.h_bf_new[key], pk["head1"].t())
-            check(k.r2_dueling_fwd(ptr(zz), ptr(pk["head_b1"]), ptr(pk["head_w2"]), ptr(pk["head_b2"]),
-                                   ptr(self.q[key]), 0, E, self.A, L.HD, s), "dueling_fwd")
+                                      self.cfg.model, self.Xn[key])
+        gemm(*[Gemm(self.Xn[key], w.pk["w_ih"].t(), self.xp[key], bias=w.lstm_b) for key, w in nets])
+        self._chains = np.asarray(
+            [[ptr(self.xp[key]), ptr(w.pk["w_hh"]), ptr(self.h_bf[key]), ptr(self.c[key]),
+              ptr(self.h_bf_new[key]), ptr(self.c_new[key]), ptr(self.h32_new[key]), 0, 0]
+             for key, w in nets], dtype=np.int64)
+        check(k.r2_lstm_fwd_persist(self._chains.ctypes.data, 2, E, 1, H, ptr(self.ctr),
+                                    ptr(self.err), s), "lstm_step")
+        gemm(*[Gemm(self.h_bf_new[key], w.pk["head1"].t(), self.zh[key]) for key, w in nets])
+        self._djobs = np.asarray(
+            [[ptr(self.zh[key]), ptr(w.pk["head_b1"]), ptr(w.pk["head_w2"]), ptr(w.pk["head_b2"]),
+              ptr(self.q[key]), 0, E] for key, w in nets], dtype=np.int64)
+        check(k.r2_dueling_fwd_multi(self._djobs.ctypes.data, 2, self.A, L.HD, s), "dueling_fwd")
 
     # ------------------------------------------------------------------ one env step
     @property
