@@ -37,11 +37,7 @@ target_mode (config.learner.target_mode):
 """
 from __future__ import annotations
 
-import math
-import time
 from typing import Dict, Optional
-
-import os
 
 import numpy as np
 import torch
@@ -587,7 +583,7 @@ class LearnerEngine:
             x_job = Gemm(self.dgates, pk["w_ih"], self.dX)                # (N, D) bf16
         # tagged BPTT: these GEMMs run on helper workgroups of the same launch, each K / row
         # tile as soon as the recurrence has stored the dgates it reads
-        helpers = os.environ.get("R2D2_BPTT_HELPERS", lc.bptt_helpers).split(",")
+        helpers = lc.bptt_helpers.split(",")
         ok = tagged and N % 64 == 0
         bias_done, taken = self._lstm_bwd(dh, w_jobs if ok and "w" in helpers else None,
                                           x_job if ok and "x" in helpers else None)
@@ -620,9 +616,9 @@ class LearnerEngine:
 
     def _group_splits(self, w_jobs, x_job):
         """K splits of the grouped post-BPTT launch ([dW_ih, dW_hh, dW_head1, dX]) or None for
-        separate launches.  ``learner.bwd_gemm`` (env R2D2_BWD_GEMM): "group" = no split,
+        separate launches.  ``learner.bwd_gemm``: "group" = no split,
         "group:a,b,c,d" = explicit splits, "separate".  Needs every K % 64 == 0."""
-        mode = os.environ.get("R2D2_BWD_GEMM", self.cfg.learner.bwd_gemm)
+        mode = self.cfg.learner.bwd_gemm
         if not mode.startswith("group"):
             return None
         splits = [int(v) for v in mode.split(":")[1].split(",")] if ":" in mode else [1, 1, 1, 1]
