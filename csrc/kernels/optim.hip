@@ -170,21 +170,38 @@ __global__ void pack_step_kernel(const float* __restrict__ master, float* __rest
                                  float* __restrict__ lstm_b, float* __restrict__ lstm_b_t, int64_t G,
                                  const int64_t* __restrict__ step, int64_t interval) {
   const bool due = interval <= 1 || ((*step) + 1) % interval == 0;
-  const int64_t total = (due ? n_master : 0) + n_bf + n_f + G;
+  // work items: [target copy, 4 floats each (due only)] [bf pack, 4 elements each: one 16-B
+  // index load, 4 gathers, one 8-B store] [bf tail] [f32 gather] [lstm bias]
+  const int64_t nm4 = due ? n_master >> 2 : 0, nb4 = n_bf >> 2, nbt = n_bf & 3;
+  const int64_t total = nm4 + nb4 + nbt + n_f + G;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += stride) {
     int64_t j = i;
-    if (due) {
-      if (j < n_master) { target[j] = master[j]; continue; }
-      j -= n_master;
+    if (j < nm4) {
+      ((f32x4*)target)[j] = ((const f32x4*)master)[j];
+      continue;
     }
-    if (j < n_bf) {
+    j -= nm4;
+    if (j < nb4) {
+      const int4 ix = ((const int4*)bf_idx)[j];
+      bf16x4 v;
+      v[0] = (bf16)master[ix.x];
+      v[1] = (bf16)master[ix.y];
+      v[2] = (bf16)master[ix.z];
+      v[3] = (bf16)master[ix.w];
+      ((bf16x4*)bf)[j] = v;
+      if (due) ((bf16x4*)bf_t)[j] = v;
+      continue;
+    }
+    j -= nb4;
+    if (j < nbt) {
+      j += nb4 << 2;
       const bf16 v = (bf16)master[bf_idx[j]];
       bf[j] = v;
       if (due) bf_t[j] = v;
       continue;
     }
-    j -= n_bf;
+    j -= nbt;
     if (j < n_f) {
       const float v = master[f_idx[j]];
       f32[j] = v;
@@ -203,6 +220,9 @@ extern "C" int r2_pack_step(const float* master, float* target, int64_t n_master
                             float* f32_t, int64_t n_f, int64_t o_bih, int64_t o_bhh, float* lstm_b,
                             float* lstm_b_t, int64_t G, const int64_t* step, int64_t interval,
                             void* stream) {
+  if ((n_master & 3) || (((uintptr_t)master | (uintptr_t)target | (uintptr_t)bf_idx) & 15) ||
+      (((uintptr_t)bf | (uintptr_t)bf_t) & 7))
+    return -1;   // vector paths: 16-B master / target / index rows, 8-B packs
   hipLaunchKernelGGL(pack_step_kernel, dim3(1024), dim3(256), 0, (hipStream_t)stream, master, target,
                      n_master, bf_idx, bf, bf_t, n_bf, f_idx, f32, f32_t, n_f, o_bih, o_bhh, lstm_b,
                      lstm_b_t, G, step, interval);
