@@ -175,19 +175,32 @@ __global__ void seqprio_refresh_kernel(const int* __restrict__ starts, int B,
                                        int upd_hi, int cap_e, float eta,
                                        int* __restrict__ dirty, int* __restrict__ count,
                                        int max_dirty) {
-  const int lane = threadIdx.x & 63;
-  const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (b >= B) return;
+  // one workgroup per sampled start: the waves scan 64-offset chunks of the candidate range into
+  // an LDS list, then take the listed starts round-robin (a wave per start, not a start loop)
+  constexpr int MAXC = 2048;     // host checks the candidate range fits
+  __shared__ int list[MAXC];
+  __shared__ int n_list;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int b = blockIdx.x;
+  if (threadIdx.x == 0) n_list = 0;
+  __syncthreads();
   const int sb = starts[b];
   const int lo = upd_lo - T + 1, hi = upd_hi - 1;  // candidate offsets, inclusive
-  for (int k0 = lo; k0 <= hi; k0 += 64) {
+  for (int k0 = lo + 64 * wave; k0 <= hi; k0 += 64 * nw) {
     const int k = k0 + lane;
     const bool cand = (k <= hi) && is_start[ring_row_s(sb, k, cap_e)];
-    unsigned long long m = __ballot(cand);
-    while (m) {
-      const int bit = __ffsll((long long)m) - 1;
-      m &= m - 1;
-      const int s = ring_row_s(sb, k0 + bit, cap_e);
+    const unsigned long long m = __ballot(cand);
+    int base = 0;
+    if (lane == 0 && m) base = atomicAdd(&n_list, __popcll(m));
+    base = __shfl(base, 0, 64);
+    const int pos = base + __popcll(m & ((1ull << lane) - 1));
+    if (cand && pos < MAXC) list[pos] = ring_row_s(sb, k, cap_e);
+  }
+  __syncthreads();
+  const int nl = min(n_list, MAXC);
+  for (int i = wave; i < nl; i += nw) {
+    {
+      const int s = list[i];
       float mx = 0.f, sm = 0.f;
       for (int t = lane; t < T; t += 64) {
         const float p = priority[ring_row_s(s, t, cap_e)];
@@ -343,7 +356,9 @@ extern "C" int r2_seqprio_refresh(const int* starts, int B, const uint8_t* is_st
                                   const float* priority, float* leaves, int T, int upd_lo,
                                   int upd_hi, int cap_e, float eta, int* dirty, int* count,
                                   int max_dirty, void* stream) {
-  hipLaunchKernelGGL(seqprio_refresh_kernel, dim3((B + 3) / 4), dim3(256), 0, (hipStream_t)stream,
+  if (upd_hi - upd_lo + T - 1 > 2048) return -2;   // candidate list (seqprio_refresh_kernel MAXC)
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(seqprio_refresh_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream,
                      starts, B, is_start, priority, leaves, T, upd_lo, upd_hi, cap_e, eta, dirty,
                      count, max_dirty);
   R2_CHECK_LAUNCH();
