@@ -332,6 +332,36 @@ __global__ void frames_to_bf16_nhwc_kernel(const uint8_t* __restrict__ frames,
   }
 }
 
+// Any frame geometry (the library conv path, e.g. DMLab 3x72x96): gather replay rows of C
+// uint8 planes of HW pixels and write channels-last bf16 (N, H, W, C) * scale in one pass --
+// replaces index_select + dtype cast + channels-last copy (three full passes over the batch).
+__global__ void frames_gather_nhwc_kernel(const uint8_t* __restrict__ frames, int64_t row_bytes,
+                                          const int* __restrict__ rows, int C, int HW, float scale,
+                                          bf16* __restrict__ out) {
+  const int f = blockIdx.y;
+  const size_t row = rows ? (size_t)rows[f] : (size_t)f;
+  const uint8_t* src = frames + row * row_bytes;
+  bf16* dst = out + (size_t)f * HW * C;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += gridDim.x * blockDim.x)
+    for (int c = 0; c < C; ++c) dst[(size_t)p * C + c] = (bf16)((float)src[(size_t)c * HW + p] * scale);
+}
+
+extern "C" int r2_frames_gather_nhwc(const uint8_t* frames, int64_t row_bytes, const int* rows,
+                                     int n_frames, int C, int HW, float scale, bf16* out,
+                                     void* stream) {
+  if (n_frames <= 0) return 0;
+  if (n_frames > 65535 * 16 || C < 1 || HW < 1 || (int64_t)C * HW > row_bytes) return -1;
+  const int bx = (HW + 255) / 256 < 64 ? (HW + 255) / 256 : 64;
+  for (int f0 = 0; f0 < n_frames; f0 += 65535) {   // grid.y limit
+    const int nf = n_frames - f0 < 65535 ? n_frames - f0 : 65535;
+    hipLaunchKernelGGL(frames_gather_nhwc_kernel, dim3(bx, nf), dim3(256), 0, (hipStream_t)stream,
+                       rows ? frames : frames + (size_t)f0 * row_bytes, row_bytes,
+                       rows ? rows + f0 : nullptr, C, HW, scale, out + (size_t)f0 * HW * C);
+  }
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
 // grad * (act > 0) on bf16 tensors with identical memory layout (ReLU backward from output)
 __global__ void relu_mask_bf16_kernel(const bf16* __restrict__ g, const bf16* __restrict__ act,
                                       bf16* __restrict__ out, int64_t n8) {

@@ -47,7 +47,7 @@ from ..models.qnet import QNet
 from ..ops._lib import check, kernels, ptr, stream_handle
 from ..ops.gemm import Gemm, gemm, gemm_group, group_ws_bytes
 from ..models.qnet import torso_dims
-from ..ops.torso_lib import fused_torso_supported, torso_forward_library
+from ..ops.torso_lib import fused_torso_supported, gather_frames_nhwc, torso_forward_library
 from .layout import ParamLayout, UNITS
 from .replay_hbm import HBMReplay
 
@@ -286,22 +286,6 @@ class LearnerEngine:
         self._pack(always=True)
 
     # ------------------------------------------------------------------ pieces
-    def _torso(self, pk, rows: torch.Tensor, out: torch.Tensor, save=False):
-        n = rows.numel()
-        if n == 0:
-            return
-        if not self.fused_torso:
-            flat = self.master if pk is self.pk else self.target
-            torso_forward_library(self.replay.frames, rows, self.layout, flat, self.cfg.env,
-                                  self.cfg.model, out, self.act1 if save else None,
-                                  self.act2 if save else None)
-            return
-        k = kernels()
-        check(k.r2_torso_fwd(ptr(self.replay.frames), ptr(rows), n, ptr(pk["conv1"]), ptr(pk["b1"]),
-                             ptr(pk["conv2"]), ptr(pk["b2"]), ptr(pk["conv3"]), ptr(pk["b3"]),
-                             ptr(out), ptr(self.act1) if save else 0, ptr(self.act2) if save else 0,
-                             256, stream_handle()), "torso_fwd")
-
     def _chain_desc(self, xproj, pk, h0, c0, hseq, cseq, gates=None, save_from=0):
         return [ptr(xproj), ptr(pk["w_hh"]), ptr(h0), ptr(c0), ptr(hseq), ptr(cseq), 0,
                 ptr(gates), save_from]
@@ -456,11 +440,11 @@ class LearnerEngine:
             self._tjobs = np.asarray(jobs, dtype=np.int64)          # kept alive for capture
             check(k.r2_torso_fwd_multi(ptr(rp.frames), self._tjobs.ctypes.data, len(jobs), 256,
                                        0, 0, s), "torso_fwd_multi")
-        else:
-            self._torso(pk, rows[: Lb * B], self.X_on[: Lb * B])
-            self._torso(pk, rows[Lb * B: T * B], self.X_on[Lb * B: T * B], save=True)
-            self._torso(pk, rows[T * B:], self.X_on[T * B:])
-            self._torso(pt, rows[self.t_lo_tg * B:], self.X_tg)
+        else:   # library convs: one call per net over all its frames (bigger, fewer launches)
+            torso_forward_library(rp.frames, rows, L, self.master, self.cfg.env, self.cfg.model,
+                                  self.X_on, self.act1, self.act2, save_lo=Lb * B)
+            torso_forward_library(rp.frames, rows[self.t_lo_tg * B:], L, self.target, self.cfg.env,
+                                  self.cfg.model, self.X_tg)
         # input projections (one GEMM per net over every row)
         if self.use_gemm:
             xp_on, xp_tg = self.xp_on, self.xp_tg
@@ -739,8 +723,7 @@ class LearnerEngine:
             check(k.r2_frames_to_bf16_nhwc(ptr(self.replay.frames), ptr(rows), N,
                                            ptr(self.frames_bf), s), "frames_to_bf16_nhwc")
         else:   # exact 0..255 values; the 1/255 is applied to dW1 in fp32 below
-            fr_nchw = self.replay.frames.index_select(0, rows.long()).view(N, cin, fh, fw)
-            self.frames_bf.view(N, fh, fw, cin).copy_(fr_nchw.permute(0, 2, 3, 1))
+            gather_frames_nhwc(self.replay.frames, rows, cin, fh, fw, out=self.frames_bf)
         fr = self.frames_bf.view(N, fh, fw, cin).permute(0, 3, 1, 2)
         _, dw1, db1 = cb(g1, fr, w1, [c1], [4, 4], [0, 0], [1, 1], False, [0, 0], 1,
                          [False, True, True])

@@ -19,28 +19,57 @@ def fused_torso_supported(env: EnvConfig, model: ModelConfig) -> bool:
             and env.frame_h == 84 and env.frame_w == 84 and tuple(model.conv_channels) == (32, 32, 32))
 
 
+def gather_frames_nhwc(frames: torch.Tensor, rows: Optional[torch.Tensor], cin: int, fh: int,
+                       fw: int, out: Optional[torch.Tensor] = None,
+                       scale: float = 1.0) -> torch.Tensor:
+    """(n, cin, fh, fw) bf16 view in channels-last memory of frames[rows] (uint8 (C,H,W) rows)
+    * scale.  On the GPU one pass of torso.hip frames_gather_nhwc_kernel; on the CPU torch ops."""
+    n = frames.shape[0] if rows is None else rows.numel()
+    if frames.is_cuda:
+        from ._lib import check, kernels, ptr, stream_handle
+        if out is None:
+            out = torch.empty((n, fh, fw, cin), dtype=torch.bfloat16, device=frames.device)
+        r = None if rows is None else rows.to(torch.int32)
+        check(kernels().r2_frames_gather_nhwc(ptr(frames), frames.stride(0), ptr(r), n, cin,
+                                              fh * fw, float(scale), ptr(out), stream_handle()),
+              "frames_gather_nhwc")
+        return out.view(n, fh, fw, cin).permute(0, 3, 1, 2)
+    x = frames if rows is None else frames.index_select(0, rows.long())
+    x = (x[:, : cin * fh * fw].view(n, cin, fh, fw).float() * scale).to(torch.bfloat16)
+    if out is not None:
+        out.view(n, fh, fw, cin).copy_(x.permute(0, 2, 3, 1))
+        return out.view(n, fh, fw, cin).permute(0, 3, 1, 2)
+    return x.contiguous(memory_format=torch.channels_last)
+
+
+def conv_relu(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride: int) -> torch.Tensor:
+    """ReLU(conv2d(x, w) + b) through MIOpen (channels-last bf16).  MIOpen's fused
+    ``miopen_convolution_relu`` measured 24x slower here (78 vs 3.3 ms per DMLab learner step)."""
+    return F.conv2d(x, w, b, stride=stride).relu_()
+
+
 def torso_forward_library(frames: torch.Tensor, rows: Optional[torch.Tensor], layout, flat: torch.Tensor,
                           env: EnvConfig, model: ModelConfig, out: torch.Tensor,
-                          act1: Optional[torch.Tensor] = None, act2: Optional[torch.Tensor] = None):
+                          act1: Optional[torch.Tensor] = None, act2: Optional[torch.Tensor] = None,
+                          save_lo: int = 0):
     """out (n, C3*h3*w3) bf16 = ReLU-conv stack of frames[rows] / 255 (frames stored (C,H,W) uint8
-    per row); optionally saves conv1/conv2 activations channels-last into act1 / act2."""
+    per row); optionally saves the conv1/conv2 activations of frames [save_lo, save_lo +
+    len(act)) channels-last into act1 / act2."""
     cin = env.channels_per_frame * env.n_stacks
     fh, fw = env.frame_h, env.frame_w
-    x = frames if rows is None else frames.index_select(0, rows.long())
-    n = x.shape[0]
     # uint8 0..255 is exact in bf16; the 1/255 of the reference's normalisation is folded into
     # the fp32 conv1 weights before their bf16 rounding (as the fused kernel applies it in fp32)
-    x = x[:, : cin * fh * fw].view(n, cin, fh, fw).to(torch.bfloat16)
-    x = x.contiguous(memory_format=torch.channels_last)
+    x = gather_frames_nhwc(frames, rows, cin, fh, fw)
+    n = x.shape[0]
     w = {k: layout.view(flat, k).to(torch.bfloat16) for k in
          ("vis_layers.0.bias", "vis_layers.2.weight", "vis_layers.2.bias",
           "vis_layers.4.weight", "vis_layers.4.bias")}
     w["vis_layers.0.weight"] = (layout.view(flat, "vis_layers.0.weight") * (1.0 / 255)).to(torch.bfloat16)
-    y1 = F.conv2d(x, w["vis_layers.0.weight"], w["vis_layers.0.bias"], stride=4).relu_()
-    y2 = F.conv2d(y1, w["vis_layers.2.weight"], w["vis_layers.2.bias"], stride=2).relu_()
-    y3 = F.conv2d(y2, w["vis_layers.4.weight"], w["vis_layers.4.bias"], stride=1).relu_()
+    y1 = conv_relu(x, w["vis_layers.0.weight"], w["vis_layers.0.bias"], 4)
+    y2 = conv_relu(y1, w["vis_layers.2.weight"], w["vis_layers.2.bias"], 2)
+    y3 = conv_relu(y2, w["vis_layers.4.weight"], w["vis_layers.4.bias"], 1)
     out.copy_(y3.contiguous().view(n, -1))                   # torch (C,H,W) flatten order
-    if act1 is not None:
-        act1[:n].copy_(y1.permute(0, 2, 3, 1).reshape(n, -1, y1.shape[1]))
-    if act2 is not None:
-        act2[:n].copy_(y2.permute(0, 2, 3, 1).reshape(n, -1, y2.shape[1]))
+    for act, y in ((act1, y1), (act2, y2)):
+        if act is not None:
+            m = min(act.shape[0], n - save_lo)
+            act[:m].copy_(y[save_lo:save_lo + m].permute(0, 2, 3, 1).reshape(m, -1, y.shape[1]))
