@@ -429,3 +429,18 @@ def test_head_grads_and_colsum_match_torch(N):
     assert int(ticket.abs().sum().item()) == 0          # last arrivers reset their tickets
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("C,H,W,rows", [(3, 72, 96, True), (4, 84, 84, False), (3, 7, 5, True)])
+def test_frames_gather_nhwc_matches_torch(C, H, W, rows):
+    """torso.hip frames_gather_nhwc (vector form for HW % 4 == 0, scalar otherwise): replay
+    uint8 (C,H,W) rows -> channels-last bf16, row list or identity, row stride > C*H*W."""
+    from pytorch_r2d2_amd.ops.torso_lib import gather_frames_nhwc
+    g = torch.Generator(device=DEV).manual_seed(C * H * W)
+    frames = torch.randint(0, 256, (50, C * H * W + 16), dtype=torch.uint8, device=DEV, generator=g)
+    idx = torch.randperm(50, device=DEV, generator=g)[:17].to(torch.int32) if rows else None
+    x = gather_frames_nhwc(frames, idx, C, H, W)
+    src = frames if idx is None else frames[idx.long()]
+    ref = src[:, : C * H * W].view(-1, C, H, W).float()
+    assert x.shape == ref.shape and x.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(x.float(), ref)
