@@ -398,6 +398,31 @@ extern "C" int r2_frames_gather_nhwc(const uint8_t* frames, int64_t row_bytes, c
   return 0;
 }
 
+// x = relu(x + bias[c]) in place on a channels-last bf16 activation (C % 8 == 0): the library
+// conv path's bias add + ReLU in one pass (MIOpen's separate bias op + a clamp pass were two).
+__global__ void bias_relu_nhwc_kernel(bf16* __restrict__ x, const float* __restrict__ bias, int C,
+                                      int64_t n8) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += stride) {
+    bf16x8 v = ((bf16x8*)x)[i];
+    const int c0 = (int)((i * 8) % C);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (bf16)fmaxf((float)v[e] + bias[c0 + e], 0.f);
+    ((bf16x8*)x)[i] = v;
+  }
+}
+
+extern "C" int r2_bias_relu_nhwc_bf16(bf16* x, const float* bias, int C, int64_t n, void* stream) {
+  if (n <= 0) return 0;
+  if (C % 8 || n % C || ((uintptr_t)x & 15)) return -1;
+  int64_t blocks = (n / 8 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(bias_relu_nhwc_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                     (hipStream_t)stream, x, bias, C, n / 8);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
 // grad * (act > 0) on bf16 tensors with identical memory layout (ReLU backward from output)
 __global__ void relu_mask_bf16_kernel(const bf16* __restrict__ g, const bf16* __restrict__ act,
                                       bf16* __restrict__ out, int64_t n8) {

@@ -34,6 +34,7 @@ _SIGS = {
     "r2_frames_to_bf16": [P, P, I, P, P],
     "r2_frames_to_bf16_nhwc": [P, P, I, P, P],
     "r2_frames_gather_nhwc": [P, I64, P, I, I, I, F, P, P],
+    "r2_bias_relu_nhwc_bf16": [P, P, I, I64, P],
     "r2_relu_mask_bf16": [P, P, P, I64, P],
     "r2_dueling_fwd": [P, P, P, P, P, P, I, I, I, P],
     "r2_dueling_bwd": [P, P, P, P, P, I, I, I, P],

@@ -43,9 +43,18 @@ def gather_frames_nhwc(frames: torch.Tensor, rows: Optional[torch.Tensor], cin: 
 
 
 def conv_relu(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, stride: int) -> torch.Tensor:
-    """ReLU(conv2d(x, w) + b) through MIOpen (channels-last bf16).  MIOpen's fused
-    ``miopen_convolution_relu`` measured 24x slower here (78 vs 3.3 ms per DMLab learner step)."""
-    return F.conv2d(x, w, b, stride=stride).relu_()
+    """ReLU(conv2d(x, w) + b): the MIOpen convolution without bias, then bias + ReLU in one
+    in-place pass (torso.hip bias_relu_nhwc_kernel) on the channels-last output.  (MIOpen's own
+    fused ``miopen_convolution_relu`` measured 24x slower here: 78 vs 3.3 ms per DMLab step.)"""
+    y = F.conv2d(x, w, None, stride=stride)
+    C = y.shape[1]
+    if y.is_cuda and C % 8 == 0 and y.is_contiguous(memory_format=torch.channels_last):
+        from ._lib import check, kernels, ptr, stream_handle
+        bf = b.float().contiguous()
+        check(kernels().r2_bias_relu_nhwc_bf16(ptr(y), ptr(bf), C, y.numel(), stream_handle()),
+              "bias_relu_nhwc")
+        return y
+    return y.add_(b.view(1, -1, 1, 1)).relu_()
 
 
 def torso_forward_library(frames: torch.Tensor, rows: Optional[torch.Tensor], layout, flat: torch.Tensor,
