@@ -107,6 +107,9 @@ class LearnerConfig:
     # ~15 us and a chunk's x-projection GEMM is tile-latency bound; profiles/r01_v9_pipelined.txt)
     fwd_chunks: int = 0
     torso_bwd: str = "fused"          # fused (HIP kernel) | library (MIOpen convolution_backward)
+    # library conv path (frame geometries without the fused HIP torso, e.g. DMLab): MIOpen find
+    # mode (torch.backends.cudnn.benchmark) instead of its immediate-mode heuristics
+    conv_autotune: bool = True
     use_graph: bool = True            # capture the whole step in a HIP graph
     save_dir: str = "save"
 
