@@ -116,6 +116,78 @@ __device__ __forceinline__ void g2_epilogue(const GemmProb& P, int m0, int n0, i
   }
 }
 
+// The same epilogue staged through LDS (>= 33 KB at `lds`, free: every operand read retired):
+// each 64-row half of the tile is written fp32 to LDS in the accumulator layout, then stored
+// row-contiguous, 4 columns per thread (one 16-B fp32 / 8-B bf16 store, one crow load per row).
+// The register epilogue above unrolls 64 scalar stores per lane behind 4 uniform branches each
+// (3.7k instructions, ~10 us per launch at any tile count: tools/gemm_floor_probe.py); this one
+// is a short loop.  Threads 0..255 of the workgroup, raw barriers.
+__device__ __forceinline__ void g2_epilogue_lds(const GemmProb& P, int m0, int n0, int wm, int wn,
+                                                int lane, const f32x16 (&acc)[2][2], uint8_t* lds_raw) {
+  constexpr int LS = 136;                      // fp32 row stride: rows r, r+4 on disjoint banks
+  float* L = (float*)lds_raw;
+  const int tid = threadIdx.x, l32 = lane & 31, h = lane >> 5;
+  const bool f32 = P.c_f32 != 0;
+  const bool vec = ((uintptr_t)P.C % 16 == 0) && (P.ldc % 4 == 0);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();              // LDS free (operands, or the previous half)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int lr = (wm >> 6) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        L[lr * LS + wn + 32 * j + l32] = acc[i][j][r];
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#pragma unroll 2
+    for (int pass = 0; pass < 8; ++pass) {
+      const int q = pass * 256 + tid;           // 64 rows x 32 four-column chunks
+      const int lr = q >> 5, cc = (q & 31) * 4;
+      const int row = m0 + (lr >> 5) * 64 + 32 * i + (lr & 31);
+      const int col = n0 + cc;
+      if (row >= P.M || col >= P.N) continue;
+      const f32x4 a = *(const f32x4*)(L + lr * LS + cc);
+      const int orow = P.crow ? P.crow[row] : row;
+      const size_t o = (size_t)orow * P.ldc + col;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = P.alpha * a[e] + (P.bias && col + e < P.N ? P.bias[col + e] : 0.f);
+      if (vec && col + 4 <= P.N) {
+        if (f32) {
+          f32x4* c = (f32x4*)((float*)P.C + o);
+          f32x4 w = {v[0], v[1], v[2], v[3]};
+          if (P.accumulate) w += *c;
+          *c = w;
+        } else {
+          bf16x4* c = (bf16x4*)((bf16*)P.C + o);
+          if (P.accumulate) {
+            const bf16x4 old = *c;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += (float)old[e];
+          }
+          bf16x4 w;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] = (bf16)v[e];
+          *c = w;
+        }
+      } else {
+        for (int e = 0; e < 4 && col + e < P.N; ++e) {
+          if (f32) {
+            float* c = (float*)P.C + o + e;
+            *c = P.accumulate ? *c + v[e] : v[e];
+          } else {
+            bf16* c = (bf16*)P.C + o + e;
+            *c = (bf16)(P.accumulate ? (float)*c + v[e] : v[e]);
+          }
+        }
+      }
+    }
+  }
+}
+
 // One 128x128 output tile (tm, tn) of problem P by threads 0..255 (4 waves) of a workgroup,
 // usable inside other kernels: 2-stage LDS-DMA ring at `lds` (2 x 32 KB), K tiles visited in
 // ascending or descending order; ready(kt) is called by EVERY wave before it issues the DMA of K

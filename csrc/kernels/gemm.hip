@@ -206,30 +206,7 @@ __global__ __launch_bounds__(256) void gemm2_kernel(const GemmArgs args) {
     }
   }
 
-  const int l32 = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int col = n0 + wn + 32 * j + l32;
-    if (col >= P.N) continue;
-    const float bv = P.bias ? P.bias[col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (row >= P.M) continue;
-        const int orow = P.crow ? P.crow[row] : row;
-        const float v = P.alpha * acc[i][j][r] + bv;
-        const size_t o = (size_t)orow * P.ldc + col;
-        if (P.c_f32) {
-          float* c = (float*)P.C + o;
-          *c = P.accumulate ? *c + v : v;
-        } else {
-          bf16* c = (bf16*)P.C + o;
-          *c = (bf16)(P.accumulate ? (float)*c + v : v);
-        }
-      }
-  }
+  g2_epilogue_lds(P, m0, n0, wm, wn, lane, acc, &lds[0][0][0]);
 }
 
 // ============================================================================================
@@ -386,30 +363,69 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmArgs args, int tot
     }
   }
 
-  // C[m0 + wr*128 + 16i + 4(l>>4) + e][n0 + wc*BN/4 + 16j + (l&15)] = acc[i][j][e]
+  // C[m0 + wr*128 + 16i + 4(l>>4) + e][n0 + wc*BN/4 + 16j + (l&15)] = acc[i][j][e], staged
+  // through LDS two i at a time (64 rows x BN fp32) and stored row-contiguous, 4 columns per
+  // thread (the per-element register epilogue was 7k instructions behind 800 branches)
+  constexpr int LS = BN + 16;                  // fp32 row stride: rows 4g+e on disjoint banks
+  float* L = (float*)lds4;
   const int l16 = lane & 15, g = lane >> 4;
+  const bool f32 = P.c_f32 != 0;
+  const bool vec = ((uintptr_t)P.C % 16 == 0) && (P.ldc % 4 == 0);
 #pragma unroll
-  for (int j = 0; j < TNW; ++j) {
-    const int col = n0 + wc * (BN / 4) + 16 * j + l16;
-    if (col >= P.N) continue;
-    const float bv = P.bias ? P.bias[col] : 0.f;
+  for (int p = 0; p < 4; ++p) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int ii = 0; ii < 2; ++ii)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = m0 + wr * 128 + 16 * i + 4 * g + e;
-        if (row >= P.M) continue;
-        const int orow = P.crow ? P.crow[row] : row;
-        const float v = P.alpha * acc[i][j][e] + bv;
-        const size_t o = (size_t)orow * P.ldc + col;
-        if (P.c_f32) {
-          float* c = (float*)P.C + o;
-          *c = P.accumulate ? *c + v : v;
+      for (int j = 0; j < TNW; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          L[(wr * 32 + ii * 16 + 4 * g + e) * LS + wc * (BN / 4) + 16 * j + l16] = acc[2 * p + ii][j][e];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#pragma unroll 2
+    for (int q = tid; q < 64 * (BN / 4); q += 512) {
+      const int lr = q / (BN / 4), cc = (q % (BN / 4)) * 4;
+      const int row = m0 + (lr >> 5) * 128 + 32 * p + (lr & 31);
+      const int col = n0 + cc;
+      if (row >= P.M || col >= P.N) continue;
+      const f32x4 a = *(const f32x4*)(L + lr * LS + cc);
+      const int orow = P.crow ? P.crow[row] : row;
+      const size_t o = (size_t)orow * P.ldc + col;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = P.alpha * a[e] + (P.bias && col + e < P.N ? P.bias[col + e] : 0.f);
+      if (vec && col + 4 <= P.N) {
+        if (f32) {
+          f32x4* c = (f32x4*)((float*)P.C + o);
+          f32x4 w = {v[0], v[1], v[2], v[3]};
+          if (P.accumulate) w += *c;
+          *c = w;
         } else {
-          bf16* c = (bf16*)P.C + o;
-          *c = (bf16)(P.accumulate ? (float)*c + v : v);
+          bf16x4* c = (bf16x4*)((bf16*)P.C + o);
+          if (P.accumulate) {
+            const bf16x4 old = *c;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += (float)old[e];
+          }
+          bf16x4 w;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) w[e] = (bf16)v[e];
+          *c = w;
+        }
+      } else {
+        for (int e = 0; e < 4 && col + e < P.N; ++e) {
+          if (f32) {
+            float* c = (float*)P.C + o + e;
+            *c = P.accumulate ? *c + v[e] : v[e];
+          } else {
+            bf16* c = (bf16*)P.C + o + e;
+            *c = (bf16)(P.accumulate ? (float)*c + v[e] : v[e]);
+          }
         }
       }
+    }
   }
 }
 
@@ -504,30 +520,7 @@ __global__ __launch_bounds__(256) void gemm3_kernel(const GemmArgs args, int tot
     }
   }
 
-  const int l32 = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int col = n0 + wn + 32 * j + l32;
-    if (col >= P.N) continue;
-    const float bv = P.bias ? P.bias[col] : 0.f;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (row >= P.M) continue;
-        const int orow = P.crow ? P.crow[row] : row;
-        const float v = P.alpha * acc[i][j][r] + bv;
-        const size_t o = (size_t)orow * P.ldc + col;
-        if (P.c_f32) {
-          float* c = (float*)P.C + o;
-          *c = P.accumulate ? *c + v : v;
-        } else {
-          bf16* c = (bf16*)P.C + o;
-          *c = (bf16)(P.accumulate ? (float)*c + v : v);
-        }
-      }
-  }
+  g2_epilogue_lds(P, m0, n0, wm, wn, lane, acc, lds3);
 }
 
 template <int NS>
@@ -628,10 +621,10 @@ __global__ __launch_bounds__(256) void gemm_group_kernel(const GroupArgs a) {
       }
     }
     if (tid == 0) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    g2_epilogue(P, tm * g2::BM, tn * g2::BN, wm, wn, lane, sum);
+    g2_epilogue_lds(P, tm * g2::BM, tn * g2::BN, wm, wn, lane, sum, lds);
     return;
   }
-  g2_epilogue(P, tm * g2::BM, tn * g2::BN, wm, wn, lane, acc);
+  g2_epilogue_lds(P, tm * g2::BM, tn * g2::BN, wm, wn, lane, acc, lds);
 }
 
 // descs: np x 16 int64 (ops/gemm.py layout); split[i] >= 1; ws: sum over split problems of

@@ -135,6 +135,11 @@ class DistConfig:
     grad_bucket_mb: float = 8.0
     grad_dtype: str = "fp32"          # fp32 | bf16 (compressed all-reduce)
     overlap_allreduce: bool = True
+    # CUs the fused conv backward leaves free while the core gradient bucket is being all-reduced
+    # (world > 1): torso_bwd_kernel fills every VGPR of each CU it runs on (248 VGPRs x 8 waves),
+    # so without a reservation the RCCL kernel cannot start until the conv backward has finished
+    # (no overlap at all).  0 = whole chip (the world == 1 layout).
+    comm_reserve_cus: int = 32
 
 
 @dataclass

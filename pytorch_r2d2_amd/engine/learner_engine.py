@@ -80,7 +80,29 @@ def addmm_f32(bias: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> torch.Ten
     return torch.mm(a, b).float() + bias
 
 
+def torso_bwd_grid(n_frames: int, reserve_cus: int = 0, n_cus: int = 256) -> int:
+    """Workgroups of the fused conv backward (one per CU, grid-stride over frames).
+
+    With ``reserve_cus`` > 0 (DP: the core gradient bucket's all-reduce runs beside it) the grid
+    leaves at least that many CUs free, then shrinks further while the busiest workgroup's frame
+    count stays the same: 2560 frames on 256 - 32 CUs is 12 frames per workgroup either way, so
+    214 workgroups do it and 42 CUs go to RCCL at no extra conv time."""
+    avail = max(8, n_cus - max(0, reserve_cus))
+    if n_frames <= avail:
+        return max(1, n_frames)
+    if reserve_cus <= 0:
+        return avail
+    per = -(-n_frames // avail)
+    return -(-n_frames // per)
+
+
 class LearnerEngine:
+    def _comm_reserve(self) -> int:
+        dc = self.cfg.dist
+        if self.world > 1 and dc.overlap_allreduce and self.device.type == "cuda":
+            return int(dc.comm_reserve_cus)
+        return 0
+
     def __init__(self, cfg: R2D2Config, replay: HBMReplay, device="cuda", rank: int = 0,
                  world: int = 1, process_group=None, init_module: Optional[QNet] = None):
         self.cfg = cfg
@@ -204,7 +226,7 @@ class LearnerEngine:
         # never lazily: the step must be capturable without warm-up)
         if self.fused_torso:
             n_slab = int(kernels().r2_torso_bwd_slab_floats())
-            self._tb_grid = min(256, Ll * B)
+            self._tb_grid = torso_bwd_grid(Ll * B, self._comm_reserve())
             self._tb_slab = z(self._tb_grid * n_slab)
             dst, scale = L.torso_grad_map()
             self._tb_dst, self._tb_scale = dst.to(d), scale.to(d)
@@ -764,11 +786,12 @@ class LearnerEngine:
         # (learner.py:107-108) with the target packs written only then
         self._pack_step(int(lc.target_update_interval), s)
 
-    def _priorities(self):
+    def _priorities(self, end: bool = True):
         rp = self.replay
         rp.refresh_sequences(self.starts, self.B, self.Lb, self.T)
         rp.update_tree()
-        rp.step_end()
+        if end:
+            rp.step_end()
 
     # ------------------------------------------------------------------ public API
     def _sync(self):
@@ -789,22 +812,34 @@ class LearnerEngine:
         self._update()
         self._priorities()
 
+    # DP (world > 1): the priority refresh + tree repair need only the forward's TD errors, so
+    # they run while the torso bucket is all-reduced; the update and the step counter follow
+    def _seg_prio(self):
+        self._priorities(end=False)
+
+    def _seg_update(self):
+        self._update()
+        self.replay.step_end()
+
     def step_eager(self):
         L = self.layout
         self._seg_core()
         if self.world > 1:   # core bucket all-reduce overlaps the conv backward
             self._sync().start(0, L.torso_offset)
         self._seg_torso()
-        if self.world > 1:
+        if self.world > 1:   # torso bucket all-reduce overlaps the priority tail
             self._sync().start(L.torso_offset, L.padded)
+            self._seg_prio()
             self._sync().finish()
-        self._seg_tail()
+            self._seg_update()
+        else:
+            self._seg_tail()
         self.steps_done += 1
 
     def capture(self, warmup: int = 2):
         """Capture the step into HIP graphs.  world == 1: one graph for the whole step.
-        world > 1: three graphs (core fwd/bwd | conv bwd | update) with the two bucket
-        all-reduces issued between them on the communication stream."""
+        world > 1: four graphs (core fwd/bwd | conv bwd | priorities | update) with the two
+        bucket all-reduces issued between them on the communication stream."""
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
@@ -814,7 +849,7 @@ class LearnerEngine:
         torch.cuda.synchronize(self.device)
         self.graphs = []
         if self.world > 1:
-            segs = [self._seg_core, self._seg_torso, self._seg_tail]
+            segs = [self._seg_core, self._seg_torso, self._seg_prio, self._seg_update]
         else:
             segs = [lambda: (self._seg_core(), self._seg_torso(), self._seg_tail())]
         pool = None
@@ -835,13 +870,14 @@ class LearnerEngine:
             self.graphs[0].replay()
         else:
             L = self.layout
-            g_core, g_torso, g_tail = self.graphs
+            g_core, g_torso, g_prio, g_update = self.graphs
             g_core.replay()
             self._sync().start(0, L.torso_offset)
             g_torso.replay()
             self._sync().start(L.torso_offset, L.padded)
+            g_prio.replay()
             self._sync().finish()
-            g_tail.replay()
+            g_update.replay()
         self.steps_done += 1
 
     def loss_value(self) -> float:

@@ -156,7 +156,7 @@ def _free_port():
     return p
 
 
-def _dp_worker(rank, world, port, outdir, graph=False):
+def _dp_worker(rank, world, port, outdir, graph=False, same_data=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK="0")
     import torch.distributed as dist
@@ -165,11 +165,21 @@ def _dp_worker(rank, world, port, outdir, graph=False):
     cfg = get_config("atari57", **{"learner.batch_size": 8, "replay.burn_in": 4, "replay.learn": 4,
                                    "replay.overlap": 4, "learner.use_graph": False, "seed": 11})
     rp = HBMReplay(cfg, DEV, capacity=8 * 200, n_subrings=8)
-    rp.fill_synthetic(episode_len=50, seed=rank)          # different data per rank
+    rp.fill_synthetic(episode_len=50, seed=0 if same_data else rank)   # different data per rank
     torch.manual_seed(5)
     eng = LearnerEngine(cfg, rp, DEV, rank=rank, world=world, process_group=dist.group.WORLD,
                         init_module=QNet("cpu", cfg.model, cfg.env))
-    if graph:   # 3 graph segments with the bucket all-reduces issued between them
+    if same_data and rank == 0:
+        # the same data on one rank (world 1, one graph / one eager sequence) for comparison
+        rp1 = HBMReplay(cfg, DEV, capacity=8 * 200, n_subrings=8)
+        rp1.fill_synthetic(episode_len=50, seed=0)
+        torch.manual_seed(5)
+        one = LearnerEngine(cfg, rp1, DEV, init_module=QNet("cpu", cfg.model, cfg.env))
+        for _ in range(3):
+            one.step_eager()
+        torch.save({"master": one.master.cpu(), "loss": one.loss_value()},
+                   os.path.join(outdir, "single.pt"))
+    if graph:   # 4 graph segments with the bucket all-reduces issued between them
         eng.capture(warmup=1)
         for _ in range(2):
             eng.step()
@@ -190,6 +200,19 @@ def test_dp_engine_ranks_stay_identical(tmp_path, graph):
     b = torch.load(tmp_path / "dp1.pt", weights_only=True)
     assert torch.equal(a["master"], b["master"])       # synchronous DP: identical replicas
     assert a["loss"] != b["loss"]                       # ...trained on different local batches
+
+
+@pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
+def test_dp_engine_on_identical_shards_matches_single_rank(tmp_path, graph):
+    """Two ranks on identical replay shards = one rank: the DP step order (core bucket beside the
+    conv backward, priority refresh + tree repair beside the torso bucket, then update + step
+    counter) must reproduce the single-rank trajectory, sampling included."""
+    import torch.multiprocessing as tmp
+    tmp.spawn(_dp_worker, args=(2, _free_port(), str(tmp_path), graph, True), nprocs=2, join=True)
+    a = torch.load(tmp_path / "dp0.pt", weights_only=True)
+    one = torch.load(tmp_path / "single.pt", weights_only=True)
+    torch.testing.assert_close(a["master"], one["master"], rtol=0, atol=1e-6)
+    assert abs(a["loss"] - one["loss"]) <= 1e-5 * max(1.0, abs(one["loss"]))
 
 
 def test_native_loop_learns_synthetic_cue_task():

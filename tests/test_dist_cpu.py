@@ -121,3 +121,19 @@ def test_collectives_bench_gloo_world2():
     assert res["world"] == 2 and res["backend"] == "gloo"
     assert res["all_reduce_all_fp32"]["bytes"] == 2_037_095 * 4
     assert all(res[k]["us"] > 0 for k in res if isinstance(res[k], dict))
+
+
+def test_torso_bwd_grid_leaves_cus_for_the_allreduce():
+    from pytorch_r2d2_amd.engine.learner_engine import torso_bwd_grid
+    # world == 1: one workgroup per CU, or per frame when there are fewer frames
+    assert torso_bwd_grid(2560, 0) == 256
+    assert torso_bwd_grid(100, 0) == 100
+    # DP: at least 32 CUs free, and no more workgroups than the busiest one's frame count needs
+    g = torso_bwd_grid(2560, 32)
+    assert g <= 224 and -(-2560 // g) == -(-2560 // 224)
+    assert g == 214
+    for n in (64, 320, 2560, 5120, 10000):
+        for r in (0, 16, 32, 64):
+            g = torso_bwd_grid(n, r)
+            assert 1 <= g <= min(n, 256 - r if r else 256)
+            assert -(-n // g) == -(-n // min(n, 256 - r))   # same per-workgroup frame count
