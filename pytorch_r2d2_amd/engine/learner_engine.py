@@ -570,8 +570,12 @@ class LearnerEngine:
         gw1 = L.span(g, "val.0.weight", "adv.0.weight", (2 * HD, H))
         if self.use_gemm:
             dh = self.dh
-            # (a K split of this 40-tile GEMM through gemm_group measured no faster)
-            gemm(Gemm(self.dz, pk["head1"], dh))                          # (N, H) fp32
+            # a plain 40-tile GEMM (M=2560, N=256, K=512): hipBLASLt runs it in 7.4 us vs 13.1
+            # for the 128x128 MFMA kernel and 18-45 us split-K (tools/dh_split_probe.py)
+            if lc.dh_gemm == "blaslt":
+                torch.mm(self.dz, pk["head1"], out_dtype=torch.float32, out=dh)   # (N, H) fp32
+            else:
+                gemm(Gemm(self.dz, pk["head1"], dh))
         else:
             gw1.copy_(mm_f32(self.dz.t(), h_learn))
             dh = mm_f32(self.dz, pk["head1"])                           # (N, H)
