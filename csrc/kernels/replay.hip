@@ -165,6 +165,61 @@ __global__ void tree_update_level_kernel(float* __restrict__ tree, TreeGeom g, i
   }
 }
 
+// ---- the same repair at level 1 (-> level 2) with the small upper levels folded into the
+// launch: every workgroup publishes its level-2 sums write-through (sc1 stores, drained), one
+// lane per workgroup adds to an arrival ticket, and the workgroup whose add comes last
+// recomputes every node of levels 3.. from the level below (sc1 loads; the same wave_sum order,
+// so the values are bit-identical to the per-level launches) and, with end_step, also does
+// step_end_kernel's work.  Replaces levels - 2 launches (+ step_end) of ~4.5 us each in a graph
+// (MI355X_MICROARCH.md hand-off table: last-arriver row).  Needs every level >= 3 to have
+// at most 64 * 64 nodes below it (host checks).
+__global__ void tree_update_tail_kernel(float* __restrict__ tree, TreeGeom g,
+                                        const int* __restrict__ dirty, int* __restrict__ count,
+                                        int max_dirty, unsigned* __restrict__ ticket,
+                                        int64_t* __restrict__ step) {
+  __shared__ int last;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int n = min(*count, max_dirty);
+  const int nwaves = gridDim.x * nw;
+  {
+    const float* child = tree + g.off[1];
+    float* parent = tree + g.off[2];
+    for (int e = blockIdx.x * nw + wave; e < n; e += nwaves) {
+      const int64_t p = (((int64_t)dirty[e]) >> 6) >> 6;
+      const int64_t c = p * 64 + lane;
+      float v = c < g.size[1] ? child[c] : 0.f;
+      v = wave_sum(v);
+      if (lane == 0) __hip_atomic_store(parent + p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  for (int l = 2; l + 1 < g.levels; ++l) {
+    const float* child = tree + g.off[l];
+    float* parent = tree + g.off[l + 1];
+    for (int64_t p = wave; p < g.size[l + 1]; p += nw) {
+      const int64_t c = p * 64 + lane;
+      float v = c < g.size[l] ? __hip_atomic_load(child + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+      v = wave_sum(v);
+      if (lane == 0) __hip_atomic_store(parent + p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    *ticket = 0u;
+    if (step) {
+      *step += 1;
+      *count = 0;
+    }
+  }
+}
+
 // ---- eta-mixed sequence priority of every marked start overlapping the updated window
 // For sampled start s_b the learner rewrote rows [s_b + upd_lo, s_b + upd_hi).  Sequence s
 // (rows [s, s+T)) overlaps iff s in (s_b + upd_lo - T, s_b + upd_hi).
@@ -348,6 +403,27 @@ extern "C" int r2_tree_update(float* tree, const int64_t* offs, const int64_t* s
   for (int l = 0; l + 1 < levels; ++l)
     hipLaunchKernelGGL(tree_update_level_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream,
                        tree, g, l, dirty, count, max_dirty);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
+// Level 0 as its own launch, then level 1 with every upper level (and, given `step`, the step
+// counter + dirty-list reset) folded into one launch (tree_update_tail_kernel).  ticket: one
+// zeroed uint, reset by the kernel.  -3: the tree is too shallow or too wide for the fold.
+extern "C" int r2_tree_update_fused(float* tree, const int64_t* offs, const int64_t* sizes,
+                                    int levels, const int* dirty, int* count, int max_dirty,
+                                    unsigned* ticket, int64_t* step, void* stream) {
+  if (levels < 4 || levels > TREE_MAX_LEVELS) return -3;
+  for (int l = 3; l < levels; ++l)
+    if (sizes[l - 1] > 64 * 64) return -3;
+  TreeGeom g = make_geom(offs, sizes, levels);
+  int nb = (max_dirty + 3) / 4;
+  if (nb > 256) nb = 256;
+  if (nb < 1) nb = 1;
+  hipLaunchKernelGGL(tree_update_level_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream,
+                     tree, g, 0, dirty, count, max_dirty);
+  hipLaunchKernelGGL(tree_update_tail_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream,
+                     tree, g, dirty, count, max_dirty, ticket, step);
   R2_CHECK_LAUNCH();
   return 0;
 }

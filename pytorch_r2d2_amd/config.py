@@ -58,6 +58,9 @@ class ReplayConfig:
     beta: float = 0.0                 # IS exponent; 0 == reference (no IS weights, Q10)
     stored_state: str = "post"        # post == reference (Q6); pre == paper
     n_subrings: int = 1               # one contiguous sub-ring per actor env (HBM replay)
+    # learner tail: sum-tree levels >= 2 and the step counter folded into the level-1 repair
+    # launch (last-arriving workgroup), 2 launches instead of levels - 1 + 1
+    fused_tree_tail: bool = True
 
     @property
     def seq_len(self) -> int:

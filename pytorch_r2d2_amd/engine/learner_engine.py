@@ -793,6 +793,8 @@ class LearnerEngine:
     def _priorities(self, end: bool = True):
         rp = self.replay
         rp.refresh_sequences(self.starts, self.B, self.Lb, self.T)
+        if self.cfg.replay.fused_tree_tail and rp.update_tree_and_end_step(end):
+            return
         rp.update_tree()
         if end:
             rp.step_end()

@@ -85,6 +85,8 @@ class HBMReplay:
         self.dirty_count = torch.zeros(1, dtype=torch.int32, device=d)
         self.n_valid = torch.zeros(1, dtype=torch.int32, device=d)
         self.step = torch.zeros(1, dtype=torch.int64, device=d)
+        # arrival ticket of the fused tree repair (allocated before any graph capture)
+        self.tree_ticket = torch.zeros(1, dtype=torch.int32, device=d) if d.type == "cuda" else None
         self.seed = int(cfg.seed) * 0x9E3779B1 + 12345
         self.heads = np.zeros(n_sub, dtype=np.int64)   # per-sub-ring write heads (host mirror)
         self.total_written = 0
@@ -145,6 +147,24 @@ class HBMReplay:
         check(k.r2_tree_update(ptr(self.tree), self.tree_offs.ctypes.data, self.tree_sizes.ctypes.data,
                                self.tree_levels, ptr(self.dirty), ptr(self.dirty_count),
                                self.max_dirty, self._ts(stream)), "tree_update")
+
+    def update_tree_and_end_step(self, end_step: bool = True, stream=None) -> bool:
+        """Learner tail: tree repair in two launches (level 0, then level 1 with the small upper
+        levels folded in by the last-arriving workgroup, replay.hip tree_update_tail_kernel) and,
+        with ``end_step``, the step counter + dirty-list reset in the same launch.  Returns False
+        (nothing launched) when the tree shape does not allow the fold."""
+        if self.tree_ticket is None:
+            if self.tree.device.type != "cuda":
+                return False
+            self.tree_ticket = torch.zeros(1, dtype=torch.int32, device=self.tree.device)
+        rc = kernels().r2_tree_update_fused(
+            ptr(self.tree), self.tree_offs.ctypes.data, self.tree_sizes.ctypes.data,
+            self.tree_levels, ptr(self.dirty), ptr(self.dirty_count), self.max_dirty,
+            ptr(self.tree_ticket), ptr(self.step) if end_step else 0, self._ts(stream))
+        if rc == -3:
+            return False
+        check(rc, "tree_update_fused")
+        return True
 
     def refresh_sequences(self, starts: torch.Tensor, B: int, upd_lo: int, upd_hi: int,
                           stream=None) -> None:

@@ -390,6 +390,43 @@ def test_sum_tree_sample_and_update():
     assert torch.allclose(inc, rp.tree, rtol=1e-5, atol=1e-3)
 
 
+@pytest.mark.parametrize("cap", [1_000_000, 70_000])
+def test_fused_tree_tail_matches_per_level_repair(cap):
+    """replay.hip tree_update_tail_kernel: level-1 repair + upper levels by the last-arriving
+    workgroup (+ step counter / dirty reset) == the per-level launches + step_end, bit for bit,
+    three rounds in a row (the arrival ticket resets itself)."""
+    from pytorch_r2d2_amd.engine.replay_hbm import HBMReplay
+    cfg = get_config("reference", **{"replay.capacity": cap, "replay.n_subrings": 8})
+    a = HBMReplay(cfg, DEV)
+    a.fill_synthetic(episode_len=120, seed=5)
+    b = HBMReplay(cfg, DEV)
+    b.fill_synthetic(episode_len=120, seed=5)
+    assert a.tree_levels >= 4 and torch.equal(a.tree, b.tree)
+    g = torch.Generator(device=DEV).manual_seed(cap)
+    for rnd in range(3):
+        B = 64
+        idx = torch.zeros(B, dtype=torch.int32, device=DEV)
+        prob = torch.zeros(B, device=DEV)
+        a.sample(B, idx, prob)
+        pr = torch.rand(cap, generator=g, device=DEV) * 3
+        for r in (a, b):
+            r.priority.copy_(pr)
+            r.refresh_sequences(idx, B, 0, cfg.replay.seq_len)
+        assert a.update_tree_and_end_step(True)
+        b.update_tree()
+        b.step_end()
+        torch.cuda.synchronize()
+        assert torch.equal(a.tree, b.tree), rnd
+        assert int(a.step.item()) == int(b.step.item()) == rnd + 1
+        assert int(a.dirty_count.item()) == 0 and int(a.tree_ticket.item()) == 0
+    # without end_step the counter and the dirty list are left alone
+    a.refresh_sequences(idx, 64, 0, cfg.replay.seq_len)
+    n = int(a.dirty_count.item())
+    assert a.update_tree_and_end_step(False)
+    torch.cuda.synchronize()
+    assert int(a.step.item()) == 3 and int(a.dirty_count.item()) == n
+
+
 @pytest.mark.parametrize("N", [2560, 333])
 def test_head_grads_and_colsum_match_torch(N):
     """gradsum.hip: dueling last-layer weight/bias grads, layer-1 bias grads and the permuted
