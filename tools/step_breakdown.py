@@ -5,12 +5,13 @@ import glob
 import sys
 
 
-def main(path_glob, out=None, last=1, marker='step_end'):
+def main(path_glob, out=None, last=1, marker=('step_end', 'tree_update_tail')):
     import os
     paths = sorted(glob.glob(path_glob), key=os.path.getmtime, reverse=True)
     rows = list(csv.DictReader(open(paths[0])))
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
-    ends = [i for i, r in enumerate(rows) if marker in r['Kernel_Name']]
+    marks = (marker,) if isinstance(marker, str) else marker
+    ends = [i for i, r in enumerate(rows) if any(m in r['Kernel_Name'] for m in marks)]
     a, b = ends[-1 - last] + 1, ends[-1] + 1
     st = rows[a:b]
     t0 = int(st[0]['Start_Timestamp'])
@@ -33,4 +34,4 @@ def main(path_glob, out=None, last=1, marker='step_end'):
 if __name__ == "__main__":
     main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None,
          int(sys.argv[3]) if len(sys.argv) > 3 else 1,
-         sys.argv[4] if len(sys.argv) > 4 else 'step_end')
+         sys.argv[4] if len(sys.argv) > 4 else ('step_end', 'tree_update_tail'))
