@@ -138,3 +138,182 @@ extern "C" int r2_td_loss(const float* q_sa, const float* q_arg, const float* q_
   R2_CHECK_LAUNCH();
   return 0;
 }
+
+// ============================================================================================
+// TD loss fused with the dueling-head backward (head.hip dueling_bwd_kernel): one WAVE per
+// transition.  dL/dQ of a row is nonzero only at the taken action, so right where the TD error is
+// known the wave also writes dva = [dV, dA_0..] and dz = relu'(z) * (dva . W2) for its row --
+// the same arithmetic, in the same order, as dueling_bwd_kernel (bit-identical dz / dva), one
+// launch instead of two (each ~9 us, most of it the launch floor of a graph node).
+// The loss is reduced deterministically: per-workgroup partials (sc1), arrival ticket, the last
+// workgroup sums the partials in a fixed order.
+struct TdDuelArgs {
+  TdArgs td;
+  const bf16* zr;       // (Tl*B, 2*HD) relu'd hidden of the online head's learning rows
+  const float* w2;      // (1 + A, HD) second-layer weights [value row; advantage rows]
+  bf16* dz;             // (Tl*B, 2*HD) out
+  float* dva;           // (Tl*B, 1 + A) out
+};
+
+template <int HD>
+__global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
+  // 16 waves per workgroup: one arrival-ticket atomic per 16 transitions (a single counter's
+  // agent-scope atomics serialise: 640 four-wave workgroups cost as much as the fusion saved)
+  constexpr int PER = HD / 64, MAXA = 8, NW = 16;
+  const TdArgs& a = args.td;
+  __shared__ float wsh[256];
+  __shared__ float red[NW];
+  __shared__ float tot_sh[NW];
+  __shared__ int last;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = a.Tl * a.B;
+  const int i = blockIdx.x * NW + wave;      // this wave's transition
+  const bool valid = i < n;
+  const int b = valid ? i % a.B : 0, tl = valid ? i / a.B : 0;
+  // ---- everything that does not depend on the TD error is loaded first, so the dependent
+  // chain below (start -> row -> action / reward / done) is the only serial part
+  const int start = valid ? a.starts[b] : 0;
+  const float NEG = -3.0e38f;
+  const float qa = (valid && lane < a.A) ? a.q_arg[(size_t)i * a.A + lane] : NEG;
+  const float qt = (valid && lane < a.A) ? a.q_tgt[(size_t)i * a.A + lane] : 0.f;
+  const float qs = (valid && lane < a.A) ? a.q_sa[(size_t)i * a.A + lane] : 0.f;
+  bf16 zv[PER], za[PER];
+  float w2v[PER], w2a[MAXA][PER];
+  if (valid) {
+    const bf16* zrow = args.zr + (size_t)i * 2 * HD;
+#pragma unroll
+    for (int e = 0; e < PER; ++e) { zv[e] = zrow[lane * PER + e]; za[e] = zrow[HD + lane * PER + e]; }
+  }
+#pragma unroll
+  for (int e = 0; e < PER; ++e) w2v[e] = args.w2[lane * PER + e];
+#pragma unroll
+  for (int k = 0; k < MAXA; ++k)
+#pragma unroll
+    for (int e = 0; e < PER; ++e)
+      w2a[k][e] = k < a.A ? args.w2[(size_t)(1 + k) * HD + lane * PER + e] : 0.f;
+  const int row = valid ? ring_row(start, a.burn_in + tl, a.cap_e) : 0;
+  const int act = valid ? (int)a.action[row] : 0;
+  const float rew = valid ? a.reward[row] : 0.f;
+  const bool dn = valid ? a.done[row] != 0 : true;
+  // ---- IS weights (B <= 256), as td_kernel
+  float w = 1.f;
+  if (tid < a.B && a.probs != nullptr && a.beta > 0.f) {
+    const float nv = a.n_valid ? (float)max(*a.n_valid, 1) : 1.f;
+    w = powf(fmaxf(nv * a.probs[tid], 1e-30f), -a.beta);
+  }
+  const float m = wave_max(tid < a.B ? w : 0.f);
+  if (lane == 0) red[wave] = m;
+  __syncthreads();
+  float wmax = red[0];
+#pragma unroll
+  for (int q = 1; q < NW; ++q) wmax = fmaxf(wmax, red[q]);
+  if (tid < a.B) {
+    wsh[tid] = w / wmax;
+    if (a.is_w && blockIdx.x == 0) a.is_w[tid] = w / wmax;
+  }
+  __syncthreads();
+
+  const float inv_n = 1.f / (float)n;
+  float lsum = 0.f;
+  if (valid) {
+    // argmax_a Q_online(s_{t+n}): first maximum, as td_kernel's sequential scan
+    float bv = qa;
+    int best = lane < a.A ? lane : 1 << 20;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(best, o, 64);
+      if (ov > bv || (ov == bv && oi < best)) { bv = ov; best = oi; }
+    }
+    float boot = __shfl(qt, best, 64);
+    if (a.value_rescale) boot = vr_hinv(boot, a.vr_eps);
+    float y = rew + (dn ? 0.f : a.gamma_n * boot);
+    if (a.value_rescale) y = vr_h(y, a.vr_eps);
+    const float delta = __shfl(qs, act, 64) - y;
+    const float wb = wsh[b];
+    const float g = wb * delta * inv_n;      // dL/dQ[act]; every other action 0
+    if (lane == 0) {
+      lsum = wb * 0.5f * delta * delta;
+      const float ad = fabsf(delta);
+      if (a.td_abs) a.td_abs[i] = ad;
+      if (a.priority) a.priority[row] = powf(ad + a.prio_eps, a.alpha);
+    }
+    if (lane < a.A) a.dq[(size_t)i * a.A + lane] = lane == act ? g : 0.f;
+    // dueling backward of row i (dueling_bwd_kernel's arithmetic on dq = g e_act)
+    float dv = 0.f;
+    for (int k = 0; k < a.A; ++k) dv += (k == act) ? g : 0.f;
+    const float dmean = dv / (float)a.A;
+    float* dvr = args.dva + (size_t)i * (1 + a.A);
+    if (lane == 0) dvr[0] = dv;
+    if (lane < a.A) dvr[1 + lane] = ((lane == act) ? g : 0.f) - dmean;
+    bf16* dzrow = args.dz + (size_t)i * 2 * HD;
+    bf16 ov[PER], oa[PER];
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const float gv = dv * w2v[e];
+      float ga = 0.f;
+#pragma unroll
+      for (int k = 0; k < MAXA; ++k)
+        if (k < a.A) ga += (((k == act) ? g : 0.f) - dmean) * w2a[k][e];
+      ov[e] = (bf16)(((float)zv[e] > 0.f) ? gv : 0.f);
+      oa[e] = (bf16)(((float)za[e] > 0.f) ? ga : 0.f);
+    }
+#pragma unroll
+    for (int e = 0; e < PER; ++e) { dzrow[lane * PER + e] = ov[e]; dzrow[HD + lane * PER + e] = oa[e]; }
+  }
+  // ---- loss: wave partial (lane 0) -> workgroup partial -> last arriver, fixed order
+  if (lane == 0) red[wave] = lsum;
+  __syncthreads();
+  if (tid == 0) {
+    float v = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) v += red[q];
+    __hip_atomic_store(a.part + blockIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = t == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  float s = 0.f;
+  for (unsigned g = tid; g < gridDim.x; g += NW * 64)
+    s += __hip_atomic_load(a.part + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  s = wave_sum(s);
+  if (lane == 0) tot_sh[wave] = s;
+  __syncthreads();
+  if (tid == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) t += tot_sh[q];
+    *a.loss = t * inv_n;
+    __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+extern "C" int r2_td_duel(const float* q_sa, const float* q_arg, const float* q_tgt,
+                          const int* starts, const float* probs, const uint8_t* action,
+                          const float* reward, const uint8_t* done, float* dq, float* loss,
+                          float* td_abs, float* priority, float* is_w, const int* n_valid,
+                          int Tl, int B, int A, int burn_in, int cap_e, float gamma_n,
+                          int value_rescale, float vr_eps, float alpha, float prio_eps,
+                          float beta, float* part, unsigned* ticket, const bf16* zr,
+                          const float* w2, bf16* dz, float* dva, int HD, void* stream) {
+  if (B > 256) return -1;
+  if (A < 1 || A > 8) return -3;              // td_duel_kernel MAXA
+  const int grid = (Tl * B + 15) / 16;
+  if (grid > 4096) return -2;   // part[] holds one float per workgroup (engine: 4096)
+  TdDuelArgs d{{q_sa, q_arg, q_tgt, starts, probs, action, reward, done, dq, loss, td_abs, priority,
+                is_w, n_valid, part, ticket, Tl, B, A, burn_in, cap_e, gamma_n, vr_eps, alpha,
+                prio_eps, beta, value_rescale},
+               zr, w2, dz, dva};
+  hipStream_t s = (hipStream_t)stream;
+  switch (HD) {
+    case 64: hipLaunchKernelGGL(td_duel_kernel<64>, dim3(grid), dim3(1024), 0, s, d); break;
+    case 128: hipLaunchKernelGGL(td_duel_kernel<128>, dim3(grid), dim3(1024), 0, s, d); break;
+    case 256: hipLaunchKernelGGL(td_duel_kernel<256>, dim3(grid), dim3(1024), 0, s, d); break;
+    case 512: hipLaunchKernelGGL(td_duel_kernel<512>, dim3(grid), dim3(1024), 0, s, d); break;
+    default: return -4;
+  }
+  R2_CHECK_LAUNCH();
+  return 0;
+}

@@ -109,6 +109,7 @@ class LearnerConfig:
     # measured 1.146 ms/step at 5 chunks vs 0.993 serial -- each cross-stream graph edge costs
     # ~15 us and a chunk's x-projection GEMM is tile-latency bound; profiles/r01_v9_pipelined.txt)
     fwd_chunks: int = 0
+    td_fuse_head_bwd: bool = True     # dueling-head backward inside the TD launch (td_duel_kernel)
     dh_gemm: str = "blaslt"           # head backward dh = dz @ W1: blaslt (hipBLASLt) | mfma
     torso_bwd: str = "fused"          # fused (HIP kernel) | library (MIOpen convolution_backward)
     # library conv path (frame geometries without the fused HIP torso, e.g. DMLab): MIOpen find

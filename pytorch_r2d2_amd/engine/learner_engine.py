@@ -523,12 +523,22 @@ class LearnerEngine:
             q_arg = self.q_nx[: Ll * B]
             q_tgt = self.q_tg[: Ll * B]
         rc = self.cfg.replay
-        check(k.r2_td_loss(ptr(q_sa), ptr(q_arg), ptr(q_tgt), ptr(self.starts), ptr(self.probs),
-                           ptr(rp.action), ptr(rp.reward), ptr(rp.done), ptr(self.dq), ptr(self.loss),
-                           ptr(self.td_abs), ptr(rp.priority), ptr(self.is_w), ptr(rp.n_valid),
-                           Ll, B, A, Lb, rp.cap_e, self.gamma_n, int(lc.value_rescale),
-                           float(lc.value_rescale_eps), float(rc.alpha), float(rc.priority_eps),
-                           float(rc.beta), ptr(self.td_part), ptr(self.td_ticket), s), "td_loss")
+        targs = (ptr(q_sa), ptr(q_arg), ptr(q_tgt), ptr(self.starts), ptr(self.probs),
+                 ptr(rp.action), ptr(rp.reward), ptr(rp.done), ptr(self.dq), ptr(self.loss),
+                 ptr(self.td_abs), ptr(rp.priority), ptr(self.is_w), ptr(rp.n_valid),
+                 Ll, B, A, Lb, rp.cap_e, self.gamma_n, int(lc.value_rescale),
+                 float(lc.value_rescale_eps), float(rc.alpha), float(rc.priority_eps),
+                 float(rc.beta), ptr(self.td_part), ptr(self.td_ticket))
+        # TD + the dueling head's backward in one launch (td.hip td_duel_kernel): dz / dva of the
+        # online learning rows are written right where dL/dQ is known
+        self._duel_done = False
+        if lc.td_fuse_head_bwd:
+            rc_ = k.r2_td_duel(*targs, ptr(self.zr_on[: Ll * B]), ptr(pk["head_w2"]), ptr(self.dz),
+                               ptr(self.dva), L.HD, s)
+            if rc_ == 0:
+                self._duel_done = True
+                return
+        check(k.r2_td_loss(*targs, s), "td_loss")
 
     def _backward_core(self):
         """Head backward, BPTT, LSTM/head weight gradients -> grad bucket 'core'."""
@@ -539,8 +549,9 @@ class LearnerEngine:
         H, A, HD, G = L.H, L.A, L.HD, L.G
         N = Ll * B
         zr = self.zr_on[:N]
-        check(k.r2_dueling_bwd(ptr(self.dq), ptr(zr), ptr(pk["head_w2"]), ptr(self.dz),
-                               ptr(self.dva), N, A, HD, s), "dueling_bwd")
+        if not getattr(self, "_duel_done", False):      # else fused into the TD launch
+            check(k.r2_dueling_bwd(ptr(self.dq), ptr(zr), ptr(pk["head_w2"]), ptr(self.dz),
+                                   ptr(self.dva), N, A, HD, s), "dueling_bwd")
         g = self.grad
         gw2 = L.span(g, "val.2.weight", "adv.2.weight", (1 + A, HD))
         gb2 = L.span(g, "val.2.bias", "adv.2.bias", (1, 1 + A))

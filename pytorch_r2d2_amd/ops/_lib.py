@@ -39,6 +39,8 @@ _SIGS = {
     "r2_dueling_fwd": [P, P, P, P, P, P, I, I, I, P],
     "r2_dueling_bwd": [P, P, P, P, P, I, I, I, P],
     "r2_td_loss": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, F, F, F, F, P, P, P],
+    "r2_td_duel": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, F, F, F, F, P, P,
+                   P, P, P, P, I, P],
     "r2_tree_sample": [P, P, P, I, I, U64, P, P, P, P],
     "r2_tree_rebuild": [P, P, P, I, P],
     "r2_tree_update": [P, P, P, I, P, P, I, P],

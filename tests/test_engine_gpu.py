@@ -173,3 +173,24 @@ def test_fused_torso_backward_matches_library():
                  "vis_layers.2.bias", "vis_layers.4.weight", "vis_layers.4.bias"):
         r = _rel(L.view(eng.grad, name), L.view(ref, name))
         assert r < 3e-2, f"{name}: rel err {r}"
+
+
+@pytest.mark.parametrize("mode", ["shifted", "reference"])
+def test_td_fused_head_backward_matches_separate_launches(mode):
+    """td.hip td_duel_kernel (TD + dueling-head backward, a wave per transition) == td_kernel +
+    head.hip dueling_bwd_kernel: dq, dz, dva, priorities and every gradient bit for bit, the loss
+    to fp32 rounding (its partial sums are grouped differently)."""
+    runs = []
+    for fuse in (True, False):
+        cfg, rp, eng, _, _ = _make(mode, B=64, **{"learner.td_fuse_head_bwd": fuse})
+        eng._forward_loss()
+        assert eng._duel_done == fuse
+        eng._backward_core()
+        eng._backward_torso()
+        torch.cuda.synchronize()
+        runs.append((eng, rp))
+    (a, ra), (b, rb) = runs
+    for name in ("dq", "dz", "dva", "td_abs", "is_w", "grad"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    assert torch.equal(ra.priority, rb.priority)
+    assert abs(a.loss_value() - b.loss_value()) <= 1e-6 * max(1.0, abs(b.loss_value()))
