@@ -253,6 +253,11 @@ __global__ void seqprio_refresh_kernel(const int* __restrict__ starts, int B,
   }
   __syncthreads();
   const int nl = min(n_list, MAXC);
+  // one dirty-list reservation per workgroup (a per-start atomicAdd on the shared counter
+  // serialised ~4 x B agent-scope atomics on one address)
+  __shared__ int dbase;
+  if (threadIdx.x == 0) dbase = nl > 0 ? atomicAdd(count, nl) : 0;
+  __syncthreads();
   for (int i = wave; i < nl; i += nw) {
     {
       const int s = list[i];
@@ -266,7 +271,7 @@ __global__ void seqprio_refresh_kernel(const int* __restrict__ starts, int B,
       sm = wave_sum(sm);
       if (lane == 0) {
         leaves[s] = eta * mx + (1.f - eta) * (sm / (float)T);
-        const int slot = atomicAdd(count, 1);
+        const int slot = dbase + i;
         if (slot < max_dirty) dirty[slot] = s;
       }
     }
@@ -422,7 +427,10 @@ extern "C" int r2_tree_update_fused(float* tree, const int64_t* offs, const int6
   if (nb < 1) nb = 1;
   hipLaunchKernelGGL(tree_update_level_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream,
                      tree, g, 0, dirty, count, max_dirty);
-  hipLaunchKernelGGL(tree_update_tail_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream,
+  // fewer workgroups than level 0: each one adds to the single arrival ticket (agent-scope
+  // atomics on one address serialise); 64 x 4 waves cover a learner step's dirty list in a pass
+  const int nbt = nb < 64 ? nb : 64;
+  hipLaunchKernelGGL(tree_update_tail_kernel, dim3(nbt), dim3(256), 0, (hipStream_t)stream,
                      tree, g, dirty, count, max_dirty, ticket, step);
   R2_CHECK_LAUNCH();
   return 0;
