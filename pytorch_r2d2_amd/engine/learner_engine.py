@@ -13,15 +13,18 @@ priority scatters.  Here a step is:
     proj      ONE MFMA GEMM launch for both nets: x . W_ih^T + (b_ih + b_hh), all T*B rows
     lstm      persistent recurrence kernel, all chains in one launch
     head      [val.0;adv.0] GEMM + fused dueling epilogue kernel (every head in one launch)
-    td        fused double-Q n-step target / loss / dL/dQ / IS weights / row priorities
-    backward  dueling backward kernel, dh GEMM, persistent BPTT (fused bias-gradient column
-              sums; head-gradient reduction on its idle workgroups), weight-gradient + dX
-              GEMMs in one grouped launch, fused conv backward from the saved activations
-    allreduce (DP) bucket "core" overlapped with the conv backward, then bucket "torso"
+    td        fused double-Q n-step target / loss / dL/dQ / IS weights / row priorities, with
+              the dueling head's backward (dz, dva) in the same launch (td_duel_kernel)
+    backward  dh GEMM (hipBLASLt), persistent BPTT (fused bias-gradient column sums;
+              head-gradient reduction on its idle workgroups), weight-gradient + dX GEMMs in
+              one grouped launch, fused conv backward from the saved activations
+    allreduce (DP) bucket "core" beside the conv backward (which leaves CUs to RCCL), bucket
+              "torso" beside the priority refresh + tree repair
     update    fused centered RMSprop (or Adam) over the flat master buffer, one pack launch
               producing every bf16 kernel layout, target sync as a device-side
               `copy_if_due` (graph-safe)
-    priority  eta-mix refresh of every overlapping sequence, tree repair, step counter
+    priority  eta-mix refresh of every overlapping sequence, tree repair in two launches (upper
+              levels and the step counter folded into the second)
 
 No host synchronisation happens inside a step, so the whole step (minus collectives) is
 captured once into a HIP graph and replayed.
@@ -138,6 +141,7 @@ class LearnerEngine:
         self.gate_inv = L.gate_inv.to(d)
         self.clip_buf = torch.zeros(1, dtype=torch.float32, device=d)
         self.steps_done = 0
+        self._duel_done = False       # the TD launch also ran the dueling-head backward
         self.graph = None
         self.stats: Dict[str, float] = {}
         self._alloc()
