@@ -492,6 +492,12 @@ __global__ __launch_bounds__(256) void lstm_bwd_persist_kernel(const PBwdArgs a)
   }
 }
 
+// CUs of the device (set by the engine from hipDeviceProp_t::multiProcessorCount): every
+// persistent grid must be co-resident at one workgroup per CU
+static int g_num_cus = 256;
+extern "C" int r2_set_num_cus(int n) { if (n > 0) g_num_cus = n; return 0; }
+extern "C" int r2_get_num_cus() { return g_num_cus; }
+
 static long long* g_pl_dbg = nullptr;
 static int g_pl_slow = 0;
 extern "C" int r2_lstm_persist_set_debug(long long* p) { g_pl_dbg = p; return 0; }
@@ -505,7 +511,7 @@ extern "C" int r2_lstm_fwd_persist(const int64_t* chain_ptrs, int n_chains, int 
   if (n_chains < 1 || n_chains > PL_MAX_CHAINS || B < 1 || B > 256) return -1;
   if (H != 64 && H != 128 && H != 256 && H != 512) return -2;
   const int MB = (B + 31) / 32;
-  if ((H / PL_UNITS) * MB * n_chains > 256 || MB > 8) return -3;  // co-resident, 1 WG per CU
+  if ((H / PL_UNITS) * MB * n_chains > g_num_cus || MB > 8) return -3;  // co-resident, 1 WG per CU
   if ((size_t)T * B * H * 2 >= (1ull << 32)) return -4;
   PFwdArgs args;
   for (int c = 0; c < n_chains; ++c) {
@@ -544,7 +550,7 @@ extern "C" int r2_lstm_bwd_persist(const float* dh_ext, const float* gates, cons
   if (B < 1 || B > 256) return -1;
   if (H != 64 && H != 128 && H != 256 && H != 512) return -2;
   const int MB = (B + 31) / 32;
-  if ((H / PL_UNITS) * MB > 256 || MB > 8) return -3;
+  if ((H / PL_UNITS) * MB > g_num_cus || MB > 8) return -3;
   if ((size_t)2 * (H / PL_UNITS) * B * H * 4 >= (1ull << 32)) return -4;
   const int nwg = H / PL_UNITS;
   const int xmap = MB <= 8 && nwg <= 32;
@@ -883,7 +889,7 @@ extern "C" int r2_lstm_fwd_tag(const int64_t* chain_ptrs, int n_chains, int B, i
   if (H != 64 && H != 128 && H != 256 && H != 512) return -2;
   const int MB = (B + PT_ROWS - 1) / PT_ROWS, nwg = H / PL_UNITS;
   const int groups = n_chains * MB;
-  if (groups * nwg > 256 || groups > PL_MAX_GROUPS) return -3;
+  if (groups * nwg > g_num_cus || groups > PL_MAX_GROUPS) return -3;
   if ((size_t)T * B * H * 4 >= (1ull << 32) || T >= 65535 ||
       r2_lstm_tag_ring_bytes(n_chains, B, H) < 0) return -4;
   PTArgs args;
@@ -1292,7 +1298,7 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
   if (B < 1 || T < 1 || t0 < 0 || t0 >= T) return -1;
   if (H != 64 && H != 128 && H != 256 && H != 512) return -2;
   const int MB = (B + PT_ROWS - 1) / PT_ROWS, nwg = H / PL_UNITS;
-  if (MB * nwg > 256 || MB > PL_MAX_GROUPS) return -3;
+  if (MB * nwg > g_num_cus || MB > PL_MAX_GROUPS) return -3;
   if ((size_t)T * B * (size_t)(4 * H) * 4 >= (1ull << 32) || r2_lstm_bwd_tag_ring_bytes(B, H) < 0 ||
       T - t0 >= 65535) return -4;
   const int xmap = MB <= 8 && nwg <= 32;
@@ -1306,7 +1312,7 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
   int taken = 0, nh = 0;
   if (hg_dva || n_gw > 0 || gx_on) {
     // helpers: every block of the 8 x 32 grid outside the recurrence's groups
-    if (!xmap || nwg > 32 || T - t0 > PT_ITER_MAX) return -6;
+    if (!xmap || nwg > 32 || T - t0 > PT_ITER_MAX || g_num_cus < 256) return -6;
     nh = 8 * 32 - MB * nwg;
     int nw = 0, nx = 0;
     if (n_gw < 0 || n_gw > 3) return -7;

@@ -90,6 +90,8 @@ class LearnerConfig:
     # "shifted": R2D2 paper form -- one online and one target chain over T+n frames;
     #            Q(s_{t+n}) is read at offset +n of the same chain.
     target_mode: str = "shifted"
+    # "fp32": the reference's precision (fp32 weights/activations/state; MFMA products as three
+    # bf16 passes over hi/lo splits, csrc/split.h) | "bf16": bf16 operands, fp32 accumulate
     compute_dtype: str = "bf16"
     lstm_impl: str = "persistent"     # persistent (one launch per sequence) | step (launch per t)
     # persistent forward hand-off: "tagged" (8-byte {h pair, tag} granules polled directly, 16-row
@@ -188,7 +190,10 @@ def apply_override(cfg: R2D2Config, dotted: str, value: Any) -> None:
 
 
 def _reference() -> R2D2Config:
-    return R2D2Config(name="reference")
+    c = R2D2Config(name="reference")
+    # the reference's 3-chain target structure (learner.py:71-93) with Q7 fixed
+    c.learner.target_mode = "fixed"
+    return c
 
 
 def _cartpole() -> R2D2Config:
@@ -222,7 +227,7 @@ def _atari57() -> R2D2Config:
                             eta=0.9, alpha=0.9, beta=0.6, stored_state="pre", n_subrings=256)
     c.learner = LearnerConfig(batch_size=64, gamma=0.997, optimizer="rmsprop_centered",
                               value_rescale=True, target_update_interval=2500,
-                              target_mode="shifted")
+                              target_mode="fixed")
     c.actor = ActorConfig(n_actors=1, envs_per_actor=256)
     return c
 

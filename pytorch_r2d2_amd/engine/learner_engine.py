@@ -83,6 +83,14 @@ def addmm_f32(bias: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> torch.Ten
     return torch.mm(a, b).float() + bias
 
 
+def device_cus(device) -> int:
+    """Multiprocessor (CU) count of ``device`` (256 on a whole MI355X; 256 for CPU tensors)."""
+    d = torch.device(device)
+    if d.type != "cuda":
+        return 256
+    return int(torch.cuda.get_device_properties(d).multi_processor_count)
+
+
 def torso_bwd_grid(n_frames: int, reserve_cus: int = 0, n_cus: int = 256) -> int:
     """Workgroups of the fused conv backward (one per CU, grid-stride over frames).
 
@@ -120,10 +128,21 @@ class LearnerEngine:
             raise NotImplementedError("LSTM kernels support hidden in {64,128,256,512}")
         self.layout = L = ParamLayout(m, e)
         d = self.device
+        # compute units of THIS device (never assume 256: a partitioned MI355X exposes fewer); the
+        # persistent kernels need their whole grid co-resident, one workgroup per CU
+        self.n_cus = device_cus(d)
+        if d.type == "cuda":
+            kernels().r2_set_num_cus(self.n_cus)
         if init_module is None:
             torch.manual_seed(cfg.seed)
             init_module = QNet("cpu", m, e)
         self.master = L.from_module(init_module, d)
+        if world > 1 and process_group is not None:
+            # data-parallel ranks must start from identical weights: rank 0's are broadcast
+            # (each rank seeds its own replay / env streams, never the model)
+            import torch.distributed as dist
+            src = dist.get_global_rank(process_group, 0) if hasattr(dist, "get_global_rank") else 0
+            dist.broadcast(self.master, src=src, group=process_group)
         self.target = self.master.clone()
         self.grad = torch.zeros_like(self.master)
         self.opt_a = torch.zeros_like(self.master)
@@ -230,7 +249,7 @@ class LearnerEngine:
         # never lazily: the step must be capturable without warm-up)
         if self.fused_torso:
             n_slab = int(kernels().r2_torso_bwd_slab_floats())
-            self._tb_grid = torso_bwd_grid(Ll * B, self._comm_reserve())
+            self._tb_grid = torso_bwd_grid(Ll * B, self._comm_reserve(), self.n_cus)
             self._tb_slab = z(self._tb_grid * n_slab)
             dst, scale = L.torso_grad_map()
             self._tb_dst, self._tb_scale = dst.to(d), scale.to(d)
@@ -367,6 +386,7 @@ class LearnerEngine:
         H = self.layout.H
         groups = 2 * ((self.B + 31) // 32)
         if (k < 2 or self.mode != "shifted" or lc.lstm_impl != "persistent" or not self.fused_torso
+                or self.n_cus != 256
                 or not self.use_gemm or self.device.type != "cuda" or groups > 8):
             return None
         Tc = self.Tc
@@ -468,7 +488,7 @@ class LearnerEngine:
                     self._torso_job(pt, rows[self.t_lo_tg * B:], self.X_tg)]
             jobs = [j for j in jobs if j[1] > 0]
             self._tjobs = np.asarray(jobs, dtype=np.int64)          # kept alive for capture
-            check(k.r2_torso_fwd_multi(ptr(rp.frames), self._tjobs.ctypes.data, len(jobs), 256,
+            check(k.r2_torso_fwd_multi(ptr(rp.frames), self._tjobs.ctypes.data, len(jobs), self.n_cus,
                                        0, 0, s), "torso_fwd_multi")
         else:   # library convs: one call per net over all its frames (bigger, fewer launches)
             torso_forward_library(rp.frames, rows, L, self.master, self.cfg.env, self.cfg.model,
@@ -842,19 +862,33 @@ class LearnerEngine:
         self._update()
         self.replay.step_end()
 
-    def step_eager(self):
+    def step_eager(self, timer=None):
+        """One step without the graph.  ``timer``: optional utils.profiling.PhaseTimer -- every
+        phase is bracketed by HIP events and a roctx range (bench.py --profile-phases)."""
+        import contextlib
         L = self.layout
-        self._seg_core()
+        ph = timer.phase if timer is not None else (lambda name: contextlib.nullcontext())
+        with ph("forward+td"):
+            self._forward_loss()
+        with ph("backward_core"):
+            self._backward_core()
         if self.world > 1:   # core bucket all-reduce overlaps the conv backward
             self._sync().start(0, L.torso_offset)
-        self._seg_torso()
+        with ph("backward_torso"):
+            self._seg_torso()
         if self.world > 1:   # torso bucket all-reduce overlaps the priority tail
             self._sync().start(L.torso_offset, L.padded)
-            self._seg_prio()
-            self._sync().finish()
-            self._seg_update()
+            with ph("priorities"):
+                self._seg_prio()
+            with ph("allreduce_wait"):
+                self._sync().finish()
+            with ph("update"):
+                self._seg_update()
         else:
-            self._seg_tail()
+            with ph("update"):
+                self._update()
+            with ph("priorities"):
+                self._priorities()
         self.steps_done += 1
 
     def capture(self, warmup: int = 2):
@@ -904,7 +938,12 @@ class LearnerEngine:
     def loss_value(self) -> float:
         return float(self.loss.item())
 
+    def error_word(self) -> int:
+        """The persistent kernels' error word (non-zero: a bounded hand-off spin timed out, so the
+        step's recurrent state is garbage).  One D2H read."""
+        return int(self.err.item())
+
     def check_errors(self) -> None:
         """Raise if a persistent kernel's bounded spin timed out (hand-off failure)."""
-        if int(self.err.item()) != 0:
+        if self.error_word() != 0:
             raise RuntimeError("persistent LSTM kernel reported a hand-off timeout")

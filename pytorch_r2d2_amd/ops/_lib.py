@@ -27,6 +27,8 @@ F = ctypes.c_float
 
 _SIGS = {
     "r2_abi_version": [],
+    "r2_set_num_cus": [I],
+    "r2_get_num_cus": [],
     "r2_lstm_fwd": [P, I, I, I, I, I, P],
     "r2_lstm_bwd": [P, P, P, P, P, P, P, P, P, I, I, I, I, P],
     "r2_torso_fwd": [P, P, I, P, P, P, P, P, P, P, P, P, I, P],
