@@ -3,6 +3,7 @@
 // the operand conventions (k-major / mn-major operands, LDS-DMA staging with source swizzles).
 #pragma once
 #include "common.h"
+#include "split.h"
 
 namespace gm {
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
@@ -24,7 +25,25 @@ struct GemmProb {
   int a_kmajor, b_kmajor, c_f32, accumulate;
   float alpha;
   int tiles_n, tile_base;  // tiles along N; first linear tile index of this problem
+  // split precision (split.h): lo planes of A / B (null = operand exact in bf16) and of C (null =
+  // C is fp32 or plain bf16).  The K loop runs npass passes over K: (A_lo,B) (A,B_lo) (A,B) with
+  // both split, (A_lo,B) (A,B) or (A,B_lo) (A,B) with one.
+  const bf16* A_lo;
+  const bf16* B_lo;
+  bf16* C_lo;
+  int npass, pad_;
 };
+
+// descriptor words per problem (ops/gemm.py Gemm.desc)
+#define GEMM_DESC 20
+
+__device__ __forceinline__ const bf16* gp_a(const GemmProb& P, int pass) {
+  return (pass == 0 && P.A_lo) ? P.A_lo : P.A;
+}
+__device__ __forceinline__ const bf16* gp_b(const GemmProb& P, int pass) {
+  if (!P.B_lo) return P.B;
+  return pass == (P.A_lo ? 1 : 0) ? P.B_lo : P.B;
+}
 
 struct GemmArgs {
   GemmProb p[gm::MAXP];
@@ -108,6 +127,8 @@ __device__ __forceinline__ void g2_epilogue(const GemmProb& P, int m0, int n0, i
         if (P.c_f32) {
           float* c = (float*)P.C + o;
           *c = P.accumulate ? *c + v : v;
+        } else if (P.C_lo) {
+          sp_split(v, ((bf16*)P.C)[o], P.C_lo[o]);
         } else {
           bf16* c = (bf16*)P.C + o;
           *c = (bf16)(P.accumulate ? (float)*c + v : v);
@@ -161,6 +182,12 @@ __device__ __forceinline__ void g2_epilogue_lds(const GemmProb& P, int m0, int n
           f32x4 w = {v[0], v[1], v[2], v[3]};
           if (P.accumulate) w += *c;
           *c = w;
+        } else if (P.C_lo) {
+          bf16x4 hi, lo;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { hi[e] = (bf16)v[e]; lo[e] = sp_lo(v[e]); }
+          *(bf16x4*)((bf16*)P.C + o) = hi;
+          *(bf16x4*)(P.C_lo + o) = lo;
         } else {
           bf16x4* c = (bf16x4*)((bf16*)P.C + o);
           if (P.accumulate) {
@@ -178,6 +205,8 @@ __device__ __forceinline__ void g2_epilogue_lds(const GemmProb& P, int m0, int n
           if (f32) {
             float* c = (float*)P.C + o + e;
             *c = P.accumulate ? *c + v[e] : v[e];
+          } else if (P.C_lo) {
+            sp_split(v[e], ((bf16*)P.C)[o + e], P.C_lo[o + e]);
           } else {
             bf16* c = (bf16*)P.C + o + e;
             *c = (bf16)(P.accumulate ? (float)*c + v[e] : v[e]);
@@ -203,12 +232,14 @@ __device__ __forceinline__ void g2_tile_acc(const GemmProb& P, int tm, int tn, u
   const int m0 = tm * BM, n0 = tn * BN;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
   const int nk = kt1 - kt0;
+  const int nkp = P.K / BK;           // K tiles per pass (kt counts over npass * nkp)
   auto stage = [&](int i) {
     const int kt = desc ? kt1 - 1 - i : kt0 + i;
     ready(kt);
+    const int pass = kt / nkp, kk = kt - pass * nkp;
     uint8_t* st = lds + (i & 1) * (2 * TILE_B);
-    g2_stage<AK, AUX>(P.A, P.lda, m0, P.M, kt * BK, st, wave, lane);
-    g2_stage<BK_, AUX>(P.B, P.ldb, n0, P.N, kt * BK, st + TILE_B, wave, lane);
+    g2_stage<AK, AUX>(gp_a(P, pass), P.lda, m0, P.M, kk * BK, st, wave, lane);
+    g2_stage<BK_, AUX>(gp_b(P, pass), P.ldb, n0, P.N, kk * BK, st + TILE_B, wave, lane);
   };
   if (nk <= 0) return;
   stage(0);
@@ -243,7 +274,7 @@ __device__ __forceinline__ void g2_tile(const GemmProb& P, int tm, int tn, uint8
                                         Ready ready) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   f32x16 acc[2][2] = {};
-  g2_tile_acc<AK, BK_, AUX>(P, tm, tn, lds, 0, P.K / g2::BK, desc, ready, acc);
+  g2_tile_acc<AK, BK_, AUX>(P, tm, tn, lds, 0, P.K / g2::BK * P.npass, desc, ready, acc);
   g2_epilogue(P, tm * g2::BM, tn * g2::BN, (wave >> 1) * 64, (wave & 1) * 64, lane, acc);
 }
 
@@ -260,6 +291,10 @@ static inline int gemm_parse_desc(const int64_t* d, GemmProb& p) {
   float al;
   __builtin_memcpy(&al, &ab, 4);
   p.alpha = al;
+  p.A_lo = (const bf16*)d[16]; p.B_lo = (const bf16*)d[17]; p.C_lo = (bf16*)d[18];
+  p.npass = 1 + (p.A_lo != nullptr) + (p.B_lo != nullptr);
+  p.pad_ = 0;
+  if (p.C_lo && (p.c_f32 || p.accumulate)) return -12;   // split output: plain store only
   if (p.M < 1 || p.N < 1 || p.K < 8 || p.K % 8) return -2;
   if (!p.b_kmajor && (p.N % 8)) return -3;
   if (!p.a_kmajor && (p.M % 8)) return -3;

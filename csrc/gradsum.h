@@ -18,9 +18,12 @@ struct HeadGradArgs {
   float* gw2;         // (1+A, HD): row 0 = val.2.weight, rows 1.. = adv.2.weight
   float* gb2;         // (1+A): val.2.bias, adv.2.bias
   float* gb1;         // (2HD): val.0.bias, adv.0.bias
-  float* ws;          // partials: (CB, RS, 64, NV)
-  unsigned* ticket;   // (CB), 0 between launches
+  float* ws;          // partials: (NP, CB, RS, 64, NV)
+  unsigned* ticket;   // (NP, CB), 0 between launches
   int N, A, HD, RS;
+  int NP;             // passes over the advantage rows (7 per pass: A <= 7 -> 1, Seaquest 18 -> 3)
+  const float* zr32;  // split precision: zr fp32 (replaces zr)
+  const bf16* dz_lo;  // split precision: lo plane of dz
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t gs_rsrc(const void* p) {
@@ -83,9 +86,11 @@ __device__ __forceinline__ void gs_gather(const float* ws_cb, int RS, int c, flo
   }
 }
 
-// One (column block cb, row split rs) work item, run by a whole workgroup of >= 256 threads:
-// threads >= 256 only take part in the barriers (the BPTT kernel's helper workgroups have 320).
-__device__ __forceinline__ void head_grads_body(const HeadGradArgs& a, int cb, int rs) {
+// One (column block cb, row split rs, advantage pass p) work item, run by a whole workgroup of
+// >= 256 threads: threads >= 256 only take part in the barriers (the BPTT kernel's helper
+// workgroups have 320).  Pass p covers advantage rows [7p, 7p + 7); the value row, the bias sums
+// and the dva column sums belong to pass 0.
+__device__ __forceinline__ void head_grads_body(const HeadGradArgs& a, int cb, int rs, int p = 0) {
   __shared__ float red[4][64][gs::NV];
   __shared__ int flag;
   const int tid = threadIdx.x, c = tid & 63, rg = min(tid >> 6, 3);
@@ -101,15 +106,18 @@ __device__ __forceinline__ void head_grads_body(const HeadGradArgs& a, int cb, i
   // rows r0+rg, +4, ...: loads of U rows issued together, then accumulated in row order
   constexpr int U = 5;
   for (int rb = r0 + rg; act && rb < r1; rb += 4 * U) {
-    float z[U], d[U], dvv[U][gs::MAXW];
+    float z[U], d[U], dvv[U][gs::MAXW], dsl[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int r = min(rb + 4 * u, r1 - 1);
       const float* dv = a.dva + (size_t)r * W;
-      z[u] = vcol ? (float)a.zr[(size_t)r * C + col] : 0.f;
-      d[u] = vcol ? (float)a.dz[(size_t)r * C + col] : 0.f;
+      const size_t o = (size_t)r * C + col;
+      z[u] = vcol ? (a.zr32 ? a.zr32[o] : (float)a.zr[o]) : 0.f;
+      d[u] = vcol ? (float)a.dz[o] + (a.dz_lo ? (float)a.dz_lo[o] : 0.f) : 0.f;
+      dvv[u][0] = dv[0];
 #pragma unroll
-      for (int i = 0; i < gs::MAXW; ++i) dvv[u][i] = i < W ? dv[i] : 0.f;
+      for (int i = 1; i < gs::MAXW; ++i) dvv[u][i] = 7 * p + i < W ? dv[7 * p + i] : 0.f;
+      dsl[u] = (cb == 0 && p == 0 && c < W) ? dv[c] : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -121,10 +129,7 @@ __device__ __forceinline__ void head_grads_body(const HeadGradArgs& a, int cb, i
 #pragma unroll
         for (int i = 0; i < gs::MAXW - 1; ++i) w[i] += dvv[u][1 + i] * z[u];
       }
-      float dsel = 0.f;
-#pragma unroll
-      for (int i = 0; i < gs::MAXW; ++i) dsel = (c == i) ? dvv[u][i] : dsel;
-      if (cb == 0) dvs += dsel;
+      dvs += dsl[u];
     }
   }
   if (act) {
@@ -139,19 +144,21 @@ __device__ __forceinline__ void head_grads_body(const HeadGradArgs& a, int cb, i
 #pragma unroll
   for (int i = 0; i < gs::NV; ++i)
     v[i] = tid < 64 ? ((red[0][c][i] + red[1][c][i]) + (red[2][c][i] + red[3][c][i])) : 0.f;
-  float* blk = a.ws + ((size_t)cb * a.RS + rs) * 64 * gs::NV;
-  if (!gs_publish(blk, v, a.ticket + cb, a.RS, &flag)) return;
+  const int CB = (2 * a.HD + 63) / 64, pcb = p * CB + cb;
+  float* blk = a.ws + ((size_t)pcb * a.RS + rs) * 64 * gs::NV;
+  if (!gs_publish(blk, v, a.ticket + pcb, a.RS, &flag)) return;
   if (tid >= 64) return;
   float t[gs::NV];
-  gs_gather(a.ws + (size_t)cb * a.RS * 64 * gs::NV, a.RS, c, t);
+  gs_gather(a.ws + (size_t)pcb * a.RS * 64 * gs::NV, a.RS, c, t);
   if (vcol) {
-    a.gb1[col] = t[0];
+    if (p == 0) a.gb1[col] = t[0];
     if (!adv) {
-      a.gw2[col] = t[2];
+      if (p == 0) a.gw2[col] = t[2];
     } else {
-      for (int i = 0; i < a.A; ++i) a.gw2[(size_t)(1 + i) * a.HD + (col - a.HD)] = t[2 + i];
+      for (int i = 0; i < 7 && 7 * p + i < a.A; ++i)
+        a.gw2[(size_t)(1 + 7 * p + i) * a.HD + (col - a.HD)] = t[2 + i];
     }
   }
-  if (cb == 0 && c < W) a.gb2[c] = t[1];
-  if (c == 0) __hip_atomic_store(a.ticket + cb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (p == 0 && cb == 0 && c < W) a.gb2[c] = t[1];
+  if (c == 0) __hip_atomic_store(a.ticket + pcb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

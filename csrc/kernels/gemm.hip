@@ -168,15 +168,16 @@ __global__ __launch_bounds__(256) void gemm2_kernel(const GemmArgs args) {
   if (m0 >= P.M) return;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  const int nk = P.K / BK;
+  const int nkp = P.K / BK, nk = nkp * P.npass;   // K tiles per pass x passes (split.h)
+  auto stage2 = [&](int kt, int st) {
+    const int pass = kt / nkp, kk = kt - pass * nkp;
+    g2_stage<AK>(gp_a(P, pass), P.lda, m0, P.M, kk * BK, lds[st][0], wave, lane);
+    g2_stage<BK_>(gp_b(P, pass), P.ldb, n0, P.N, kk * BK, lds[st][1], wave, lane);
+  };
 
   f32x16 acc[2][2] = {};
-  g2_stage<AK>(P.A, P.lda, m0, P.M, 0, lds[0][0], wave, lane);
-  g2_stage<BK_>(P.B, P.ldb, n0, P.N, 0, lds[0][1], wave, lane);
-  if (nk > 1) {
-    g2_stage<AK>(P.A, P.lda, m0, P.M, BK, lds[1][0], wave, lane);
-    g2_stage<BK_>(P.B, P.ldb, n0, P.N, BK, lds[1][1], wave, lane);
-  }
+  stage2(0, 0);
+  if (nk > 1) stage2(1, 1);
   for (int kt = 0; kt < nk; ++kt) {
     const int st = kt & 1;
     // tile kt has landed once at most the next tile's 2*GPW DMA ops remain outstanding
@@ -200,10 +201,7 @@ __global__ __launch_bounds__(256) void gemm2_kernel(const GemmArgs args) {
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();          // every wave is done reading stage st
-    if (kt + 2 < nk) {
-      g2_stage<AK>(P.A, P.lda, m0, P.M, (kt + 2) * BK, lds[st][0], wave, lane);
-      g2_stage<BK_>(P.B, P.ldb, n0, P.N, (kt + 2) * BK, lds[st][1], wave, lane);
-    }
+    if (kt + 2 < nk) stage2(kt + 2, st);
   }
 
   g2_epilogue_lds(P, m0, n0, wm, wn, lane, acc, &lds[0][0][0]);
@@ -319,7 +317,7 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmArgs args, int tot
   if (m0 >= P.M) return;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wr = wave >> 2, wc = wave & 3;
-  const int nk = (P.K + BK - 1) / BK;
+  const int nkp = (P.K + BK - 1) / BK, nk = nkp * P.npass;   // K tiles per pass x passes
 
   f32x4 acc[8][TNW];
 #pragma unroll
@@ -330,8 +328,9 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmArgs args, int tot
     int oz;
     asm volatile("v_mov_b32 %0, 0" : "=v"(oz));
     uint8_t* st = lds4 + (kt % NS) * STB;
-    g4_stage<AK, BM, BK>(P.A, P.lda, m0, P.M, kt * BK, P.K, st, wave, lane, oz);
-    g4_stage<BK_, BN, BK>(P.B, P.ldb, n0, P.N, kt * BK, P.K, st + OPA, wave, lane, oz);
+    const int pass = kt / nkp, kk = kt - pass * nkp;
+    g4_stage<AK, BM, BK>(gp_a(P, pass), P.lda, m0, P.M, kk * BK, P.K, st, wave, lane, oz);
+    g4_stage<BK_, BN, BK>(gp_b(P, pass), P.ldb, n0, P.N, kk * BK, P.K, st + OPA, wave, lane, oz);
   };
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
@@ -402,6 +401,12 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmArgs args, int tot
           f32x4 w = {v[0], v[1], v[2], v[3]};
           if (P.accumulate) w += *c;
           *c = w;
+        } else if (P.C_lo) {
+          bf16x4 hi, lo;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) { hi[e] = (bf16)v[e]; lo[e] = sp_lo(v[e]); }
+          *(bf16x4*)((bf16*)P.C + o) = hi;
+          *(bf16x4*)(P.C_lo + o) = lo;
         } else {
           bf16x4* c = (bf16x4*)((bf16*)P.C + o);
           if (P.accumulate) {
@@ -419,6 +424,8 @@ __global__ __launch_bounds__(512) void gemm4_kernel(const GemmArgs args, int tot
           if (f32) {
             float* c = (float*)P.C + o + e;
             *c = P.accumulate ? *c + v[e] : v[e];
+          } else if (P.C_lo) {
+            sp_split(v[e], ((bf16*)P.C)[o + e], P.C_lo[o + e]);
           } else {
             bf16* c = (bf16*)P.C + o + e;
             *c = (bf16)(P.accumulate ? (float)*c + v[e] : v[e]);
@@ -578,7 +585,7 @@ __global__ __launch_bounds__(256) void gemm_group_kernel(const GroupArgs a) {
   const int item = bid - a.item_base[pi];
   const int tile = item / S, ks = item % S;
   const int tm = tile / P.tiles_n, tn = tile % P.tiles_n;
-  const int nk = P.K / g2::BK, per = (nk + S - 1) / S;
+  const int nk = P.K / g2::BK * P.npass, per = (nk + S - 1) / S;
   const int kt0 = min(nk, ks * per), kt1 = min(nk, kt0 + per);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   f32x16 acc[2][2] = {};
@@ -633,7 +640,7 @@ extern "C" long long r2_gemm_group_ws_bytes(const int64_t* descs, const int* spl
   long long b = 0;
   for (int i = 0; i < np; ++i) {
     GemmProb p;
-    if (gemm_parse_desc(descs + 16 * i, p)) return -1;
+    if (gemm_parse_desc(descs + GEMM_DESC * i, p)) return -1;
     if (split[i] > 1) b += (long long)p.tiles_n * ((p.M + 127) / 128) * split[i] * 65536;
   }
   return b;
@@ -647,7 +654,7 @@ extern "C" int r2_gemm_group(const int64_t* descs, const int* split, int np, flo
   int items = 0, slabs = 0, tks = 0;
   for (int i = 0; i < np; ++i) {
     GemmProb& p = a.p[i];
-    const int rc = gemm_parse_desc(descs + 16 * i, p);
+    const int rc = gemm_parse_desc(descs + GEMM_DESC * i, p);
     if (rc) return rc;
     if (p.K % 64 || p.b_kmajor || (!p.a_kmajor && p.M % 8)) return -6;
     const int tiles = p.tiles_n * ((p.M + 127) / 128);
@@ -671,30 +678,19 @@ extern "C" int r2_gemm_group(const int64_t* descs, const int* split, int np, flo
 static int g_gemm_version = 2;   // 1 = force the register-staged kernel (tests / A-B)
 extern "C" int r2_gemm_set_version(int v) { g_gemm_version = v; return 0; }
 
-// descs: nprob x 16 int64 {A, B, C, bias, crow, M, N, K, lda, ldb, ldc, a_kmajor, b_kmajor,
-// c_f32, accumulate, alpha_bits}.  All problems of one call must share (a_kmajor, b_kmajor).
+// descs: nprob x GEMM_DESC int64 {A, B, C, bias, crow, M, N, K, lda, ldb, ldc, a_kmajor, b_kmajor,
+// c_f32, accumulate, alpha_bits, A_lo, B_lo, C_lo, 0} (lo planes: split.h; null = not split).  All problems of one call must share (a_kmajor, b_kmajor).
 extern "C" int r2_gemm(const int64_t* descs, int nprob, void* stream) {
   if (nprob < 1 || nprob > gm::MAXP) return -1;
   GemmArgs a;
   a.nprob = nprob;
   int tiles = 0, ak = -1, bk = -1;
+  bool any_split = false;
   for (int i = 0; i < nprob; ++i) {
-    const int64_t* d = descs + 16 * i;
     GemmProb& p = a.p[i];
-    p.A = (const bf16*)d[0]; p.B = (const bf16*)d[1]; p.C = (void*)d[2];
-    p.bias = (const float*)d[3]; p.crow = (const int*)d[4];
-    p.M = (int)d[5]; p.N = (int)d[6]; p.K = (int)d[7];
-    p.lda = (int)d[8]; p.ldb = (int)d[9]; p.ldc = (int)d[10];
-    p.a_kmajor = (int)d[11]; p.b_kmajor = (int)d[12]; p.c_f32 = (int)d[13];
-    p.accumulate = (int)d[14];
-    const uint32_t ab = (uint32_t)d[15];
-    p.alpha = __builtin_bit_cast(float, ab);
-    if (p.M < 1 || p.N < 1 || p.K < 8 || p.K % 8) return -2;
-    if (!p.b_kmajor && (p.N % 8)) return -3;   // mn-major loads move 8 columns at a time
-    if (!p.a_kmajor && (p.M % 8)) return -3;
-    if ((!p.a_kmajor && (p.lda % 8)) || (!p.b_kmajor && (p.ldb % 8)) ||
-        (p.a_kmajor && (p.lda % 8)) || (p.b_kmajor && (p.ldb % 8)))
-      return -4;  // 16-byte aligned rows
+    const int rc = gemm_parse_desc(descs + GEMM_DESC * i, p);
+    if (rc) return rc;
+    any_split = any_split || p.npass > 1 || p.C_lo;
     if (ak < 0) { ak = p.a_kmajor; bk = p.b_kmajor; }
     if (ak != p.a_kmajor || bk != p.b_kmajor) return -5;
     p.tiles_n = (p.N + gm::BN - 1) / gm::BN;
@@ -708,6 +704,18 @@ extern "C" int r2_gemm(const int64_t* descs, int nprob, void* stream) {
   for (int i = 0; i < nprob; ++i) {
     k8 = k8 && a.p[i].K % 8 == 0;
     t256 += (long)((a.p[i].M + 255) / 256) * ((a.p[i].N + 255) / 256);
+  }
+  if (any_split) {
+    // split precision runs on the LDS-DMA kernels only (the pass loop lives in their staging)
+    if (k8 && (t256 >= 150 || g_gemm_version == 5)) return g4_launch<256, 64, 2>(a, ak, bk, s);
+    for (int i = 0; i < nprob; ++i)
+      if (a.p[i].K % g2::BK) return g4_launch<128, 64, 3>(a, ak, bk, s);
+    if (ak && bk) hipLaunchKernelGGL((gemm2_kernel<true, true>), dim3(tiles), dim3(g2::NT), 0, s, a);
+    else if (ak) hipLaunchKernelGGL((gemm2_kernel<true, false>), dim3(tiles), dim3(g2::NT), 0, s, a);
+    else if (bk) hipLaunchKernelGGL((gemm2_kernel<false, true>), dim3(tiles), dim3(g2::NT), 0, s, a);
+    else hipLaunchKernelGGL((gemm2_kernel<false, false>), dim3(tiles), dim3(g2::NT), 0, s, a);
+    R2_CHECK_LAUNCH();
+    return 0;
   }
   if (g_gemm_version >= 5 && g_gemm_version <= 8 && k8) {   // forced 8-wave variants (tests / micro-benchmarks)
     switch (g_gemm_version) {

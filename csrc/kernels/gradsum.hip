@@ -18,7 +18,7 @@
 #include "../gradsum.h"
 
 __global__ __launch_bounds__(256) void head_grads_kernel(const HeadGradArgs a) {
-  head_grads_body(a, blockIdx.x, blockIdx.y);
+  head_grads_body(a, blockIdx.x, blockIdx.y % a.RS, blockIdx.y / a.RS);
 }
 
 struct ColsumArgs {
@@ -70,16 +70,31 @@ __global__ __launch_bounds__(256) void colsum_kernel(const ColsumArgs a) {
 // ws: >= r2_gradsum_ws_floats() floats; ticket: >= 64 unsigned, zero at first use.
 extern "C" int r2_gradsum_ws_floats() { return 64 * 32 * 64 * gs::NV; }
 
+static int head_grads_launch(HeadGradArgs a, void* stream) {
+  if (a.HD % 64 != 0 || a.N < 1 || a.A < 1 || a.A > 63) return -1;
+  const int CB = (2 * a.HD + 63) / 64;
+  a.RS = 32;
+  a.NP = (a.A + 6) / 7;
+  if (CB * a.NP > 32 || CB * a.RS * a.NP > 64 * 32) return -2;   // tickets / workspace
+  hipLaunchKernelGGL(head_grads_kernel, dim3(CB, a.RS * a.NP), dim3(gs::NT), 0, (hipStream_t)stream, a);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
+// tickets: >= 32 unsigned, zero at first use (the engine's colsum uses the next 32)
 extern "C" int r2_head_grads(const float* dva, const bf16* zr, const bf16* dz, float* gw2,
                              float* gb2, float* gb1, int N, int A, int HD, float* ws,
                              unsigned* ticket, void* stream) {
-  if (A + 1 > gs::MAXW || HD % 64 != 0 || N < 1) return -1;
-  const int CB = (2 * HD + 63) / 64, RS = 32;
-  if (CB > 64) return -2;
-  HeadGradArgs a{dva, zr, dz, gw2, gb2, gb1, ws, ticket, N, A, HD, RS};
-  hipLaunchKernelGGL(head_grads_kernel, dim3(CB, RS), dim3(gs::NT), 0, (hipStream_t)stream, a);
-  R2_CHECK_LAUNCH();
-  return 0;
+  HeadGradArgs a{dva, zr, dz, gw2, gb2, gb1, ws, ticket, N, A, HD, 32, 1, nullptr, nullptr};
+  return head_grads_launch(a, stream);
+}
+
+// split precision: zr fp32, dz as hi / lo planes
+extern "C" int r2_head_grads_sp(const float* dva, const float* zr32, const bf16* dz,
+                                const bf16* dz_lo, float* gw2, float* gb2, float* gb1, int N, int A,
+                                int HD, float* ws, unsigned* ticket, void* stream) {
+  HeadGradArgs a{dva, nullptr, dz, gw2, gb2, gb1, ws, ticket, N, A, HD, 32, 1, zr32, dz_lo};
+  return head_grads_launch(a, stream);
 }
 
 extern "C" int r2_colsum_bf16(const bf16* X, int N, int C, const int* perm, float* out,

@@ -10,6 +10,7 @@
 // One wave per row; each lane owns 4 of the 256 value-branch and 4 of the 256 advantage-branch
 // features (HD = 256).
 #include "../common.h"
+#include "../split.h"
 
 #define HEAD_MAXA 32
 
@@ -19,8 +20,9 @@
 // Up to 3 heads (online / target / online-on-next) per launch: wave w takes row w - row0[j] of
 // the head j whose row range holds it.
 #define HEAD_MAXJ 3
+// ZT = bf16 (bf16 mode) or float (split-precision mode: z from an fp32-output GEMM, zr fp32)
 struct DuelJob {
-  const bf16* z; const float* b1; const float* w2; const float* b2; float* q; bf16* zr;
+  const void* z; const float* b1; const float* w2; const float* b2; float* q; void* zr;
   int N, row0;
 };
 struct DuelArgs {
@@ -28,7 +30,7 @@ struct DuelArgs {
   int nj, A;
 };
 
-template <int HD>
+template <int HD, typename ZT>
 __global__ __launch_bounds__(256) void dueling_fwd_kernel(const DuelArgs args) {
   constexpr int PER = HD / 64;
   const int lane = threadIdx.x & 63;
@@ -40,13 +42,13 @@ __global__ __launch_bounds__(256) void dueling_fwd_kernel(const DuelArgs args) {
   const DuelJob& J = args.j[ji];
   const int row = w - J.row0, N = J.N, A = args.A;
   if (row >= N) return;
-  const bf16* __restrict__ z = J.z;
+  const ZT* __restrict__ z = (const ZT*)J.z;
   const float* __restrict__ b1 = J.b1;
   const float* __restrict__ w2 = J.w2;
   const float* __restrict__ b2 = J.b2;
   float* __restrict__ q = J.q;
-  bf16* __restrict__ zr = J.zr;
-  const bf16* zrow = z + (size_t)row * 2 * HD;
+  ZT* __restrict__ zr = (ZT*)J.zr;
+  const ZT* zrow = z + (size_t)row * 2 * HD;
   float hv[PER], ha[PER];
 #pragma unroll
   for (int e = 0; e < PER; ++e) {
@@ -55,11 +57,11 @@ __global__ __launch_bounds__(256) void dueling_fwd_kernel(const DuelArgs args) {
     ha[e] = fmaxf((float)zrow[HD + c] + b1[HD + c], 0.f);
   }
   if (zr) {
-    bf16* o = zr + (size_t)row * 2 * HD;
+    ZT* o = zr + (size_t)row * 2 * HD;
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
-      o[lane * PER + e] = (bf16)hv[e];
-      o[HD + lane * PER + e] = (bf16)ha[e];
+      o[lane * PER + e] = (ZT)hv[e];
+      o[HD + lane * PER + e] = (ZT)ha[e];
     }
   }
   float v = 0.f;
@@ -108,8 +110,8 @@ __global__ __launch_bounds__(256) void dueling_bwd_kernel(
   }
 }
 
-// jobs: nj x 7 int64 {z, b1, w2, b2, q, zr, N}
-extern "C" int r2_dueling_fwd_multi(const int64_t* jobs, int nj, int A, int HD, void* stream) {
+template <typename ZT>
+static int dueling_fwd_launch(const int64_t* jobs, int nj, int A, int HD, void* stream) {
   if (nj < 1 || nj > HEAD_MAXJ) return -3;
   if (A < 1 || A > HEAD_MAXA) return -1;
   DuelArgs a{};
@@ -119,8 +121,8 @@ extern "C" int r2_dueling_fwd_multi(const int64_t* jobs, int nj, int A, int HD, 
   for (int i = 0; i < nj; ++i) {
     const int64_t* p = jobs + 7 * i;
     DuelJob& J = a.j[i];
-    J.z = (const bf16*)p[0]; J.b1 = (const float*)p[1]; J.w2 = (const float*)p[2];
-    J.b2 = (const float*)p[3]; J.q = (float*)p[4]; J.zr = (bf16*)p[5];
+    J.z = (const void*)p[0]; J.b1 = (const float*)p[1]; J.w2 = (const float*)p[2];
+    J.b2 = (const float*)p[3]; J.q = (float*)p[4]; J.zr = (void*)p[5];
     J.N = (int)(p[6] > 0 ? p[6] : 0); J.row0 = rows;
     rows += J.N;
   }
@@ -129,14 +131,23 @@ extern "C" int r2_dueling_fwd_multi(const int64_t* jobs, int nj, int A, int HD, 
   dim3 grid((rows + 3) / 4), block(256);
   hipStream_t s = (hipStream_t)stream;
   switch (HD) {
-    case 64: hipLaunchKernelGGL(dueling_fwd_kernel<64>, grid, block, 0, s, a); break;
-    case 128: hipLaunchKernelGGL(dueling_fwd_kernel<128>, grid, block, 0, s, a); break;
-    case 256: hipLaunchKernelGGL(dueling_fwd_kernel<256>, grid, block, 0, s, a); break;
-    case 512: hipLaunchKernelGGL(dueling_fwd_kernel<512>, grid, block, 0, s, a); break;
+    case 64: hipLaunchKernelGGL((dueling_fwd_kernel<64, ZT>), grid, block, 0, s, a); break;
+    case 128: hipLaunchKernelGGL((dueling_fwd_kernel<128, ZT>), grid, block, 0, s, a); break;
+    case 256: hipLaunchKernelGGL((dueling_fwd_kernel<256, ZT>), grid, block, 0, s, a); break;
+    case 512: hipLaunchKernelGGL((dueling_fwd_kernel<512, ZT>), grid, block, 0, s, a); break;
     default: return -2;
   }
   R2_CHECK_LAUNCH();
   return 0;
+}
+
+// jobs: nj x 7 int64 {z, b1, w2, b2, q, zr, N}; z / zr bf16
+extern "C" int r2_dueling_fwd_multi(const int64_t* jobs, int nj, int A, int HD, void* stream) {
+  return dueling_fwd_launch<bf16>(jobs, nj, A, HD, stream);
+}
+// split precision: z / zr fp32
+extern "C" int r2_dueling_fwd_multi_f32(const int64_t* jobs, int nj, int A, int HD, void* stream) {
+  return dueling_fwd_launch<float>(jobs, nj, A, HD, stream);
 }
 
 extern "C" int r2_dueling_fwd(const bf16* z, const float* b1, const float* w2, const float* b2,

@@ -30,6 +30,7 @@
 // All (H/16)*ceil(B/32)*chains workgroups (<= 256 for the supported shapes) must be
 // co-resident: 256 threads, <= 40 KB LDS, one per CU is enough.
 #include "../common.h"
+#include "../split.h"
 #include "../gradsum.h"
 #include "../gemm_tile.h"
 
@@ -73,6 +74,9 @@ struct PChain {
   float* gates;        // optional (T - save_from, B, G)
   int save_from;
   int pad_;
+  // split precision (split.h; the *_sp launchers): lo planes of W_hh and of h_seq; h0 is fp32
+  const bf16* whh_lo;
+  bf16* h_seq_lo;
 };
 
 struct PFwdArgs {
@@ -626,25 +630,31 @@ __device__ __forceinline__ uint32_t pt_pack_bf16x2(float a, float b) {
   return __builtin_bit_cast(uint32_t, v);
 }
 
-template <int H>
+// SP (split precision, split.h): h_t travels as {fp32 h[u], tag} granules (one unit each), the
+// consumer splits it into hi / lo LDS images, W_hh hi / lo fragments stay in VGPRs and every
+// product is 3 MFMA passes; h_seq is written as hi / lo planes.
+template <int H, bool SP>
 __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
   constexpr int G = 4 * H;
   constexpr int NWG = H / PL_UNITS;
   constexpr int KS = H / 32;                  // 16x16x32 k-steps
   constexpr int HS = H + 8;                   // bf16 stride of a staged h row (conflict-free b128)
-  constexpr int GR = H / 2;                   // granules per row
-  constexpr int CPR = H / 4;                  // 16-B chunks (2 granules) per row
+  constexpr int UG = SP ? 1 : 2;              // hidden units per granule
+  constexpr int GR = H / UG;                  // granules per row
+  constexpr int CPR = GR / 2;                 // 16-B chunks (2 granules) per row
   constexpr int CH = PT_ROWS * CPR / 256;     // chunks per compute thread
   constexpr int XS = 20;                      // fp32 stride of a gate-exchange row
   static_assert(CH >= 1 && PT_ROWS * CPR % 256 == 0, "H");
   // LDS: staged h (2 slots), wave-private gate exchange, x-projection ring (3 slots, filled by
   // the I/O wave), per-step outputs (2 slots, drained by the I/O wave)
   __shared__ __attribute__((aligned(16))) bf16 hin[2][PT_ROWS * HS];
+  __shared__ __attribute__((aligned(16))) bf16 hinl[2][SP ? PT_ROWS * HS : 8];   // lo image (SP)
   __shared__ __attribute__((aligned(16))) float xch[4][PT_ROWS * XS];
   __shared__ __attribute__((aligned(1024))) float xl[3][PT_ROWS * PL_GCOLS];
   __shared__ __attribute__((aligned(16))) float oc[2][PT_ROWS * PL_UNITS];
   __shared__ __attribute__((aligned(16))) float oh32[2][PT_ROWS * PL_UNITS];
   __shared__ __attribute__((aligned(16))) bf16 ohs[2][PT_ROWS * PL_UNITS];
+  __shared__ __attribute__((aligned(16))) bf16 ohsl[2][SP ? PT_ROWS * PL_UNITS : 8];
   __shared__ __attribute__((aligned(16))) float og[2][PT_ROWS * PL_GCOLS];
   __shared__ int flag;
   int g, j;
@@ -695,6 +705,11 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
         if (b < B)
           *(u32x4*)(cd.h_seq + ((size_t)t * B + b) * H + j * PL_UNITS + 8 * hf) =
               *(const u32x4*)(ohs[s] + r * PL_UNITS + 8 * hf);
+      } else if (SP) {
+        const int r = (lane - 32) >> 1, hf = lane & 1, b = mb * PT_ROWS + r;
+        if (b < B)
+          *(u32x4*)(cd.h_seq_lo + ((size_t)t * B + b) * H + j * PL_UNITS + 8 * hf) =
+              *(const u32x4*)(ohsl[s] + r * PL_UNITS + 8 * hf);
       }
       if (save_any && t >= cd.save_from) {
 #pragma unroll
@@ -737,13 +752,17 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
   };
   // resident W_hh fragments: wave column c (0..15) = gate c>>2 of unit 4*wave + (c&3), i.e.
   // packed row 16*(c>>2) + 4*wave + (c&3) of this workgroup's 64
-  bf16x8 wf[KS];
+  bf16x8 wf[KS], wfl[SP ? KS : 1];
   {
     const int c = lane & 15;
     const int n = 16 * (c >> 2) + 4 * wave + (c & 3);
-    const bf16* brow = cd.whh + ((size_t)j * PL_GCOLS + n) * H + 8 * (lane >> 4);
+    const size_t o = ((size_t)j * PL_GCOLS + n) * H + 8 * (lane >> 4);
 #pragma unroll
-    for (int s = 0; s < KS; ++s) wf[s] = *(const bf16x8*)(brow + 32 * s);
+    for (int s = 0; s < KS; ++s) wf[s] = *(const bf16x8*)(cd.whh + o + 32 * s);
+    if constexpr (SP) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) wfl[s] = *(const bf16x8*)(cd.whh_lo + o + 32 * s);
+    }
   }
   // pointwise ownership: lane = (row prow, unit 4*wave + pu); c lives in a register
   const int prow = lane >> 2, pu = lane & 3;
@@ -762,12 +781,19 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
   for (int t = 0; t < T; ++t) {
     PT_TRACE(0);
     bf16* hb = hin[t & 1];
+    bf16* hbl = hinl[t & 1];
     if (t == 0) {
 #pragma unroll
       for (int i = 0; i < CH; ++i) {
         const int c = tid + 256 * i, r = c / CPR, cc = c % CPR;
         const int b = min(mb * PT_ROWS + r, B - 1);
-        *(u32x2*)(hb + r * HS + 4 * cc) = *(const u32x2*)(cd.h0 + (size_t)b * H + 4 * cc);
+        if constexpr (SP) {   // fp32 h0, units 2cc, 2cc+1
+          const float2 x = *(const float2*)((const float*)cd.h0 + (size_t)b * H + 2 * cc);
+          *(uint32_t*)(hb + r * HS + 2 * cc) = pt_pack_bf16x2(x.x, x.y);
+          *(uint32_t*)(hbl + r * HS + 2 * cc) = pt_pack_bf16x2(sp_lo(x.x), sp_lo(x.y));
+        } else {
+          *(u32x2*)(hb + r * HS + 4 * cc) = *(const u32x2*)((const bf16*)cd.h0 + (size_t)b * H + 4 * cc);
+        }
       }
     } else {
       // h_{t-1}: poll the granules themselves (all CH loads in flight, then re-poll stragglers)
@@ -805,16 +831,26 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
 #pragma unroll
       for (int i = 0; i < CH; ++i) {
         const int c = tid + 256 * i, r = c / CPR, cc = c % CPR;
-        *(u32x2*)(hb + r * HS + 4 * cc) = u32x2{v[i][0], v[i][2]};
+        if constexpr (SP) {   // {h[2cc], tag, h[2cc+1], tag} -> hi / lo images
+          const f32x4 f = __builtin_bit_cast(f32x4, v[i]);
+          *(uint32_t*)(hb + r * HS + 2 * cc) = pt_pack_bf16x2(f[0], f[2]);
+          *(uint32_t*)(hbl + r * HS + 2 * cc) = pt_pack_bf16x2(sp_lo(f[0]), sp_lo(f[2]));
+        } else {
+          *(u32x2*)(hb + r * HS + 4 * cc) = u32x2{v[i][0], v[i][2]};
+        }
       }
     }
     PT_TRACE(5);
     lds_sync();                                   // barrier t (with the I/O wave)
     PT_TRACE(1);
     // gates of this wave's 16 columns for the 16 rows: acc[e] = C[4(l>>4)+e][l&15]
-    bf16x8 av[KS];
+    bf16x8 av[KS], avl[SP ? KS : 1];
 #pragma unroll
     for (int s = 0; s < KS; ++s) av[s] = *(const bf16x8*)(hb + (lane & 15) * HS + 32 * s + 8 * (lane >> 4));
+    if constexpr (SP) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) avl[s] = *(const bf16x8*)(hbl + (lane & 15) * HS + 32 * s + 8 * (lane >> 4));
+    }
     float xv[4];
     {
       const float* xr = xl[t % 3] + prow * PL_GCOLS + ul;
@@ -824,8 +860,13 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KS; s += 2) {
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[s], wf[s], acc0, 0, 0, 0);
-      if (s + 1 < KS) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[s + 1], wf[s + 1], acc1, 0, 0, 0);
+      if constexpr (SP) {
+        acc0 = mfma16_x3(av[s], avl[s], wf[s], wfl[s], acc0);
+        if (s + 1 < KS) acc1 = mfma16_x3(av[s + 1], avl[s + 1], wf[s + 1], wfl[s + 1], acc1);
+      } else {
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[s], wf[s], acc0, 0, 0, 0);
+        if (s + 1 < KS) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[s + 1], wf[s + 1], acc1, 0, 0, 0);
+      }
     }
     // wave-private exchange: column c = (gate c>>2, unit c&3) -> xch[row][unit][gate]
     {
@@ -843,15 +884,25 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
     const float so = sigmoidf_(gp[3] + xv[3]);
     creg = sf * creg + si * tg;
     const float hv = so * tanhf_(creg);
-    const float hp = __shfl_xor(hv, 1, 64);      // partner unit of the granule
     PT_TRACE(3);
-    // publish h_t: even units store {h[u], h[u+1], tag} (one 8-byte store per granule)
-    const uint32_t hpair = pt_pack_bf16x2(hv, hp);
-    if (pv && (pu & 1) == 0) {
-      const u32x2 gr = {hpair, (ep << 16) | (unsigned)(t + 1)};
-      const uint32_t off = goff(t & 1, prow, u >> 1);
-      if (fast) __builtin_amdgcn_raw_buffer_store_b64(gr, rrs, off, 0, 0);   // stays in the XCD's L2
-      else __builtin_amdgcn_raw_buffer_store_b64(gr, rrs, off, 0, 16);       // sc1 write-through
+    if constexpr (SP) {
+      // publish h_t: every unit stores {fp32 h[u], tag}
+      if (pv) {
+        const u32x2 gr = {__float_as_uint(hv), (ep << 16) | (unsigned)(t + 1)};
+        const uint32_t off = goff(t & 1, prow, u);
+        if (fast) __builtin_amdgcn_raw_buffer_store_b64(gr, rrs, off, 0, 0);
+        else __builtin_amdgcn_raw_buffer_store_b64(gr, rrs, off, 0, 16);
+      }
+    } else {
+      const float hp = __shfl_xor(hv, 1, 64);      // partner unit of the granule
+      // publish h_t: even units store {h[u], h[u+1], tag} (one 8-byte store per granule)
+      const uint32_t hpair = pt_pack_bf16x2(hv, hp);
+      if (pv && (pu & 1) == 0) {
+        const u32x2 gr = {hpair, (ep << 16) | (unsigned)(t + 1)};
+        const uint32_t off = goff(t & 1, prow, u >> 1);
+        if (fast) __builtin_amdgcn_raw_buffer_store_b64(gr, rrs, off, 0, 0);   // stays in the XCD's L2
+        else __builtin_amdgcn_raw_buffer_store_b64(gr, rrs, off, 0, 16);       // sc1 write-through
+      }
     }
     PT_TRACE(4);
     // outputs of step t for the I/O wave (LDS; drained after barrier t + 1)
@@ -860,6 +911,7 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
       oc[s][prow * PL_UNITS + ul] = creg;
       oh32[s][prow * PL_UNITS + ul] = hv;
       ohs[s][prow * PL_UNITS + ul] = (bf16)hv;
+      if constexpr (SP) ohsl[s][prow * PL_UNITS + ul] = sp_lo(hv);
       if (save_any) {
         float* gq = og[s] + prow * PL_GCOLS + ul;
         gq[0] = si;
@@ -877,16 +929,19 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
 }
 
 extern "C" int r2_lstm_tag_ring_bytes(int n_chains, int B, int H) {
-  const long long n = (long long)n_chains * 2 * ((B + PT_ROWS - 1) / PT_ROWS) * PT_ROWS * (H / 2) * 8;
+  // one unit per 8-byte granule (the split-precision layout; the bf16 kernel uses half of it)
+  const long long n = (long long)n_chains * 2 * ((B + PT_ROWS - 1) / PT_ROWS) * PT_ROWS * H * 8;
   return n < (1ll << 31) ? (int)n : -1;
 }
 
 // Same chain layout / ctr as r2_lstm_fwd_persist; ring: r2_lstm_tag_ring_bytes bytes, any content.
 // Returns -3 when the grid cannot be co-resident at one workgroup per CU (caller falls back).
-extern "C" int r2_lstm_fwd_tag(const int64_t* chain_ptrs, int n_chains, int B, int T, int H,
-                               unsigned* ctr, unsigned* err, void* ring, void* stream) {
+template <bool SP>
+static int lstm_fwd_tag_launch(const int64_t* chain_ptrs, int words, int n_chains, int B, int T,
+                               int H, unsigned* ctr, unsigned* err, void* ring, void* stream) {
   if (n_chains < 1 || n_chains > PL_MAX_CHAINS || B < 1) return -1;
   if (H != 64 && H != 128 && H != 256 && H != 512) return -2;
+  if (SP && H > 256) return -2;    // W_hh hi/lo + h hi/lo fragments: 4*H/8 VGPRs
   const int MB = (B + PT_ROWS - 1) / PT_ROWS, nwg = H / PL_UNITS;
   const int groups = n_chains * MB;
   if (groups * nwg > g_num_cus || groups > PL_MAX_GROUPS) return -3;
@@ -894,30 +949,46 @@ extern "C" int r2_lstm_fwd_tag(const int64_t* chain_ptrs, int n_chains, int B, i
       r2_lstm_tag_ring_bytes(n_chains, B, H) < 0) return -4;
   PTArgs args;
   for (int c = 0; c < n_chains; ++c) {
-    const int64_t* p = chain_ptrs + 9 * c;
+    const int64_t* p = chain_ptrs + words * c;
     PChain& ch = args.ch[c];
     ch.xproj = (const float*)p[0]; ch.whh = (const bf16*)p[1]; ch.h0 = (const bf16*)p[2];
     ch.c0 = (const float*)p[3]; ch.h_seq = (bf16*)p[4]; ch.c_seq = (float*)p[5];
     ch.h32 = (float*)p[6]; ch.gates = (float*)p[7]; ch.save_from = (int)p[8]; ch.pad_ = 0;
+    ch.whh_lo = words > 9 ? (const bf16*)p[9] : nullptr;
+    ch.h_seq_lo = words > 10 ? (bf16*)p[10] : nullptr;
+    if (SP && (!ch.whh_lo || !ch.h_seq_lo)) return -5;
   }
   args.B = B; args.T = T; args.ctr = ctr; args.err = err; args.dbg = g_pl_dbg; args.ring = ring;
   args.MB = MB; args.groups = groups; args.xcd_map = groups <= 8 && nwg <= 32;
   args.force_slow = g_pl_slow;
   hipStream_t s = (hipStream_t)stream;   // counters are left zeroed by the previous launch
   dim3 grid(args.xcd_map ? 8 * nwg : groups * nwg), block(320);   // 4 compute waves + 1 I/O wave
-  const void* fn = H == 64 ? (const void*)lstm_fwd_tag_kernel<64>
-                 : H == 128 ? (const void*)lstm_fwd_tag_kernel<128>
-                 : H == 256 ? (const void*)lstm_fwd_tag_kernel<256>
-                            : (const void*)lstm_fwd_tag_kernel<512>;
+  const void* fn = H == 64 ? (const void*)lstm_fwd_tag_kernel<64, SP>
+                 : H == 128 ? (const void*)lstm_fwd_tag_kernel<128, SP>
+                 : H == 256 ? (const void*)lstm_fwd_tag_kernel<256, SP>
+                            : (const void*)lstm_fwd_tag_kernel<(SP ? 256 : 512), SP>;
   hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, PL_LDS_RESERVE);
   switch (H) {
-    case 64: hipLaunchKernelGGL(lstm_fwd_tag_kernel<64>, grid, block, PL_LDS_RESERVE, s, args); break;
-    case 128: hipLaunchKernelGGL(lstm_fwd_tag_kernel<128>, grid, block, PL_LDS_RESERVE, s, args); break;
-    case 256: hipLaunchKernelGGL(lstm_fwd_tag_kernel<256>, grid, block, PL_LDS_RESERVE, s, args); break;
-    default: hipLaunchKernelGGL(lstm_fwd_tag_kernel<512>, grid, block, PL_LDS_RESERVE, s, args); break;
+    case 64: hipLaunchKernelGGL((lstm_fwd_tag_kernel<64, SP>), grid, block, PL_LDS_RESERVE, s, args); break;
+    case 128: hipLaunchKernelGGL((lstm_fwd_tag_kernel<128, SP>), grid, block, PL_LDS_RESERVE, s, args); break;
+    case 256: hipLaunchKernelGGL((lstm_fwd_tag_kernel<256, SP>), grid, block, PL_LDS_RESERVE, s, args); break;
+    default: hipLaunchKernelGGL((lstm_fwd_tag_kernel<(SP ? 256 : 512), SP>), grid, block, PL_LDS_RESERVE, s, args); break;
   }
   R2_CHECK_LAUNCH();
   return 0;
+}
+
+// Same chain layout / ctr as r2_lstm_fwd_persist; ring: r2_lstm_tag_ring_bytes bytes, any content.
+// Returns -3 when the grid cannot be co-resident at one workgroup per CU (caller falls back).
+extern "C" int r2_lstm_fwd_tag(const int64_t* chain_ptrs, int n_chains, int B, int T, int H,
+                               unsigned* ctr, unsigned* err, void* ring, void* stream) {
+  return lstm_fwd_tag_launch<false>(chain_ptrs, 9, n_chains, B, T, H, ctr, err, ring, stream);
+}
+
+// Split precision: chain_ptrs n_chains x 11 int64 (the 9 above, h0 fp32, + whh_lo, h_seq_lo).
+extern "C" int r2_lstm_fwd_tag_sp(const int64_t* chain_ptrs, int n_chains, int B, int T, int H,
+                                  unsigned* ctr, unsigned* err, void* ring, void* stream) {
+  return lstm_fwd_tag_launch<true>(chain_ptrs, 11, n_chains, B, T, H, ctr, err, ring, stream);
 }
 
 // ============================================================================================
@@ -962,9 +1033,14 @@ struct PTBArgs {
   GemmProb gw[3];
   int n_gw, gw_wait, gx_on, n_wtiles;
   GemmProb gx;
+  // split precision (the _sp launcher): W_hh^T lo plane; dgates lo plane out
+  const bf16* whhT_lo;
+  bf16* dgates_lo;
 };
 
-template <int H>
+// SP (split precision, split.h): W_hh^T hi / lo fragments, dgates tile kept as hi / lo images for
+// the partial-dh MFMAs (3 passes) and written as hi / lo planes for the weight-gradient GEMMs.
+template <int H, bool SP>
 __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   constexpr int G = 4 * H;
   constexpr int NWG = H / PL_UNITS;
@@ -973,6 +1049,7 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   constexpr int SRCH = NWG / 2;               // sources per consumer half
   static_assert(NTW >= 1 && NWG % 2 == 0, "H");
   __shared__ __attribute__((aligned(16))) bf16 dgl[2][PT_ROWS * DS];
+  __shared__ __attribute__((aligned(16))) bf16 dgll[2][SP ? PT_ROWS * DS : 8];
   __shared__ __attribute__((aligned(16))) float red[2][PT_ROWS * PL_UNITS];
   __shared__ __attribute__((aligned(1024))) float gl[3][PT_ROWS * PL_GCOLS];  // saved gates
   __shared__ __attribute__((aligned(1024))) float cl[3][PT_ROWS * PL_UNITS];  // c_t
@@ -1023,7 +1100,8 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
       const int hx = h - a.n_wtiles, nx = nh - a.n_wtiles;
       if (a.hg_on) {
         const int cbn = (2 * a.hg.HD + 63) / 64;
-        for (int it = hx; it < cbn * a.hg.RS; it += nx) head_grads_body(a.hg, it % cbn, it / cbn);
+        for (int it = hx; it < cbn * a.hg.RS * a.hg.NP; it += nx)
+          head_grads_body(a.hg, it % cbn, (it / cbn) % a.hg.RS, it / (cbn * a.hg.RS));
       }
       if (a.gx_on) {
         // dX tiles, latest rows (first produced) first
@@ -1081,15 +1159,18 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
     };
     const int nload = a.dh_ext ? 7 : 6;     // DMA instructions per io_load
     const __amdgpu_buffer_rsrc_t drs = pl_rsrc(a.dgates, (uint32_t)((size_t)K * B * G * 2));
+    const __amdgpu_buffer_rsrc_t drsl = pl_rsrc(SP ? a.dgates_lo : a.dgates, (uint32_t)((size_t)K * B * G * 2));
     auto io_store = [&](int k) {      // dgates tile of iteration k (write-through: helpers read it)
       const int tl = T - 1 - k - t0, s = k & 1;
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int c = lane + 64 * q, r = c >> 3, ch = c & 7, b = mb * PT_ROWS + r;
-        if (b < B)
-          __builtin_amdgcn_raw_buffer_store_b128(*(const u32x4*)(dgl[s] + r * DS + 8 * ch), drs,
-                                                 (uint32_t)((((size_t)tl * B + b) * G + j * PL_GCOLS + 8 * ch) * 2),
-                                                 0, 16);
+        if (b < B) {
+          const uint32_t off = (uint32_t)((((size_t)tl * B + b) * G + j * PL_GCOLS + 8 * ch) * 2);
+          __builtin_amdgcn_raw_buffer_store_b128(*(const u32x4*)(dgl[s] + r * DS + 8 * ch), drs, off, 0, 16);
+          if constexpr (SP)
+            __builtin_amdgcn_raw_buffer_store_b128(*(const u32x4*)(dgll[s] + r * DS + 8 * ch), drsl, off, 0, 16);
+        }
       }
     };
     auto io_progress = [&](int k) {    // after this wave's dgates stores of iteration k completed
@@ -1122,13 +1203,17 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
 
   // ================= compute waves 0..3
   // W_hh^T fragments: N tile q of this wave = units (H/4)*wave + 16*q + (l&15); B[k][n] = Whh_pk[j][k][n]
-  bf16x8 wt[NTW][2];
+  bf16x8 wt[NTW][2], wtl[SP ? NTW : 1][2];
 #pragma unroll
   for (int q = 0; q < NTW; ++q) {
     const int n = (H / 4) * wave + 16 * q + (lane & 15);
-    const bf16* brow = a.whhT + ((size_t)j * H + n) * PL_GCOLS + 8 * (lane >> 4);
+    const size_t o = ((size_t)j * H + n) * PL_GCOLS + 8 * (lane >> 4);
 #pragma unroll
-    for (int s = 0; s < 2; ++s) wt[q][s] = *(const bf16x8*)(brow + 32 * s);
+    for (int s = 0; s < 2; ++s) wt[q][s] = *(const bf16x8*)(a.whhT + o + 32 * s);
+    if constexpr (SP) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) wtl[q][s] = *(const bf16x8*)(a.whhT_lo + o + 32 * s);
+    }
   }
   const int prow = lane >> 2, pu = lane & 3;
   const int ul = 4 * wave + pu;
@@ -1204,18 +1289,36 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
     drow[16] = (bf16)dgf;
     drow[32] = (bf16)dgg;
     drow[48] = (bf16)dgo;
+    if constexpr (SP) {
+      bf16* drl = dgll[k & 1] + prow * DS + ul;
+      drl[0] = sp_lo(dgi);
+      drl[16] = sp_lo(dgf);
+      drl[32] = sp_lo(dgg);
+      drl[48] = sp_lo(dgo);
+    }
     lds_sync();                           // barrier B_k: dgates tile complete
     if (t > t0) {
       // ---- partial dh_{t-1}[r][n] = sum_k dg[r][k] Whh_pk[j][k][n], published as granules
       const bf16* arow = dgl[k & 1] + (lane & 15) * DS + 8 * (lane >> 4);
       const bf16x8 a0 = *(const bf16x8*)arow, a1 = *(const bf16x8*)(arow + 32);
+      bf16x8 a0l, a1l;
+      if constexpr (SP) {
+        const bf16* arl = dgll[k & 1] + (lane & 15) * DS + 8 * (lane >> 4);
+        a0l = *(const bf16x8*)arl;
+        a1l = *(const bf16x8*)(arl + 32);
+      }
       const unsigned tag = (ep << 16) | (unsigned)(k + 1);
       const int slot = k & 1;
 #pragma unroll
       for (int q = 0; q < NTW; ++q) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, wt[q][0], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, wt[q][1], acc, 0, 0, 0);
+        if constexpr (SP) {
+          acc = mfma16_x3(a0, a0l, wt[q][0], wtl[q][0], acc);
+          acc = mfma16_x3(a1, a1l, wt[q][1], wtl[q][1], acc);
+        } else {
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, wt[q][0], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, wt[q][1], acc, 0, 0, 0);
+        }
         const int n = (H / 4) * wave + 16 * q + (lane & 15);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1269,6 +1372,10 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   }
 }
 
+// lo planes handed from r2_lstm_bwd_tag_sp to the shared launcher body (host-side, per call)
+static const bf16* g_bwd_whhT_lo = nullptr;
+static bf16* g_bwd_dgates_lo = nullptr;
+
 extern "C" int r2_lstm_bwd_tag_ring_bytes(int B, int H) {
   const long long n = 2ll * (H / PL_UNITS) * ((B + PT_ROWS - 1) / PT_ROWS) * PT_ROWS * H * 8;
   return n < (1ll << 31) ? (int)n : -1;
@@ -1306,7 +1413,7 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
   PTBArgs args{dh_ext, gates, c_seq, c0, whhT, dgates, ring, B, T, t0, ctr, err, MB, xmap, g_pl_slow, 0,
                bias_ws, perm, db1, db2,
                HeadGradArgs{hg_dva, hg_zr, hg_dz, hg_gw2, hg_gb2, hg_gb1, hg_ws, hg_ticket, hg_N, hg_A,
-                            hg_HD, 8},
+                            hg_HD, 8, (hg_A + 6) / 7, nullptr, nullptr},
                0};
   args.n_gw = 0; args.gw_wait = 0; args.gx_on = 0; args.n_wtiles = 0;
   int taken = 0, nh = 0;
@@ -1318,18 +1425,20 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
     if (n_gw < 0 || n_gw > 3) return -7;
     for (int i = 0; i < n_gw + (gx_on ? 1 : 0); ++i) {
       GemmProb& p = i < n_gw ? args.gw[i] : args.gx;
-      const int rc = gemm_parse_desc(gemm_descs + 16 * i, p);
+      const int rc = gemm_parse_desc(gemm_descs + GEMM_DESC * i, p);
       if (rc) return -20 + rc;
+      if (p.npass > 1 || p.C_lo) return -11;   // helpers: bf16 operands only
       if (p.K % 64) return -8;
       const bool is_x = i == n_gw;
       if (is_x ? (!p.a_kmajor || p.b_kmajor) : (p.a_kmajor || p.b_kmajor)) return -9;
       const int tiles = p.tiles_n * ((p.M + 127) / 128);
       if (is_x) nx = tiles; else nw += tiles;
     }
-    const int hgi = hg_dva ? ((2 * hg_HD + 63) / 64) * 8 : 0;
+    const int hgi = hg_dva ? ((2 * hg_HD + 63) / 64) * 8 * ((hg_A + 6) / 7) : 0;
     if (nw >= nh || (hgi + nx > 0 && nh - nw < 16)) return -10;   // too few helpers
     if (hg_dva) {
-      if (hg_A + 1 > gs::MAXW || hg_N < 1 || hg_HD % 64) return -5;
+      if (hg_A > 63 || ((2 * hg_HD + 63) / 64) * ((hg_A + 6) / 7) > 32 || hg_N < 1 || hg_HD % 64)
+        return -5;
       args.hg_on = 1;
       taken |= 1;
     }
@@ -1337,21 +1446,53 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
     if (n_gw) taken |= 2;
     if (gx_on) taken |= 4;
   }
+  args.whhT_lo = g_bwd_whhT_lo;
+  args.dgates_lo = g_bwd_dgates_lo;
+  const bool sp = g_bwd_whhT_lo != nullptr;
+  if (sp && (!args.dgates_lo || H > 256 || taken)) return -11;
   hipStream_t s = (hipStream_t)stream;   // counters are left zeroed by the previous launch
   dim3 grid(nh ? 256 : (xmap ? 8 * nwg : MB * nwg)), block(320);
-  const void* fn = H == 64 ? (const void*)lstm_bwd_tag_kernel<64>
-                 : H == 128 ? (const void*)lstm_bwd_tag_kernel<128>
-                 : H == 256 ? (const void*)lstm_bwd_tag_kernel<256>
-                            : (const void*)lstm_bwd_tag_kernel<512>;
-  hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, PL_LDS_RESERVE);
-  switch (H) {
-    case 64: hipLaunchKernelGGL(lstm_bwd_tag_kernel<64>, grid, block, PL_LDS_RESERVE, s, args); break;
-    case 128: hipLaunchKernelGGL(lstm_bwd_tag_kernel<128>, grid, block, PL_LDS_RESERVE, s, args); break;
-    case 256: hipLaunchKernelGGL(lstm_bwd_tag_kernel<256>, grid, block, PL_LDS_RESERVE, s, args); break;
-    default: hipLaunchKernelGGL(lstm_bwd_tag_kernel<512>, grid, block, PL_LDS_RESERVE, s, args); break;
+#define R2_BWD_LAUNCH(HH, SPP)                                                                 \
+  do {                                                                                         \
+    hipFuncSetAttribute((const void*)lstm_bwd_tag_kernel<HH, SPP>,                             \
+                        hipFuncAttributeMaxDynamicSharedMemorySize, PL_LDS_RESERVE);           \
+    hipLaunchKernelGGL((lstm_bwd_tag_kernel<HH, SPP>), grid, block, PL_LDS_RESERVE, s, args);  \
+  } while (0)
+  if (sp) {
+    switch (H) {
+      case 64: R2_BWD_LAUNCH(64, true); break;
+      case 128: R2_BWD_LAUNCH(128, true); break;
+      default: R2_BWD_LAUNCH(256, true); break;
+    }
+  } else {
+    switch (H) {
+      case 64: R2_BWD_LAUNCH(64, false); break;
+      case 128: R2_BWD_LAUNCH(128, false); break;
+      case 256: R2_BWD_LAUNCH(256, false); break;
+      default: R2_BWD_LAUNCH(512, false); break;
+    }
   }
+#undef R2_BWD_LAUNCH
   R2_CHECK_LAUNCH();
   return taken;   // bit 0: head grads, 1: weight grads, 2: dX done here
+}
+
+// Split precision: the same launch with W_hh^T given as hi / lo planes and dgates written as hi /
+// lo planes (no helper jobs).  Same argument list as r2_lstm_bwd_tag plus the two lo pointers.
+extern "C" int r2_lstm_bwd_tag_sp(const float* dh_ext, const float* gates, const float* c_seq,
+                                  const float* c0, const bf16* whhT, const bf16* whhT_lo,
+                                  bf16* dgates, bf16* dgates_lo, int B, int T, int t0, int H,
+                                  unsigned* ctr, unsigned* err, void* ring, float* bias_ws,
+                                  const int* perm, float* db1, float* db2, void* stream) {
+  if (!whhT_lo || !dgates_lo) return -5;
+  g_bwd_whhT_lo = whhT_lo;
+  g_bwd_dgates_lo = dgates_lo;
+  const int rc = r2_lstm_bwd_tag(dh_ext, gates, c_seq, c0, whhT, dgates, B, T, t0, H, ctr, err, ring,
+                                 bias_ws, perm, db1, db2, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                 nullptr, 0, 0, 0, nullptr, nullptr, nullptr, 0, 0, 0, stream);
+  g_bwd_whhT_lo = nullptr;
+  g_bwd_dgates_lo = nullptr;
+  return rc;
 }
 
 extern "C" int r2_lstm_persist_ctr_words() { return PT_CTR_WORDS; }

@@ -85,6 +85,18 @@ __global__ void pack_bf16_kernel(const float* __restrict__ src, const int* __res
     out[i] = (bf16)src[idx[i]];
 }
 
+// split precision (split.h): hi = bf16(x) at out[i], lo = bf16(x - hi) at out[i + lo_off]
+__global__ void pack_split_kernel(const float* __restrict__ src, const int* __restrict__ idx,
+                                  bf16* __restrict__ out, int64_t n, int64_t lo_off) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float x = src[idx[i]];
+    const bf16 h = (bf16)x;
+    out[i] = h;
+    out[i + lo_off] = (bf16)(x - (float)h);
+  }
+}
+
 __global__ void gather_f32_kernel(const float* __restrict__ src, const int* __restrict__ idx,
                                   float* __restrict__ out, int64_t n) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -142,6 +154,14 @@ extern "C" int r2_pack_bf16(const float* src, const int* idx, bf16* out, int64_t
   return 0;
 }
 
+extern "C" int r2_pack_split(const float* src, const int* idx, bf16* out, int64_t n,
+                             int64_t lo_off, void* stream) {
+  hipLaunchKernelGGL(pack_split_kernel, dim3(grid_for(n, 2)), dim3(256), 0, (hipStream_t)stream,
+                     src, idx, out, n, lo_off);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int r2_gather_f32(const float* src, const int* idx, float* out, int64_t n, void* stream) {
   hipLaunchKernelGGL(gather_f32_kernel, dim3(grid_for(n, 2)), dim3(256), 0, (hipStream_t)stream,
                      src, idx, out, n);
@@ -168,7 +188,7 @@ __global__ void pack_step_kernel(const float* __restrict__ master, float* __rest
                                  const int* __restrict__ f_idx, float* __restrict__ f32,
                                  float* __restrict__ f32_t, int64_t n_f, int64_t o_bih, int64_t o_bhh,
                                  float* __restrict__ lstm_b, float* __restrict__ lstm_b_t, int64_t G,
-                                 const int64_t* __restrict__ step, int64_t interval) {
+                                 const int64_t* __restrict__ step, int64_t interval, int64_t lo_off) {
   const bool due = interval <= 1 || ((*step) + 1) % interval == 0;
   // work items: [target copy, 4 floats each (due only)] [bf pack, 4 elements each: one 16-B
   // index load, 4 gathers, one 8-B store] [bf tail] [f32 gather] [lstm bias]
@@ -191,14 +211,29 @@ __global__ void pack_step_kernel(const float* __restrict__ master, float* __rest
       v[3] = (bf16)master[ix.w];
       ((bf16x4*)bf)[j] = v;
       if (due) ((bf16x4*)bf_t)[j] = v;
+      if (lo_off) {   // split precision: lo plane (split.h)
+        bf16x4 l;
+        l[0] = (bf16)(master[ix.x] - (float)v[0]);
+        l[1] = (bf16)(master[ix.y] - (float)v[1]);
+        l[2] = (bf16)(master[ix.z] - (float)v[2]);
+        l[3] = (bf16)(master[ix.w] - (float)v[3]);
+        ((bf16x4*)(bf + lo_off))[j] = l;
+        if (due) ((bf16x4*)(bf_t + lo_off))[j] = l;
+      }
       continue;
     }
     j -= nb4;
     if (j < nbt) {
       j += nb4 << 2;
-      const bf16 v = (bf16)master[bf_idx[j]];
+      const float x = master[bf_idx[j]];
+      const bf16 v = (bf16)x;
       bf[j] = v;
       if (due) bf_t[j] = v;
+      if (lo_off) {
+        const bf16 l = (bf16)(x - (float)v);
+        bf[j + lo_off] = l;
+        if (due) bf_t[j + lo_off] = l;
+      }
       continue;
     }
     j -= nbt;
@@ -219,13 +254,13 @@ extern "C" int r2_pack_step(const float* master, float* target, int64_t n_master
                             bf16* bf, bf16* bf_t, int64_t n_bf, const int* f_idx, float* f32,
                             float* f32_t, int64_t n_f, int64_t o_bih, int64_t o_bhh, float* lstm_b,
                             float* lstm_b_t, int64_t G, const int64_t* step, int64_t interval,
-                            void* stream) {
+                            int64_t lo_off, void* stream) {
   if ((n_master & 3) || (((uintptr_t)master | (uintptr_t)target | (uintptr_t)bf_idx) & 15) ||
-      (((uintptr_t)bf | (uintptr_t)bf_t) & 7))
+      (((uintptr_t)bf | (uintptr_t)bf_t) & 7) || (lo_off & 3))
     return -1;   // vector paths: 16-B master / target / index rows, 8-B packs
   hipLaunchKernelGGL(pack_step_kernel, dim3(1024), dim3(256), 0, (hipStream_t)stream, master, target,
                      n_master, bf_idx, bf, bf_t, n_bf, f_idx, f32, f32_t, n_f, o_bih, o_bhh, lstm_b,
-                     lstm_b_t, G, step, interval);
+                     lstm_b_t, G, step, interval, lo_off);
   R2_CHECK_LAUNCH();
   return 0;
 }

@@ -105,6 +105,7 @@ struct SampleBatchArgs {
   float* c[3];
   int off[3];
   int B, Tn, cap_e, H, nstate;
+  int h_f32;      // split-precision learner: h out as fp32 (the h pointers are float*)
 };
 
 __global__ __launch_bounds__(256) void sample_batch_kernel(const SampleBatchArgs a) {
@@ -125,7 +126,8 @@ __global__ __launch_bounds__(256) void sample_batch_kernel(const SampleBatchArgs
   for (int j = 0; j < a.nstate; ++j) {
     const float* src = a.hs[j] + (size_t)ring_row_s(s, a.off[j], a.cap_e) * 2 * a.H;
     for (int k = tid; k < a.H; k += blockDim.x) {
-      a.h[j][(size_t)b * a.H + k] = (bf16)src[k];
+      if (a.h_f32) ((float*)a.h[j])[(size_t)b * a.H + k] = src[k];
+      else a.h[j][(size_t)b * a.H + k] = (bf16)src[k];
       a.c[j][(size_t)b * a.H + k] = src[a.H + k];
     }
   }
@@ -361,12 +363,11 @@ extern "C" int r2_tree_sample(const float* tree, const int64_t* offs, const int6
   return 0;
 }
 
-// hs/h/c: nstate pointers each (host arrays, int64); off: nstate row offsets
-extern "C" int r2_sample_batch(const float* tree, const int64_t* offs, const int64_t* sizes,
+static int sample_batch_launch(const float* tree, const int64_t* offs, const int64_t* sizes,
                                int levels, int B, uint64_t seed, const int64_t* step, int* starts,
                                float* probs, int* rows, int Tn, int cap_e, int H, int nstate,
                                const int64_t* hs, const int* off, const int64_t* h,
-                               const int64_t* c, void* stream) {
+                               const int64_t* c, int h_f32, void* stream) {
   if (levels < 2 || levels > TREE_MAX_LEVELS || nstate < 0 || nstate > 3 || B < 1) return -1;
   SampleBatchArgs a;
   a.tree = tree; a.g = make_geom(offs, sizes, levels); a.seed = seed; a.step = step;
@@ -377,10 +378,30 @@ extern "C" int r2_sample_batch(const float* tree, const int64_t* offs, const int
     a.c[j] = j < nstate ? (float*)c[j] : nullptr;
     a.off[j] = j < nstate ? off[j] : 0;
   }
-  a.B = B; a.Tn = Tn; a.cap_e = cap_e; a.H = H; a.nstate = nstate;
+  a.B = B; a.Tn = Tn; a.cap_e = cap_e; a.H = H; a.nstate = nstate; a.h_f32 = h_f32;
   hipLaunchKernelGGL(sample_batch_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, a);
   R2_CHECK_LAUNCH();
   return 0;
+}
+
+// hs/h/c: nstate pointers each (host arrays, int64); off: nstate row offsets; h bf16
+extern "C" int r2_sample_batch(const float* tree, const int64_t* offs, const int64_t* sizes,
+                               int levels, int B, uint64_t seed, const int64_t* step, int* starts,
+                               float* probs, int* rows, int Tn, int cap_e, int H, int nstate,
+                               const int64_t* hs, const int* off, const int64_t* h,
+                               const int64_t* c, void* stream) {
+  return sample_batch_launch(tree, offs, sizes, levels, B, seed, step, starts, probs, rows, Tn,
+                             cap_e, H, nstate, hs, off, h, c, 0, stream);
+}
+
+// the same with h written fp32 (split-precision learner)
+extern "C" int r2_sample_batch_f32h(const float* tree, const int64_t* offs, const int64_t* sizes,
+                                    int levels, int B, uint64_t seed, const int64_t* step,
+                                    int* starts, float* probs, int* rows, int Tn, int cap_e, int H,
+                                    int nstate, const int64_t* hs, const int* off,
+                                    const int64_t* h, const int64_t* c, void* stream) {
+  return sample_batch_launch(tree, offs, sizes, levels, B, seed, step, starts, probs, rows, Tn,
+                             cap_e, H, nstate, hs, off, h, c, 1, stream);
 }
 
 extern "C" int r2_tree_rebuild(float* tree, const int64_t* offs, const int64_t* sizes, int levels,

@@ -13,7 +13,9 @@
 // row priorities.  The loss is reduced deterministically: every workgroup publishes its partial
 // (sc1 store, drained), takes a ticket with an agent-scope atomic, and the last arriver sums the
 // partials in workgroup order with sc1 loads (MI355X_MICROARCH.md hand-off table, row 1).
+#include <type_traits>
 #include "../common.h"
+#include "../split.h"
 
 __device__ __forceinline__ float vr_h(float x, float eps) {
   return copysignf(sqrtf(fabsf(x) + 1.f) - 1.f, x) + eps * x;
@@ -149,13 +151,16 @@ extern "C" int r2_td_loss(const float* q_sa, const float* q_arg, const float* q_
 // workgroup sums the partials in a fixed order.
 struct TdDuelArgs {
   TdArgs td;
-  const bf16* zr;       // (Tl*B, 2*HD) relu'd hidden of the online head's learning rows
+  const void* zr;       // (Tl*B, 2*HD) relu'd hidden of the online head's learning rows (ZT)
   const float* w2;      // (1 + A, HD) second-layer weights [value row; advantage rows]
-  bf16* dz;             // (Tl*B, 2*HD) out
+  bf16* dz;             // (Tl*B, 2*HD) out (hi plane in split precision)
   float* dva;           // (Tl*B, 1 + A) out
+  bf16* dz_lo;          // split precision: lo plane of dz
 };
 
-template <int HD>
+// SP: zr fp32, dz written as hi / lo planes (split.h).  Actions beyond the MAXA register-resident
+// second-layer rows are read from memory inside the same loop (same order, same bits).
+template <int HD, bool SP>
 __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
   // 16 waves per workgroup: one arrival-ticket atomic per 16 transitions (a single counter's
   // agent-scope atomics serialise: 640 four-wave workgroups cost as much as the fusion saved)
@@ -177,10 +182,11 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
   const float qa = (valid && lane < a.A) ? a.q_arg[(size_t)i * a.A + lane] : NEG;
   const float qt = (valid && lane < a.A) ? a.q_tgt[(size_t)i * a.A + lane] : 0.f;
   const float qs = (valid && lane < a.A) ? a.q_sa[(size_t)i * a.A + lane] : 0.f;
-  bf16 zv[PER], za[PER];
+  typedef typename std::conditional<SP, float, bf16>::type ZT;
+  ZT zv[PER], za[PER];
   float w2v[PER], w2a[MAXA][PER];
   if (valid) {
-    const bf16* zrow = args.zr + (size_t)i * 2 * HD;
+    const ZT* zrow = (const ZT*)args.zr + (size_t)i * 2 * HD;
 #pragma unroll
     for (int e = 0; e < PER; ++e) { zv[e] = zrow[lane * PER + e]; za[e] = zrow[HD + lane * PER + e]; }
   }
@@ -247,7 +253,7 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
     if (lane == 0) dvr[0] = dv;
     if (lane < a.A) dvr[1 + lane] = ((lane == act) ? g : 0.f) - dmean;
     bf16* dzrow = args.dz + (size_t)i * 2 * HD;
-    bf16 ov[PER], oa[PER];
+    float ov[PER], oa[PER];
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
       const float gv = dv * w2v[e];
@@ -255,11 +261,21 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
 #pragma unroll
       for (int k = 0; k < MAXA; ++k)
         if (k < a.A) ga += (((k == act) ? g : 0.f) - dmean) * w2a[k][e];
-      ov[e] = (bf16)(((float)zv[e] > 0.f) ? gv : 0.f);
-      oa[e] = (bf16)(((float)za[e] > 0.f) ? ga : 0.f);
+      for (int k = MAXA; k < a.A; ++k)     // many-action heads (Seaquest 18, DMLab 15)
+        ga += (((k == act) ? g : 0.f) - dmean) * args.w2[(size_t)(1 + k) * HD + lane * PER + e];
+      ov[e] = ((float)zv[e] > 0.f) ? gv : 0.f;
+      oa[e] = ((float)za[e] > 0.f) ? ga : 0.f;
     }
 #pragma unroll
-    for (int e = 0; e < PER; ++e) { dzrow[lane * PER + e] = ov[e]; dzrow[HD + lane * PER + e] = oa[e]; }
+    for (int e = 0; e < PER; ++e) {
+      dzrow[lane * PER + e] = (bf16)ov[e];
+      dzrow[HD + lane * PER + e] = (bf16)oa[e];
+      if constexpr (SP) {
+        bf16* dzl = args.dz_lo + (size_t)i * 2 * HD;
+        dzl[lane * PER + e] = sp_lo(ov[e]);
+        dzl[HD + lane * PER + e] = sp_lo(oa[e]);
+      }
+    }
   }
   // ---- loss: wave partial (lane 0) -> workgroup partial -> last arriver, fixed order
   if (lane == 0) red[wave] = lsum;
@@ -290,30 +306,37 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
   }
 }
 
+template <bool SP>
+static int td_duel_launch(const TdDuelArgs& d, int HD, int grid, hipStream_t s) {
+  switch (HD) {
+    case 64: hipLaunchKernelGGL((td_duel_kernel<64, SP>), dim3(grid), dim3(1024), 0, s, d); break;
+    case 128: hipLaunchKernelGGL((td_duel_kernel<128, SP>), dim3(grid), dim3(1024), 0, s, d); break;
+    case 256: hipLaunchKernelGGL((td_duel_kernel<256, SP>), dim3(grid), dim3(1024), 0, s, d); break;
+    case 512: hipLaunchKernelGGL((td_duel_kernel<512, SP>), dim3(grid), dim3(1024), 0, s, d); break;
+    default: return -4;
+  }
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
+// zr: bf16 (dz_lo null) or fp32 (split precision: dz_lo = the lo plane of dz)
 extern "C" int r2_td_duel(const float* q_sa, const float* q_arg, const float* q_tgt,
                           const int* starts, const float* probs, const uint8_t* action,
                           const float* reward, const uint8_t* done, float* dq, float* loss,
                           float* td_abs, float* priority, float* is_w, const int* n_valid,
                           int Tl, int B, int A, int burn_in, int cap_e, float gamma_n,
                           int value_rescale, float vr_eps, float alpha, float prio_eps,
-                          float beta, float* part, unsigned* ticket, const bf16* zr,
-                          const float* w2, bf16* dz, float* dva, int HD, void* stream) {
+                          float beta, float* part, unsigned* ticket, const void* zr,
+                          const float* w2, bf16* dz, float* dva, int HD, bf16* dz_lo,
+                          void* stream) {
   if (B > 256) return -1;
-  if (A < 1 || A > 8) return -3;              // td_duel_kernel MAXA
+  if (A < 1 || A > 64) return -3;             // one lane per action
   const int grid = (Tl * B + 15) / 16;
   if (grid > 4096) return -2;   // part[] holds one float per workgroup (engine: 4096)
   TdDuelArgs d{{q_sa, q_arg, q_tgt, starts, probs, action, reward, done, dq, loss, td_abs, priority,
                 is_w, n_valid, part, ticket, Tl, B, A, burn_in, cap_e, gamma_n, vr_eps, alpha,
                 prio_eps, beta, value_rescale},
-               zr, w2, dz, dva};
+               zr, w2, dz, dva, dz_lo};
   hipStream_t s = (hipStream_t)stream;
-  switch (HD) {
-    case 64: hipLaunchKernelGGL(td_duel_kernel<64>, dim3(grid), dim3(1024), 0, s, d); break;
-    case 128: hipLaunchKernelGGL(td_duel_kernel<128>, dim3(grid), dim3(1024), 0, s, d); break;
-    case 256: hipLaunchKernelGGL(td_duel_kernel<256>, dim3(grid), dim3(1024), 0, s, d); break;
-    case 512: hipLaunchKernelGGL(td_duel_kernel<512>, dim3(grid), dim3(1024), 0, s, d); break;
-    default: return -4;
-  }
-  R2_CHECK_LAUNCH();
-  return 0;
+  return dz_lo ? td_duel_launch<true>(d, HD, grid, s) : td_duel_launch<false>(d, HD, grid, s);
 }

@@ -482,3 +482,12 @@ extern "C" int r2_torso_bwd(const uint8_t* frames, const int* rows, int n, const
 }
 
 extern "C" int r2_torso_bwd_slab_floats() { return tb::SLAB; }
+
+// slab reduction alone (used by the split-precision backward, torso_sp.hip)
+extern "C" int r2_torso_grad_reduce(const float* slab, int grid, const int* dst, const float* scale,
+                                    float* grad, void* stream) {
+  hipLaunchKernelGGL(torso_grad_reduce_kernel, dim3((tb::SLAB + 63) / 64), dim3(256), 0,
+                     (hipStream_t)stream, slab, grid, dst, scale, grad);
+  R2_CHECK_LAUNCH();
+  return 0;
+}

@@ -149,14 +149,28 @@ class LearnerEngine:
         self.opt_b = torch.zeros_like(self.master)
         self.bf_index = L.bf_index.to(d)
         self.f_index = L.f_index.to(d)
-        self.bf = torch.zeros(L.bf_numel, dtype=torch.bfloat16, device=d)
+        # split precision (compute_dtype "fp32", csrc/split.h): every bf16 kernel layout is packed as
+        # a hi plane and a lo plane, (2, bf_numel); pk / pk_t view the hi planes, pk_lo / pk_t_lo
+        # the lo planes
+        self.sp = cfg.learner.compute_dtype == "fp32"
+        if cfg.learner.compute_dtype not in ("fp32", "bf16"):
+            raise ValueError(f"learner.compute_dtype must be fp32 or bf16, not {cfg.learner.compute_dtype!r}")
+        nb = (2, L.bf_numel) if self.sp else (L.bf_numel,)
+        self.bf = torch.zeros(nb, dtype=torch.bfloat16, device=d)
         self.f32 = torch.zeros(L.f_numel, dtype=torch.float32, device=d)
         self.bf_t = torch.zeros_like(self.bf)
         self.f32_t = torch.zeros_like(self.f32)
         self.lstm_b = torch.zeros(L.G, dtype=torch.float32, device=d)
         self.lstm_b_t = torch.zeros_like(self.lstm_b)
-        self.pk = L.packed_views(self.bf, self.f32)
-        self.pk_t = L.packed_views(self.bf_t, self.f32_t)
+        if self.sp:
+            self.pk = L.packed_views(self.bf[0], self.f32)
+            self.pk_t = L.packed_views(self.bf_t[0], self.f32_t)
+            self.pk_lo = L.packed_views(self.bf[1], self.f32)
+            self.pk_t_lo = L.packed_views(self.bf_t[1], self.f32_t)
+        else:
+            self.pk = L.packed_views(self.bf, self.f32)
+            self.pk_t = L.packed_views(self.bf_t, self.f32_t)
+            self.pk_lo = self.pk_t_lo = None
         self.gate_inv = L.gate_inv.to(d)
         self.clip_buf = torch.zeros(1, dtype=torch.float32, device=d)
         self.steps_done = 0
@@ -183,17 +197,33 @@ class LearnerEngine:
         self.Tc = Tn if mode == "shifted" else T  # chain length of the online chain
         bf16, f32 = torch.bfloat16, torch.float32
         z = lambda *s, dt=f32: torch.zeros(s, dtype=dt, device=d)  # noqa: E731
+        sp = self.sp
+
+        def zsp(*s):
+            """An MFMA operand: bf16, or (split precision) a (2, *s) hi / lo pair -> (hi, lo)."""
+            if sp:
+                t = z(2, *s, dt=bf16)
+                return t[0], t[1]
+            return z(*s, dt=bf16), None
+        # the MFMA operands an op reads as an fp32 value: fp32 in split precision, else bf16
+        act_dt = f32 if sp else bf16
         self.starts = z(B, dt=torch.int32)
         self.probs = z(B)
         self.rows = z(Tn * B, dt=torch.int32)
-        self.X_on = z(Tn * B, D, dt=bf16)
+        self.X_on, self.X_on_lo = zsp(Tn * B, D)
         t_lo = 0 if mode == "shifted" else n       # first frame the target net needs
         self.t_lo_tg = t_lo
-        self.X_tg = z((Tn - t_lo) * B, D, dt=bf16)
+        self.X_tg, self.X_tg_lo = zsp((Tn - t_lo) * B, D)
         # conv activations of the learning frames, channels-last (N, h*w, c); the fused HIP torso
         # kernels cover the Atari geometry (4x84x84 -> 32x20x20 -> 32x9x9 -> 32x7x7), every other
         # geometry (e.g. DMLab RGB 3x72x96) runs the library conv path with the same buffers
         self.fused_torso = fused_torso_supported(cfg.env, cfg.model)
+        if sp and not (self.fused_torso and d.type == "cuda" and L.H <= 256
+                       and lc.lstm_impl == "persistent" and lc.lstm_handoff == "tagged"):
+            raise NotImplementedError(
+                "compute_dtype=fp32 (split precision) runs the fused Atari torso (4x84x84), hidden "
+                "<= 256 and the tagged persistent LSTM on a GPU; use compute_dtype=bf16 or the torch "
+                "learner (learner_ref.py) for other configurations")
         if not self.fused_torso and cfg.learner.conv_autotune and d.type == "cuda":
             # library conv path: let MIOpen benchmark its solutions once per shape (find mode);
             # DMLab-30: 463 -> 503 learner steps/s
@@ -202,23 +232,25 @@ class LearnerEngine:
             cin, dims, _ = torso_dims(cfg.env, cfg.model)
             c1, c2, _c3 = cfg.model.conv_channels
             self.tdims = (cin, dims)
-            self.act1 = z(Ll * B, dims[0][0] * dims[0][1], c1, dt=bf16)
-            self.act2 = z(Ll * B, dims[1][0] * dims[1][1], c2, dt=bf16)
+            self.act1, self.act1_lo = zsp(Ll * B, dims[0][0] * dims[0][1], c1)
+            self.act2, self.act2_lo = zsp(Ll * B, dims[1][0] * dims[1][1], c2)
             self.frames_bf = z(Ll * B, cfg.env.frame_h * cfg.env.frame_w * cin, dt=bf16)
-        self.h0 = {k: z(B, H, dt=bf16) for k in ("on", "tg", "nx")}
+        self.h0 = {k: z(B, H, dt=act_dt) for k in ("on", "tg", "nx")}
         self.c0 = {k: z(B, H) for k in ("on", "tg", "nx")}
         Tc = self.Tc
-        self.hseq = {"on": z(Tc, B, H, dt=bf16), "tg": z(T if mode != "shifted" else Tn, B, H, dt=bf16)}
+        self.hseq, self.hseq_lo = {}, {}
+        self.hseq["on"], self.hseq_lo["on"] = zsp(Tc, B, H)
+        self.hseq["tg"], self.hseq_lo["tg"] = zsp(T if mode != "shifted" else Tn, B, H)
         self.cseq = {"on": z(Tc, B, H), "tg": z(T if mode != "shifted" else Tn, B, H)}
         if mode != "shifted":
             Tnx = T if mode == "fixed" else Ll
-            self.hseq["nx"] = z(Tnx, B, H, dt=bf16)
+            self.hseq["nx"], self.hseq_lo["nx"] = zsp(Tnx, B, H)
             self.cseq["nx"] = z(Tnx, B, H)
         self.gates = z(Tc - Lb, B, G)
         # head rows: online from Lb..Tc, target/next likewise
         self.Nh = (Tc - Lb) * B
         self.q_on = z(self.Nh, A)
-        self.zr_on = z(self.Nh, 2 * HD, dt=bf16)
+        self.zr_on = z(self.Nh, 2 * HD, dt=act_dt)
         Ntg = (self.hseq["tg"].shape[0] - Lb) * B
         self.q_tg = z(Ntg, A)
         if mode != "shifted":
@@ -228,7 +260,7 @@ class LearnerEngine:
         self.loss = z(1)
         self.td_abs = z(Ll * B)
         self.is_w = z(B)
-        self.dz = z(Ll * B, 2 * HD, dt=bf16)
+        self.dz, self.dz_lo = zsp(Ll * B, 2 * HD)
         self.dva = z(Ll * B, 1 + A)
         nwg = H // UNITS
         self.slab0 = z(nwg, B, H)
@@ -241,7 +273,7 @@ class LearnerEngine:
         self.ring_b = z(max(int(kernels().r2_lstm_bwd_tag_ring_bytes(B, H)), 16) // 4, dt=torch.int32)
         self.bias_ws = z((B + 15) // 16, G)      # per-tile LSTM bias-gradient partials (tagged BPTT)
         self.err = z(1, dt=torch.int32)
-        self.dgates = z(Ll * B, G, dt=bf16)
+        self.dgates, self.dgates_lo = zsp(Ll * B, G)
         self.gamma_n = float(lc.gamma ** n)
         self.td_part = z(4096)                          # TD loss partials, one per workgroup
         self.td_ticket = z(1, dt=torch.int32)           # reset by the kernel's last workgroup
@@ -261,14 +293,14 @@ class LearnerEngine:
                          and (2 * HD) % 8 == 0 and G % 8 == 0)
         self.xp_on = z(Tn * B, G)
         self.xp_tg = z(self.X_tg.shape[0], G)
-        self.z_on = z(self.Nh, 2 * HD, dt=bf16)
-        self.z_tg = z(Ntg, 2 * HD, dt=bf16)
+        self.z_on = z(self.Nh, 2 * HD, dt=act_dt)
+        self.z_tg = z(Ntg, 2 * HD, dt=act_dt)
         if mode != "shifted":
-            self.z_nx = z(Nnx, 2 * HD, dt=bf16)
+            self.z_nx = z(Nnx, 2 * HD, dt=act_dt)
         self.dh = z(Ll * B, H)
         self._chunks = self._plan_chunks()
         self._side = torch.cuda.Stream(device=d) if self._chunks is not None else None
-        self.dX = z(Ll * B, D, dt=bf16)
+        self.dX, self.dX_lo = zsp(Ll * B, D)
         self.gate_perm_i32 = L.gate_perm.to(d, torch.int32)
         self.gs_ws = torch.zeros(int(kernels().r2_gradsum_ws_floats()), dtype=torch.float32, device=d)
         self.gs_ticket = torch.zeros(64, dtype=torch.int32, device=d)
@@ -279,11 +311,20 @@ class LearnerEngine:
         k = kernels()
         s = stream_handle(stream)
         L = self.layout
-        check(k.r2_pack_bf16(ptr(self.master), ptr(self.bf_index), ptr(self.bf), L.bf_numel, s), "pack")
+        if self.sp:
+            check(k.r2_pack_split(ptr(self.master), ptr(self.bf_index), ptr(self.bf), L.bf_numel,
+                                  L.bf_numel, s), "pack_split")
+        else:
+            check(k.r2_pack_bf16(ptr(self.master), ptr(self.bf_index), ptr(self.bf), L.bf_numel, s), "pack")
         check(k.r2_gather_f32(ptr(self.master), ptr(self.f_index), ptr(self.f32), L.f_numel, s), "gather")
         torch.add(self.pk["b_ih"], self.pk["b_hh"], out=self.lstm_b)
         if always:
-            check(k.r2_pack_bf16(ptr(self.target), ptr(self.bf_index), ptr(self.bf_t), L.bf_numel, s), "pack_t")
+            if self.sp:
+                check(k.r2_pack_split(ptr(self.target), ptr(self.bf_index), ptr(self.bf_t), L.bf_numel,
+                                      L.bf_numel, s), "pack_split_t")
+            else:
+                check(k.r2_pack_bf16(ptr(self.target), ptr(self.bf_index), ptr(self.bf_t), L.bf_numel, s),
+                      "pack_t")
             check(k.r2_gather_f32(ptr(self.target), ptr(self.f_index), ptr(self.f32_t), L.f_numel, s), "gather_t")
             torch.add(self.pk_t["b_ih"], self.pk_t["b_hh"], out=self.lstm_b_t)
 
@@ -294,7 +335,7 @@ class LearnerEngine:
                                      ptr(self.f32), ptr(self.f32_t), L.f_numel,
                                      L.f_offsets["b_ih"][0], L.f_offsets["b_hh"][0],
                                      ptr(self.lstm_b), ptr(self.lstm_b_t), L.G, ptr(self.replay.step),
-                                     interval, s), "pack_step")
+                                     interval, L.bf_numel if self.sp else 0, s), "pack_step")
 
     def state_dict(self):
         return self.layout.state_dict(self.master)
@@ -335,13 +376,23 @@ class LearnerEngine:
         self._pack(always=True)
 
     # ------------------------------------------------------------------ pieces
-    def _chain_desc(self, xproj, pk, h0, c0, hseq, cseq, gates=None, save_from=0):
-        return [ptr(xproj), ptr(pk["w_hh"]), ptr(h0), ptr(c0), ptr(hseq), ptr(cseq), 0,
-                ptr(gates), save_from]
+    def _chain_desc(self, xproj, pk, h0, c0, hseq, cseq, gates=None, save_from=0, pk_lo=None,
+                    hseq_lo=None):
+        d = [ptr(xproj), ptr(pk["w_hh"]), ptr(h0), ptr(c0), ptr(hseq), ptr(cseq), 0,
+             ptr(gates), save_from]
+        if self.sp:   # + W_hh lo plane, h_seq lo plane (h0 is fp32)
+            d += [ptr(pk_lo["w_hh"]), ptr(hseq_lo)]
+        return d
 
     def _lstm(self, chains, T, t_begin=0):
         k = kernels()
         arr = np.asarray([v for c in chains for v in c], dtype=np.int64)
+        if self.sp:
+            self._chain_arr = arr        # kept alive for capture
+            check(k.r2_lstm_fwd_tag_sp(arr.ctypes.data, len(chains), self.B, T, self.layout.H,
+                                       ptr(self.ctr), ptr(self.err), ptr(self.ring), stream_handle()),
+                  "lstm_fwd_tag_sp")
+            return
         if self.cfg.learner.lstm_impl == "persistent" and t_begin == 0:
             if self.cfg.learner.lstm_handoff == "tagged":
                 rc = k.r2_lstm_fwd_tag(arr.ctypes.data, len(chains), self.B, T, self.layout.H,
@@ -356,10 +407,15 @@ class LearnerEngine:
             check(k.r2_lstm_fwd(arr.ctypes.data, len(chains), self.B, T, self.layout.H, t_begin,
                                 stream_handle()), "lstm_fwd")
 
-    def _heads(self, jobs):
+    def _heads(self, jobs, lo=None):
         """jobs: [(pk, h (N,H) bf16, z buffer, q out, zr out or None)].  Layer-1 GEMMs of all heads
-        in one launch, then one dueling kernel per head."""
-        if self.use_gemm:
+        in one launch, then one dueling kernel per head.  Split precision: ``lo`` = [(pk_lo, h lo
+        plane)] per job; z / zr are fp32."""
+        if self.sp:
+            gemm(*[Gemm(h, pk["head1"].t(), zb, a_lo=hl, b_lo=pkl["head1"].t())
+                   for (pk, h, zb, _, _), (pkl, hl) in zip(jobs, lo)])
+            zs = [zb for _, _, zb, _, _ in jobs]
+        elif self.use_gemm:
             gemm(*[Gemm(h, pk["head1"].t(), zb) for pk, h, zb, _, _ in jobs])
             zs = [zb for _, _, zb, _, _ in jobs]
         else:
@@ -368,8 +424,9 @@ class LearnerEngine:
         self._djobs = np.asarray([[ptr(z), ptr(pk["head_b1"]), ptr(pk["head_w2"]), ptr(pk["head_b2"]),
                                    ptr(q), ptr(zr), h.shape[0]]
                                   for (pk, h, _, q, zr), z in zip(jobs, zs)], dtype=np.int64)
-        check(kernels().r2_dueling_fwd_multi(self._djobs.ctypes.data, len(jobs), self.layout.A,
-                                             self.layout.HD, stream_handle()), "dueling_fwd")
+        fn = kernels().r2_dueling_fwd_multi_f32 if self.sp else kernels().r2_dueling_fwd_multi
+        check(fn(self._djobs.ctypes.data, len(jobs), self.layout.A, self.layout.HD, stream_handle()),
+              "dueling_fwd")
 
     # ------------------------------------------------------------------ pipelined forward
     def _plan_chunks(self):
@@ -415,6 +472,18 @@ class LearnerEngine:
             s2 = self.act2.data_ptr() + save_at * B * P2 * 2
         return [ptr(rows), rows.numel(), ptr(pk["conv1"]), ptr(pk["b1"]), ptr(pk["conv2"]),
                 ptr(pk["b2"]), ptr(pk["conv3"]), ptr(pk["b3"]), ptr(out), s1, s2, 0]
+
+    def _torso_job_sp(self, pk, pkl, rows, out, out_lo, save_at=None):
+        """torso_sp.hip job (20 int64): weights hi / lo, features hi / lo, saved activations."""
+        B = self.B
+        s = [0, 0, 0, 0]
+        if save_at is not None:
+            r0, r1 = save_at * B, save_at * B + rows.numel()
+            s = [ptr(self.act1[r0:r1]), ptr(self.act1_lo[r0:r1]), ptr(self.act2[r0:r1]),
+                 ptr(self.act2_lo[r0:r1])]
+        return [ptr(rows), rows.numel(), ptr(pk["conv1"]), ptr(pkl["conv1"]), ptr(pk["b1"]),
+                ptr(pk["conv2"]), ptr(pkl["conv2"]), ptr(pk["b2"]), ptr(pk["conv3"]),
+                ptr(pkl["conv3"]), ptr(pk["b3"]), ptr(out), ptr(out_lo)] + s + [0, 0, 0]
 
     def _forward_pipelined(self):
         k = kernels()
@@ -470,7 +539,7 @@ class LearnerEngine:
                   (rp.target_hs_cs, st_off["tg"], self.h0["tg"], self.c0["tg"])]
         if self.mode == "fixed":
             states.append((rp.hs_cs, n, self.h0["nx"], self.c0["nx"]))
-        rp.sample_batch(B, self.starts, self.probs, self.rows, Tn, states)
+        rp.sample_batch(B, self.starts, self.probs, self.rows, Tn, states, h_f32=self.sp)
         rows = self.rows
         if self._chunks is not None:
             self._forward_pipelined()
@@ -478,7 +547,19 @@ class LearnerEngine:
             self._xp = (xp_on, xp_tg)
             return self._forward_tail()
         # torso: online over all Tn frames (save activations of the learning frames) and target
-        if self.fused_torso:
+        if self.sp:
+            pkl, ptl = self.pk_lo, self.pk_t_lo
+            Xo, Xol, Xt, Xtl = self.X_on, self.X_on_lo, self.X_tg, self.X_tg_lo
+            jobs = [self._torso_job_sp(pk, pkl, rows[: Lb * B], Xo[: Lb * B], Xol[: Lb * B]),
+                    self._torso_job_sp(pk, pkl, rows[Lb * B: T * B], Xo[Lb * B: T * B],
+                                       Xol[Lb * B: T * B], save_at=0),
+                    self._torso_job_sp(pk, pkl, rows[T * B:], Xo[T * B:], Xol[T * B:]),
+                    self._torso_job_sp(pt, ptl, rows[self.t_lo_tg * B:], Xt, Xtl)]
+            jobs = [j for j in jobs if j[1] > 0]
+            self._tjobs = np.asarray(jobs, dtype=np.int64)          # kept alive for capture
+            check(k.r2_torso_fwd_sp_multi(ptr(rp.frames), self._tjobs.ctypes.data, len(jobs),
+                                          self.n_cus, s), "torso_fwd_sp_multi")
+        elif self.fused_torso:
             # one launch, workers dealt to the 4 jobs in proportion to their frames: separate
             # launches each ended in a partly idle last round of frames (18.6 us for the 320
             # tail frames alone)
@@ -496,7 +577,13 @@ class LearnerEngine:
             torso_forward_library(rp.frames, rows[self.t_lo_tg * B:], L, self.target, self.cfg.env,
                                   self.cfg.model, self.X_tg)
         # input projections (one GEMM per net over every row)
-        if self.use_gemm:
+        if self.sp:
+            xp_on, xp_tg = self.xp_on, self.xp_tg
+            gemm(Gemm(self.X_on, pk["w_ih"].t(), xp_on, bias=self.lstm_b, a_lo=self.X_on_lo,
+                      b_lo=self.pk_lo["w_ih"].t()),
+                 Gemm(self.X_tg, pt["w_ih"].t(), xp_tg, bias=self.lstm_b_t, a_lo=self.X_tg_lo,
+                      b_lo=self.pk_t_lo["w_ih"].t()))
+        elif self.use_gemm:
             xp_on, xp_tg = self.xp_on, self.xp_tg
             gemm(Gemm(self.X_on, pk["w_ih"].t(), xp_on, bias=self.lstm_b),
                  Gemm(self.X_tg, pt["w_ih"].t(), xp_tg, bias=self.lstm_b_t))
@@ -505,21 +592,27 @@ class LearnerEngine:
             xp_tg = addmm_f32(self.lstm_b_t, self.X_tg, pt["w_ih"].t())
         self._xp = (xp_on, xp_tg)
         G = L.G
+        hl = self.hseq_lo
+        pkl, ptl = self.pk_lo, self.pk_t_lo
         on = self._chain_desc(xp_on, pk, self.h0["on"], self.c0["on"], self.hseq["on"],
-                              self.cseq["on"], self.gates, Lb)
-        tg = self._chain_desc(xp_tg, pt, self.h0["tg"], self.c0["tg"], self.hseq["tg"], self.cseq["tg"])
+                              self.cseq["on"], self.gates, Lb, pkl, hl.get("on"))
+        tg = self._chain_desc(xp_tg, pt, self.h0["tg"], self.c0["tg"], self.hseq["tg"], self.cseq["tg"],
+                              None, 0, ptl, hl.get("tg"))
         if self.mode == "shifted":
             self._lstm([on, tg], self.Tc)
         elif self.mode == "fixed":
             nx = self._chain_desc(xp_on[n * B:], pk, self.h0["nx"], self.c0["nx"], self.hseq["nx"],
-                                  self.cseq["nx"])
+                                  self.cseq["nx"], None, 0, pkl, hl.get("nx"))
             self._lstm([on, tg, nx], T)
         else:  # reference: Q7 -- online-on-next continues from the online chain's final state
             self._lstm([on, tg], T)
-            self.h0["nx"].copy_(self.hseq["on"][T - 1])
+            if self.sp:
+                torch.add(self.hseq["on"][T - 1].float(), hl["on"][T - 1].float(), out=self.h0["nx"])
+            else:
+                self.h0["nx"].copy_(self.hseq["on"][T - 1])
             self.c0["nx"].copy_(self.cseq["on"][T - 1])
             nx = self._chain_desc(xp_on[(n + Lb) * B:], pk, self.h0["nx"], self.c0["nx"],
-                                  self.hseq["nx"], self.cseq["nx"])
+                                  self.hseq["nx"], self.cseq["nx"], None, 0, pkl, hl.get("nx"))
             self._lstm([nx], Ll)
         self._forward_tail()
 
@@ -534,10 +627,16 @@ class LearnerEngine:
         # heads (rows from the first learning step on)
         jobs = [(pk, self.hseq["on"][Lb:].reshape(-1, H), self.z_on, self.q_on, self.zr_on),
                 (pt, self.hseq["tg"][Lb:].reshape(-1, H), self.z_tg, self.q_tg, None)]
+        lo = None
+        if self.sp:
+            hl = self.hseq_lo
+            lo = [(self.pk_lo, hl["on"][Lb:].reshape(-1, H)), (self.pk_t_lo, hl["tg"][Lb:].reshape(-1, H))]
         if self.mode != "shifted":
             nx_from = Lb if self.mode == "fixed" else 0
             jobs.append((pk, self.hseq["nx"][nx_from:].reshape(-1, H), self.z_nx, self.q_nx, None))
-        self._heads(jobs)
+            if self.sp:
+                lo.append((self.pk_lo, self.hseq_lo["nx"][nx_from:].reshape(-1, H)))
+        self._heads(jobs, lo)
         if self.mode == "shifted":
             q_sa = self.q_on[: Ll * B]
             q_arg = self.q_on[n * B:(n + Ll) * B]
@@ -558,14 +657,74 @@ class LearnerEngine:
         self._duel_done = False
         if lc.td_fuse_head_bwd:
             rc_ = k.r2_td_duel(*targs, ptr(self.zr_on[: Ll * B]), ptr(pk["head_w2"]), ptr(self.dz),
-                               ptr(self.dva), L.HD, s)
+                               ptr(self.dva), L.HD, ptr(self.dz_lo), s)
             if rc_ == 0:
                 self._duel_done = True
                 return
+            if self.sp:
+                check(rc_, "td_duel")
         check(k.r2_td_loss(*targs, s), "td_loss")
+
+    def _backward_core_sp(self):
+        """Split-precision backward core: head gradients, dh GEMM, BPTT, weight-gradient + dX
+        GEMMs, every MFMA operand as hi / lo planes (the same launches as the bf16 path minus the
+        BPTT side jobs)."""
+        k = kernels()
+        s = stream_handle()
+        B, T, Lb, Ll = self.B, self.T, self.Lb, self.Ll
+        L, pk, pkl = self.layout, self.pk, self.pk_lo
+        H, A, HD, G = L.H, L.A, L.HD, L.G
+        N = Ll * B
+        g = self.grad
+        gw2 = L.span(g, "val.2.weight", "adv.2.weight", (1 + A, HD))
+        gb2 = L.span(g, "val.2.bias", "adv.2.bias", (1, 1 + A))
+        gb1 = L.span(g, "val.0.bias", "adv.0.bias", (1, 2 * HD))
+        check(k.r2_head_grads_sp(ptr(self.dva), ptr(self.zr_on[:N]), ptr(self.dz), ptr(self.dz_lo),
+                                 ptr(gw2), ptr(gb2), ptr(gb1), N, A, HD, ptr(self.gs_ws),
+                                 ptr(self.gs_ticket), s), "head_grads_sp")
+        dh = self.dh
+        gemm(Gemm(self.dz, pk["head1"], dh, a_lo=self.dz_lo, b_lo=pkl["head1"]))
+        check(k.r2_lstm_bwd_tag_sp(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]), ptr(self.c0["on"]),
+                                   ptr(pk["w_hhT"]), ptr(pkl["w_hhT"]), ptr(self.dgates),
+                                   ptr(self.dgates_lo), B, T, Lb, H, ptr(self.ctr), ptr(self.err),
+                                   ptr(self.ring_b), ptr(self.bias_ws), ptr(self.gate_perm_i32),
+                                   ptr(L.view(g, "lstm.bias_ih")), ptr(L.view(g, "lstm.bias_hh")), s),
+              "lstm_bwd_tag_sp")
+        hs, hl = self.hseq["on"], self.hseq_lo["on"]
+        h_learn, h_learn_l = hs[Lb:T].reshape(N, H), hl[Lb:T].reshape(N, H)
+        if Lb >= 1:
+            h_prev, h_prev_l = hs[Lb - 1: T - 1].reshape(N, H), hl[Lb - 1: T - 1].reshape(N, H)
+        else:   # the stored h0 (fp32) -> a split pair, then the chain's outputs
+            if getattr(self, "_hprev_sp", None) is None:
+                self._hprev_sp = torch.zeros(2, N, H, dtype=torch.bfloat16, device=self.device)
+            h0 = self.h0["on"]
+            hi0 = h0.to(torch.bfloat16)
+            self._hprev_sp[0, :B].copy_(hi0)
+            self._hprev_sp[1, :B].copy_((h0 - hi0.float()).to(torch.bfloat16))
+            self._hprev_sp[0, B:].copy_(hs[: T - 1].reshape(-1, H))
+            self._hprev_sp[1, B:].copy_(hl[: T - 1].reshape(-1, H))
+            h_prev, h_prev_l = self._hprev_sp[0], self._hprev_sp[1]
+        gw1 = L.span(g, "val.0.weight", "adv.0.weight", (2 * HD, H))
+        X, Xl = self.X_on[Lb * B: T * B], self.X_on_lo[Lb * B: T * B]
+        dgT, dgTl = self.dgates.t(), self.dgates_lo.t()
+        w_jobs = [Gemm(self.dz.t(), h_learn, gw1, a_lo=self.dz_lo.t(), b_lo=h_learn_l),
+                  Gemm(dgT, h_prev, L.view(g, "lstm.weight_hh"), crow=self.gate_perm_i32,
+                       a_lo=dgTl, b_lo=h_prev_l),
+                  Gemm(dgT, X, L.view(g, "lstm.weight_ih"), crow=self.gate_perm_i32, a_lo=dgTl, b_lo=Xl)]
+        x_job = Gemm(self.dgates, pk["w_ih"], self.dX, a_lo=self.dgates_lo, b_lo=pkl["w_ih"],
+                     c_lo=self.dX_lo)
+        splits = self._group_splits(w_jobs, x_job)
+        if splits:
+            gemm_group([w_jobs[2], w_jobs[1], w_jobs[0], x_job], splits, self.gg_ws, self.gg_tickets)
+        else:
+            gemm(w_jobs[2], w_jobs[1], w_jobs[0])
+            gemm(x_job)
+        self._dX = self.dX
 
     def _backward_core(self):
         """Head backward, BPTT, LSTM/head weight gradients -> grad bucket 'core'."""
+        if self.sp:
+            return self._backward_core_sp()
         k = kernels()
         s = stream_handle()
         B, T, Lb, Ll = self.B, self.T, self.Lb, self.Ll
@@ -736,6 +895,16 @@ class LearnerEngine:
         return grad * (act > 0)
 
     def _backward_torso(self):
+        if self.sp:
+            B, Lb, T = self.B, self.Lb, self.T
+            pk, pkl = self.pk, self.pk_lo
+            check(kernels().r2_torso_bwd_sp(
+                ptr(self.replay.frames), ptr(self.rows[Lb * B: T * B]), self.Ll * B, ptr(self.act1),
+                ptr(self.act1_lo), ptr(self.act2), ptr(self.act2_lo), ptr(self.dX), ptr(self.dX_lo),
+                ptr(self.X_on[Lb * B: T * B]), ptr(pk["conv3_dg"]), ptr(pkl["conv3_dg"]),
+                ptr(pk["conv2_dg"]), ptr(pkl["conv2_dg"]), ptr(self._tb_slab), self._tb_grid,
+                ptr(self._tb_dst), ptr(self._tb_scale), ptr(self.grad), stream_handle()), "torso_bwd_sp")
+            return
         if self.cfg.learner.torso_bwd == "fused" and self.fused_torso:
             self._backward_torso_fused()
         else:

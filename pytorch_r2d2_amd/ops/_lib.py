@@ -42,7 +42,10 @@ _SIGS = {
     "r2_dueling_bwd": [P, P, P, P, P, I, I, I, P],
     "r2_td_loss": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, F, F, F, F, P, P, P],
     "r2_td_duel": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, F, F, F, F, P, P,
-                   P, P, P, P, I, P],
+                   P, P, P, P, I, P, P],
+    "r2_dueling_fwd_multi_f32": [P, I, I, I, P],
+    "r2_lstm_fwd_tag_sp": [P, I, I, I, I, P, P, P, P],
+    "r2_lstm_bwd_tag_sp": [P, P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P, P, P],
     "r2_tree_sample": [P, P, P, I, I, U64, P, P, P, P],
     "r2_tree_rebuild": [P, P, P, I, P],
     "r2_tree_update": [P, P, P, I, P, P, I, P],
@@ -51,6 +54,10 @@ _SIGS = {
     "r2_mark_starts": [P, P, I, P, P, P, I, I, F, P, P, P, I, P],
     "r2_make_rows": [P, I, I, I, I, P, P],
     "r2_sample_batch": [P, P, P, I, I, U64, P, P, P, P, I, I, I, I, P, P, P, P, P],
+    "r2_sample_batch_f32h": [P, P, P, I, I, U64, P, P, P, P, I, I, I, I, P, P, P, P, P],
+    "r2_torso_fwd_sp_multi": [P, P, I, I, P],
+    "r2_torso_bwd_sp": [P, P, I, P, P, P, P, P, P, P, P, P, P, P, P, I, P, P, P, P],
+    "r2_torso_grad_reduce": [P, I, P, P, P, P],
     "r2_gather_state": [P, P, I, I, I, I, P, P, P, P],
     "r2_step_end": [P, P, P],
     "r2_rmsprop_centered": [P, P, P, P, I64, F, F, F, F, P, F, P],
@@ -70,7 +77,8 @@ _SIGS = {
     "r2_actor_post": [P, P],
     "r2_actor_tail": [P, P],
     "r2_actor_args_bytes": [],
-    "r2_pack_step": [P, P, I64, P, P, P, I64, P, P, P, I64, I64, I64, P, P, I64, P, I64, P],
+    "r2_pack_step": [P, P, I64, P, P, P, I64, P, P, P, I64, I64, I64, P, P, I64, P, I64, I64, P],
+    "r2_pack_split": [P, P, P, I64, I64, P],
     "r2_torso_bwd_set_debug": [P],
     "r2_torso_fwd_set_debug": [P],
     "r2_lstm_persist_set_debug": [P],
@@ -78,6 +86,7 @@ _SIGS = {
     "r2_xcc_probe": [P, I, I, I, P],
     "r2_gradsum_ws_floats": [],
     "r2_head_grads": [P, P, P, P, P, P, I, I, I, P, P, P],
+    "r2_head_grads_sp": [P, P, P, P, P, P, P, I, I, I, P, P, P],
     "r2_colsum_bf16": [P, I, I, P, P, P, P, P, P],
     "r2_lstm_fwd_persist": [P, I, I, I, I, P, P, P],
     "r2_lstm_fwd_tag": [P, I, I, I, I, P, P, P, P],

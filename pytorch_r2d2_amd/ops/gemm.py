@@ -37,9 +37,16 @@ class Gemm:
     crow: Optional[torch.Tensor] = None
     accumulate: bool = False
     alpha: float = 1.0
+    # split precision (csrc/split.h): lo planes with the same shape / strides as a, b, c
+    a_lo: Optional[torch.Tensor] = None
+    b_lo: Optional[torch.Tensor] = None
+    c_lo: Optional[torch.Tensor] = None
 
     def desc(self) -> List[int]:
         a, b, c = self.a, self.b, self.c
+        for x, lo in ((a, self.a_lo), (b, self.b_lo), (c, self.c_lo)):
+            if lo is not None:
+                assert lo.shape == x.shape and lo.stride() == x.stride() and lo.dtype == torch.bfloat16
         assert a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
         M, K = a.shape
         K2, N = b.shape
@@ -54,7 +61,10 @@ class Gemm:
                 0 if self.bias is None else self.bias.data_ptr(),
                 0 if self.crow is None else self.crow.data_ptr(),
                 M, N, K, lda, ldb, c.stride(0), ak, bk, int(c.dtype == torch.float32),
-                int(self.accumulate), alpha_bits]
+                int(self.accumulate), alpha_bits,
+                0 if self.a_lo is None else self.a_lo.data_ptr(),
+                0 if self.b_lo is None else self.b_lo.data_ptr(),
+                0 if self.c_lo is None else self.c_lo.data_ptr(), 0]
 
 
 def gemm(*problems: Gemm, stream=None) -> None:
