@@ -191,8 +191,10 @@ def apply_override(cfg: R2D2Config, dotted: str, value: Any) -> None:
 
 def _reference() -> R2D2Config:
     c = R2D2Config(name="reference")
-    # the reference's 3-chain target structure (learner.py:71-93) with Q7 fixed
+    # the reference's 3-chain target structure (learner.py:71-93) with Q7 fixed, at the
+    # reference's precision (fp32 end to end: model.py / learner.py use no reduced precision)
     c.learner.target_mode = "fixed"
+    c.learner.compute_dtype = "fp32"
     return c
 
 
@@ -227,7 +229,7 @@ def _atari57() -> R2D2Config:
                             eta=0.9, alpha=0.9, beta=0.6, stored_state="pre", n_subrings=256)
     c.learner = LearnerConfig(batch_size=64, gamma=0.997, optimizer="rmsprop_centered",
                               value_rescale=True, target_update_interval=2500,
-                              target_mode="fixed")
+                              target_mode="fixed", compute_dtype="fp32")
     c.actor = ActorConfig(n_actors=1, envs_per_actor=256)
     return c
 
@@ -249,6 +251,9 @@ def _dmlab30() -> R2D2Config:
                       channels_per_frame=3, n_actions=15)
     c.model.n_actions = 15
     c.actor = ActorConfig(n_actors=8, envs_per_actor=64)
+    # BASELINE config 5 names a bf16 LSTM for DMLab; the split-precision mode needs the fused
+    # Atari torso
+    c.learner.compute_dtype = "bf16"
     return c
 
 

@@ -1,4 +1,4 @@
-"""End-to-end HIP learner step vs the fp32 PyTorch autograd oracle (learner_ref.py)."""
+"""End-to-end bf16 HIP learner step vs the fp32 PyTorch autograd oracle (learner_ref.py)."""
 import copy
 
 import pytest
@@ -20,8 +20,9 @@ def _rel(a, b):
 
 
 def _make(mode, B=16, preset="atari57", **kw):
+    # the bf16 engine (the fp32 / split-precision engine: tests/test_split_gpu.py)
     over = {"learner.batch_size": B, "learner.target_mode": mode, "replay.capacity": 40000,
-            "replay.n_subrings": 8, "learner.use_graph": False}
+            "replay.n_subrings": 8, "learner.use_graph": False, "learner.compute_dtype": "bf16"}
     if preset == "atari57":
         over.update({"replay.burn_in": 6, "replay.learn": 8, "replay.overlap": 7})
     over.update(kw)
