@@ -21,6 +21,14 @@
 //                      finished return into the return ring, reset / advance the LSTM state.
 //   mark_starts_kernel + tree update (replay.hip), then
 //   actor_tail_kernel  (1 thread): t += 1, head = (head + 1) % cap_e, return count, dirty reset.
+//
+// Deferred mode (defer_D > 0; the concurrent actor / learner topology, engine/concurrent.py): the
+// actor never touches the sequence-start flags, the sum tree, n_valid or the dirty list -- the
+// learner reads those while it runs on other CUs.  Instead every start it would clear or mark is
+// appended to a pending list (mark: row >= 0; clear: -2 - row) that the learner's stream applies
+// between its steps (replay.hip apply_pending_kernel).  Rows are invalidated defer_D steps AHEAD
+// of the write head, so by the time a row is overwritten every learner step that could have
+// sampled a sequence through it has finished.
 #include "../common.h"
 
 struct ActArgs {
@@ -65,9 +73,12 @@ struct ActArgs {
   float* ret_ring;            // (R)
   int64_t* ret_cnt;           // (1)
   int* marks;                 // (E * (n + 2)) start rows to mark, -1 = none
+  int* pend;                  // deferred mode: pending start edits (mark row | clear -2-row)
+  int* pend_cnt;              // (1) entries appended (reset by the learner's apply)
   long long FB;
   unsigned long long seed;
   int E, A, H, n, T, stride, cap_e, W, wrap, max_dirty, R, value_rescale;
+  int pend_cap, defer_D;      // defer_D > 0: deferred mode, invalidate defer_D rows ahead
   float gamma, gamma_n, prio_eps, alpha, vr_eps;
 };
 
@@ -116,14 +127,25 @@ __device__ __forceinline__ void clear_row(const ActArgs& a, long long r) {
   }
 }
 
+__device__ __forceinline__ void pend_push(const ActArgs& a, int v) {
+  const int slot = atomicAdd(a.pend_cnt, 1);
+  if (slot < a.pend_cap) a.pend[slot] = v;      // overflow is detected by the apply kernel
+}
+
 __global__ __launch_bounds__(256) void actor_pre_kernel(const ActArgs a) {
   const int e = blockIdx.x, tid = threadIdx.x;
   const long long t = *a.t, head = *a.head;
   const long long base = (long long)e * a.cap_e, row = base + head;
-  // 1. rows about to be overwritten stop being sequence starts
-  if (tid == 0) clear_row(a, row);
-  if (a.wrap)
-    for (int i = tid; i < a.W - 1; i += blockDim.x) clear_row(a, base + a.cap_e - a.W + 1 + i);
+  // 1. rows about to be overwritten stop being sequence starts (deferred: defer_D rows ahead)
+  if (a.defer_D > 0) {
+    if (tid == 0) pend_push(a, -2 - (int)(base + (head + a.defer_D) % a.cap_e));
+    if (a.wrap)
+      for (int i = tid; i < a.W - 1; i += blockDim.x) pend_push(a, -2 - (int)(base + a.cap_e - a.W + 1 + i));
+  } else {
+    if (tid == 0) clear_row(a, row);
+    if (a.wrap)
+      for (int i = tid; i < a.W - 1; i += blockDim.x) clear_row(a, base + a.cap_e - a.W + 1 + i);
+  }
   // 2. observation -> replay row (16-byte vectors when aligned)
   {
     const uint8_t* src = a.obs + (size_t)e * a.FB;
@@ -206,7 +228,12 @@ __global__ __launch_bounds__(256) void actor_post_kernel(const ActArgs a) {
   {
     const long long o = (t - n) - ep0 - a.T + 1;
     const bool ok = o >= 0 && o % a.stride == 0;
-    a.marks[e] = ok ? (int)(base + pymod(head - (t - ep0) + o, a.cap_e)) : -1;
+    const int m = ok ? (int)(base + pymod(head - (t - ep0) + o, a.cap_e)) : -1;
+    if (a.defer_D > 0) {
+      if (m >= 0) pend_push(a, m);
+    } else {
+      a.marks[e] = m;
+    }
   }
   // episode end: every pending transition gets its truncated return, done = 1 (no bootstrap);
   // starts whose windows end inside the just-finalised tail, plus the final start L - T
@@ -226,7 +253,12 @@ __global__ __launch_bounds__(256) void actor_post_kernel(const ActArgs a) {
   for (int jj = 0; jj <= n; ++jj) {
     const long long o = L - a.T - jj;
     const bool ok = dn && o >= 0 && o > prev_newest - a.T + 1 && (o % a.stride == 0 || jj == 0);
-    a.marks[(size_t)(1 + jj) * E + e] = ok ? (int)(base + pymod(head - (t - ep0) + o, a.cap_e)) : -1;
+    const int m = ok ? (int)(base + pymod(head - (t - ep0) + o, a.cap_e)) : -1;
+    if (a.defer_D > 0) {
+      if (m >= 0) pend_push(a, m);
+    } else {
+      a.marks[(size_t)(1 + jj) * E + e] = m;
+    }
   }
   if (dn) a.ep_start[e] = t + 1;
 }
@@ -239,12 +271,13 @@ __global__ void actor_tail_kernel(int64_t* t, int64_t* head, int cap_e, const ui
   *ret_cnt += nd;
   *t += 1;
   *head = (*head + 1) % cap_e;
-  *dcount = 0;
+  if (dcount) *dcount = 0;
 }
 
 static bool act_args_ok(const ActArgs& a) {
   return a.E > 0 && a.A > 0 && a.A <= 64 && a.H > 0 && a.n > 0 && a.T > 0 && a.stride > 0 &&
-         a.cap_e > a.W && a.R > 0 && a.FB >= 0;
+         a.cap_e > a.W && a.R > 0 && a.FB >= 0 &&
+         (a.defer_D <= 0 || (a.pend && a.pend_cnt && a.pend_cap > 0 && a.cap_e > a.defer_D + a.W));
 }
 
 extern "C" int r2_actor_pre(const ActArgs* a, void* stream) {
@@ -263,7 +296,7 @@ extern "C" int r2_actor_post(const ActArgs* a, void* stream) {
 
 extern "C" int r2_actor_tail(const ActArgs* a, void* stream) {
   hipLaunchKernelGGL(actor_tail_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, a->t, a->head,
-                     a->cap_e, a->env_done, a->E, a->ret_cnt, a->dcount);
+                     a->cap_e, a->env_done, a->E, a->ret_cnt, a->defer_D > 0 ? nullptr : a->dcount);
   R2_CHECK_LAUNCH();
   return 0;
 }

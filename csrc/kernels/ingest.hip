@@ -1,0 +1,159 @@
+// Trajectory ingest: scatter one packed actor record (parallel/trajectory.py pack_rows: header +
+// SoA fields at 64-byte aligned offsets) from device memory into an HBM replay sub-ring.
+//
+// Replaces the reference learner's replay-file ingest (replay_memory.py:155-173 -> :107-119:
+// unpickle 233 MB per 5k rows, numpy ring writes) and round 1's host-side ingest_memory (a full
+// tree rebuild and a host sync per file).  The record is parsed ON THE DEVICE, so the same
+// launch serves records DMA'd from a CPU actor's shared-memory ring (engine/ingest.py) and
+// records received over RCCL straight into device memory (RcclTrajectoryChannel.recv_into):
+//
+//   ingest_rows_kernel  one workgroup per row: frames (16-byte vectors), both stored LSTM states,
+//                       the scalars; the sequence-start flag / sum-tree leaf / n_valid follow the
+//                       record (the rows it overwrites stop being starts), changed leaves go to
+//                       the dirty list (or, for very large records, the caller rebuilds the tree)
+//   ingest_tail_kernel  advances the sub-ring's device write head and the rows counter
+//
+// No host work besides the launch: the write head lives on the device.
+#include "../common.h"
+
+#define ING_FIELDS 10   // state hs_cs target_hs_cs action reward done stack_count priority seqprio start
+#define ING_MAGIC 0x52324454ll
+
+struct IngestArgs {
+  const uint8_t* rec;       // device record
+  long long rec_bytes;
+  int sub, max_rows;        // destination sub-ring, grid rows (>= rows kept)
+  long long* ihead;         // (n_sub) device write heads
+  long long* rows_total;    // (1) rows ingested
+  unsigned* err;            // bit 0: malformed record
+  uint8_t* frames;          // (cap, FB)
+  float* hs_cs;             // (cap, 2H)
+  float* ths_cs;            // (cap, 2H)
+  uint8_t* action;
+  float* reward;
+  uint8_t* done;
+  float* priority;
+  uint8_t* is_start;
+  float* leaves;
+  int* n_valid;
+  int* dirty;               // null: no dirty list (the caller rebuilds the tree)
+  int* count;
+  int max_dirty;
+  int FB, H2, cap_e;
+};
+
+struct RecView {
+  long long n;
+  long long off[ING_FIELDS];
+  int code[ING_FIELDS];
+  long long per_row[ING_FIELDS];
+  long long nbytes[ING_FIELDS];
+};
+
+__device__ __forceinline__ long long pad64(long long x) { return (x + 63) & ~63ll; }
+
+// false if the record does not match the replay schema
+__device__ bool parse_record(const IngestArgs& a, RecView& v) {
+  const long long* h = reinterpret_cast<const long long*>(a.rec);
+  if (h[0] != ING_MAGIC || h[2] != ING_FIELDS) return false;
+  v.n = h[1];
+  long long off = pad64(24 + 24 * ING_FIELDS);
+  for (int f = 0; f < ING_FIELDS; ++f) {
+    v.code[f] = (int)h[3 + 3 * f];
+    v.per_row[f] = h[4 + 3 * f];
+    v.nbytes[f] = h[5 + 3 * f];
+    v.off[f] = off;
+    off += pad64(v.nbytes[f]);
+  }
+  if (off > a.rec_bytes || v.n < 0) return false;
+  // state uint8 x FB, states fp32 x 2H, 1-byte or fp32 scalars
+  if (v.code[0] != 0 || v.per_row[0] != a.FB) return false;
+  if (v.code[1] != 2 || v.per_row[1] != a.H2 || v.code[2] != 2 || v.per_row[2] != a.H2) return false;
+  if (v.code[4] != 2 || v.code[7] != 2 || v.code[8] != 2) return false;
+  if (v.code[3] == 2 || v.code[9] == 2) return false;
+  return true;
+}
+
+__device__ __forceinline__ float scalar_at(const uint8_t* base, int code, long long i) {
+  if (code == 2) return reinterpret_cast<const float*>(base)[i];
+  if (code == 1) return (float)reinterpret_cast<const int8_t*>(base)[i];
+  return (float)base[i];
+}
+
+__global__ __launch_bounds__(256) void ingest_rows_kernel(const IngestArgs a) {
+  RecView v;
+  const bool ok = parse_record(a, v);
+  const int tid = threadIdx.x;
+  if (!ok) {
+    if (blockIdx.x == 0 && tid == 0) atomicOr(a.err, 1u);
+    return;
+  }
+  const long long keep = v.n < a.cap_e ? v.n : a.cap_e;
+  const long long i = blockIdx.x;
+  if (i >= keep) return;
+  const long long src = v.n - keep + i;                 // only the newest cap_e rows survive
+  const long long head = a.ihead[a.sub];
+  const long long row = (long long)a.sub * a.cap_e + (head + i) % a.cap_e;
+  // frames: 16-byte vectors (fields are 64-byte aligned; FB % 16 == 0 for every frame geometry)
+  {
+    const uint8_t* s = a.rec + v.off[0] + src * a.FB;
+    uint8_t* d = a.frames + row * a.FB;
+    if ((a.FB & 15) == 0) {
+      const int nv = a.FB >> 4;
+      for (int k = tid; k < nv; k += blockDim.x)
+        reinterpret_cast<u32x4*>(d)[k] = reinterpret_cast<const u32x4*>(s)[k];
+    } else {
+      for (int k = tid; k < a.FB; k += blockDim.x) d[k] = s[k];
+    }
+  }
+  {
+    const float* s1 = reinterpret_cast<const float*>(a.rec + v.off[1]) + src * a.H2;
+    const float* s2 = reinterpret_cast<const float*>(a.rec + v.off[2]) + src * a.H2;
+    float* d1 = a.hs_cs + row * a.H2;
+    float* d2 = a.ths_cs + row * a.H2;
+    for (int k = tid; k < a.H2; k += blockDim.x) {
+      d1[k] = s1[k];
+      d2[k] = s2[k];
+    }
+  }
+  if (tid != 0) return;
+  a.action[row] = (uint8_t)(int)scalar_at(a.rec + v.off[3], v.code[3], src);
+  a.reward[row] = scalar_at(a.rec + v.off[4], 2, src);
+  a.done[row] = scalar_at(a.rec + v.off[5], v.code[5], src) > 0.f ? 1 : 0;
+  a.priority[row] = scalar_at(a.rec + v.off[7], 2, src);
+  const int st = scalar_at(a.rec + v.off[9], v.code[9], src) != 0.f;
+  const float leaf = st ? scalar_at(a.rec + v.off[8], 2, src) : 0.f;
+  const int was = a.is_start[row];
+  a.is_start[row] = (uint8_t)st;
+  if (was != st) atomicAdd(a.n_valid, st - was);
+  if (was || st || a.leaves[row] != 0.f) {
+    a.leaves[row] = leaf;
+    if (a.dirty) {
+      const int slot = atomicAdd(a.count, 1);
+      if (slot < a.max_dirty) a.dirty[slot] = (int)row;
+    }
+  }
+}
+
+__global__ void ingest_tail_kernel(const IngestArgs a) {
+  if (threadIdx.x != 0) return;
+  const long long* h = reinterpret_cast<const long long*>(a.rec);
+  if (h[0] != ING_MAGIC || h[1] < 0) return;
+  const long long keep = h[1] < a.cap_e ? h[1] : a.cap_e;
+  a.ihead[a.sub] = (a.ihead[a.sub] + keep) % a.cap_e;
+  *a.rows_total += keep;
+}
+
+extern "C" int r2_ingest_args_bytes() { return (int)sizeof(IngestArgs); }
+
+// One record -> one sub-ring.  max_rows bounds the grid (rows kept = min(n, cap_e) <= max_rows is
+// the caller's contract: it knows the record length, and rows / record >= FB bytes each).
+extern "C" int r2_ingest_record(const IngestArgs* a, void* stream) {
+  if (!a->rec || a->max_rows <= 0 || a->cap_e <= 0 || a->FB <= 0 || a->H2 <= 0) return -1;
+  if ((reinterpret_cast<uintptr_t>(a->rec) & 63) != 0) return -2;
+  const int grid = a->max_rows < a->cap_e ? a->max_rows : a->cap_e;
+  hipLaunchKernelGGL(ingest_rows_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, *a);
+  hipLaunchKernelGGL(ingest_tail_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, *a);
+  R2_CHECK_LAUNCH();
+  return 0;
+}

@@ -310,6 +310,59 @@ __global__ void mark_starts_kernel(const int* __restrict__ rows, const int* __re
   }
 }
 
+// ---- deferred start edits of a concurrent actor group (actor.hip deferred mode), applied on the
+// learner's stream between its steps: entry >= 0 marks a start (flag, eta-mix leaf, n_valid),
+// entry <= -2 clears row -2 - entry (flag, leaf, n_valid).  One wave per entry; the flag byte is
+// flipped with a word atomic so duplicate entries never double-count n_valid.  Changed leaves go to
+// the dirty list.  err bit 2: the pending list overflowed (entries were lost).
+__device__ __forceinline__ int flag_exchange(uint8_t* flags, int row, int v) {
+  unsigned* w = reinterpret_cast<unsigned*>(flags) + (row >> 2);
+  const int sh = (row & 3) * 8;
+  const unsigned old = v ? atomicOr(w, 1u << sh) : atomicAnd(w, ~(0xFFu << sh));
+  return (int)((old >> sh) & 0xFF);
+}
+
+__global__ void apply_pending_kernel(const int* __restrict__ pend, const int* __restrict__ pend_cnt,
+                                     int pend_cap, uint8_t* __restrict__ is_start,
+                                     const float* __restrict__ priority, float* __restrict__ leaves,
+                                     int T, int cap_e, float eta, int* __restrict__ n_valid,
+                                     int* __restrict__ dirty, int* __restrict__ count, int max_dirty,
+                                     unsigned* __restrict__ err) {
+  const int lane = threadIdx.x & 63;
+  const int cnt = *pend_cnt;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && cnt > pend_cap) atomicOr(err, 2u);
+  const int n = min(cnt, pend_cap);
+  const int nwv = gridDim.x * (blockDim.x >> 6);
+  for (int w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); w < n; w += nwv) {
+    const int v = pend[w];
+    if (v >= 0) {
+      float mx = 0.f, sm = 0.f;
+      for (int t = lane; t < T; t += 64) {
+        const float p = priority[ring_row_s(v, t, cap_e)];
+        mx = fmaxf(mx, p);
+        sm += p;
+      }
+      mx = wave_max(mx);
+      sm = wave_sum(sm);
+      if (lane == 0) {
+        if (!flag_exchange(is_start, v, 1)) atomicAdd(n_valid, 1);
+        leaves[v] = eta * mx + (1.f - eta) * (sm / (float)T);
+        const int slot = atomicAdd(count, 1);
+        if (slot < max_dirty) dirty[slot] = v;
+      }
+    } else if (lane == 0) {
+      const int r = -2 - v;
+      const int was = flag_exchange(is_start, r, 0);
+      if (was) atomicSub(n_valid, 1);
+      if (was || leaves[r] != 0.f) {
+        leaves[r] = 0.f;
+        const int slot = atomicAdd(count, 1);
+        if (slot < max_dirty) dirty[slot] = r;
+      }
+    }
+  }
+}
+
 // ---- time-major row list for (T x B) frames of sampled sequences: rows[t*B+b] = row(s_b, off+t)
 __global__ void make_rows_kernel(const int* __restrict__ starts, int B, int Tn, int off,
                                  int cap_e, int* __restrict__ rows) {
@@ -477,6 +530,21 @@ extern "C" int r2_mark_starts(const int* rows, const int* n_rows, int max_rows, 
   hipLaunchKernelGGL(mark_starts_kernel, dim3((max_rows + 3) / 4), dim3(256), 0,
                      (hipStream_t)stream, rows, n_rows, max_rows, is_start, priority, leaves, T,
                      cap_e, eta, n_valid, dirty, count, max_dirty);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
+// grid-stride over the pending list (fixed grid: capture-safe for any count)
+extern "C" int r2_apply_pending(const int* pend, const int* pend_cnt, int pend_cap, uint8_t* is_start,
+                                const float* priority, float* leaves, int T, int cap_e, float eta,
+                                int* n_valid, int* dirty, int* count, int max_dirty, unsigned* err,
+                                void* stream) {
+  if (pend_cap <= 0) return -1;
+  int nb = (pend_cap + 3) / 4;
+  if (nb > 512) nb = 512;
+  hipLaunchKernelGGL(apply_pending_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, pend,
+                     pend_cnt, pend_cap, is_start, priority, leaves, T, cap_e, eta, n_valid, dirty,
+                     count, max_dirty, err);
   R2_CHECK_LAUNCH();
   return 0;
 }

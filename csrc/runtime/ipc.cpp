@@ -152,9 +152,33 @@ int64_t r2rt_ring_pop(void* rp, void* out, uint32_t maxlen) {
   return len;
 }
 
+int64_t r2rt_ring_front(void* rp, const void** payload) {
+  auto* r = static_cast<Ring*>(rp);
+  uint64_t tail = r->hdr->tail.load(std::memory_order_relaxed), pos;
+  const int64_t len = ring_front(r, &tail, &pos);
+  if (len < 0) return -1;
+  *payload = r->data + pos + 4;
+  return len;
+}
+
+void r2rt_ring_release(void* rp) {
+  auto* r = static_cast<Ring*>(rp);
+  uint64_t tail = r->hdr->tail.load(std::memory_order_relaxed), pos;
+  const int64_t len = ring_front(r, &tail, &pos);
+  if (len < 0) return;
+  r->hdr->tail.store(tail + pad8(4 + (uint64_t)len), std::memory_order_release);
+}
+
 uint64_t r2rt_ring_used(void* rp) {
   auto* r = static_cast<Ring*>(rp);
   return r->hdr->head.load(std::memory_order_acquire) - r->hdr->tail.load(std::memory_order_acquire);
+}
+
+// the whole mapping (header + payload): registered with the HIP runtime for zero-copy DMA
+void* r2rt_ring_mapping(void* rp, uint64_t* len) {
+  auto* r = static_cast<Ring*>(rp);
+  *len = r->map_len;
+  return r->hdr;
 }
 
 uint64_t r2rt_ring_capacity(void* rp) { return static_cast<Ring*>(rp)->hdr->capacity; }
@@ -164,6 +188,82 @@ void r2rt_ring_close(void* rp, int unlink_it) {
   munmap(r->hdr, r->map_len);
   if (unlink_it) shm_unlink(r->name.c_str());
   delete r;
+}
+
+// ---------------------------------------------------------------- seqlock slot
+struct alignas(64) SlotHdr {
+  uint64_t magic;
+  uint64_t bytes;
+  alignas(64) std::atomic<uint64_t> seq;      // odd while a write is in progress
+  std::atomic<int64_t> version;
+};
+
+struct Slot {
+  SlotHdr* hdr;
+  uint8_t* data;
+  size_t map_len;
+  std::string name;
+};
+
+void* r2rt_slot_open(const char* name, uint64_t bytes, int create) {
+  const size_t len = sizeof(SlotHdr) + pad8(bytes);
+  void* p = map_shm(name, len, create);
+  if (!p) return nullptr;
+  auto* hdr = static_cast<SlotHdr*>(p);
+  if (create) {
+    new (&hdr->seq) std::atomic<uint64_t>(0);
+    new (&hdr->version) std::atomic<int64_t>(-1);
+    hdr->bytes = bytes;
+    std::atomic_thread_fence(std::memory_order_release);
+    hdr->magic = RING_MAGIC + 2;
+  } else if (hdr->magic != RING_MAGIC + 2 || hdr->bytes != bytes) {
+    munmap(p, len);
+    return nullptr;
+  }
+  return new Slot{hdr, static_cast<uint8_t*>(p) + sizeof(SlotHdr), len, name};
+}
+
+void r2rt_slot_write(void* sp, const void* data, uint64_t bytes, int64_t version) {
+  auto* s = static_cast<Slot*>(sp);
+  if (bytes > s->hdr->bytes) bytes = s->hdr->bytes;
+  const uint64_t q = s->hdr->seq.load(std::memory_order_relaxed);
+  s->hdr->seq.store(q + 1, std::memory_order_relaxed);
+  std::atomic_thread_fence(std::memory_order_release);
+  memcpy(s->data, data, bytes);
+  s->hdr->version.store(version, std::memory_order_relaxed);
+  s->hdr->seq.store(q + 2, std::memory_order_release);
+}
+
+int r2rt_slot_read(void* sp, void* out, uint64_t bytes, int64_t have, int64_t* version) {
+  auto* s = static_cast<Slot*>(sp);
+  if (bytes > s->hdr->bytes) bytes = s->hdr->bytes;
+  for (int attempt = 0; attempt < 64; ++attempt) {
+    const uint64_t q0 = s->hdr->seq.load(std::memory_order_acquire);
+    if (q0 & 1) {
+      usleep(50);
+      continue;
+    }
+    const int64_t v = s->hdr->version.load(std::memory_order_relaxed);
+    if (v <= have) return 0;
+    memcpy(out, s->data, bytes);
+    std::atomic_thread_fence(std::memory_order_acquire);
+    if (s->hdr->seq.load(std::memory_order_relaxed) == q0) {
+      *version = v;
+      return 1;
+    }
+  }
+  return -1;
+}
+
+int64_t r2rt_slot_version(void* sp) {
+  return static_cast<Slot*>(sp)->hdr->version.load(std::memory_order_acquire);
+}
+
+void r2rt_slot_close(void* sp, int unlink_it) {
+  auto* s = static_cast<Slot*>(sp);
+  munmap(s->hdr, s->map_len);
+  if (unlink_it) shm_unlink(s->name.c_str());
+  delete s;
 }
 
 // ---------------------------------------------------------------- fcntl locks

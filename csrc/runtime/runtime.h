@@ -30,6 +30,10 @@ void* r2rt_ring_open(const char* name, uint64_t capacity, int create);
 int r2rt_ring_push(void* r, const void* data, uint32_t len);
 int64_t r2rt_ring_pop(void* r, void* out, uint32_t maxlen);
 int64_t r2rt_ring_peek(void* r);
+// zero-copy consumer: pointer to the front record's payload (valid until r2rt_ring_release)
+int64_t r2rt_ring_front(void* r, const void** payload);
+void r2rt_ring_release(void* r);
+void* r2rt_ring_mapping(void* r, uint64_t* len);
 uint64_t r2rt_ring_used(void* r);
 uint64_t r2rt_ring_capacity(void* r);
 void r2rt_ring_close(void* r, int unlink);
@@ -49,4 +53,13 @@ uint64_t r2rt_now_ns();
 void r2rt_hb_close(void* h, int unlink);
 
 int r2rt_version();
+
+// versioned single-writer / many-reader blob in shared memory (seqlock): weight publication
+// from the learner process to CPU actor processes
+void* r2rt_slot_open(const char* name, uint64_t bytes, int create);
+void r2rt_slot_write(void* s, const void* data, uint64_t bytes, int64_t version);
+// 1 = copied a version newer than `have`, 0 = nothing newer, -1 = torn after retries
+int r2rt_slot_read(void* s, void* out, uint64_t bytes, int64_t have, int64_t* version);
+int64_t r2rt_slot_version(void* s);
+void r2rt_slot_close(void* s, int unlink);
 }

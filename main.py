@@ -7,6 +7,12 @@ for weights).  Modes:
                                                supervised, synthetic Atari env by default)
   python main.py --mode native --config pong --steps 2000
                                                MI355X-native: batched GPU actors + HIP learner
+  python main.py --mode native --config pong --concurrent --steps 2000
+                                               ... actors and learner running at the same time on
+                                               disjoint CU sets of the GPU
+  python main.py --mode native --config pong --cpu-actors 64 --steps 2000
+                                               1 GPU learner + 64 CPU actor processes (shared-
+                                               memory rings DMA'd into the HBM replay)
   torchrun --nproc-per-node 8 --master-addr 127.0.0.1 main.py --mode native --config seaquest8
                                                8-GPU data-parallel learner, actors on every GPU
   python main.py --mode inproc --config cartpole --steps 2000
@@ -37,6 +43,12 @@ def build_parser():
     p.add_argument("--capacity", type=int, default=None)
     p.add_argument("--set", nargs="*", default=[], help="dotted config overrides key=value")
     p.add_argument("--resume", default=None, help="full-state checkpoint to continue from (native)")
+    p.add_argument("--cpu-actors", type=int, default=0,
+                   help="native: N CPU actor processes feeding the GPU learner (instead of GPU actors)")
+    p.add_argument("--concurrent", action="store_true",
+                   help="native: GPU actor group and learner run simultaneously on disjoint CUs")
+    p.add_argument("--actor-cus-per-xcd", type=int, default=4)
+    p.add_argument("--actor-steps", type=int, default=1, help="native: env steps per learner step")
     return p
 
 
@@ -48,11 +60,19 @@ def run(argv=None):
     if args.env:
         overrides["env.name"] = args.env
     cfg = get_config(preset, **overrides)
-    if args.mode == "native":
+    if args.mode == "native" and args.cpu_actors > 0:
+        from pytorch_r2d2_amd.runner import run_native_cpu_actors
+        out = run_native_cpu_actors(cfg, args.cpu_actors, steps=args.steps or 1000,
+                                    capacity=args.capacity, metrics_path=args.metrics)
+        out.pop("supervisor", None)
+    elif args.mode == "native":
         from pytorch_r2d2_amd.runner import run_native
         out = run_native(cfg, steps=args.steps or 1000, metrics_path=args.metrics,
                          checkpoint_dir=args.checkpoint_dir, capacity=args.capacity,
-                         resume=args.resume)
+                         resume=args.resume, concurrent=args.concurrent,
+                         actor_cus_per_xcd=args.actor_cus_per_xcd,
+                         actor_steps_per_update=args.actor_steps)
+        out.pop("driver", None)
     elif args.mode == "inproc":
         from pytorch_r2d2_amd.runner import run_inproc
         out = run_inproc(cfg, steps=args.steps or 1000, n_actors=args.n_actors,

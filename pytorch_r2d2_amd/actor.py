@@ -38,11 +38,22 @@ from .replay.nstep import NStepMemory
 
 def actor_process(actor_id, n_actors, shared_dict, device="cuda:0", cfg: Optional[R2D2Config] = None,
                   max_steps: Optional[int] = None, max_episodes: Optional[int] = None,
-                  memory_path: Optional[str] = None):
+                  memory_path: Optional[str] = None, beat=None, shm_ring: Optional[str] = None,
+                  shm_weights: Optional[str] = None, seed: int = 0):
+    """Actor process entry.  ``beat``: supervisor heartbeat (utils/supervisor.py).  Native
+    transport (main.py --mode native --cpu-actors N): ``shm_ring`` = name of this actor's
+    shared-memory trajectory ring into the learner's HBM replay, ``shm_weights`` = the learner's
+    shared-memory weight slot (seqlock); without them the reference file / Manager-dict transport."""
     if isinstance(device, str) and device.startswith("cuda") and not torch.cuda.is_available():
         device = "cpu"
-    actor = Actor(actor_id, n_actors, shared_dict, device, cfg=cfg, memory_path=memory_path)
-    actor.run(max_steps=max_steps, max_episodes=max_episodes)
+    actor = Actor(actor_id, n_actors, shared_dict, device, cfg=cfg, memory_path=memory_path, seed=seed)
+    if shm_ring:
+        from .parallel.trajectory import ShmTrajectoryWriter
+        actor.transport = ShmTrajectoryWriter(shm_ring)
+    if shm_weights:
+        from .parallel.weights import ShmWeightsReader
+        actor.weights_reader = ShmWeightsReader(shm_weights, actor.cfg)
+    actor.run(max_steps=max_steps, max_episodes=max_episodes, beat=beat)
 
 
 class Actor:
@@ -92,6 +103,9 @@ class Actor:
         self.total_steps = 0
         self.memory_count = 0
         self.episode_returns = []
+        self.transport = None           # ShmTrajectoryWriter (native) | None (reference files)
+        self.weights_reader = None      # ShmWeightsReader (native) | None (Manager dict)
+        self.pushed_rows = 0
         self.state = self.env.reset()
 
     def _new_memory(self) -> ReplayMemory:
@@ -107,13 +121,17 @@ class Actor:
                             obs_dtype=np.float32)
 
     # ------------------------------------------------------------------ loop
-    def run(self, max_steps: Optional[int] = None, max_episodes: Optional[int] = None):
+    def run(self, max_steps: Optional[int] = None, max_episodes: Optional[int] = None, beat=None):
+        from .utils.faults import Liveness
+        live = Liveness("actor", self.actor_id, beat)
         while True:
             if max_steps is not None and self.total_steps >= max_steps:
                 break
             if max_episodes is not None and self.n_episodes >= max_episodes:
                 break
+            live.tick(self.total_steps)
             self.step()
+        self.flush()
 
     def _emit(self, q_boot, tq_boot, done):
         pre_q, state, h, c, th, tc, action, reward, stack_count = self.n_steps_memory.get()
@@ -189,15 +207,37 @@ class Actor:
         self.stack_count = max(1, self.n_stacks // self.action_repeat)
         self.n_steps_memory = NStepMemory(self.bootstrap_steps, self.gamma, legacy=self.legacy)
         if self.n_episodes % self.memory_save_interval == 0:
-            self.replay_memory.save(self.memory_path, self.actor_id)
-            self.replay_memory = self._new_memory()
-            self.episode_start_index = 0
-            gc.collect()
+            self.flush()
         if self.n_episodes % self.net_load_interval == 0:
             self.load_model()
 
+    def flush(self) -> None:
+        """Ship the local replay to the learner (replay_memory.py:125-152 file save, or one record
+        into the shared-memory ring of the native transport) and start a new one."""
+        if self.replay_memory.size == 0:
+            return
+        if self.transport is not None:
+            from .utils.faults import faults
+            mem = {k: v[: self.replay_memory.size] for k, v in self.replay_memory.memory.items()}
+            if not faults().drop("push", self.actor_id):
+                self.transport.push(mem)
+                self.pushed_rows += self.replay_memory.size
+        else:
+            self.replay_memory.save(self.memory_path, self.actor_id)
+        self.replay_memory = self._new_memory()
+        self.episode_start_index = 0
+        gc.collect()
+
     def load_model(self):
         """actor.py:137-142; reads a consistent (net, target) pair published under one version."""
+        if self.weights_reader is not None:
+            got = self.weights_reader.fetch(self.weights_version)
+            if got is not None:
+                sd_on, sd_tg, v = got
+                self.net.load_state_dict(sd_on)
+                self.target_net.load_state_dict(sd_tg)
+                self.weights_version = v
+            return got is not None
         try:
             sd = self.shared_dict
             self.net.load_state_dict(sd["net_state"])

@@ -47,10 +47,12 @@ class ActArgs(ctypes.Structure):
         (name, _VP * 2) for name in ("st_h", "st_c", "h_new", "c_new", "h32", "c", "h_bf")] + [
         (name, _VP) for name in (
             "h_row", "h_q", "h_a", "h_r", "h_step", "h_valid", "ep_start", "t", "head", "eps", "act",
-            "env_reward", "env_done", "env_finished", "ret_ring", "ret_cnt", "marks")] + [
+            "env_reward", "env_done", "env_finished", "ret_ring", "ret_cnt", "marks", "pend",
+            "pend_cnt")] + [
         ("FB", ctypes.c_longlong), ("seed", ctypes.c_ulonglong)] + [
         (name, ctypes.c_int) for name in ("E", "A", "H", "n", "T", "stride", "cap_e", "W", "wrap",
-                                          "max_dirty", "R", "value_rescale")] + [
+                                          "max_dirty", "R", "value_rescale", "pend_cap",
+                                          "defer_D")] + [
         (name, ctypes.c_float) for name in ("gamma", "gamma_n", "prio_eps", "alpha", "vr_eps")]
 
 
@@ -157,8 +159,28 @@ class BatchedActor:
         self._returns = []
         self.env_steps = 0
         self.graphs = None
+        # concurrent topology (engine/concurrent.py): start edits go to one of two pending lists
+        # (round parity) instead of the tree, and the LSTM runs as the plain step kernel (no
+        # persistent co-residency requirement on the actor's few CUs)
+        self.defer = None            # dict(pend=[2 x int32], cnt=[2 x int32], cap, D)
+        self.lstm_step = False
+        self.n_workers = 256         # torso workgroups (grid-stride over frames)
         if hasattr(env, "reset_all"):
             env.reset_all()
+
+    def set_weights(self, online, target) -> None:
+        """Point inference at other packed weights (captured graphs must be re-captured)."""
+        self.online, self.target = online, target
+        self.graphs = None
+
+    def enable_deferred(self, pend, cnt, cap: int, lookahead: int) -> None:
+        """Deferred (concurrent) mode: ``pend``/``cnt`` = two pending lists + counts (round
+        parity); rows are invalidated ``lookahead`` steps ahead of the write head."""
+        if self.replay.cap_e <= lookahead + self.T + self.n:
+            raise ValueError(f"sub-ring of {self.replay.cap_e} rows too small for lookahead {lookahead}")
+        self.defer = dict(pend=pend, cnt=cnt, cap=int(cap), D=int(lookahead))
+        self.lstm_step = True
+        self.graphs = None
 
     @property
     def finished_returns(self):
@@ -186,19 +208,36 @@ class BatchedActor:
                 [[0, E, ptr(w.pk["conv1"]), ptr(w.pk["b1"]), ptr(w.pk["conv2"]), ptr(w.pk["b2"]),
                   ptr(w.pk["conv3"]), ptr(w.pk["b3"]), ptr(self.Xn[key]), 0, 0, 0] for key, w in nets],
                 dtype=np.int64)
-            check(k.r2_torso_fwd_multi(ptr(self.env.frames), self._tjobs.ctypes.data, 2, 256, 0, 0, s),
+            check(k.r2_torso_fwd_multi(ptr(self.env.frames), self._tjobs.ctypes.data, 2,
+                                       self.n_workers, 0, 0, s),
                   "torso_fwd_multi")
         else:
             for key, w in nets:
                 torso_forward_library(self.env.frames.reshape(E, -1), None, L, w.flat, self.cfg.env,
                                       self.cfg.model, self.Xn[key])
         gemm(*[Gemm(self.Xn[key], w.pk["w_ih"].t(), self.xp[key], bias=w.lstm_b) for key, w in nets])
-        self._chains = np.asarray(
-            [[ptr(self.xp[key]), ptr(w.pk["w_hh"]), ptr(self.h_bf[key]), ptr(self.c[key]),
-              ptr(self.h_bf_new[key]), ptr(self.c_new[key]), ptr(self.h32_new[key]), 0, 0]
-             for key, w in nets], dtype=np.int64)
-        check(k.r2_lstm_fwd_persist(self._chains.ctypes.data, 2, E, 1, H, ptr(self.ctr),
-                                    ptr(self.err), s), "lstm_step")
+        if self.lstm_step:
+            # plain step kernel (lstm.hip, <= 128 rows per chain): no inter-workgroup hand-off,
+            # so it runs on any CU subset; E > 128 is split into two row halves per net
+            Bc = E if E <= 128 else (E + 1) // 2
+            if E > 128 and (E % 2 or Bc > 128):
+                raise ValueError("step-kernel LSTM: E <= 128 or an even E <= 256")
+            G = self.layout.G
+            rows = [(r0, Bc) for r0 in range(0, E, Bc)]
+            self._chains = np.asarray(
+                [[ptr(self.xp[key]) + r0 * G * 4, ptr(w.pk["w_hh"]), ptr(self.h_bf[key]) + r0 * H * 2,
+                  ptr(self.c[key]) + r0 * H * 4, ptr(self.h_bf_new[key]) + r0 * H * 2,
+                  ptr(self.c_new[key]) + r0 * H * 4, ptr(self.h32_new[key]) + r0 * H * 4, 0, 0]
+                 for key, w in nets for r0, _ in rows], dtype=np.int64)
+            check(k.r2_lstm_fwd(self._chains.ctypes.data, len(self._chains), Bc, 1, H, 0, s),
+                  "lstm_step_kernel")
+        else:
+            self._chains = np.asarray(
+                [[ptr(self.xp[key]), ptr(w.pk["w_hh"]), ptr(self.h_bf[key]), ptr(self.c[key]),
+                  ptr(self.h_bf_new[key]), ptr(self.c_new[key]), ptr(self.h32_new[key]), 0, 0]
+                 for key, w in nets], dtype=np.int64)
+            check(k.r2_lstm_fwd_persist(self._chains.ctypes.data, 2, E, 1, H, ptr(self.ctr),
+                                        ptr(self.err), s), "lstm_step")
         gemm(*[Gemm(self.h_bf_new[key], w.pk["head1"].t(), self.zh[key]) for key, w in nets])
         self._djobs = np.asarray(
             [[ptr(self.zh[key]), ptr(w.pk["head_b1"]), ptr(w.pk["head_w2"]), ptr(w.pk["head_b2"]),
@@ -219,32 +258,35 @@ class BatchedActor:
         side = torch.cuda.Stream(device=self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         gens = [self.env.g] if hasattr(self.env, "g") else []
-        graphs, pool = [], None
-        for wrap in (False, True):
-            g = torch.cuda.CUDAGraph()
-            for gen in gens:
-                g.register_generator_state(gen)
-            with torch.cuda.graph(g, pool=pool, stream=side):
-                self._body(wrap)
-            pool = g.pool()
-            graphs.append(g)
+        graphs, pool = {}, None
+        # variants: (sub-ring wrap step?, pending-list parity) -- parity only in deferred mode
+        for parity in ((0, 1) if self.defer else (0,)):
+            for wrap in (False, True):
+                g = torch.cuda.CUDAGraph()
+                for gen in gens:
+                    g.register_generator_state(gen)
+                with torch.cuda.graph(g, pool=pool, stream=side):
+                    self._body(wrap, parity)
+                pool = g.pool()
+                graphs[(wrap, parity)] = g
         torch.cuda.current_stream(self.device).wait_stream(side)
         self.graphs = graphs
 
     @torch.no_grad()
-    def step(self):
+    def step(self, parity: int = 0):
+        """One env step of every env.  ``parity``: pending list of the current round (deferred)."""
         wrap = self.head == 0
         if self.graphs is not None:
-            self.graphs[int(wrap)].replay()
+            self.graphs[(wrap, parity if self.defer else 0)].replay()
         else:
-            self._body(wrap)
+            self._body(wrap, parity)
         rp = self.replay
         self.t += 1
         self.head = (self.head + 1) % rp.cap_e
         rp.total_written += self.E
         self.env_steps += self.E
 
-    def _args(self, wrap: bool) -> ActArgs:
+    def _args(self, wrap: bool, parity: int = 0) -> ActArgs:
         rp, rc, lc = self.replay, self.cfg.replay, self.cfg.learner
         pre = rc.stored_state == "pre"
         a = ActArgs()
@@ -267,24 +309,28 @@ class BatchedActor:
         a.E, a.A, a.H, a.n, a.T, a.stride = self.E, self.A, self.H, self.n, self.T, self.stride
         a.cap_e, a.W, a.wrap = rp.cap_e, self.T + self.n, int(wrap)
         a.max_dirty, a.R, a.value_rescale = rp.max_dirty, self.R, int(lc.value_rescale)
+        if self.defer:
+            a.pend, a.pend_cnt = ptr(self.defer["pend"][parity]), ptr(self.defer["cnt"][parity])
+            a.pend_cap, a.defer_D = self.defer["cap"], self.defer["D"]
         a.gamma, a.gamma_n = self.gamma, self.gamma_n
         a.prio_eps, a.alpha, a.vr_eps = rc.priority_eps, rc.alpha, lc.value_rescale_eps
         return a
 
-    def _body(self, wrap: bool):
+    def _body(self, wrap: bool, parity: int = 0):
         """One env step for all E envs, device-only (no host sync, capture-safe): inference of
         both nets, then actor.hip's fused bookkeeping around the device env step."""
         k = kernels()
         s = stream_handle()
         self._infer()
-        a = self._args(wrap)
+        a = self._args(wrap, parity)
         check(k.r2_actor_pre(ctypes.byref(a), s), "actor_pre")
         reward, done, finished = self.env.step(self.act)
         a.env_reward, a.env_finished = ptr(reward.float().contiguous()), ptr(finished.contiguous())
         a.env_done = ptr(done.to(torch.bool).contiguous())
         check(k.r2_actor_post(ctypes.byref(a), s), "actor_post")
-        self.replay.mark_starts(self.marks)
-        self.replay.update_tree()
+        if not self.defer:   # deferred: the learner's stream applies the pending list
+            self.replay.mark_starts(self.marks)
+            self.replay.update_tree()
         check(k.r2_actor_tail(ctypes.byref(a), s), "actor_tail")
 
     def run(self, n_steps: int):

@@ -115,7 +115,8 @@ class LearnerEngine:
         return 0
 
     def __init__(self, cfg: R2D2Config, replay: HBMReplay, device="cuda", rank: int = 0,
-                 world: int = 1, process_group=None, init_module: Optional[QNet] = None):
+                 world: int = 1, process_group=None, init_module: Optional[QNet] = None,
+                 n_cus: Optional[int] = None):
         self.cfg = cfg
         self.device = torch.device(device)
         self.replay = replay
@@ -129,8 +130,9 @@ class LearnerEngine:
         self.layout = L = ParamLayout(m, e)
         d = self.device
         # compute units of THIS device (never assume 256: a partitioned MI355X exposes fewer); the
-        # persistent kernels need their whole grid co-resident, one workgroup per CU
-        self.n_cus = device_cus(d)
+        # persistent kernels need their whole grid co-resident, one workgroup per CU.  ``n_cus``:
+        # the CUs of the learner's CU-masked stream when it shares the chip (engine/concurrent.py)
+        self.n_cus = int(n_cus) if n_cus else device_cus(d)
         if d.type == "cuda":
             kernels().r2_set_num_cus(self.n_cus)
         if init_module is None:

@@ -90,6 +90,11 @@ class HBMReplay:
         self.seed = int(cfg.seed) * 0x9E3779B1 + 12345
         self.heads = np.zeros(n_sub, dtype=np.int64)   # per-sub-ring write heads (host mirror)
         self.total_written = 0
+        # trajectory ingest (engine/ingest.py, csrc/kernels/ingest.hip): device-side sub-ring
+        # write heads, rows counter and malformed-record flag
+        self.ihead = torch.zeros(n_sub, dtype=torch.int64, device=d)
+        self.rows_total_d = torch.zeros(1, dtype=torch.int64, device=d)
+        self.ingest_err = torch.zeros(1, dtype=torch.int32, device=d)
 
     # ------------------------------------------------------------------ properties
     @property
@@ -241,25 +246,68 @@ class HBMReplay:
         torch.cuda.synchronize(d) if d.type == "cuda" else None
 
     # ------------------------------------------------------------------ ingestion (host -> HBM)
+    def repair_after_ingest(self, full: bool = False) -> None:
+        """Sum-tree repair after ingest launches: the dirty list, or a full rebuild when a record
+        was too large for it."""
+        if full:
+            self.rebuild_tree()
+        else:
+            self.update_tree()
+        self.dirty_count.zero_()
+
+    def ingest_device_record(self, rec: torch.Tensor, head: Optional[np.ndarray], subring: int,
+                             repair: bool = True) -> int:
+        """Scatter a packed record (``parallel.trajectory.pack_rows``) that already lives in device
+        memory (64-byte aligned) into sub-ring ``subring`` (csrc/kernels/ingest.hip).  ``head``:
+        the record header on the host if known (only to report the row count)."""
+        from ..parallel.trajectory import record_layout
+        from .ingest import ingest_args
+        n = record_layout(head)[0] if head is not None else 0
+        use_dirty = head is not None and min(n, self.cap_e) * 2 <= self.max_dirty
+        a = ingest_args(self, ptr(rec), rec.numel(), subring, use_dirty)
+        import ctypes
+        check(kernels().r2_ingest_record(ctypes.byref(a), ctypes.c_void_p(stream_handle())), "ingest")
+        if repair:
+            self.repair_after_ingest(full=not use_dirty)
+        kept = min(n, self.cap_e)
+        self.total_written += kept
+        return kept
+
     @torch.no_grad()
     def ingest_memory(self, mem, subring: Optional[int] = None) -> int:
         """Write a ReplayMemory-schema dict (numpy / tensors, e.g. an actor transport file) as a
-        contiguous block into one sub-ring; sequence starts / priorities come with the block."""
+        contiguous block into one sub-ring: packed once on the host, one async H2D copy, then the
+        device ingest kernel (no host read-back, dirty-list tree repair)."""
+        from ..parallel.trajectory import pack_rows
         n = int(mem["state"].shape[0])
         if n == 0:
             return 0
         sub = (self.total_written // max(n, 1)) % self.n_sub if subring is None else subring % self.n_sub
+        mem = {k: (v.numpy() if isinstance(v, torch.Tensor) else np.asarray(v)) for k, v in mem.items()}
+        if self.obs is not None:
+            return self._ingest_obs(mem, sub)
+        buf = pack_rows(mem)
+        host = torch.from_numpy(buf)
+        if self.device.type == "cuda":
+            host = host.pin_memory()
+        dev = torch.empty(buf.size + 64, dtype=torch.uint8, device=self.device)
+        off = (-dev.data_ptr()) % 64
+        rec = dev[off: off + buf.size]
+        rec.copy_(host, non_blocking=True)
+        kept = self.ingest_device_record(rec, buf[:512], sub)
+        self._keep_alive = (host, dev)     # until the async copy has been consumed
+        return kept
+
+    def _ingest_obs(self, mem, sub: int) -> int:
+        """Vector observations (fp32 rows, CartPole): torch scatter path."""
+        n = int(mem["state"].shape[0])
         keep = min(n, self.cap_e)
         sl = slice(n - keep, n)
         head = int(self.heads[sub])
         base = sub * self.cap_e
         rows = torch.as_tensor(base + (head + np.arange(keep)) % self.cap_e, device=self.device)
-        t = lambda k, dt=None: torch.as_tensor(np.asarray(mem[k])[sl]).to(self.device)  # noqa: E731
-        st = t("state")
-        if self.obs is not None:
-            self.obs[rows] = st.reshape(keep, -1).float()
-        else:
-            self.frames[rows] = st.reshape(keep, -1).to(torch.uint8)
+        t = lambda k: torch.as_tensor(np.asarray(mem[k])[sl]).to(self.device)  # noqa: E731
+        self.obs[rows] = t("state").reshape(keep, -1).float()
         self.hs_cs[rows] = t("hs_cs").float()
         self.target_hs_cs[rows] = t("target_hs_cs").float()
         self.action[rows] = t("action").reshape(-1).to(torch.uint8)
@@ -267,11 +315,12 @@ class HBMReplay:
         self.done[rows] = (t("done").reshape(-1) > 0).to(torch.uint8)
         self.priority[rows] = t("priority").reshape(-1).float()
         starts = t("is_seq_start").reshape(-1).to(torch.uint8)
+        old = self.is_start[rows].to(torch.int32)
+        self.n_valid.add_((starts.to(torch.int32) - old).sum().view(1).to(torch.int32))
         self.is_start[rows] = starts
         self.tree[rows] = t("sequence_priority").reshape(-1).float() * starts.float()
         self.heads[sub] = (head + keep) % self.cap_e
         self.total_written += keep
-        self.n_valid.fill_(int(self.is_start.sum().item()))
         self.rebuild_tree()
         return keep
 

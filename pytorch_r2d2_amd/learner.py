@@ -37,10 +37,10 @@ from .utils.metrics import MetricsLogger
 
 def learner_process(n_actors, shared_dict, device: Optional[str] = None, cfg: Optional[R2D2Config] = None,
                     max_steps: Optional[int] = None, memory_path: Optional[str] = None,
-                    metrics_path: Optional[str] = None):
+                    metrics_path: Optional[str] = None, beat=None):
     learner = Learner(n_actors, shared_dict, device=device, cfg=cfg, memory_path=memory_path,
                       metrics_path=metrics_path)
-    learner.run(max_steps=max_steps)
+    learner.run(max_steps=max_steps, beat=beat)
 
 
 def _pick_backend(cfg: R2D2Config, device: str) -> str:
@@ -133,8 +133,14 @@ class Learner:
                 print(f"ingest error actor {i}: {e!r}", flush=True)
         return n
 
-    def run(self, max_steps: Optional[int] = None, idle_sleep: float = 0.01):
+    def run(self, max_steps: Optional[int] = None, idle_sleep: float = 0.01, beat=None):
+        """learner.py:53-66, plus liveness: heartbeat + fault hooks every iteration and, on the
+        HIP backend, the persistent kernels' error word at every weight publication (a timed-out
+        hand-off raises instead of training on garbage state)."""
+        from .utils.faults import Liveness
+        live = Liveness("learner", 0, beat)
         while max_steps is None or self.n_epochs < max_steps:
+            live.tick(self.n_epochs)
             if self.replay_size() > self.initial_exploration:
                 self.train()
                 self.n_epochs += 1
@@ -196,6 +202,8 @@ class Learner:
         if self.n_epochs % self.target_update_interval == 0 and self.backend == "torch":
             self.target_net.load_state_dict(self.net.state_dict())
         if self.n_epochs % self.net_save_interval == 0:
+            if self.backend == "hip":
+                self.engine.check_errors()
             self.save_model()
         if self.n_epochs % self.memory_load_interval == 0:
             self.ingest()

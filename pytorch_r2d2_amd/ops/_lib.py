@@ -96,6 +96,14 @@ _SIGS = {
     "r2_lstm_bwd_tag_hg_ok": [I, I, I],
     "r2_lstm_bwd_tag_ring_bytes": [I, I],
     "r2_lstm_bwd_persist": [P, P, P, P, P, P, P, I, I, I, I, P, P, P],
+    "r2_apply_pending": [P, P, I, P, P, P, I, I, F, P, P, P, I, P, P],
+    "r2_stream_create_cumask": [P, I, P],
+    "r2_stream_get_cumask": [P, P, I],
+    "r2_stream_destroy": [P],
+    "r2_cu_probe": [P, I, I, P],
+    "r2_memcpy_h2d_async": [P, P, I64, P],
+    "r2_host_register": [P, I64],
+    "r2_host_unregister": [P],
 }
 
 

@@ -8,13 +8,16 @@ Two MI355X-native transports, both moving *packed rows* (uint8 frames + fp32 [h|
 scalars, the §2.5 schema) in fixed-size chunks:
 
 * ``RcclTrajectoryChannel`` -- GPU actor groups on one rank, learner replay shard on another:
-  a chunk is one ``dist.send`` of a header tensor + one of a packed byte tensor (device memory,
-  RCCL over xGMI), received with ``dist.recv`` directly into device memory and written into
-  the HBM replay with ``HBMReplay.ingest_memory``.
+  a chunk is one ``dist.send`` of a size tensor + one of a packed byte tensor (device memory,
+  RCCL over xGMI), received with ``dist.recv`` into device memory and scattered into the HBM
+  replay by the ingest kernel (``HBMReplay.ingest_device_record``) -- the bytes never visit the
+  host.
 * ``ShmTrajectoryWriter/Reader`` -- CPU actor processes on the same host: records go through
-  the native shared-memory SPSC ring (``runtime.ShmRing``) -- no files, no pickles, no locks.
+  the native shared-memory SPSC ring (``runtime.ShmRing``) -- no files, no pickles, no locks --
+  and the learner DMAs them into HBM (``engine/ingest.py``).
 
-``pack_rows`` / ``unpack_rows`` define the wire format (a single uint8 buffer + header).
+``pack_rows`` / ``unpack_rows`` define the wire format (a single uint8 buffer: header + SoA
+fields at 64-byte aligned offsets, ``record_layout``).
 """
 from __future__ import annotations
 
@@ -31,37 +34,67 @@ ORDER = ("state", "hs_cs", "target_hs_cs", "action", "reward", "done", "stack_co
 MAGIC = 0x52324454  # "R2DT"
 
 
+ALIGN = 64          # every field starts 64-byte aligned (16-byte vector loads on the device)
+CODES = {np.dtype(np.uint8): 0, np.dtype(np.int8): 1, np.dtype(np.float32): 2}
+
+
+def _pad(x: int) -> int:
+    return (x + ALIGN - 1) // ALIGN * ALIGN
+
+
+def record_layout(buf_head: np.ndarray):
+    """Parse a record header -> (n_rows, {name: (code, per_row, nbytes, byte offset)})."""
+    head = np.asarray(buf_head[:24], dtype=np.uint8).view(np.int64)
+    if int(head[0]) != MAGIC:
+        raise ValueError("bad trajectory record")
+    n, k = int(head[1]), int(head[2])
+    meta = np.asarray(buf_head[24:24 + 24 * k], dtype=np.uint8).view(np.int64).reshape(k, 3)
+    off = _pad(24 + 24 * k)
+    fields = {}
+    for name, (code, per_row, nbytes) in zip(ORDER, meta):
+        fields[name] = (int(code), int(per_row), int(nbytes), off)
+        off += _pad(int(nbytes))
+    return n, fields
+
+
+def header_bytes(k: int = len(ORDER)) -> int:
+    return _pad(24 + 24 * k)
+
+
 def pack_rows(mem: Dict[str, np.ndarray]) -> np.ndarray:
-    """Row-schema dict -> one contiguous uint8 buffer: [header int64 x (3 + 3*K)] + payloads."""
+    """Row-schema dict -> one contiguous uint8 record: header int64 x (3 + 3*K), then every field
+    (SoA, the §2.5 schema) at a 64-byte aligned offset."""
     n = int(np.asarray(mem["state"]).shape[0])
-    parts, meta = [], []
+    arrs, meta = [], []
     for k in ORDER:
         a = np.ascontiguousarray(np.asarray(mem[k]))
-        code = {np.dtype(np.uint8): 0, np.dtype(np.int8): 1, np.dtype(np.float32): 2}[a.dtype]
+        if a.dtype == np.bool_:
+            a = a.astype(np.uint8)
         per_row = int(a.size // max(n, 1)) if n else int(np.prod(a.shape[1:]))
-        meta += [code, per_row, a.nbytes]
-        parts.append(a.view(np.uint8).reshape(-1))
+        meta += [CODES[a.dtype], per_row, a.nbytes]
+        arrs.append(a)
+    total = header_bytes() + sum(_pad(a.nbytes) for a in arrs)
+    out = np.zeros(total, dtype=np.uint8)
     hdr = np.asarray([MAGIC, n, len(ORDER)] + meta, dtype=np.int64).view(np.uint8)
-    return np.concatenate([hdr] + parts)
+    out[: hdr.size] = hdr
+    off = header_bytes()
+    for a in arrs:
+        out[off: off + a.nbytes] = a.view(np.uint8).reshape(-1)
+        off += _pad(a.nbytes)
+    return out
 
 
 def unpack_rows(buf: np.ndarray, state_shape=None) -> Dict[str, np.ndarray]:
     buf = np.asarray(buf, dtype=np.uint8)
-    head = buf[:24].view(np.int64)
-    if int(head[0]) != MAGIC:
-        raise ValueError("bad trajectory record")
-    n, k = int(head[1]), int(head[2])
-    meta = buf[24:24 + 24 * k].view(np.int64).reshape(k, 3)
-    off = 24 + 24 * k
+    n, fields = record_layout(buf)
     out = {}
     dts = {0: np.uint8, 1: np.int8, 2: np.float32}
-    for name, (code, per_row, nbytes) in zip(ORDER, meta):
-        a = buf[off:off + int(nbytes)].view(dts[int(code)])
-        off += int(nbytes)
+    for name, (code, per_row, nbytes, off) in fields.items():
+        a = buf[off:off + nbytes].view(dts[code])
         if name == "state" and state_shape is not None:
             a = a.reshape(n, *state_shape)
         elif per_row > 1:
-            a = a.reshape(n, int(per_row))
+            a = a.reshape(n, per_row)
         elif name in ("action", "reward", "done"):
             a = a.reshape(n, 1)
         out[name] = a
@@ -116,8 +149,21 @@ class RcclTrajectoryChannel:
         dist.send(buf, dst, group=self.group)
 
     def recv(self, src: int, state_shape=None) -> Dict[str, np.ndarray]:
+        """Host copy of a record (tests / tools); the learner path is ``recv_into``."""
+        buf = self._recv_buf(src)
+        return unpack_rows(buf.cpu().numpy(), state_shape)
+
+    def _recv_buf(self, src: int) -> torch.Tensor:
         size = torch.zeros(1, dtype=torch.int64, device=self.device)
         dist.recv(size, src, group=self.group)
+        # the record length is the only value read on the host (it sizes the receive buffer)
         buf = torch.empty(int(size.item()), dtype=torch.uint8, device=self.device)
         dist.recv(buf, src, group=self.group)
-        return unpack_rows(buf.cpu().numpy(), state_shape)
+        return buf
+
+    def recv_into(self, replay, src: int, subring: int) -> int:
+        """Receive one record straight into the HBM replay's sub-ring ``subring``: the payload
+        stays in device memory and the ingest kernel scatters it (no D2H).  Returns rows."""
+        buf = self._recv_buf(src)
+        head = buf[: header_bytes()].cpu().numpy()       # header only (<= 320 bytes)
+        return replay.ingest_device_record(buf, head, subring)

@@ -26,23 +26,37 @@ from .config import R2D2Config
 def run_native(cfg: R2D2Config, steps: int = 1000, actor_steps_per_update: int = 1,
                warmup_rows: Optional[int] = None, metrics_path: Optional[str] = None,
                checkpoint_dir: Optional[str] = None, log_every: int = 100, use_graph: bool = True,
-               capacity: Optional[int] = None, resume: Optional[str] = None) -> Dict:
+               capacity: Optional[int] = None, resume: Optional[str] = None,
+               concurrent: bool = False, actor_cus_per_xcd: int = 4, beat=None,
+               check_every: int = 200, on_step=None) -> Dict:
+    """``concurrent``: actor group and learner run simultaneously on disjoint CU sets
+    (engine/concurrent.py; ``actor_steps_per_update`` env steps per learner step), else they
+    alternate on one stream.  ``beat``: supervisor heartbeat; the persistent kernels' error word
+    is checked every ``check_every`` steps (a hand-off timeout stops the run with an error)."""
     from .actor_batched import BatchedActor, engine_weights
     from .engine.learner_engine import LearnerEngine
     from .engine.replay_hbm import HBMReplay
     from .envs.synthetic import VecSyntheticAtari
     from .parallel.dist import init_distributed
     from .utils.checkpoint import save_full_checkpoint, save_reference_checkpoint
+    from .utils.faults import Liveness
     from .utils.metrics import MetricsLogger
 
     info = init_distributed()
     dev = info.device
     E = cfg.actor.envs_per_actor
     torch.manual_seed(cfg.seed)
+    s_act = s_learn = None
+    n_cus_learner = None
+    n_cus_actor = 256
+    if concurrent and dev.type == "cuda" and actor_cus_per_xcd > 0:
+        from .parallel.placement import split_chip
+        s_act, s_learn, n_cus_actor, n_cus_learner = split_chip(dev, actor_cus_per_xcd)
     replay = HBMReplay(cfg, dev, capacity=capacity or cfg.replay.capacity, n_subrings=E)
     import torch.distributed as dist
     eng = LearnerEngine(cfg, replay, dev, rank=info.rank, world=info.world,
-                        process_group=dist.group.WORLD if info.world > 1 else None)
+                        process_group=dist.group.WORLD if info.world > 1 else None,
+                        n_cus=n_cus_learner)
     env = VecSyntheticAtari(E, dev, seed=cfg.seed + 101 * info.rank, episode_len=cfg.env.episode_len,
                             n_actions=cfg.model.n_actions,
                             n_stacks=cfg.env.channels_per_frame * cfg.env.n_stacks,
@@ -58,45 +72,190 @@ def run_native(cfg: R2D2Config, steps: int = 1000, actor_steps_per_update: int =
     actor = BatchedActor(cfg, replay, env, on, tg, global_env_offset=info.rank * E,
                          total_envs=info.world * E, seed=cfg.seed + info.rank)
     mlog = MetricsLogger(metrics_path, rank=info.rank) if metrics_path else None
+    live = Liveness("learner", info.rank, beat)
     warm = warmup_rows if warmup_rows is not None else min(cfg.learner.initial_exploration,
                                                            replay.capacity // 2)
     t0 = time.perf_counter()
     while replay.total_written < warm or int(replay.n_valid.item()) < cfg.learner.batch_size:
         actor.step()
+        live.tick(0)
     if info.world > 1:
         dist.barrier()
     t_warm = time.perf_counter() - t0
     if use_graph and cfg.learner.use_graph:
         eng.capture(warmup=1)
-    if use_graph and cfg.actor.use_graph and actor.can_capture:
+    drv = None
+    if concurrent:
+        from .engine.concurrent import ConcurrentDriver
+        actor.n_workers = n_cus_actor
+        drv = ConcurrentDriver(eng, actor, steps_per_round=actor_steps_per_update,
+                               actor_stream=s_act.stream if s_act else None,
+                               learner_stream=s_learn.stream if s_learn else None,
+                               capture=use_graph and cfg.actor.use_graph and actor.can_capture)
+        if on_step is not None:
+            drv.on_learner_step = on_step
+    elif use_graph and cfg.actor.use_graph and actor.can_capture:
         actor.capture(warmup=1)
     losses = []
+    env0 = actor.env_steps
     t1 = time.perf_counter()
     for it in range(steps):
-        for _ in range(actor_steps_per_update):
-            actor.step()
-        eng.step()
+        live.tick(start + it)
+        if drv is not None:
+            drv.round()
+        else:
+            for _ in range(actor_steps_per_update):
+                actor.step()
+            eng.step()
+            if on_step is not None:
+                on_step(it)
+        if check_every and (it + 1) % check_every == 0:
+            eng.check_errors()
         if (it + 1) % log_every == 0 or it == steps - 1:
+            if drv is not None:
+                torch.cuda.current_stream(dev).wait_stream(drv.s_learn)
             loss = eng.loss_value()
             losses.append(loss)
             rets = actor.finished_returns[-64:]
+            el = time.perf_counter() - t1
             rec = dict(step=it + 1, loss=loss, replay_rows=replay.size,
                        n_valid=int(replay.n_valid.item()), env_steps=actor.env_steps,
                        mean_return=float(np.mean(rets)) if rets else None,
-                       learner_steps_per_s=(it + 1) / (time.perf_counter() - t1))
+                       learner_steps_per_s=(it + 1) / el,
+                       env_steps_per_s=(actor.env_steps - env0) / el)
             if mlog:
                 mlog.log("native", **rec)
             if info.is_main:
                 print("[native]", rec, flush=True)
         if checkpoint_dir and info.is_main and (start + it + 1) % cfg.learner.checkpoint_interval == 0:
+            if drv is not None:
+                torch.cuda.current_stream(dev).wait_stream(drv.s_learn)
             save_reference_checkpoint(eng.state_dict(), start + it + 1, checkpoint_dir)
+    if drv is not None:
+        drv.finish()
+        drv.check_errors()
     torch.cuda.synchronize(dev)
+    train_s = time.perf_counter() - t1
     eng.check_errors()
-    out = {"steps": steps, "warmup_s": t_warm, "train_s": time.perf_counter() - t1,
-           "losses": losses, "returns": list(actor.finished_returns), "env_steps": actor.env_steps}
+    out = {"steps": steps, "warmup_s": t_warm, "train_s": train_s,
+           "learner_steps_per_s": steps / train_s,
+           "env_steps_per_s": (actor.env_steps - env0) / train_s,
+           "losses": losses, "returns": list(actor.finished_returns), "env_steps": actor.env_steps,
+           "concurrent": bool(concurrent), "learner_cus": eng.n_cus,
+           "weights_version": drv.version if drv is not None else None}
     if checkpoint_dir and info.is_main:
         save_full_checkpoint(os.path.join(checkpoint_dir, "full_last.pt"), eng.state_dict(),
                              eng.target_state_dict(), None, start + steps, cfg, eng.full_state_extra())
+    if drv is not None:
+        out["driver"] = drv
+    for s_ in (s_act, s_learn):
+        if s_ is not None:
+            s_.close()
+    return out
+
+
+def run_native_cpu_actors(cfg: R2D2Config, n_actors: int, steps: int = 1000,
+                          actor_max_steps: Optional[int] = None, warmup_rows: Optional[int] = None,
+                          capacity: Optional[int] = None, log_every: int = 100,
+                          use_graph: bool = True, stall_timeout_s: float = 60.0,
+                          timeout_s: Optional[float] = None, ring_bytes: int = 256 << 20,
+                          metrics_path: Optional[str] = None) -> Dict:
+    """BASELINE config 2 topology: ONE learner process on the GPU (HBM replay, HIP learner) fed by
+    ``n_actors`` CPU actor processes (the reference ``Actor`` with its env on the CPU) through the
+    native transport -- shared-memory trajectory rings DMA'd into HBM (engine/ingest.py) and a
+    shared-memory weight slot (parallel/weights.py ShmWeightsWriter) -- under the supervisor
+    (dead / stalled actors are restarted as fresh processes)."""
+    import uuid
+
+    from .actor import actor_process
+    from .engine.ingest import HBMIngestor
+    from .engine.learner_engine import LearnerEngine
+    from .engine.replay_hbm import HBMReplay
+    from .parallel.dist import init_distributed
+    from .parallel.weights import ShmWeightsWriter
+    from .utils.metrics import MetricsLogger
+    from .utils.supervisor import RoleSpec, Supervisor
+
+    info = init_distributed()
+    dev = info.device
+    torch.manual_seed(cfg.seed)
+    replay = HBMReplay(cfg, dev, capacity=capacity or cfg.replay.capacity, n_subrings=n_actors)
+    eng = LearnerEngine(cfg, replay, dev)
+    tag = f"{os.getpid()}_{uuid.uuid4().hex[:6]}"
+    ring_names = [f"/r2d2_traj_{tag}_{i}" for i in range(n_actors)]
+    ingest = HBMIngestor(replay, ring_names, ring_bytes=ring_bytes)
+    wname = f"/r2d2_w_{tag}"
+    weights = ShmWeightsWriter(wname, eng.layout.padded, dev)
+    version = 0
+    weights.publish(eng.master, eng.target, version)
+    weights.poll(wait=True)
+    roles = [RoleSpec(f"actor{i}", actor_process, (i, n_actors, None, "cpu"),
+                      dict(cfg=cfg, shm_ring=ring_names[i], shm_weights=wname,
+                           max_steps=actor_max_steps, seed=cfg.seed + 17 * i),
+                      stall_timeout_s=stall_timeout_s) for i in range(n_actors)]
+    sup = Supervisor(roles)
+    mlog = MetricsLogger(metrics_path) if metrics_path else None
+    warm = warmup_rows if warmup_rows is not None else min(cfg.learner.initial_exploration,
+                                                           replay.capacity // 2)
+    lc = cfg.learner
+    out = {"steps": 0, "ingested_rows": 0, "records": 0}
+    sup.start()
+    t0 = time.perf_counter()
+    t_ing = 0.0
+    it = 0
+    last_poll = 0.0
+    captured = False
+    t_train0 = None
+    try:
+        while it < steps:
+            now = time.perf_counter()
+            if timeout_s is not None and now - t0 > timeout_s:
+                break
+            if now - last_poll > 0.2:
+                last_poll = now
+                if not sup.poll():
+                    break
+            ta = time.perf_counter()
+            got = ingest.poll()
+            t_ing += time.perf_counter() - ta if got else 0.0
+            if replay.total_written < warm or ingest.records == 0:
+                if not got:
+                    time.sleep(0.002)
+                continue
+            if not captured:
+                if int(replay.n_valid.item()) < lc.batch_size:
+                    time.sleep(0.002)
+                    continue
+                if use_graph and lc.use_graph:
+                    eng.capture(warmup=1)
+                captured = True
+                t_train0 = time.perf_counter()
+            eng.step()
+            it += 1
+            if it % lc.publish_interval == 0:
+                version += 1
+                weights.publish(eng.master, eng.target, version)
+                eng.check_errors()
+            weights.poll()
+            if it % log_every == 0 or it == steps:
+                loss = eng.loss_value()
+                rec = dict(step=it, loss=loss, rows=ingest.rows, records=ingest.records,
+                           learner_steps_per_s=it / (time.perf_counter() - t_train0))
+                if mlog:
+                    mlog.log("native_cpu", **rec)
+                print("[native-cpu]", rec, flush=True)
+        torch.cuda.synchronize(dev)
+        eng.check_errors()
+    finally:
+        sup.stop()
+        ingest.close()
+        weights.close()
+    t_end = time.perf_counter()
+    out.update(steps=it, ingested_rows=ingest.rows, records=ingest.records, ingest_bytes=ingest.bytes,
+               wall_s=t_end - t0, ingest_host_s=t_ing,
+               learner_steps_per_s=(it / (t_end - t_train0)) if t_train0 and it else 0.0,
+               ingest_rows_per_s=ingest.rows / (t_end - t0), weights_version=version,
+               supervisor=sup.report, zero_copy=[b is not None for b in ingest.registered])
     return out
 
 
@@ -143,8 +302,10 @@ def run_inproc(cfg: R2D2Config, steps: int = 1000, n_actors: int = 1, device: st
 def run_compat(cfg: R2D2Config, n_actors: int, steps: Optional[int] = None,
                actor_device: str = "cpu", learner_device: Optional[str] = None,
                memory_path: Optional[str] = None, timeout_s: Optional[float] = None,
-               stall_timeout_s: float = 0.0) -> Dict:
-    """Reference process topology under the supervisor."""
+               stall_timeout_s: float = 0.0, learner_stall_timeout_s: float = 0.0) -> Dict:
+    """Reference process topology under the supervisor.  Every role heartbeats (``beat``) and
+    honours the fault hooks; a stalled learner (no beat for ``learner_stall_timeout_s``) stops the
+    job, a dead / stalled actor is restarted as a fresh process."""
     import multiprocessing as mp
 
     from .actor import actor_process
@@ -157,7 +318,7 @@ def run_compat(cfg: R2D2Config, n_actors: int, steps: Optional[int] = None,
     memory_path = memory_path or os.path.join(".", "logs", "memory")
     roles = [RoleSpec("learner", learner_process, (n_actors, shared),
                       dict(device=learner_device, cfg=cfg, max_steps=steps, memory_path=memory_path),
-                      restartable=False)]
+                      restartable=False, stall_timeout_s=learner_stall_timeout_s)]
     for i in range(n_actors):
         dev = actor_device
         if actor_device == "cuda" and torch.cuda.is_available():

@@ -33,6 +33,14 @@ _SIGS = {
     "r2rt_ring_pop": (I64, [P, P, U32]),
     "r2rt_ring_peek": (I64, [P]),
     "r2rt_ring_used": (U64, [P]),
+    "r2rt_ring_front": (I64, [P, P]),
+    "r2rt_ring_release": (None, [P]),
+    "r2rt_ring_mapping": (P, [P, P]),
+    "r2rt_slot_open": (P, [ctypes.c_char_p, U64, I]),
+    "r2rt_slot_write": (None, [P, P, U64, I64]),
+    "r2rt_slot_read": (I, [P, P, U64, I64, P]),
+    "r2rt_slot_version": (I64, [P]),
+    "r2rt_slot_close": (None, [P, I]),
     "r2rt_ring_capacity": (U64, [P]),
     "r2rt_ring_close": (None, [P, I]),
     "r2rt_lock_open": (I, [ctypes.c_char_p]),
@@ -145,12 +153,69 @@ class ShmRing:
             return None
         return self._buf.raw[:got]
 
+    def front(self):
+        """Zero-copy view of the front record: (address, length) or None.  The bytes stay valid
+        (the producer cannot reuse them) until ``release()``."""
+        p = ctypes.c_void_p()
+        n = lib().r2rt_ring_front(self._h, ctypes.byref(p))
+        if n < 0:
+            return None
+        return p.value, int(n)
+
+    def release(self) -> None:
+        lib().r2rt_ring_release(self._h)
+
+    def mapping(self):
+        """(address, bytes) of the whole shared mapping (for hipHostRegister)."""
+        n = ctypes.c_uint64()
+        base = lib().r2rt_ring_mapping(self._h, ctypes.byref(n))
+        return int(base), int(n.value)
+
     def used(self) -> int:
         return int(lib().r2rt_ring_used(self._h))
 
     def close(self, unlink: Optional[bool] = None):
         if self._h:
             lib().r2rt_ring_close(self._h, int(self.owner if unlink is None else unlink))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close(unlink=False)
+        except Exception:
+            pass
+
+
+class ShmSlot:
+    """Versioned blob in shared memory (seqlock): one writer process, any number of readers;
+    a reader never observes a torn write."""
+
+    def __init__(self, name: str, nbytes: int, create: bool):
+        self.name = name if name.startswith("/") else "/" + name
+        self.nbytes = int(nbytes)
+        self._h = lib().r2rt_slot_open(self.name.encode(), self.nbytes, int(create))
+        if not self._h:
+            raise OSError(f"cannot open shm slot {self.name}")
+        self.owner = create
+
+    def write(self, arr: np.ndarray, version: int) -> None:
+        a = np.ascontiguousarray(arr)
+        if a.nbytes > self.nbytes:
+            raise ValueError("blob larger than the slot")
+        lib().r2rt_slot_write(self._h, a.ctypes.data, a.nbytes, int(version))
+
+    def read(self, out: np.ndarray, have: int = -1) -> Optional[int]:
+        """Copy a version newer than ``have`` into ``out``; returns its version or None."""
+        v = ctypes.c_int64()
+        rc = lib().r2rt_slot_read(self._h, out.ctypes.data, out.nbytes, int(have), ctypes.byref(v))
+        return int(v.value) if rc == 1 else None
+
+    def version(self) -> int:
+        return int(lib().r2rt_slot_version(self._h))
+
+    def close(self, unlink: Optional[bool] = None):
+        if self._h:
+            lib().r2rt_slot_close(self._h, int(self.owner if unlink is None else unlink))
             self._h = None
 
     def __del__(self):
@@ -234,4 +299,4 @@ class HeartbeatTable:
             self._h = None
 
 
-__all__ = ["SumTree", "ShmRing", "FileLock", "HeartbeatTable", "now_ns", "lib"]
+__all__ = ["SumTree", "ShmRing", "ShmSlot", "FileLock", "HeartbeatTable", "now_ns", "lib"]

@@ -70,3 +70,20 @@ def set_faults(spec: str) -> FaultPlan:
     os.environ["R2D2_FAULTS"] = spec
     _plan = FaultPlan(spec)
     return _plan
+
+
+class Liveness:
+    """Per-role liveness hook: fault-injection check every tick, heartbeat (supervisor
+    ``Beat``) at most every ``every_s`` seconds.  Roles call ``tick(step)`` once per iteration."""
+
+    def __init__(self, role: str, rid: int, beat=None, every_s: float = 0.25):
+        self.role, self.rid, self.beat, self.every_s = role, int(rid), beat, every_s
+        self._last = 0.0
+
+    def tick(self, step: int, status: int = 0) -> None:
+        faults().check(self.role, self.rid, step)
+        if self.beat is not None:
+            now = time.monotonic()
+            if now - self._last >= self.every_s:
+                self._last = now
+                self.beat(int(step), status)

@@ -1,0 +1,247 @@
+"""Native run paths on the GPU: device-side trajectory ingest (files / shared-memory rings /
+device records), CU-masked streams, the concurrent actor + learner driver (replay and weight
+consistency invariants), and the CPU-actor -> HBM learner topology."""
+import ctypes
+import uuid
+
+import numpy as np
+import pytest
+import torch
+
+from pytorch_r2d2_amd.config import get_config
+from pytorch_r2d2_amd.engine.replay_hbm import HBMReplay
+from pytorch_r2d2_amd.ops._lib import kernels
+from pytorch_r2d2_amd.replay.memory import ReplayMemory
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _small_cfg(**over):
+    kw = {"replay.burn_in": 4, "replay.learn": 6, "replay.overlap": 5, "replay.n_step": 3,
+          "learner.batch_size": 8}
+    kw.update(over)
+    return get_config("atari57", **kw)
+
+
+def _record(n, seed, T=10, H=256):
+    """An actor-style local replay of n rows with starts every 5 rows (window inside)."""
+    rng = np.random.default_rng(seed)
+    rm = ReplayMemory(n, 8, 3, (84, 84), H, 4, 4, obs_shape=(4, 84, 84))
+    m = rm.memory
+    m["state"][:] = rng.integers(0, 256, m["state"].shape, dtype=np.uint8)
+    m["hs_cs"][:] = rng.normal(size=m["hs_cs"].shape)
+    m["target_hs_cs"][:] = rng.normal(size=m["target_hs_cs"].shape)
+    m["action"][:] = rng.integers(0, 6, m["action"].shape)
+    m["reward"][:] = rng.normal(size=m["reward"].shape)
+    m["done"][:] = (np.arange(n) >= n - 3)[:, None]
+    m["priority"][:] = rng.random(n) + 0.1
+    st = (np.arange(n) % 5 == 0) & (np.arange(n) <= n - T)
+    m["is_seq_start"][:] = st
+    m["sequence_priority"][:] = np.where(st, rng.random(n) + 0.5, 0)
+    return m
+
+
+def _check_replay_rows(rp, m, sub, head):
+    n = m["state"].shape[0]
+    rows = sub * rp.cap_e + (head + np.arange(n)) % rp.cap_e
+    r = torch.as_tensor(rows, device=DEV)
+    np.testing.assert_array_equal(rp.frames[r].cpu().numpy(), m["state"].reshape(n, -1))
+    np.testing.assert_array_equal(rp.hs_cs[r].cpu().numpy(), m["hs_cs"])
+    np.testing.assert_array_equal(rp.target_hs_cs[r].cpu().numpy(), m["target_hs_cs"])
+    np.testing.assert_array_equal(rp.action[r].cpu().numpy(), m["action"].reshape(-1).astype(np.uint8))
+    np.testing.assert_array_equal(rp.reward[r].cpu().numpy(), m["reward"].reshape(-1))
+    np.testing.assert_array_equal(rp.done[r].cpu().numpy(), (m["done"].reshape(-1) > 0).astype(np.uint8))
+    np.testing.assert_array_equal(rp.priority[r].cpu().numpy(), m["priority"])
+    np.testing.assert_array_equal(rp.is_start[r].cpu().numpy(), m["is_seq_start"])
+    np.testing.assert_array_equal(rp.tree[r].cpu().numpy(),
+                                  (m["sequence_priority"] * m["is_seq_start"]).astype(np.float32))
+
+
+def _tree_consistent(rp):
+    leaves = rp.tree[: rp.capacity].double().sum().item()
+    assert abs(rp.total_priority() - leaves) <= 1e-4 * max(1.0, leaves)
+    assert int(rp.n_valid.item()) == int(rp.is_start.sum().item())
+
+
+def test_ingest_memory_scatters_on_device_and_overwrites_old_starts():
+    cfg = _small_cfg()
+    rp = HBMReplay(cfg, DEV, capacity=2 * 300, n_subrings=2)
+    m1, m2, m3 = _record(200, 1), _record(150, 2), _record(120, 3)
+    assert rp.ingest_memory(m1, subring=0) == 200
+    assert rp.ingest_memory(m2, subring=1) == 150
+    torch.cuda.synchronize()
+    _check_replay_rows(rp, m1, 0, 0)
+    _check_replay_rows(rp, m2, 1, 0)
+    _tree_consistent(rp)
+    # sub-ring 0 wraps: rows 200..299 then 0..19 are overwritten; old starts there disappear
+    assert rp.ingest_memory(m3, subring=0) == 120
+    torch.cuda.synchronize()
+    _check_replay_rows(rp, m3, 0, 200)
+    assert int(rp.ihead[0].item()) == 20 and int(rp.rows_total_d.item()) == 470
+    _tree_consistent(rp)
+    assert int(rp.ingest_err.item()) == 0
+
+
+def test_ingest_rejects_malformed_record():
+    from pytorch_r2d2_amd.parallel.trajectory import pack_rows
+    cfg = _small_cfg()
+    rp = HBMReplay(cfg, DEV, capacity=256, n_subrings=1)
+    m = _record(40, 5)
+    m["hs_cs"] = m["hs_cs"][:, :100].copy()          # wrong state width
+    buf = pack_rows(m)
+    dev = torch.empty(buf.size + 64, dtype=torch.uint8, device=DEV)
+    off = (-dev.data_ptr()) % 64
+    dev[off: off + buf.size].copy_(torch.from_numpy(buf))
+    rp.ingest_device_record(dev[off: off + buf.size], buf[:512], 0)
+    torch.cuda.synchronize()
+    assert int(rp.ingest_err.item()) & 1
+    assert int(rp.n_valid.item()) == 0
+
+
+def test_shm_ring_ingestor_dma_into_hbm():
+    from pytorch_r2d2_amd.engine.ingest import HBMIngestor
+    from pytorch_r2d2_amd.parallel.trajectory import ShmTrajectoryWriter
+    cfg = _small_cfg()
+    rp = HBMReplay(cfg, DEV, capacity=3 * 400, n_subrings=3)
+    names = [f"/r2d2_gt_{uuid.uuid4().hex[:6]}_{i}" for i in range(3)]
+    ing = HBMIngestor(rp, names, ring_bytes=64 << 20)
+    try:
+        writers = [ShmTrajectoryWriter(n, 64 << 20) for n in names]
+        recs = {i: [_record(100 + 10 * i + j, 10 * i + j) for j in range(2)] for i in range(3)}
+        for i, w in enumerate(writers):
+            for m in recs[i]:
+                w.push(m)
+        total = 0
+        for _ in range(10):
+            total += ing.poll()
+            ing._release_done(wait=True)
+        torch.cuda.synchronize()
+        assert total == sum(m["state"].shape[0] for ms in recs.values() for m in ms)
+        for i in range(3):
+            head = 0
+            for m in recs[i]:
+                _check_replay_rows(rp, m, i, head)
+                head += m["state"].shape[0]
+        _tree_consistent(rp)
+        assert all(ws.ring.used() >= 0 for ws in writers)
+        assert all(r.ring.front() is None for r in ing.readers)
+        print("zero-copy registered rings:", [b is not None for b in ing.registered])
+    finally:
+        ing.close()
+
+
+def test_cu_masked_streams_partition_the_chip():
+    from pytorch_r2d2_amd.parallel.placement import split_chip
+    sa, sl, na, nl = split_chip(DEV, 4)
+    try:
+        assert na == 32 and nl == torch.cuda.get_device_properties(0).multi_processor_count - 32
+        k = kernels()
+        seen = {}
+        for name, s in (("actor", sa), ("learner", sl)):
+            out = torch.zeros(2 * 2048, dtype=torch.int32, device=DEV)
+            # eager launch and the same launch replayed as a graph on the masked stream
+            g = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream()
+            with torch.cuda.graph(g, stream=side):
+                assert k.r2_cu_probe(ctypes.c_void_p(out.data_ptr()), 2048, 2,
+                                     ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
+            with torch.cuda.stream(s.stream):
+                g.replay()
+            torch.cuda.synchronize()
+            v = out.view(-1, 2).cpu().numpy()
+            cus = {(int(x), (int(h) >> 8) & 15, (int(h) >> 13) & 7) for x, h in v}
+            seen[name] = cus
+            per = np.bincount([c[0] for c in cus], minlength=8)
+            assert len(per) == 8 and (per == (4 if name == "actor" else 28)).all(), (name, per)
+        assert not (seen["actor"] & seen["learner"])
+    finally:
+        sa.close()
+        sl.close()
+
+
+def _concurrent_setup(E=16, cap_e=512, M=2, masked=True, **over):
+    from pytorch_r2d2_amd.actor_batched import BatchedActor, engine_weights
+    from pytorch_r2d2_amd.engine.concurrent import ConcurrentDriver
+    from pytorch_r2d2_amd.engine.learner_engine import LearnerEngine
+    from pytorch_r2d2_amd.envs.synthetic import VecSyntheticAtari
+    from pytorch_r2d2_amd.parallel.placement import split_chip
+    cfg = _small_cfg(**{"learner.publish_interval": 5, "actor.envs_per_actor": E,
+                        "learner.target_update_interval": 7, **over})
+    sa = sl = None
+    na, nl = 256, None
+    if masked:
+        sa, sl, na, nl = split_chip(DEV, 4)
+    rp = HBMReplay(cfg, DEV, capacity=E * cap_e, n_subrings=E)
+    eng = LearnerEngine(cfg, rp, DEV, n_cus=nl)
+    env = VecSyntheticAtari(E, DEV, seed=3, episode_len=37, n_actions=cfg.model.n_actions)
+    on, tg = engine_weights(eng)
+    actor = BatchedActor(cfg, rp, env, on, tg, seed=1)
+    while int(rp.n_valid.item()) < 4 * cfg.learner.batch_size:
+        actor.step()
+    eng.capture(warmup=1)
+    actor.n_workers = na
+    drv = ConcurrentDriver(eng, actor, steps_per_round=M,
+                           actor_stream=sa.stream if sa else None,
+                           learner_stream=sl.stream if sl else None)
+    return cfg, rp, eng, actor, drv, (sa, sl)
+
+
+def test_concurrent_driver_never_samples_rows_being_written():
+    cfg, rp, eng, actor, drv, streams = _concurrent_setup()
+    B, Tn = cfg.learner.batch_size, cfg.replay.seq_len + cfg.replay.n_step
+    R = 120
+    hist = torch.zeros(R, B, dtype=torch.int32, device=DEV)
+
+    def log_starts(i):
+        if i < R:
+            hist[i].copy_(eng.starts)
+    drv.on_learner_step = log_starts
+    drv.run(R)
+    drv.finish()
+    drv.check_errors()
+    starts = hist.cpu().numpy()
+    cap_e, M = rp.cap_e, drv.M
+    for r in range(R):
+        written = {(drv.heads[r] + j) % cap_e for j in range(M)}
+        for s in starts[r]:
+            off = s % cap_e
+            window = {(off + t) % cap_e for t in range(Tn)}
+            assert not (window & written), (r, s)
+    # weights: published every 5 learner steps; the actor's copy is the last published master
+    assert drv.version == R // 5
+    torch.testing.assert_close(drv.w_on.flat, drv.stage_on, rtol=0, atol=0)
+    # replay bookkeeping stayed consistent while both roles mutated it
+    _tree_consistent(rp)
+    for s in streams:
+        if s is not None:
+            s.close()
+
+
+def test_run_native_concurrent_and_serial_train():
+    from pytorch_r2d2_amd.runner import run_native
+    cfg = _small_cfg(**{"actor.envs_per_actor": 32, "learner.publish_interval": 10})
+    outs = {}
+    for conc in (False, True):
+        out = run_native(cfg, steps=60, actor_steps_per_update=2, warmup_rows=32 * 120,
+                         capacity=32 * 600, log_every=30, concurrent=conc, check_every=20)
+        assert all(np.isfinite(out["losses"]))
+        outs[conc] = out
+        print("concurrent" if conc else "serial", {k: out[k] for k in
+              ("learner_steps_per_s", "env_steps_per_s", "learner_cus")})
+    assert outs[True]["learner_cus"] < outs[False]["learner_cus"]
+    assert outs[True]["weights_version"] == 6
+
+
+@pytest.mark.slow
+def test_cpu_actor_processes_feed_the_hbm_learner(tmp_path):
+    from pytorch_r2d2_amd.runner import run_native_cpu_actors
+    cfg = get_config("pong", **{"replay.burn_in": 4, "replay.learn": 6, "replay.overlap": 5,
+                                "env.episode_len": 40, "actor.memory_save_interval": 1,
+                                "actor.net_load_interval": 1, "learner.publish_interval": 5})
+    out = run_native_cpu_actors(cfg, 2, steps=20, warmup_rows=150, capacity=2 * 4096,
+                                log_every=10, timeout_s=240, stall_timeout_s=120)
+    assert out["steps"] == 20, out
+    assert out["ingested_rows"] >= 150 and out["records"] >= 2
+    print({k: out[k] for k in ("ingest_rows_per_s", "learner_steps_per_s", "zero_copy",
+                               "ingested_rows")})
