@@ -157,6 +157,12 @@ class ConcurrentDriver:
             with torch.cuda.stream(self.s_learn):
                 self.s_learn.wait_event(self.ev_act[p])
                 self._replay_apply(p)
+            if self._repack:   # the actor picks up the last publication
+                with torch.cuda.stream(self.s_act):
+                    self.s_act.wait_event(self.ev_learn)
+                    self.w_on.load_flat(self.stage_on, self.version)
+                    self.w_tg.load_flat(self.stage_tg, self.version)
+                self._repack = False
         torch.cuda.synchronize(self.rp.device)
 
     def run(self, rounds: int) -> None:

@@ -71,6 +71,9 @@ def run_native(cfg: R2D2Config, steps: int = 1000, actor_steps_per_update: int =
     on, tg = engine_weights(eng)
     actor = BatchedActor(cfg, replay, env, on, tg, global_env_offset=info.rank * E,
                          total_envs=info.world * E, seed=cfg.seed + info.rank)
+    if concurrent:
+        # the actor group's kernels must never need co-residency on the learner's CUs
+        actor.lstm_step = True
     mlog = MetricsLogger(metrics_path, rank=info.rank) if metrics_path else None
     live = Liveness("learner", info.rank, beat)
     warm = warmup_rows if warmup_rows is not None else min(cfg.learner.initial_exploration,

@@ -201,16 +201,27 @@ def test_concurrent_driver_never_samples_rows_being_written():
     drv.finish()
     drv.check_errors()
     starts = hist.cpu().numpy()
-    cap_e, M = rp.cap_e, drv.M
+    done = rp.done.cpu().numpy()
+    cap_e, M, T = rp.cap_e, drv.M, cfg.replay.seq_len
+    assert drv.rounds * M + drv.heads[0] < cap_e          # no wrap: rows keep their round's data
+    n_ext = 0
     for r in range(R):
         written = {(drv.heads[r] + j) % cap_e for j in range(M)}
         for s in starts[r]:
-            off = s % cap_e
-            window = {(off + t) % cap_e for t in range(Tn)}
+            off, base = s % cap_e, s - s % cap_e
+            window = {(off + t) % cap_e for t in range(T)}
             assert not (window & written), (r, s)
+            # the n bootstrap frames past the window may be the next episode's first rows (being
+            # written): only for a final start, whose last learning row is terminal (masked)
+            ext = {(off + t) % cap_e for t in range(T, Tn)}
+            if ext & written:
+                n_ext += 1
+                assert done[base + (off + T - 1) % cap_e] == 1, (r, s)
+    print("samples whose masked bootstrap frames were being written:", n_ext)
     # weights: published every 5 learner steps; the actor's copy is the last published master
     assert drv.version == R // 5
     torch.testing.assert_close(drv.w_on.flat, drv.stage_on, rtol=0, atol=0)
+    assert drv.w_on.version == drv.version
     # replay bookkeeping stayed consistent while both roles mutated it
     _tree_consistent(rp)
     for s in streams:
