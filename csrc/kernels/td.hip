@@ -50,7 +50,27 @@ struct TdArgs {
   int Tl, B, A, burn_in, cap_e;
   float gamma_n, vr_eps, alpha, prio_eps, beta;
   int value_rescale;
+  // data-parallel global prioritized sampling (parallel/sharded_replay.py), or null:
+  // {W*S_k/S, S_k/S, N_global, global max of the weights}; the weight of sample b is
+  // (W*S_k/S) * (N_global * P_global(b))^-beta / gmax with P_global = probs[b] * S_k/S
+  const float* dp;
 };
+
+// un-normalised IS weight of sample b (b < B); *global_norm: already normalised across ranks
+__device__ __forceinline__ float is_weight(const TdArgs& a, int b, bool* global_norm) {
+  *global_norm = a.dp != nullptr;
+  if (a.dp != nullptr) {
+    const float f = a.dp[0];
+    const float w = (a.beta > 0.f && a.probs != nullptr)
+                        ? powf(fmaxf(a.dp[2] * a.probs[b] * a.dp[1], 1e-30f), -a.beta) : 1.f;
+    return f * w / a.dp[3];
+  }
+  if (a.probs != nullptr && a.beta > 0.f) {
+    const float nv = a.n_valid ? (float)max(*a.n_valid, 1) : 1.f;
+    return powf(fmaxf(nv * a.probs[b], 1e-30f), -a.beta);
+  }
+  return 1.f;
+}
 
 __global__ __launch_bounds__(256) void td_kernel(const TdArgs a) {
   __shared__ float red[8];
@@ -58,15 +78,12 @@ __global__ __launch_bounds__(256) void td_kernel(const TdArgs a) {
   __shared__ int last;
   const int tid = threadIdx.x;
   // ---- IS weights w_b = (N * P_b)^-beta / max_b  (B <= 256; recomputed per workgroup)
-  float w = 1.f;
-  if (tid < a.B && a.probs != nullptr && a.beta > 0.f) {
-    const float nv = a.n_valid ? (float)max(*a.n_valid, 1) : 1.f;
-    w = powf(fmaxf(nv * a.probs[tid], 1e-30f), -a.beta);
-  }
+  bool gn = false;
+  const float w = tid < a.B ? is_weight(a, tid, &gn) : 1.f;
   float m = wave_max(tid < a.B ? w : 0.f);
   if ((tid & 63) == 0) red[tid >> 6] = m;
   __syncthreads();
-  const float wmax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float wmax = gn ? 1.f : fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   if (tid < a.B) {
     wsh[tid] = w / wmax;
     if (a.is_w && blockIdx.x == 0) a.is_w[tid] = w / wmax;
@@ -129,13 +146,14 @@ extern "C" int r2_td_loss(const float* q_sa, const float* q_arg, const float* q_
                           float* td_abs, float* priority, float* is_w, const int* n_valid,
                           int Tl, int B, int A, int burn_in, int cap_e, float gamma_n,
                           int value_rescale, float vr_eps, float alpha, float prio_eps,
-                          float beta, float* part, unsigned* ticket, void* stream) {
+                          float beta, float* part, unsigned* ticket, const float* dp,
+                          void* stream) {
   if (B > 256) return -1;
   const int grid = (Tl * B + 255) / 256;
   if (grid > 4096) return -2;   // part[] holds one float per workgroup (engine: 4096)
   TdArgs a{q_sa, q_arg, q_tgt, starts, probs, action, reward, done, dq, loss, td_abs, priority,
            is_w, n_valid, part, ticket, Tl, B, A, burn_in, cap_e, gamma_n, vr_eps, alpha, prio_eps,
-           beta, value_rescale};
+           beta, value_rescale, dp};
   hipLaunchKernelGGL(td_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, a);
   R2_CHECK_LAUNCH();
   return 0;
@@ -202,17 +220,15 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
   const float rew = valid ? a.reward[row] : 0.f;
   const bool dn = valid ? a.done[row] != 0 : true;
   // ---- IS weights (B <= 256), as td_kernel
-  float w = 1.f;
-  if (tid < a.B && a.probs != nullptr && a.beta > 0.f) {
-    const float nv = a.n_valid ? (float)max(*a.n_valid, 1) : 1.f;
-    w = powf(fmaxf(nv * a.probs[tid], 1e-30f), -a.beta);
-  }
+  bool gn = false;
+  const float w = tid < a.B ? is_weight(a, tid, &gn) : 1.f;
   const float m = wave_max(tid < a.B ? w : 0.f);
   if (lane == 0) red[wave] = m;
   __syncthreads();
   float wmax = red[0];
 #pragma unroll
   for (int q = 1; q < NW; ++q) wmax = fmaxf(wmax, red[q]);
+  if (gn) wmax = 1.f;
   if (tid < a.B) {
     wsh[tid] = w / wmax;
     if (a.is_w && blockIdx.x == 0) a.is_w[tid] = w / wmax;
@@ -328,14 +344,14 @@ extern "C" int r2_td_duel(const float* q_sa, const float* q_arg, const float* q_
                           int value_rescale, float vr_eps, float alpha, float prio_eps,
                           float beta, float* part, unsigned* ticket, const void* zr,
                           const float* w2, bf16* dz, float* dva, int HD, bf16* dz_lo,
-                          void* stream) {
+                          const float* dp, void* stream) {
   if (B > 256) return -1;
   if (A < 1 || A > 64) return -3;             // one lane per action
   const int grid = (Tl * B + 15) / 16;
   if (grid > 4096) return -2;   // part[] holds one float per workgroup (engine: 4096)
   TdDuelArgs d{{q_sa, q_arg, q_tgt, starts, probs, action, reward, done, dq, loss, td_abs, priority,
                 is_w, n_valid, part, ticket, Tl, B, A, burn_in, cap_e, gamma_n, vr_eps, alpha,
-                prio_eps, beta, value_rescale},
+                prio_eps, beta, value_rescale, dp},
                zr, w2, dz, dva, dz_lo};
   hipStream_t s = (hipStream_t)stream;
   return dz_lo ? td_duel_launch<true>(d, HD, grid, s) : td_duel_launch<false>(d, HD, grid, s);

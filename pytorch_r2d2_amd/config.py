@@ -147,6 +147,9 @@ class DistConfig:
     # so without a reservation the RCCL kernel cannot start until the conv backward has finished
     # (no overlap at all).  0 = whole chip (the world == 1 layout).
     comm_reserve_cus: int = 32
+    # globally proportional prioritized sampling over the ranks' replay shards
+    # (parallel/sharded_replay.py: one 12-byte all-gather per step, shard-ratio loss weights)
+    global_sampling: bool = True
 
 
 @dataclass

@@ -176,6 +176,8 @@ class LearnerEngine:
         self.gate_inv = L.gate_inv.to(d)
         self.clip_buf = torch.zeros(1, dtype=torch.float32, device=d)
         self.steps_done = 0
+        # data-parallel global prioritized sampling (parallel/sharded_replay.py)
+        self.dp_global = bool(world > 1 and process_group is not None and cfg.dist.global_sampling)
         self._duel_done = False       # the TD launch also ran the dueling-head backward
         self.graph = None
         self.stats: Dict[str, float] = {}
@@ -306,6 +308,10 @@ class LearnerEngine:
         self.gate_perm_i32 = L.gate_perm.to(d, torch.int32)
         self.gs_ws = torch.zeros(int(kernels().r2_gradsum_ws_floats()), dtype=torch.float32, device=d)
         self.gs_ticket = torch.zeros(64, dtype=torch.int32, device=d)
+        # DP global sampling: local shard stats, the all-gathered (W, 3) stats, TD's 4 parameters
+        self.dp_send = z(3)
+        self.dp_recv = z(max(1, self.world) * 3)
+        self.dp_params = z(4)
 
     # ------------------------------------------------------------------ weights
     def _pack(self, always: bool = False, stream=None):
@@ -528,20 +534,43 @@ class LearnerEngine:
 
     # ------------------------------------------------------------------ the step
     def _forward_loss(self):
-        k = kernels()
-        s = stream_handle()
-        B, T, Tn, Lb, Ll, n = self.B, self.T, self.Tn, self.Lb, self.Ll, self.n
-        L, rp, lc = self.layout, self.replay, self.cfg.learner
-        H, A = L.H, L.A
-        pk, pt = self.pk, self.pk_t
-        # sample -> time-major row list -> stored recurrent states, one launch
-        # (replay_memory.py:224-262: multinomial over a host scan + per-row Python gathers)
+        self._sample()
+        if self.dp_global:
+            self._gather_dp()
+        self._forward_rest()
+
+    def _sample(self):
+        """sample -> time-major row list -> stored recurrent states, one launch
+        (replay_memory.py:224-262: multinomial over a host scan + per-row Python gathers)."""
+        B, Tn, n = self.B, self.Tn, self.n
+        rp = self.replay
         st_off = {"on": 0, "tg": 0 if self.mode == "shifted" else n, "nx": n}
         states = [(rp.hs_cs, 0, self.h0["on"], self.c0["on"]),
                   (rp.target_hs_cs, st_off["tg"], self.h0["tg"], self.c0["tg"])]
         if self.mode == "fixed":
             states.append((rp.hs_cs, n, self.h0["nx"], self.c0["nx"]))
         rp.sample_batch(B, self.starts, self.probs, self.rows, Tn, states, h_f32=self.sp)
+        if self.dp_global:
+            from ..parallel.sharded_replay import local_stats
+            root = rp.tree[int(rp.tree_offs[-1]): int(rp.tree_offs[-1]) + 1]
+            local_stats(root, rp.n_valid, self.probs, out=self.dp_send)
+
+    def _gather_dp(self):
+        """The step's one extra collective (DP global sampling): 3 floats per rank."""
+        from ..parallel.sharded_replay import gather_stats
+        gather_stats(self.dp_send, self.world, self.pg, out=self.dp_recv)
+
+    def _forward_rest(self):
+        k = kernels()
+        s = stream_handle()
+        B, T, Tn, Lb, Ll, n = self.B, self.T, self.Tn, self.Lb, self.Ll, self.n
+        L, rp, lc = self.layout, self.replay, self.cfg.learner
+        H, A = L.H, L.A
+        pk, pt = self.pk, self.pk_t
+        if self.dp_global:
+            from ..parallel.sharded_replay import global_is_params
+            global_is_params(self.dp_recv.view(self.world, 3), self.rank, float(self.cfg.replay.beta),
+                             out=self.dp_params)
         rows = self.rows
         if self._chunks is not None:
             self._forward_pipelined()
@@ -654,18 +683,19 @@ class LearnerEngine:
                  Ll, B, A, Lb, rp.cap_e, self.gamma_n, int(lc.value_rescale),
                  float(lc.value_rescale_eps), float(rc.alpha), float(rc.priority_eps),
                  float(rc.beta), ptr(self.td_part), ptr(self.td_ticket))
+        dp = ptr(self.dp_params) if self.dp_global else 0
         # TD + the dueling head's backward in one launch (td.hip td_duel_kernel): dz / dva of the
         # online learning rows are written right where dL/dQ is known
         self._duel_done = False
         if lc.td_fuse_head_bwd:
             rc_ = k.r2_td_duel(*targs, ptr(self.zr_on[: Ll * B]), ptr(pk["head_w2"]), ptr(self.dz),
-                               ptr(self.dva), L.HD, ptr(self.dz_lo), s)
+                               ptr(self.dva), L.HD, ptr(self.dz_lo), dp, s)
             if rc_ == 0:
                 self._duel_done = True
                 return
             if self.sp:
                 check(rc_, "td_duel")
-        check(k.r2_td_loss(*targs, s), "td_loss")
+        check(k.r2_td_loss(*targs, dp, s), "td_loss")
 
     def _backward_core_sp(self):
         """Split-precision backward core: head gradients, dh GEMM, BPTT, weight-gradient + dX
@@ -1017,6 +1047,15 @@ class LearnerEngine:
         self._forward_loss()
         self._backward_core()
 
+    # DP with global sampling: the sampled batch's shard stats are all-gathered between the
+    # sampling launch and the rest of the forward
+    def _seg_sample(self):
+        self._sample()
+
+    def _seg_core_rest(self):
+        self._forward_rest()
+        self._backward_core()
+
     def _seg_torso(self):
         self._backward_torso()
 
@@ -1040,7 +1079,7 @@ class LearnerEngine:
         L = self.layout
         ph = timer.phase if timer is not None else (lambda name: contextlib.nullcontext())
         with ph("forward+td"):
-            self._forward_loss()
+            self._forward_loss()      # (DP global sampling: includes the stats all-gather)
         with ph("backward_core"):
             self._backward_core()
         if self.world > 1:   # core bucket all-reduce overlaps the conv backward
@@ -1065,7 +1104,9 @@ class LearnerEngine:
     def capture(self, warmup: int = 2):
         """Capture the step into HIP graphs.  world == 1: one graph for the whole step.
         world > 1: four graphs (core fwd/bwd | conv bwd | priorities | update) with the two
-        bucket all-reduces issued between them on the communication stream."""
+        bucket all-reduces issued between them on the communication stream; with global
+        sampling the core graph is split after the sampling launch for the 12-byte shard-stats
+        all-gather (five graphs)."""
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
@@ -1076,6 +1117,8 @@ class LearnerEngine:
         self.graphs = []
         if self.world > 1:
             segs = [self._seg_core, self._seg_torso, self._seg_prio, self._seg_update]
+            if self.dp_global:
+                segs = [self._seg_sample, self._seg_core_rest] + segs[1:]
         else:
             segs = [lambda: (self._seg_core(), self._seg_torso(), self._seg_tail())]
         pool = None
@@ -1096,7 +1139,12 @@ class LearnerEngine:
             self.graphs[0].replay()
         else:
             L = self.layout
-            g_core, g_torso, g_prio, g_update = self.graphs
+            if self.dp_global:
+                g_sample, g_core, g_torso, g_prio, g_update = self.graphs
+                g_sample.replay()
+                self._gather_dp()
+            else:
+                g_core, g_torso, g_prio, g_update = self.graphs
             g_core.replay()
             self._sync().start(0, L.torso_offset)
             g_torso.replay()

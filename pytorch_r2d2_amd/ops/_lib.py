@@ -40,9 +40,10 @@ _SIGS = {
     "r2_relu_mask_bf16": [P, P, P, I64, P],
     "r2_dueling_fwd": [P, P, P, P, P, P, I, I, I, P],
     "r2_dueling_bwd": [P, P, P, P, P, I, I, I, P],
-    "r2_td_loss": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, F, F, F, F, P, P, P],
+    "r2_td_loss": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, F, F, F, F, P, P, P,
+                   P],
     "r2_td_duel": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, F, F, F, F, P, P,
-                   P, P, P, P, I, P, P],
+                   P, P, P, P, I, P, P, P],
     "r2_dueling_fwd_multi_f32": [P, I, I, I, P],
     "r2_lstm_fwd_tag_sp": [P, I, I, I, I, P, P, P, P],
     "r2_lstm_bwd_tag_sp": [P, P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P, P, P],

@@ -166,4 +166,6 @@ class RcclTrajectoryChannel:
         stays in device memory and the ingest kernel scatters it (no D2H).  Returns rows."""
         buf = self._recv_buf(src)
         head = buf[: header_bytes()].cpu().numpy()       # header only (<= 320 bytes)
+        if buf.device != replay.device:                   # gloo (CPU) transport: one H2D copy
+            buf = buf.to(replay.device)
         return replay.ingest_device_record(buf, head, subring)

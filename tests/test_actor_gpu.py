@@ -181,13 +181,20 @@ def _dp_worker(rank, world, port, outdir, graph=False, same_data=False):
                    os.path.join(outdir, "single.pt"))
     if graph:   # 4 graph segments with the bucket all-reduces issued between them
         eng.capture(warmup=1)
-        for _ in range(2):
-            eng.step()
+        steps = [eng.step] * 2
     else:
-        for _ in range(3):
-            eng.step_eager()
+        steps = [eng.step_eager] * 3
+    for fn in steps[:-1]:
+        fn()
     torch.cuda.synchronize()
-    torch.save({"master": eng.master.cpu(), "loss": eng.loss_value()}, os.path.join(outdir, f"dp{rank}.pt"))
+    root0, nv0 = float(rp.total_priority()), int(rp.n_valid.item())   # what the last step samples
+    steps[-1]()
+    torch.cuda.synchronize()
+    torch.save({"master": eng.master.cpu(), "loss": eng.loss_value(), "probs": eng.probs.cpu(),
+                "is_w": eng.is_w.cpu(), "dp_params": eng.dp_params.cpu(), "dp_recv": eng.dp_recv.cpu(),
+                "root": root0, "n_valid": nv0,
+                "beta": float(cfg.replay.beta), "dp_global": eng.dp_global},
+               os.path.join(outdir, f"dp{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -231,3 +238,25 @@ def test_native_loop_learns_synthetic_cue_task():
     random_return = ep / cfg.model.n_actions
     assert len(rets) > 500
     assert rets[-200:].mean() > 3 * random_return, (rets[:200].mean(), rets[-200:].mean())
+
+
+@pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
+def test_dp_engine_global_sampling_weights(tmp_path, graph):
+    """Different shards per rank: the TD kernel's IS weights are the two-level global ones
+    (parallel/sharded_replay.py) computed from the all-gathered shard stats."""
+    from pytorch_r2d2_amd.parallel.sharded_replay import dp_is_weights, global_is_params
+    import torch.multiprocessing as tmp
+    tmp.spawn(_dp_worker, args=(2, _free_port(), str(tmp_path), graph), nprocs=2, join=True)
+    r = [torch.load(os.path.join(tmp_path, f"dp{k}.pt"), weights_only=True) for k in range(2)]
+    assert r[0]["dp_global"] and r[1]["dp_global"]
+    stats = r[0]["dp_recv"].view(2, 3)
+    torch.testing.assert_close(stats, r[1]["dp_recv"].view(2, 3))
+    for k in range(2):
+        assert abs(float(stats[k, 0]) - r[k]["root"]) <= 1e-5 * r[k]["root"]
+        assert int(stats[k, 1]) == r[k]["n_valid"]
+        assert float(stats[k, 2]) == float(r[k]["probs"].min())
+        params = global_is_params(stats, k, r[k]["beta"])
+        torch.testing.assert_close(r[k]["dp_params"], params, rtol=1e-6, atol=0)
+        torch.testing.assert_close(r[k]["is_w"], dp_is_weights(r[k]["probs"], params, r[k]["beta"]),
+                                   rtol=2e-6, atol=1e-7)
+    assert max(float(r[k]["is_w"].max()) for k in range(2)) == pytest.approx(1.0, rel=1e-6)

@@ -256,3 +256,38 @@ def test_cpu_actor_processes_feed_the_hbm_learner(tmp_path):
     assert out["ingested_rows"] >= 150 and out["records"] >= 2
     print({k: out[k] for k in ("ingest_rows_per_s", "learner_steps_per_s", "zero_copy",
                                "ingested_rows")})
+
+
+def _traj_worker(rank, world, port, outdir):
+    import os
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    from pytorch_r2d2_amd.parallel.trajectory import RcclTrajectoryChannel
+    dist.init_process_group("gloo")
+    ch = RcclTrajectoryChannel("cpu")
+    if rank == 0:
+        for j in range(2):
+            ch.send(_record(90 + j, 40 + j), 1)
+    else:
+        rp = HBMReplay(_small_cfg(), DEV, capacity=2 * 256, n_subrings=2)
+        got = [ch.recv_into(rp, 0, subring=1) for _ in range(2)]
+        torch.cuda.synchronize()
+        _check_replay_rows(rp, _record(90, 40), 1, 0)
+        _check_replay_rows(rp, _record(91, 41), 1, 90)
+        _tree_consistent(rp)
+        torch.save({"got": got}, os.path.join(outdir, "traj.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_trajectory_channel_recv_into_hbm_replay(tmp_path):
+    import os
+    import socket
+    import torch.multiprocessing as tmp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    tmp.spawn(_traj_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    assert torch.load(os.path.join(tmp_path, "traj.pt"), weights_only=True)["got"] == [90, 91]

@@ -1,0 +1,109 @@
+"""Globally proportional prioritized sampling over data-parallel replay shards (gloo, world 2 and
+4, CPU).  Each rank samples its fixed local batch proportionally within its own shard; the
+all-gathered shard stats turn that into the distribution of ONE merged replay (weighted
+chi-square), and the IS weights equal the single-replay formula."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as tmp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _shard(rank, M=24):
+    """Deliberately unequal shards: different sizes of total priority per rank."""
+    g = np.random.default_rng(100 + rank)
+    return (g.random(M) + 0.05) * (1.0 + 2.0 * rank)
+
+
+def _stratified(p, B, g):
+    c = np.cumsum(p)
+    u = (np.arange(B) + g.random(B)) / B * c[-1]
+    idx = np.minimum(np.searchsorted(c, u, side="right"), len(p) - 1)
+    return idx, p[idx] / c[-1]
+
+
+def _worker(rank, world, port, outdir, rounds, B, beta):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from pytorch_r2d2_amd.parallel.dist import init_distributed
+    from pytorch_r2d2_amd.parallel.sharded_replay import (dp_is_weights, gather_stats,
+                                                          global_is_params, local_stats,
+                                                          single_replay_is_weights)
+    init_distributed(backend="gloo", device_type="cpu")
+    p = _shard(rank)
+    M = len(p)
+    g = np.random.default_rng(7 + rank)
+    acc = torch.zeros(world * M, dtype=torch.float64)     # weighted counts, global item index
+    acc2 = torch.zeros(world * M, dtype=torch.float64)    # sum of squared weights (variance)
+    raw = torch.zeros(world * M, dtype=torch.float64)     # unweighted counts
+    is_err = 0.0
+    for r in range(rounds):
+        idx, q = _stratified(p, B, g)
+        probs = torch.tensor(q, dtype=torch.float32)
+        st = local_stats(torch.tensor([p.sum()], dtype=torch.float32),
+                         torch.tensor([M], dtype=torch.int32), probs)
+        stats = gather_stats(st, world)
+        params = global_is_params(stats, rank, 0.0)
+        w = dp_is_weights(probs, params, 0.0).double()
+        gi = torch.as_tensor(rank * M + idx)
+        acc.index_add_(0, gi, w)
+        acc2.index_add_(0, gi, w * w)
+        raw.index_add_(0, gi, torch.ones(B, dtype=torch.float64))
+        if r < 8 and beta > 0:
+            # IS weights vs the single-replay formula over the merged global batch
+            pb = beta_params = global_is_params(stats, rank, beta)
+            wb = dp_is_weights(probs, pb, beta)
+            allp = [torch.zeros(B) for _ in range(world)]
+            S = stats[:, 0]
+            dist.all_gather(allp, probs * S[rank] / S.sum())          # global P of every sample
+            merged = torch.cat(allp)
+            ref = single_replay_is_weights(merged, float(stats[:, 1].sum()), beta)
+            factor = beta_params[0]
+            # shard ratio times the single-replay weight, up to ONE global constant
+            ratio = (wb / factor) / ref[rank * B:(rank + 1) * B]
+            rs = [torch.zeros(B) for _ in range(world)]
+            dist.all_gather(rs, ratio)
+            allr = torch.cat(rs)
+            is_err = max(is_err, float((allr / allr[0] - 1).abs().max()))
+            assert float(wb.max()) <= 1.0 + 1e-6
+    for t in (acc, acc2, raw):
+        dist.all_reduce(t)
+    if rank == 0:
+        P = torch.tensor(np.concatenate([_shard(k) for k in range(world)]), dtype=torch.float64)
+        P = P / P.sum()
+        tot = acc.sum()
+        E = tot * P
+        # per-item variance of a weighted count: sum of squared weights (Poisson approximation)
+        chi2 = float((((acc - E) ** 2) / acc2.clamp_min(1e-12)).sum())
+        chi2_raw = float((((raw / raw.sum() * tot - E) ** 2) / acc2.clamp_min(1e-12)).sum())
+        torch.save({"chi2": chi2, "chi2_raw": chi2_raw, "dof": world * M - 1, "is_err": is_err,
+                    "tv": float((acc / tot - P).abs().sum() / 2),
+                    "tv_raw": float((raw / raw.sum() - P).abs().sum() / 2)},
+                   os.path.join(outdir, "res.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_two_level_sampling_matches_merged_replay(tmp_path, world):
+    from scipy.stats import chi2 as chi2_dist
+    port = _free_port()
+    tmp.spawn(_worker, args=(world, port, str(tmp_path), 400, 16, 0.6), nprocs=world, join=True)
+    res = torch.load(os.path.join(tmp_path, "res.pt"), weights_only=True)
+    print(world, res)
+    crit = chi2_dist.ppf(0.999, res["dof"])
+    assert res["chi2"] < crit, res
+    # the test has power: the uncorrected per-shard sampling is far from the merged distribution
+    assert res["chi2_raw"] > 10 * crit and res["tv_raw"] > 0.05, res
+    assert res["tv"] < 0.03, res
+    assert res["is_err"] < 1e-5, res
