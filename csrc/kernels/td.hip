@@ -56,6 +56,27 @@ struct TdArgs {
   const float* dp;
 };
 
+// Deterministic row-priority scatter.  Two sampled sequences can share learning rows (overlapping
+// starts, or one start sampled twice); the reference resolves the duplicate indices of
+// `update_priority(index[burn_in:].reshape(-1), ...)` (learner.py:101-103) as numpy does: the
+// LAST element in (t, b) row-major order wins.  Transition (tl, b) therefore writes only if no
+// (tl', b') with tl' * B + b' > tl * B + b maps to the same ring row.  `st`: the B starts.
+__device__ __forceinline__ bool prio_owner(const int* st, int B, int Tl, int burn_in, int cap_e,
+                                           int tl, int b, int lane0, int lanes) {
+  const int sb = st[b];
+  const int base = sb - sb % cap_e, ob = sb - base;
+  bool own = true;
+  for (int c = lane0; c < B; c += lanes) {
+    const int sc = st[c];
+    if (sc - sc % cap_e != base) continue;                 // another sub-ring
+    // tl' with start_c + burn_in + tl' == start_b + burn_in + tl (mod cap_e)
+    int d = (ob - (sc - base) + tl) % cap_e;
+    if (d < 0) d += cap_e;
+    if (d < Tl && d * B + c > tl * B + b) own = false;
+  }
+  return own;
+}
+
 // un-normalised IS weight of sample b (b < B); *global_norm: already normalised across ranks
 __device__ __forceinline__ float is_weight(const TdArgs& a, int b, bool* global_norm) {
   *global_norm = a.dp != nullptr;
@@ -75,8 +96,10 @@ __device__ __forceinline__ float is_weight(const TdArgs& a, int b, bool* global_
 __global__ __launch_bounds__(256) void td_kernel(const TdArgs a) {
   __shared__ float red[8];
   __shared__ float wsh[256];
+  __shared__ int sst[256];
   __shared__ int last;
   const int tid = threadIdx.x;
+  if (tid < a.B) sst[tid] = a.starts[tid];
   // ---- IS weights w_b = (N * P_b)^-beta / max_b  (B <= 256; recomputed per workgroup)
   bool gn = false;
   const float w = tid < a.B ? is_weight(a, tid, &gn) : 1.f;
@@ -117,7 +140,8 @@ __global__ __launch_bounds__(256) void td_kernel(const TdArgs a) {
     for (int k = 0; k < a.A; ++k) d[k] = (k == act) ? wb * delta * inv_n : 0.f;
     const float ad = fabsf(delta);
     if (a.td_abs) a.td_abs[i] = ad;
-    if (a.priority) a.priority[row] = powf(ad + a.prio_eps, a.alpha);
+    if (a.priority && prio_owner(sst, a.B, a.Tl, a.burn_in, a.cap_e, tl, b, 0, 1))
+      a.priority[row] = powf(ad + a.prio_eps, a.alpha);
   }
   lsum = wave_sum(lsum);
   __syncthreads();
@@ -185,10 +209,12 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
   constexpr int PER = HD / 64, MAXA = 8, NW = 16;
   const TdArgs& a = args.td;
   __shared__ float wsh[256];
+  __shared__ int sst[256];
   __shared__ float red[NW];
   __shared__ float tot_sh[NW];
   __shared__ int last;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < a.B) sst[tid] = a.starts[tid];
   const int n = a.Tl * a.B;
   const int i = blockIdx.x * NW + wave;      // this wave's transition
   const bool valid = i < n;
@@ -254,11 +280,14 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
     const float delta = __shfl(qs, act, 64) - y;
     const float wb = wsh[b];
     const float g = wb * delta * inv_n;      // dL/dQ[act]; every other action 0
+    // the wave checks the B starts 64 at a time for a later duplicate of this row
+    const bool own = a.priority ? __all(prio_owner(sst, a.B, a.Tl, a.burn_in, a.cap_e, tl, b, lane, 64))
+                                : false;
     if (lane == 0) {
       lsum = wb * 0.5f * delta * delta;
       const float ad = fabsf(delta);
       if (a.td_abs) a.td_abs[i] = ad;
-      if (a.priority) a.priority[row] = powf(ad + a.prio_eps, a.alpha);
+      if (own) a.priority[row] = powf(ad + a.prio_eps, a.alpha);
     }
     if (lane < a.A) a.dq[(size_t)i * a.A + lane] = lane == act ? g : 0.f;
     // dueling backward of row i (dueling_bwd_kernel's arithmetic on dq = g e_act)

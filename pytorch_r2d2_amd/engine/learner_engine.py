@@ -771,7 +771,8 @@ class LearnerEngine:
         gw2 = L.span(g, "val.2.weight", "adv.2.weight", (1 + A, HD))
         gb2 = L.span(g, "val.2.bias", "adv.2.bias", (1, 1 + A))
         gb1 = L.span(g, "val.0.bias", "adv.0.bias", (1, 2 * HD))
-        fused_hg = self.use_gemm and A + 1 <= 8 and HD % 64 == 0
+        # gradsum.hip head_grads: any head up to 63 actions (Seaquest 18, DMLab 15) in one launch
+        fused_hg = self.use_gemm and A <= 63 and HD % 64 == 0
         lc = self.cfg.learner
         # the tagged BPTT kernel's idle workgroups take the head-gradient reduction beside the
         # recurrence when they are enough; otherwise it runs as its own launch here

@@ -130,10 +130,12 @@ def run_native(cfg: R2D2Config, steps: int = 1000, actor_steps_per_update: int =
                 mlog.log("native", **rec)
             if info.is_main:
                 print("[native]", rec, flush=True)
-        if checkpoint_dir and info.is_main and (start + it + 1) % cfg.learner.checkpoint_interval == 0:
+        # the learner step counter is the engine's (it also counts the capture warm-up steps,
+        # which really trained), so checkpoint names / resume agree with the device step
+        if checkpoint_dir and info.is_main and eng.steps_done % cfg.learner.checkpoint_interval == 0:
             if drv is not None:
                 torch.cuda.current_stream(dev).wait_stream(drv.s_learn)
-            save_reference_checkpoint(eng.state_dict(), start + it + 1, checkpoint_dir)
+            save_reference_checkpoint(eng.state_dict(), eng.steps_done, checkpoint_dir)
     if drv is not None:
         drv.finish()
         drv.check_errors()
@@ -148,7 +150,7 @@ def run_native(cfg: R2D2Config, steps: int = 1000, actor_steps_per_update: int =
            "weights_version": drv.version if drv is not None else None}
     if checkpoint_dir and info.is_main:
         save_full_checkpoint(os.path.join(checkpoint_dir, "full_last.pt"), eng.state_dict(),
-                             eng.target_state_dict(), None, start + steps, cfg, eng.full_state_extra())
+                             eng.target_state_dict(), None, eng.steps_done, cfg, eng.full_state_extra())
     if drv is not None:
         out["driver"] = drv
     for s_ in (s_act, s_learn):

@@ -195,3 +195,34 @@ def test_td_fused_head_backward_matches_separate_launches(mode):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
     assert torch.equal(ra.priority, rb.priority)
     assert abs(a.loss_value() - b.loss_value()) <= 1e-6 * max(1.0, abs(b.loss_value()))
+
+
+def test_engine_bf16_seaquest_18_actions_fused_path():
+    """bf16 engine, 18-action head (seaquest8 preset): TD + head backward fused (td_duel_kernel)
+    and the head-gradient reduction in one gradsum launch -- no torch.mm fallback -- vs the fp32
+    autograd oracle."""
+    cfg, rp, eng, net, tgt = _make("fixed", preset="seaquest8",
+                                   **{"replay.burn_in": 6, "replay.learn": 8, "replay.overlap": 7})
+    assert eng.layout.A == 18
+    calls = []
+    orig = torch.mm
+    torch.mm = lambda *a, **k: (calls.append(1), orig(*a, **k))[1]   # noqa: E731
+    try:
+        eng._forward_loss()
+        eng._backward_core()
+        eng._backward_torso()
+    finally:
+        torch.mm = orig
+    torch.cuda.synchronize()
+    assert eng._duel_done
+    assert not calls or cfg.learner.dh_gemm == "blaslt" and len(calls) == 1, len(calls)
+    online = copy.deepcopy(net).to(DEV)
+    target = copy.deepcopy(tgt).to(DEV)
+    batch = batch_from_hbm(rp, eng.starts, eng.probs, cfg, DEV)
+    out = r2d2_loss(online, target, batch, cfg, "fixed")
+    out["loss"].backward()
+    assert abs(eng.loss.item() - out["loss"].item()) / out["loss"].item() < 3e-2
+    got = eng.layout.views(eng.grad)
+    for name, p in online.named_parameters():
+        r = _rel(got[name], p.grad)
+        assert r < 8e-2, f"{name}: rel err {r}"

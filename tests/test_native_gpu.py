@@ -291,3 +291,51 @@ def test_trajectory_channel_recv_into_hbm_replay(tmp_path):
     s.close()
     tmp.spawn(_traj_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
     assert torch.load(os.path.join(tmp_path, "traj.pt"), weights_only=True)["got"] == [90, 91]
+
+
+@pytest.mark.parametrize("fused", [False, True], ids=["td_kernel", "td_duel"])
+def test_td_row_priorities_last_write_wins(fused):
+    """Overlapping / duplicate sampled sequences: the row priority written is the one of the LAST
+    (t, b) in row-major order, as numpy resolves the reference's duplicate-index assignment
+    (learner.py:101-103); deterministic across runs."""
+    from pytorch_r2d2_amd.ops._lib import ptr
+    k = kernels()
+    g = torch.Generator(device="cpu").manual_seed(0)
+    Tl, B, A, Lb, cap_e, HD = 6, 8, 6, 2, 64, 64
+    starts = torch.tensor([3, 5, 3, 64 + 10, 60, 7, 5, 62], dtype=torch.int32)   # dups, overlaps, wrap
+    q = [torch.randn(Tl * B, A, generator=g) for _ in range(3)]
+    cap = 2 * cap_e
+    action = torch.randint(0, A, (cap,), generator=g).to(torch.uint8)
+    reward = torch.randn(cap, generator=g)
+    done = torch.zeros(cap, dtype=torch.uint8)
+    d = lambda t: t.to(DEV).contiguous()  # noqa: E731
+    qs, qa, qt = (d(x) for x in q)
+    st, act, rew, dn = d(starts), d(action), d(reward), d(done)
+    outs = []
+    for rep in range(2):
+        prio = torch.full((cap,), -1.0, device=DEV)
+        dq = torch.zeros(Tl * B, A, device=DEV)
+        loss, tdabs = torch.zeros(1, device=DEV), torch.zeros(Tl * B, device=DEV)
+        part, ticket = torch.zeros(4096, device=DEV), torch.zeros(1, dtype=torch.int32, device=DEV)
+        args = (ptr(qs), ptr(qa), ptr(qt), ptr(st), 0, ptr(act), ptr(rew), ptr(dn), ptr(dq), ptr(loss),
+                ptr(tdabs), ptr(prio), 0, 0, Tl, B, A, Lb, cap_e, 0.99, 0, 1e-3, 0.9, 1e-6, 0.0,
+                ptr(part), ptr(ticket))
+        if fused:
+            zr = torch.randn(Tl * B, 2 * HD, generator=g).to(torch.bfloat16).to(DEV)
+            w2 = torch.randn(1 + A, HD, generator=g).to(DEV)
+            dz = torch.zeros(Tl * B, 2 * HD, dtype=torch.bfloat16, device=DEV)
+            dva = torch.zeros(Tl * B, 1 + A, device=DEV)
+            assert k.r2_td_duel(*args, ptr(zr), ptr(w2), ptr(dz), ptr(dva), HD, 0, 0,
+                                torch.cuda.current_stream().cuda_stream) == 0
+        else:
+            assert k.r2_td_loss(*args, 0, torch.cuda.current_stream().cuda_stream) == 0
+        torch.cuda.synchronize()
+        outs.append(prio.cpu())
+        ad = tdabs.cpu().numpy().reshape(Tl, B)
+    # numpy reference: index[burn_in:].reshape(-1) = prio.reshape(-1), last write wins
+    ref = np.full(cap, -1.0, dtype=np.float32)
+    s = starts.numpy().astype(np.int64)
+    rows = (s - s % cap_e)[None, :] + (s % cap_e + Lb + np.arange(Tl)[:, None]) % cap_e   # (Tl, B)
+    ref[rows.reshape(-1)] = ((ad + 1e-6) ** 0.9).reshape(-1)
+    np.testing.assert_allclose(outs[0].numpy(), ref, rtol=1e-6)
+    assert torch.equal(outs[0], outs[1])
