@@ -1,0 +1,437 @@
+// Fused split-precision GEMM (gfx950): C = A.B with A, B given as bf16 hi / lo planes
+// (split.h) and ALL THREE products taken from ONE pass over K.
+//
+// The round-1 split path (gemm.hip gemm4 / gemm_group) ran the products as three passes over K,
+// each re-staging its operand pair through LDS: 3x the operand traffic of a bf16 GEMM and 3x the
+// K loop.  Here every K tile stages A_hi, A_lo, B_hi, B_lo once (2x the bf16 traffic) and each
+// fragment pair feeds three MFMAs (lo.hi, hi.lo, hi.hi, small terms first) -- the same
+// arithmetic as split.h mfma16_x3 -- so the MFMA pipe, not the operand path, sets the pace.
+// A plane that is null (an operand exact in bf16) is neither staged nor multiplied.
+//
+// Tile BM x BN x 64 (BM in {128, 192, 256}, BN in {64, 128}), 8 waves = 2 (M) x 4 (N), wave
+// (BM/2) x (BN/4) as (BM/32) x (BN/64) v_mfma_f32_16x16x32_bf16 accumulators, two waves per
+// SIMD.  LDS: 2 stages x {A_hi, A_lo, B_hi, B_lo} filled by global_load_lds (16 B/lane) with
+// the bank swizzles of gemm.hip v4 (k-major [rows][64], chunk c of row r at c ^ ((r >> 1) & 7);
+// mn-major per 128-column half [64][128], chunk c of k-row k at c ^ 2((k & 3) | ((k >> 3) & 1) << 2));
+// BM = 192 needs a k-major A.  Up to 4 problems per launch, each with its own A layout and a
+// K split S: a split item publishes its fp32 partial tile write-through, takes the tile's
+// ticket, and the last arriver sums the S partials in split order (bit-reproducible) and runs the
+// epilogue (alpha, bias, output row map, fp32 / bf16 / split-bf16 output, optional +=).
+// Blocks are remapped so that consecutive items (same A rows) share an XCD and its L2.
+#include "../common.h"
+
+#include "../gemm_tile.h"
+
+__device__ __attribute__((aligned(16))) bf16 g5_zero[8];
+
+__device__ __forceinline__ f32x4 g5_mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int g5_mnswz(int k) { return 2 * ((k & 3) | (((k >> 3) & 1) << 2)); }
+template <int BK>
+__device__ __forceinline__ int g5_kswz(int r) { return BK == 64 ? ((r >> 1) & 7) : 3 * ((r >> 3) & 1); }
+
+// Stage one R x BK operand plane: R*BK*2/1024 1-KB blocks, dealt evenly over the 8 waves.
+template <bool KMAJ, int R, int BK>
+__device__ __forceinline__ void g5_stage(const bf16* X, int ld, int i0, int imax, int k0, int kmax,
+                                         uint8_t* tile, int wave, int lane, int oz) {
+  constexpr int NBLK = R * BK * 2 / 1024, PW = NBLK / 8;
+  static_assert(NBLK % 8 == 0, "blocks per wave");
+  static_assert(KMAJ || R % 128 == 0, "mn-major images are 128-column halves");
+#pragma unroll
+  for (int j = 0; j < PW; ++j) {
+    const int blk = wave * PW + j;
+    int off;
+    bool kin;
+    if (KMAJ) {
+      constexpr int CPR = BK / 8, RPB = 64 / CPR;            // chunks per row, rows per block
+      const int row = blk * RPB + lane / CPR, cp = lane % CPR;
+      const int c = cp ^ g5_kswz<BK>(row);
+      const int k = k0 + c * 8;
+      kin = k < kmax;
+      off = min(i0 + row, imax - 1) * ld + k;
+    } else {
+      constexpr int BPH = BK / 4;                            // blocks per 128-column half
+      const int h = blk / BPH, kr = (blk % BPH) * 4 + (lane >> 4), cp = lane & 15;
+      const int c = cp ^ g5_mnswz(kr);
+      const int col = i0 + h * 128 + c * 8;
+      kin = k0 + kr < kmax;
+      off = (k0 + kr) * ld + (col < imax ? col : imax - 8);
+    }
+    const bf16* src = kin ? X + (off + oz) : g5_zero;
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(tile + blk * 1024),
+                                     16, 0, 0);
+  }
+}
+
+// 16x16x32 fragment (k-step ks of the tile): lane l holds X[i0 + (l & 15)][32 ks + 8 (l >> 4) .. +7]
+template <bool KMAJ, int BK>
+__device__ __forceinline__ bf16x8 g5_frag(const uint8_t* tile, int i0, int ks, int lane) {
+  const int l16 = lane & 15, g = lane >> 4;
+  if (KMAJ) {
+    const int r = i0 + l16, c = 4 * ks + g;
+    return *(const bf16x8*)(tile + r * (BK * 2) + ((c ^ g5_kswz<BK>(r)) * 16));
+  }
+  const int q = (lane >> 2) & 3, p = lane & 3;
+  const uint8_t* half = tile + (i0 >> 7) * (BK * 256);
+  const int kr = 32 * ks + 8 * g + q;
+  const int c = ((i0 & 127) >> 3) + (p >> 1);
+  const uint8_t* b0 = half + kr * 256 + ((c ^ g5_mnswz(kr)) * 16) + 8 * (p & 1);
+  return gm_tr8((const bf16*)b0, (const bf16*)(b0 + 4 * 256));
+}
+
+template <int N>
+__device__ __forceinline__ void g5_vmwait() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
+}
+
+struct G5Args {
+  GemmProb p[gm::MAXP];
+  int split[gm::MAXP];
+  int item_base[gm::MAXP];
+  long long slab_base[gm::MAXP];   // first partial slab (BM x BN fp32) of each problem
+  int ticket_base[gm::MAXP];
+  int np, total;
+  float* ws;
+  unsigned* tickets;
+};
+
+// K loop of one item: acc += A[m0.., k] B[k, n0..] over K tiles [kt0, kt1), NS-stage LDS ring,
+// every operand split (A_hi, A_lo, B_hi, B_lo staged; 3 MFMAs per fragment pair)
+template <bool AK, bool BKM, int BM, int BN, int BK, int NS>
+__device__ __forceinline__ void g5_mainloop(const GemmProb& P, int m0, int n0, int kt0, int kt1,
+                                            uint8_t* lds, int wave, int lane,
+                                            f32x4 (&acc)[BM / 32][BN / 64]) {
+  constexpr int FM = BM / 32, FN = BN / 64;
+  constexpr int OPA = BM * BK * 2, OPB = BN * BK * 2, STB = 2 * (OPA + OPB);
+  constexpr int NDMA = 2 * (BM + BN) * BK * 2 / (512 * 16);   // DMA instructions per thread per tile
+  const int wr = wave >> 2, wc = wave & 3;
+  auto stage = [&](int kt) {
+    int oz;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(oz));
+    uint8_t* st = lds + ((kt - kt0) % NS) * STB;
+    const int k0 = kt * BK;
+    g5_stage<AK, BM, BK>(P.A, P.lda, m0, P.M, k0, P.K, st, wave, lane, oz);
+    g5_stage<AK, BM, BK>(P.A_lo, P.lda, m0, P.M, k0, P.K, st + OPA, wave, lane, oz);
+    g5_stage<BKM, BN, BK>(P.B, P.ldb, n0, P.N, k0, P.K, st + 2 * OPA, wave, lane, oz);
+    g5_stage<BKM, BN, BK>(P.B_lo, P.ldb, n0, P.N, k0, P.K, st + 2 * OPA + OPB, wave, lane, oz);
+  };
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (kt0 + s < kt1) stage(kt0 + s);
+  for (int kt = kt0; kt < kt1; ++kt) {
+    // tile kt has landed once only the DMAs of tiles kt+1 .. kt+NS-2 (those issued) remain
+    const int ahead = kt1 - 1 - kt;
+    if (NS >= 4 && ahead >= 2) g5_vmwait<(NS >= 4 ? 2 : 0) * NDMA>();
+    else if (NS >= 3 && ahead >= 1) g5_vmwait<(NS >= 3 ? 1 : 0) * NDMA>();
+    else g5_vmwait<0>();
+    __builtin_amdgcn_s_barrier();     // tile kt visible; everyone finished reading tile kt-1
+    if (kt + NS - 1 < kt1) stage(kt + NS - 1);
+    const uint8_t* ah = lds + ((kt - kt0) % NS) * STB;
+    const uint8_t* al = ah + OPA;
+    const uint8_t* bh = ah + 2 * OPA;
+    const uint8_t* bl = bh + OPB;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 fbh[FN], fbl[FN], fah[FM], fal[FM];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        fbh[j] = g5_frag<BKM, BK>(bh, wc * (BN / 4) + 16 * j, ks, lane);
+        fbl[j] = g5_frag<BKM, BK>(bl, wc * (BN / 4) + 16 * j, ks, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        fah[i] = g5_frag<AK, BK>(ah, wr * (BM / 2) + 16 * i, ks, lane);
+        fal[i] = g5_frag<AK, BK>(al, wr * (BM / 2) + 16 * i, ks, lane);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          acc[i][j] = g5_mfma(fal[i], fbh[j], acc[i][j]);
+          acc[i][j] = g5_mfma(fah[i], fbl[j], acc[i][j]);
+          acc[i][j] = g5_mfma(fah[i], fbh[j], acc[i][j]);
+        }
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// C epilogue of 4 consecutive columns (row already mapped)
+__device__ __forceinline__ void g5_emit(const GemmProb& P, int row, int col, f32x4 a, bool vec) {
+  const int orow = P.crow ? P.crow[row] : row;
+  const size_t o = (size_t)orow * P.ldc + col;
+  float v[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = P.alpha * a[e] + (P.bias && col + e < P.N ? P.bias[col + e] : 0.f);
+  if (vec && col + 4 <= P.N) {
+    if (P.c_f32) {
+      f32x4* c = (f32x4*)((float*)P.C + o);
+      f32x4 w = {v[0], v[1], v[2], v[3]};
+      if (P.accumulate) w += *c;
+      *c = w;
+    } else if (P.C_lo) {
+      bf16x4 hi, lo;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { hi[e] = (bf16)v[e]; lo[e] = sp_lo(v[e]); }
+      *(bf16x4*)((bf16*)P.C + o) = hi;
+      *(bf16x4*)(P.C_lo + o) = lo;
+    } else {
+      bf16x4* c = (bf16x4*)((bf16*)P.C + o);
+      if (P.accumulate) {
+        const bf16x4 old = *c;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] += (float)old[e];
+      }
+      bf16x4 w;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[e] = (bf16)v[e];
+      *c = w;
+    }
+    return;
+  }
+  for (int e = 0; e < 4 && col + e < P.N; ++e) {
+    if (P.c_f32) {
+      float* c = (float*)P.C + o + e;
+      *c = P.accumulate ? *c + v[e] : v[e];
+    } else if (P.C_lo) {
+      sp_split(v[e], ((bf16*)P.C)[o + e], P.C_lo[o + e]);
+    } else {
+      bf16* c = (bf16*)P.C + o + e;
+      *c = (bf16)(P.accumulate ? (float)*c + v[e] : v[e]);
+    }
+  }
+}
+
+template <bool BKM, int BM, int BN, int BK, int NS>
+__global__ __launch_bounds__(512) void gemm5_kernel(const G5Args a) {
+  constexpr int FM = BM / 32, FN = BN / 64;
+  extern __shared__ __attribute__((aligned(1024))) uint8_t lds5[];
+  // the split-K arrival flag lives past the epilogue's staging rows (static LDS would push the
+  // (192, 128) tile past 160 KB)
+  int& last = *(int*)(lds5 + 64 * (BN + 16) * 4);
+  int bid;
+  {
+    const int b = blockIdx.x, x = b & 7, qn = a.total >> 3, r = a.total & 7;
+    bid = (x < r ? x * (qn + 1) : r * (qn + 1) + (x - r) * qn) + (b >> 3);
+  }
+  int pi = 0;
+#pragma unroll
+  for (int i = 1; i < gm::MAXP; ++i)
+    if (i < a.np && bid >= a.item_base[i]) pi = i;
+  const GemmProb& P = a.p[pi];
+  const int S = a.split[pi];
+  const int item = bid - a.item_base[pi];
+  const int tile = item / S, ksp = item % S;
+  const int tm = tile / P.tiles_n, tn = tile % P.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = (P.K + BK - 1) / BK, per = (nk + S - 1) / S;
+  const int kt0 = min(nk, ksp * per), kt1 = min(nk, kt0 + per);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave >> 2, wc = wave & 3;
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (BM % 128 == 0) {
+    if (P.a_kmajor) g5_mainloop<true, BKM, BM, BN, BK, NS>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc);
+    else g5_mainloop<false, BKM, BM, BN, BK, NS>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc);
+  } else {
+    g5_mainloop<true, BKM, BM, BN, BK, NS>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc);
+  }
+
+  // ---- epilogue: 64 rows at a time through LDS (row-contiguous, 4 columns per thread)
+  // acc[i][j][e] = tile[wr*(BM/2) + 16i + 4(l>>4) + e][wc*(BN/4) + 16j + (l&15)]
+  constexpr int LS = BN + 16;
+  constexpr int NP = FM / 2;                // 32 rows per wave row per pass -> 64 rows per pass
+  float* L = (float*)lds5;
+  const int l16 = lane & 15, g = lane >> 4;
+  const bool vec = ((uintptr_t)P.C % 16 == 0) && (P.ldc % 4 == 0);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.ws, 0, 0x7fffffff, 0x00020000);
+  const long long slab0 = a.slab_base[pi] + (long long)tile * S;
+  // slab layout: [split][BM][BN] fp32; element (r, c) of split s at ((slab0 + s) * BM + r) * BN + c
+  auto soff = [&](int s, int r, int c) {
+    return (uint32_t)((((slab0 + s) * BM + r) * BN + c) * 4);
+  };
+  if (S > 1) {
+    // publish this item's partial tile write-through (sc1), drain, take the tile's ticket
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      __builtin_amdgcn_s_barrier();
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            L[(wr * 32 + ii * 16 + 4 * g + e) * LS + wc * (BN / 4) + 16 * j + l16] = acc[2 * p + ii][j][e];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      for (int q = tid; q < 64 * (BN / 4); q += 512) {
+        const int lr = q / (BN / 4), cc = (q % (BN / 4)) * 4;
+        const int r = (lr >> 5) * (BM / 2) + 32 * p + (lr & 31);
+        const f32x4 v = *(const f32x4*)(L + lr * LS + cc);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, soff(ksp, r, cc), 0, 16);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned* tk = a.tickets + a.ticket_base[pi] + tile;
+    if (tid == 0)
+      last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(S - 1);
+    __syncthreads();
+    if (!last) return;
+    for (int q = tid; q < BM * (BN / 4); q += 512) {
+      const int r = q / (BN / 4), cc = (q % (BN / 4)) * 4;
+      const int row = m0 + r, col = n0 + cc;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < S; ++s)
+        v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, soff(s, r, cc), 0, 16));
+      if (row < P.M && col < P.N) g5_emit(P, row, col, v, vec);
+    }
+    if (tid == 0) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          L[(wr * 32 + ii * 16 + 4 * g + e) * LS + wc * (BN / 4) + 16 * j + l16] = acc[2 * p + ii][j][e];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#pragma unroll 2
+    for (int q = tid; q < 64 * (BN / 4); q += 512) {
+      const int lr = q / (BN / 4), cc = (q % (BN / 4)) * 4;
+      const int row = m0 + (lr >> 5) * (BM / 2) + 32 * p + (lr & 31);
+      const int col = n0 + cc;
+      if (row >= P.M || col >= P.N) continue;
+      g5_emit(P, row, col, *(const f32x4*)(L + lr * LS + cc), vec);
+    }
+  }
+}
+
+template <bool BKM, int BM, int BN, int BK, int NS>
+static void g5_kernel_launch(const G5Args& a, hipStream_t s) {
+  constexpr int LDS = NS * 2 * (BM + BN) * BK * 2;
+  static_assert(LDS <= 160 * 1024, "LDS");
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)gemm5_kernel<BKM, BM, BN, BK, NS>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm5_kernel<BKM, BM, BN, BK, NS>), dim3(a.total), dim3(512), LDS, s, a);
+}
+
+// tile configurations: {BM, BN, BK, NS}
+static const int g5_cfgs[][4] = {{192, 128, 64, 2}, {128, 128, 64, 2}, {256, 128, 32, 3},
+                                 {256, 256, 32, 2}, {256, 64, 64, 2}, {128, 64, 64, 2}};
+static const int g5_ncfg = 6;
+
+static int g5_tiles(const GemmProb& p, int bm, int bn) {
+  return ((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn);
+}
+
+// descs: np x GEMM_DESC (gemm.hip r2_gemm layout), every operand split (A_lo and B_lo set), one B
+// layout per launch.  split: np K splits (null = 1).  cfg: index into g5_cfgs, or -1 = pick by a
+// CU-utilisation model for n_cus resident workgroups (one per CU).  Returns the cfg used (>= 0)
+// or an error (< 0).
+extern "C" int r2_gemm5(const int64_t* descs, const int* split, int np, int cfg, float* ws,
+                        long long ws_bytes, unsigned* tickets, int n_tickets, int n_cus, void* stream) {
+  if (np < 1 || np > gm::MAXP) return -1;
+  G5Args a;
+  a.np = np; a.ws = ws; a.tickets = tickets;
+  int bkm = -1;
+  bool all_k = true;
+  for (int i = 0; i < np; ++i) {
+    const int rc = gemm_parse_desc(descs + GEMM_DESC * i, a.p[i]);
+    if (rc) return rc;
+    if (!a.p[i].A_lo || !a.p[i].B_lo) return -10;      // split operands only
+    if (bkm < 0) bkm = a.p[i].b_kmajor;
+    if (bkm != a.p[i].b_kmajor) return -5;
+    all_k = all_k && a.p[i].a_kmajor;
+    a.split[i] = split && split[i] > 1 ? split[i] : 1;
+  }
+  auto ok = [&](int c) {
+    const int bm = g5_cfgs[c][0], bn = g5_cfgs[c][1];
+    if (bm % 128 && !all_k) return false;
+    if (bn % 128 && !bkm) return false;
+    return true;
+  };
+  if (cfg < 0) {   // smallest (rounds x per-item MFMA work / model efficiency)
+    double best = 1e30;
+    const int nc = n_cus > 0 ? n_cus : 256;
+    for (int c = 0; c < g5_ncfg; ++c) {
+      if (!ok(c)) continue;
+      const int bm = g5_cfgs[c][0], bn = g5_cfgs[c][1];
+      long long items = 0;
+      double work = 0;
+      for (int i = 0; i < np; ++i) {
+        items += (long long)g5_tiles(a.p[i], bm, bn) * a.split[i];
+        work = fmax(work, (double)bm * bn * ((a.p[i].K + a.split[i] - 1) / a.split[i]));
+      }
+      const long long rounds = (items + nc - 1) / nc;
+      // operand bytes per MFMA fall with the tile's perimeter / area
+      const double eff = 1.0 / (1.0 + 96.0 * (1.0 / bm + 1.0 / bn));
+      const double cost = rounds * work / eff;
+      if (cost < best) { best = cost; cfg = c; }
+    }
+  }
+  if (cfg < 0 || cfg >= g5_ncfg || !ok(cfg)) return -8;
+  const int bm = g5_cfgs[cfg][0], bn = g5_cfgs[cfg][1];
+  int items = 0, tks = 0;
+  long long slabs = 0;
+  for (int i = 0; i < np; ++i) {
+    GemmProb& p = a.p[i];
+    p.tiles_n = (p.N + bn - 1) / bn;
+    const int t = g5_tiles(p, bm, bn);
+    a.item_base[i] = items;
+    a.slab_base[i] = slabs;
+    a.ticket_base[i] = tks;
+    items += t * a.split[i];
+    if (a.split[i] > 1) { slabs += (long long)t * a.split[i]; tks += t; }
+  }
+  for (int i = np; i < gm::MAXP; ++i) { a.p[i] = a.p[0]; a.split[i] = 1; a.item_base[i] = 1 << 30; }
+  a.total = items;
+  if (slabs * bm * bn * 4 > ws_bytes || tks > n_tickets) return -7;
+  hipStream_t s = (hipStream_t)stream;
+  switch (cfg * 2 + bkm) {
+    case 0: g5_kernel_launch<false, 192, 128, 64, 2>(a, s); break;
+    case 1: g5_kernel_launch<true, 192, 128, 64, 2>(a, s); break;
+    case 2: g5_kernel_launch<false, 128, 128, 64, 2>(a, s); break;
+    case 3: g5_kernel_launch<true, 128, 128, 64, 2>(a, s); break;
+    case 4: g5_kernel_launch<false, 256, 128, 32, 3>(a, s); break;
+    case 5: g5_kernel_launch<true, 256, 128, 32, 3>(a, s); break;
+    case 6: g5_kernel_launch<false, 256, 256, 32, 2>(a, s); break;
+    case 7: g5_kernel_launch<true, 256, 256, 32, 2>(a, s); break;
+    case 9: g5_kernel_launch<true, 256, 64, 64, 2>(a, s); break;
+    case 11: g5_kernel_launch<true, 128, 64, 64, 2>(a, s); break;
+    default: return -8;
+  }
+  R2_CHECK_LAUNCH();
+  return cfg;
+}
+
+// bytes of split-K workspace for configuration cfg
+extern "C" long long r2_gemm5_ws_bytes(const int64_t* descs, const int* split, int np, int cfg) {
+  if (cfg < 0 || cfg >= g5_ncfg) return -1;
+  long long b = 0;
+  for (int i = 0; i < np; ++i) {
+    GemmProb p;
+    if (gemm_parse_desc(descs + GEMM_DESC * i, p)) return -1;
+    if (split && split[i] > 1)
+      b += (long long)g5_tiles(p, g5_cfgs[cfg][0], g5_cfgs[cfg][1]) * split[i] * g5_cfgs[cfg][0] *
+           g5_cfgs[cfg][1] * 4;
+  }
+  return b;
+}

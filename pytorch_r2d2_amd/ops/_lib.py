@@ -98,6 +98,10 @@ _SIGS = {
     "r2_lstm_bwd_tag_ring_bytes": [I, I],
     "r2_lstm_bwd_persist": [P, P, P, P, P, P, P, I, I, I, I, P, P, P],
     "r2_apply_pending": [P, P, I, P, P, P, I, I, F, P, P, P, I, P, P],
+    "r2_gemm5": [P, P, I, I, P, I64, P, I, I, P],
+    "r2_gemm5_ws_bytes": [P, P, I, I],
+    "r2_ingest_record": [P, P],
+    "r2_ingest_args_bytes": [],
     "r2_stream_create_cumask": [P, I, P],
     "r2_stream_get_cumask": [P, P, I],
     "r2_stream_destroy": [P],
@@ -136,7 +140,7 @@ def kernels():
             if fn is None:
                 continue
             fn.argtypes = argtypes
-            fn.restype = ctypes.c_int
+            fn.restype = ctypes.c_longlong if name.endswith("_ws_bytes") else ctypes.c_int
         _lib = lib
         return lib
 

@@ -93,3 +93,51 @@ def gemm_group(problems: List[Gemm], splits: List[int], ws: torch.Tensor, ticket
     check(kernels().r2_gemm_group(arr.ctypes.data, sp.ctypes.data, len(problems), ws.data_ptr(),
                                   ws.numel() * ws.element_size(), tickets.data_ptr(), tickets.numel(),
                                   stream or stream_handle()), "gemm_group")
+
+
+_G5_WS = {}
+# csrc/kernels/gemm_sp.hip g5_cfgs: (BM, BN, BK, stages)
+G5_CFGS = [(192, 128, 64, 2), (128, 128, 64, 2), (256, 128, 32, 3), (256, 256, 32, 2),
+           (256, 64, 64, 2), (128, 64, 64, 2)]
+
+
+def gemm_sp(problems: List[Gemm], splits: Optional[List[int]] = None, cfg: int = -1,
+            ws: Optional[torch.Tensor] = None, tickets: Optional[torch.Tensor] = None,
+            n_cus: int = 0, stream=None) -> int:
+    """Fused split-precision GEMM (csrc/kernels/gemm_sp.hip): up to 4 problems (every operand
+    split, shared B layout, any A layout) in one launch, each with a K split; all three hi / lo
+    products from ONE pass over K.  ``cfg``: index into ``G5_CFGS`` or -1 = the launcher picks the
+    tile for ``n_cus`` CUs.  ``ws`` / ``tickets``: split-K workspace (fp32) and zeroed int32
+    tickets; allocated (and cached per device) when omitted -- pass them explicitly inside a graph
+    capture.  Returns the configuration used."""
+    arr = np.asarray([v for p in problems for v in p.desc()], dtype=np.int64)
+    sp = np.asarray(splits if splits is not None else [1] * len(problems), dtype=np.int32)
+    k = kernels()
+    if ws is None or tickets is None:
+        dev = problems[0].c.device
+        need = 0
+        if (sp > 1).any():
+            for c in ([cfg] if cfg >= 0 else range(len(G5_CFGS))):
+                need = max(need, int(k.r2_gemm5_ws_bytes(arr.ctypes.data, sp.ctypes.data,
+                                                         len(problems), c)))
+        key = str(dev)
+        cur = _G5_WS.get(key)
+        if cur is None or cur[0].numel() * 4 < need:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("gemm_sp: pass ws / tickets when capturing a graph")
+            cur = (torch.zeros(max(need // 4, 1), dtype=torch.float32, device=dev),
+                   torch.zeros(4096, dtype=torch.int32, device=dev))
+            _G5_WS[key] = cur
+        ws, tickets = cur
+    rc = k.r2_gemm5(arr.ctypes.data, sp.ctypes.data, len(problems), int(cfg), ws.data_ptr(),
+                    ws.numel() * ws.element_size(), tickets.data_ptr(), tickets.numel(), int(n_cus),
+                    stream or stream_handle())
+    if rc < 0:
+        raise RuntimeError(f"gemm_sp failed with code {rc}")
+    return rc
+
+
+def gemm_sp_ws_bytes(problems: List[Gemm], splits: List[int], cfg: int) -> int:
+    arr = np.asarray([v for p in problems for v in p.desc()], dtype=np.int64)
+    sp = np.asarray(splits, dtype=np.int32)
+    return int(kernels().r2_gemm5_ws_bytes(arr.ctypes.data, sp.ctypes.data, len(problems), cfg))
