@@ -113,6 +113,11 @@ class LearnerConfig:
     fwd_chunks: int = 0
     td_fuse_head_bwd: bool = True     # dueling-head backward inside the TD launch (td_duel_kernel)
     dh_gemm: str = "blaslt"           # head backward dh = dz @ W1: blaslt (hipBLASLt) | mfma
+    # split precision (compute_dtype fp32) GEMMs: "fused" = gemm_sp.hip (hi / lo planes staged
+    # once, 3 MFMAs per fragment pair: x-projection 164 -> 125 us, post-BPTT group 142 -> 106 us
+    # at K splits 4,4,4,1, dh 26 -> 18 us; profiles/r02_gemm_sp_micro_v1.txt) | "multipass"
+    sp_gemm: str = "fused"
+    sp_group_splits: str = "4,4,4,1"  # K splits of the fused post-BPTT group (dW_ih, dW_hh, dW_head1, dX)
     torso_bwd: str = "fused"          # fused (HIP kernel) | library (MIOpen convolution_backward)
     # library conv path (frame geometries without the fused HIP torso, e.g. DMLab): MIOpen find
     # mode (torch.backends.cudnn.benchmark) instead of its immediate-mode heuristics

@@ -48,7 +48,7 @@ import torch
 from ..config import R2D2Config
 from ..models.qnet import QNet
 from ..ops._lib import check, kernels, ptr, stream_handle
-from ..ops.gemm import Gemm, gemm, gemm_group, group_ws_bytes
+from ..ops.gemm import G5_CFGS, Gemm, gemm, gemm_group, gemm_sp, gemm_sp_ws_bytes, group_ws_bytes
 from ..models.qnet import torso_dims
 from ..ops.torso_lib import fused_torso_supported, gather_frames_nhwc, torso_forward_library
 from .layout import ParamLayout, UNITS
@@ -610,10 +610,11 @@ class LearnerEngine:
         # input projections (one GEMM per net over every row)
         if self.sp:
             xp_on, xp_tg = self.xp_on, self.xp_tg
-            gemm(Gemm(self.X_on, pk["w_ih"].t(), xp_on, bias=self.lstm_b, a_lo=self.X_on_lo,
-                      b_lo=self.pk_lo["w_ih"].t()),
-                 Gemm(self.X_tg, pt["w_ih"].t(), xp_tg, bias=self.lstm_b_t, a_lo=self.X_tg_lo,
-                      b_lo=self.pk_t_lo["w_ih"].t()))
+            self._gemm_sp("xproj", [
+                Gemm(self.X_on, pk["w_ih"].t(), xp_on, bias=self.lstm_b, a_lo=self.X_on_lo,
+                     b_lo=self.pk_lo["w_ih"].t()),
+                Gemm(self.X_tg, pt["w_ih"].t(), xp_tg, bias=self.lstm_b_t, a_lo=self.X_tg_lo,
+                     b_lo=self.pk_t_lo["w_ih"].t())])
         elif self.use_gemm:
             xp_on, xp_tg = self.xp_on, self.xp_tg
             gemm(Gemm(self.X_on, pk["w_ih"].t(), xp_on, bias=self.lstm_b),
@@ -715,7 +716,7 @@ class LearnerEngine:
                                  ptr(gw2), ptr(gb2), ptr(gb1), N, A, HD, ptr(self.gs_ws),
                                  ptr(self.gs_ticket), s), "head_grads_sp")
         dh = self.dh
-        gemm(Gemm(self.dz, pk["head1"], dh, a_lo=self.dz_lo, b_lo=pkl["head1"]))
+        self._gemm_sp("dh", [Gemm(self.dz, pk["head1"], dh, a_lo=self.dz_lo, b_lo=pkl["head1"])])
         check(k.r2_lstm_bwd_tag_sp(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]), ptr(self.c0["on"]),
                                    ptr(pk["w_hhT"]), ptr(pkl["w_hhT"]), ptr(self.dgates),
                                    ptr(self.dgates_lo), B, T, Lb, H, ptr(self.ctr), ptr(self.err),
@@ -745,6 +746,11 @@ class LearnerEngine:
                   Gemm(dgT, X, L.view(g, "lstm.weight_ih"), crow=self.gate_perm_i32, a_lo=dgTl, b_lo=Xl)]
         x_job = Gemm(self.dgates, pk["w_ih"], self.dX, a_lo=self.dgates_lo, b_lo=pkl["w_ih"],
                      c_lo=self.dX_lo)
+        if self.cfg.learner.sp_gemm == "fused":
+            splits = [int(v) for v in self.cfg.learner.sp_group_splits.split(",")]
+            self._gemm_sp("group", [w_jobs[2], w_jobs[1], w_jobs[0], x_job], splits)
+            self._dX = self.dX
+            return
         splits = self._group_splits(w_jobs, x_job)
         if splits:
             gemm_group([w_jobs[2], w_jobs[1], w_jobs[0], x_job], splits, self.gg_ws, self.gg_tickets)
@@ -752,6 +758,24 @@ class LearnerEngine:
             gemm(w_jobs[2], w_jobs[1], w_jobs[0])
             gemm(x_job)
         self._dX = self.dX
+
+    def _gemm_sp(self, site: str, probs, splits=None):
+        """Split-precision GEMMs of one call site: the fused one-pass kernel (gemm_sp.hip) with a
+        per-site split-K workspace sized before capture, or the multi-pass kernels
+        (``learner.sp_gemm``)."""
+        if self.cfg.learner.sp_gemm != "fused":
+            gemm(*probs)
+            return
+        splits = splits or [1] * len(probs)
+        if not hasattr(self, "_sp_ws"):
+            self._sp_ws = {}
+        cur = self._sp_ws.get(site)
+        if cur is None:   # (inside a capture: from the graph's pool, kept alive here)
+            need = max(gemm_sp_ws_bytes(probs, splits, c) for c in range(len(G5_CFGS)))
+            cur = (torch.zeros(max(need // 4, 1), dtype=torch.float32, device=self.device),
+                   torch.zeros(4096, dtype=torch.int32, device=self.device))
+            self._sp_ws[site] = cur
+        gemm_sp(probs, splits=splits, ws=cur[0], tickets=cur[1], n_cus=self.n_cus)
 
     def _backward_core(self):
         """Head backward, BPTT, LSTM/head weight gradients -> grad bucket 'core'."""
