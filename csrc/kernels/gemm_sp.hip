@@ -99,7 +99,7 @@ struct G5Args {
 
 // K loop of one item: acc += A[m0.., k] B[k, n0..] over K tiles [kt0, kt1), NS-stage LDS ring,
 // every operand split (A_hi, A_lo, B_hi, B_lo staged; 3 MFMAs per fragment pair)
-template <bool AK, bool BKM, int BM, int BN, int BK, int NS>
+template <bool AK, bool BKM, int BM, int BN, int BK, int NS, bool IL>
 __device__ __forceinline__ void g5_mainloop(const GemmProb& P, int m0, int n0, int kt0, int kt1,
                                             uint8_t* lds, int wave, int lane,
                                             f32x4 (&acc)[BM / 32][BN / 64]) {
@@ -132,6 +132,50 @@ __device__ __forceinline__ void g5_mainloop(const GemmProb& P, int m0, int n0, i
     const uint8_t* al = ah + OPA;
     const uint8_t* bh = ah + 2 * OPA;
     const uint8_t* bl = bh + OPB;
+    if constexpr (IL) {
+      // fragments of k-step ks+1 are read from LDS while the MFMAs of k-step ks issue, one
+      // ds_read per MFMA pair (sched_group_barrier), so neither pipe waits for the other
+      constexpr int KS = BK / 32, NF = 2 * (FM + FN);
+      bf16x8 fr[2][NF];   // [buffer][B hi (FN), B lo (FN), A hi (FM), A lo (FM)]
+      auto load = [&](int ks, bf16x8 (&f)[NF]) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          f[j] = g5_frag<BKM, BK>(bh, wc * (BN / 4) + 16 * j, ks, lane);
+          f[FN + j] = g5_frag<BKM, BK>(bl, wc * (BN / 4) + 16 * j, ks, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          f[2 * FN + i] = g5_frag<AK, BK>(ah, wr * (BM / 2) + 16 * i, ks, lane);
+          f[2 * FN + FM + i] = g5_frag<AK, BK>(al, wr * (BM / 2) + 16 * i, ks, lane);
+        }
+      };
+      load(0, fr[0]);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        bf16x8 (&f)[NF] = fr[ks & 1];
+        if (ks + 1 < KS) load(ks + 1, fr[(ks + 1) & 1]);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            acc[i][j] = g5_mfma(f[2 * FN + FM + i], f[j], acc[i][j]);
+            acc[i][j] = g5_mfma(f[2 * FN + i], f[FN + j], acc[i][j]);
+            acc[i][j] = g5_mfma(f[2 * FN + i], f[j], acc[i][j]);
+          }
+        __builtin_amdgcn_s_setprio(0);
+        if (ks + 1 < KS) {
+          // interleave: NF fragment reads (ds_read_b128 or 2 x ds_read_b64_tr) over 3 FM FN MFMAs
+#pragma unroll
+          for (int q = 0; q < NF; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x100, BKM && AK ? 1 : 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, (3 * FM * FN) / NF, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 3 * FM * FN - NF * ((3 * FM * FN) / NF), 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       bf16x8 fbh[FN], fbl[FN], fah[FM], fal[FM];
@@ -156,6 +200,7 @@ __device__ __forceinline__ void g5_mainloop(const GemmProb& P, int m0, int n0, i
         }
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
+    }
     }
   }
 }
@@ -206,7 +251,7 @@ __device__ __forceinline__ void g5_emit(const GemmProb& P, int row, int col, f32
   }
 }
 
-template <bool BKM, int BM, int BN, int BK, int NS>
+template <bool BKM, int BM, int BN, int BK, int NS, bool IL>
 __global__ __launch_bounds__(512) void gemm5_kernel(const G5Args a) {
   constexpr int FM = BM / 32, FN = BN / 64;
   extern __shared__ __attribute__((aligned(1024))) uint8_t lds5[];
@@ -238,10 +283,10 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const G5Args a) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   if constexpr (BM % 128 == 0) {
-    if (P.a_kmajor) g5_mainloop<true, BKM, BM, BN, BK, NS>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc);
-    else g5_mainloop<false, BKM, BM, BN, BK, NS>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc);
+    if (P.a_kmajor) g5_mainloop<true, BKM, BM, BN, BK, NS, IL>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc);
+    else g5_mainloop<false, BKM, BM, BN, BK, NS, IL>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc);
   } else {
-    g5_mainloop<true, BKM, BM, BN, BK, NS>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc);
+    g5_mainloop<true, BKM, BM, BN, BK, NS, IL>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc);
   }
 
   // ---- epilogue: 64 rows at a time through LDS (row-contiguous, 4 columns per thread)
@@ -320,17 +365,25 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const G5Args a) {
   }
 }
 
-template <bool BKM, int BM, int BN, int BK, int NS>
-static void g5_kernel_launch(const G5Args& a, hipStream_t s) {
+static int g5_il = 1;   // interleaved fragment loads (r2_gemm5_set_mode)
+extern "C" int r2_gemm5_set_mode(int il) { g5_il = il; return 0; }
+
+template <bool BKM, int BM, int BN, int BK, int NS, bool IL>
+static void g5_kernel_launch_il(const G5Args& a, hipStream_t s) {
   constexpr int LDS = NS * 2 * (BM + BN) * BK * 2;
   static_assert(LDS <= 160 * 1024, "LDS");
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)gemm5_kernel<BKM, BM, BN, BK, NS>,
+    hipFuncSetAttribute((const void*)gemm5_kernel<BKM, BM, BN, BK, NS, IL>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm5_kernel<BKM, BM, BN, BK, NS>), dim3(a.total), dim3(512), LDS, s, a);
+  hipLaunchKernelGGL((gemm5_kernel<BKM, BM, BN, BK, NS, IL>), dim3(a.total), dim3(512), LDS, s, a);
+}
+template <bool BKM, int BM, int BN, int BK, int NS>
+static void g5_kernel_launch(const G5Args& a, hipStream_t s) {
+  if (g5_il) g5_kernel_launch_il<BKM, BM, BN, BK, NS, true>(a, s);
+  else g5_kernel_launch_il<BKM, BM, BN, BK, NS, false>(a, s);
 }
 
 // tile configurations: {BM, BN, BK, NS}

@@ -61,7 +61,8 @@ struct TSJob {
 struct TSArgs {
   const uint8_t* frames;
   TSJob job[TS_MAX_JOBS];
-  int njobs, pad_[3];
+  int njobs, dbg, pad_[2];   // dbg: timing-probe bits (r2_torso_sp_debug), 0 in production
+  long long* trace;          // optional per-phase clock stamps (r2_torso_sp_trace), null in production
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t ts_rsrc(const void* p, uint32_t bytes) {
@@ -118,7 +119,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp_kernel(const TSArgs args) {
     const bool have = f < n_frames;
     const int fn = f + stride;
     // =================== phase A: conv1(f) || conv3(f-1)
-    if (have) {
+    if (have && !(args.dbg & 1)) {
       const size_t row = J.rows ? (size_t)J.rows[f] : (size_t)f;
       const __amdgpu_buffer_rsrc_t frs = ts_rsrc(args.frames + row * IN_BYTES, IN_BYTES);
       for (int i = 0; i < t1n; ++i) {
@@ -162,7 +163,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp_kernel(const TSArgs args) {
         }
       }
     }
-    if (fprev >= 0 && conv3_wave) {
+    if (fprev >= 0 && conv3_wave && !(args.dbg & 4)) {
       // conv3(f-1): pixel tile (wave == 6), K = 288 = (kh 3, kw 3, ci 32); A = W3 from L2
       const int p = (wave == 6 ? 32 : 0) + l32;
       const int pc = p < P3 ? p : P3 - 1;
@@ -203,6 +204,8 @@ __global__ __launch_bounds__(512) void torso_fwd_sp_kernel(const TSArgs args) {
 
     // =================== phase B: conv2(f) on waves 0..2; act1 save + next-frame warm-up
     if (conv2_wave) {
+      if (args.dbg & 2) goto conv2_done;
+      {
       const int p = wave * 32 + l32;
       const int pc = p < P2 ? p : P2 - 1;
       const int oy = pc / 9, ox = pc % 9;
@@ -251,6 +254,8 @@ __global__ __launch_bounds__(512) void torso_fwd_sp_kernel(const TSArgs args) {
           }
         }
       }
+      }
+    conv2_done:;
     } else {
       const int t5 = tid - 192;   // 0..319
       // warm the next frame's lines into L2 / L1 (consumed below, after the act1 copy-out)
@@ -284,6 +289,318 @@ __global__ __launch_bounds__(512) void torso_fwd_sp_kernel(const TSArgs args) {
 
 // jobs: njobs x TS_JOB_WORDS int64 {rows, n, w1, w1l, b1, w2, w2l, b2, w3, w3l, b3, out, out_l,
 // s1, s1l, s2, s2l, 0, 0, 0}.  grid <= 0: one workgroup per CU (the caller passes the CU count).
+// ============================================================================================
+// Forward v2 (the default): the v1 profile (tools/sp_micro.py probe, profiles/r02_torso_sp_*)
+// showed conv1's B fragments (two 4-byte buffer loads per K step from L1 / L2) and conv3's W3
+// fragments (L2, re-read by two waves per frame: 72 KB / frame) latency-bound, the next-frame
+// warm-up waited on inside phase B, and 2-3-way bank conflicts on the padded act1 image.  v2:
+//   * the raw uint8 frame lives in LDS (28 KB): waves 3..7 load frame f+1 into registers at the
+//     start of phase A(f) (nothing else of theirs waits on vmcnt there) and store it in phase B(f);
+//     conv1 reads its B fragments with two conflict-free ds_read_b32 per K step;
+//   * act1 hi / lo unpadded (64 B per pixel) with a row-XOR swizzle (a1_off): the stride-2 conv2
+//     reads drop from ~2.8 to ~1.8 LDS cycles per group and the image shrinks by 12.8 KB, which is
+//     what makes room for the frame (LDS 159.3 KB);
+//   * conv3 runs on wave 2 alone, both pixel tiles sharing every A fragment, with W3 hi / lo held
+//     in the registers the conv1 waves use for W1 (steps 16-17 from L2): no W3 traffic per frame;
+//   * tiles: conv1 2,2,0,2 | 2,2,1,2 per wave (SIMD2 = conv3 108 MFMAs + one conv1 tile).
+namespace tsp2 {
+using tsp::NT; using tsp::IN_BYTES; using tsp::P1; using tsp::P2; using tsp::P3;
+constexpr int OFF_FR = 0;                                  // uint8 [4][84][84]
+constexpr int OFF_A1H = OFF_FR + 4 * 84 * 84;             // 28224: [100 rows][16 x 16 B]
+constexpr int OFF_A1L = OFF_A1H + 400 * 64;                // 53824
+constexpr int OFF_A2H = OFF_A1L + 400 * 64;                // 79424: [81][40] bf16 (padded)
+constexpr int OFF_A2L = OFF_A2H + 81 * 40 * 2;             // 85904
+constexpr int OFF_W2H = OFF_A2L + 81 * 40 * 2;             // 92384: [32][520] bf16
+constexpr int OFF_W2L = OFF_W2H + 32 * 520 * 2;            // 125664
+constexpr int OFF_B = OFF_W2L + 32 * 520 * 2;              // 158944: biases conv2, conv3, conv1
+constexpr int OFF_W3T = OFF_B + 96 * 4;                    // 159328: W3[:, 256:288] hi, lo
+constexpr int LDS_BYTES = OFF_W3T + 2 * 32 * 32 * 2;       // 163424
+constexpr int IN_CHUNKS2 = 4 * 84 * 84 / 16;               // 1764
+constexpr int PF = (IN_CHUNKS2 + 319) / 320;               // 6 chunks per prefetch thread
+static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+}  // namespace tsp2
+
+// act1 image: pixel P, 16-byte chunk c (channels 8c .. 8c+7) -> byte offset in one plane
+__device__ __forceinline__ int a1_off(int P, int c) {
+  return ((P >> 2) << 8) + (((((P & 3) << 2) | c) ^ ((P >> 2) & 15)) << 4);
+}
+
+__constant__ int c_s2_begin[8] = {0, 2, 4, 4, 6, 8, 10, 11};
+__constant__ int c_s2_count[8] = {2, 2, 0, 2, 2, 2, 1, 2};
+
+__global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
+  using namespace tsp2;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint8_t* fr = lds + OFF_FR;
+  uint8_t* a1h = lds + OFF_A1H;
+  uint8_t* a1l = lds + OFF_A1L;
+  bf16* a2h = (bf16*)(lds + OFF_A2H);
+  bf16* a2l = (bf16*)(lds + OFF_A2L);
+  bf16* w2h = (bf16*)(lds + OFF_W2H);
+  bf16* w2l = (bf16*)(lds + OFF_W2L);
+  float* lb = (float*)(lds + OFF_B);
+  uint8_t* w3t = lds + OFF_W3T;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int half = lane >> 5, l32 = lane & 31;
+  const int wk = blockIdx.x;
+  int ji = 0;
+#pragma unroll
+  for (int i = 1; i < TS_MAX_JOBS; ++i)
+    if (i < args.njobs && wk >= args.job[i].wbegin) ji = i;
+  const TSJob& J = args.job[ji];
+  const int stride = J.wcount;
+  if (wk - J.wbegin >= stride) return;
+  const int n_frames = J.n;
+  int f = wk - J.wbegin;
+  if (f >= n_frames) return;
+  const bool conv3_wave = wave == 2, conv2_wave = wave < 3, pf_wave = wave >= 3;
+  const int t5 = tid - 192;   // prefetch thread index (waves 3..7)
+
+  // ---- once: W2 hi / lo -> LDS; W1 (conv1 waves) or W3 (wave 2) fragments -> registers; biases;
+  //      the first frame -> LDS
+  for (int i = tid; i < 32 * 64; i += NT) {
+    const int r = i >> 6, c = i & 63;
+    *(bf16x8*)(w2h + r * 520 + c * 8) = *(const bf16x8*)(J.w2 + r * 512 + c * 8);
+    *(bf16x8*)(w2l + r * 520 + c * 8) = *(const bf16x8*)(J.w2l + r * 512 + c * 8);
+  }
+  bf16x8 wfh[16], wfl[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const bf16* ph = conv3_wave ? J.w3 + l32 * 288 + s * 16 + half * 8 : J.w1 + l32 * 256 + s * 16 + half * 8;
+    const bf16* pl = conv3_wave ? J.w3l + l32 * 288 + s * 16 + half * 8 : J.w1l + l32 * 256 + s * 16 + half * 8;
+    wfh[s] = *(const bf16x8*)ph;
+    wfl[s] = *(const bf16x8*)pl;
+  }
+  if (tid < 96) lb[tid] = tid < 32 ? J.b2[tid] : tid < 64 ? J.b3[tid - 32] : J.b1[tid - 64];
+  if (tid < 256) {   // W3 K columns 256..287, hi then lo: [32 rows][32] bf16 each
+    const int pl = tid >> 7, r = (tid >> 2) & 31, c = tid & 3;
+    *(bf16x8*)(w3t + pl * 2048 + (r * 32 + c * 8) * 2) = *(const bf16x8*)((pl ? J.w3l : J.w3) + r * 288 + 256 + c * 8);
+  }
+  {
+    const size_t row = J.rows ? (size_t)J.rows[f] : (size_t)f;
+    const u32x4* src = (const u32x4*)(args.frames + row * IN_BYTES);
+    for (int c = tid; c < IN_CHUNKS2; c += NT) ((u32x4*)fr)[c] = src[c];
+  }
+  const int t1b = c_s2_begin[wave], t1n = c_s2_count[wave];
+  int row_nx = f + stride < n_frames ? (J.rows ? J.rows[f + stride] : f + stride) : 0;
+  __syncthreads();
+
+  int fprev = -1;
+  u32x4 pf[4];
+  int it_dbg = 0;
+  long long* tr = (args.trace && blockIdx.x == 0 && lane == 0) ? args.trace + wave * 16 * 5 : nullptr;
+#define TS2_STAMP(k) \
+  if (tr && it_dbg < 16) tr[it_dbg * 5 + (k)] = (long long)__builtin_readcyclecounter();
+  for (;;) {
+    TS2_STAMP(0);
+    const bool have = f < n_frames;
+    const int fn = f + stride;
+    const int fnn = fn + stride;
+    const int row_nn = fnn < n_frames ? (J.rows ? J.rows[fnn] : fnn) : 0;
+    // a per-iteration zero: keeps the lane-constant LDS offsets of the MFMA loops from being
+    // hoisted out of the frame loop (32+ VGPRs held across every phase otherwise)
+    int oz;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(oz));
+    // =================== phase A: conv1(f) || conv3(f-1) on wave 2; frame f+1 -> registers
+    // (nothing in phase A waits on vmcnt: conv1 / conv3 operands come from LDS / registers)
+    if (have && fn < n_frames && !(args.dbg & 16)) {
+      const u32x4* src = (const u32x4*)(args.frames + (size_t)row_nx * IN_BYTES);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = tid + NT * q;
+        if (c < IN_CHUNKS2) pf[q] = src[c];
+      }
+    }
+    if (have && !(args.dbg & 1)) {
+      for (int i = 0; i < t1n; ++i) {
+        const int p = (t1b + i) * 32 + l32;
+        const int pc = p < P1 ? p : P1 - 1;
+        const int oy = pc / 20, ox = pc % 20;
+        // K step s: s2d block (by, bx) = (s>>3, (s>>2)&1), channel ci = s&3, rows dy = 2h, 2h+1,
+        // columns 0..3: bytes frame[ci][4(oy+by) + dy][4(ox+bx) .. +3]
+        const uint8_t* fb = fr + (4 * oy + 2 * half) * 84 + 4 * ox + oz;
+        constexpr int D = 6;
+        uint32_t r0[D], r1[D];
+        auto ld = [&](int s, uint32_t& x0, uint32_t& x1) {
+          const int so = (s & 3) * 7056 + (s >> 3) * 336 + ((s >> 2) & 1) * 4;
+          x0 = *(const uint32_t*)(fb + so);
+          x1 = *(const uint32_t*)(fb + so + 84);
+        };
+#pragma unroll
+        for (int s = 0; s < D; ++s) ld(s, r0[s], r1[s]);
+        f32x16 acc = {};
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+          const uint32_t x0 = r0[s % D], x1 = r1[s % D];
+          if (s + D < 16) ld(s + D, r0[s % D], r1[s % D]);
+          __builtin_amdgcn_sched_barrier(0);
+          const bf16x8 x = u8x8_to_bf16(x0, x1);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wfl[s], x, acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wfh[s], x, acc, 0, 0, 0);
+        }
+        if (p < P1) {
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            bf16x4 vh, vl;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float v = fmaxf(acc[4 * g + e] * (1.f / 255.f) + lb[64 + 8 * g + 4 * half + e], 0.f);
+              vh[e] = (bf16)v;
+              vl[e] = sp_lo(v);
+            }
+            const int o = a1_off(p, g) + 8 * half;
+            *(bf16x4*)(a1h + o) = vh;
+            *(bf16x4*)(a1l + o) = vl;
+          }
+        }
+      }
+    }
+    if (fprev >= 0 && conv3_wave && !(args.dbg & 4)) {
+      // conv3(f-1), both pixel tiles one after the other; K = 288 = (kh 3, kw 3, ci 32); A = W3
+      // (registers; steps 16-17 from the LDS tail image); B = act2 hi / lo
+#pragma unroll 1
+      for (int t = 0; t < 2; ++t) {
+        const int p = t * 32 + l32, pc = p < P3 ? p : P3 - 1;
+        const int bo = ((pc / 7) * 9 + pc % 7) * 40 + half * 8 + oz;
+        f32x16 acc = {};
+        constexpr int D = 4;
+        bf16x8 rbh[D], rbl[D];
+        auto ldb = [&](int s, bf16x8& xh, bf16x8& xl) {
+          const int khkw = s >> 1, kh = khkw / 3, kw = khkw % 3;
+          const int o = bo + (kh * 9 + kw) * 40 + (s & 1) * 16;
+          xh = *(const bf16x8*)(a2h + o);
+          xl = *(const bf16x8*)(a2l + o);
+        };
+#pragma unroll
+        for (int s = 0; s < D; ++s) ldb(s, rbh[s], rbl[s]);
+#pragma unroll
+        for (int s = 0; s < 18; ++s) {
+          const bf16x8 xh = rbh[s % D], xl = rbl[s % D];
+          if (s + D < 18) ldb(s + D, rbh[s % D], rbl[s % D]);
+          bf16x8 ah, al;
+          if (s < 16) {
+            ah = wfh[s < 16 ? s : 0];
+            al = wfl[s < 16 ? s : 0];
+          } else {
+            const int o = (l32 * 32 + (s - 16) * 16 + half * 8) * 2;
+            ah = *(const bf16x8*)(w3t + o);
+            al = *(const bf16x8*)(w3t + 2048 + o);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          acc = mfma32_x3(ah, al, xh, xl, acc);
+        }
+        if (p < P3) {
+          // one base per plane (+oz: not hoisted), the channel offsets as store immediates
+          bf16* oh = J.out + (size_t)fprev * 1568 + p + 4 * half * 49 + oz;
+          bf16* ol = J.out_l + (size_t)fprev * 1568 + p + 4 * half * 49 + oz;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int c0 = (r & 3) + 8 * (r >> 2);
+            const float v = fmaxf(acc[r] + lb[32 + c0 + 4 * half], 0.f);
+            oh[c0 * 49] = (bf16)v;
+            ol[c0 * 49] = sp_lo(v);
+          }
+        }
+      }
+    }
+    TS2_STAMP(1);
+    lds_sync();
+    TS2_STAMP(2);
+    if (!have) break;
+
+    // =================== phase B: frame f+1 -> LDS (conv1(f) finished reading the image before the
+    // barrier above); conv2(f) on waves 0..2 || act1 save on waves 3..7
+    if (fn < n_frames && !(args.dbg & 16)) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = tid + NT * q;
+        if (c < IN_CHUNKS2) ((u32x4*)fr)[c] = pf[q];
+      }
+    }
+    if (conv2_wave) {
+      if (!(args.dbg & 2)) {
+        const int p = wave * 32 + l32;
+        const int pc = p < P2 ? p : P2 - 1;
+        const int oy = pc / 9, ox = pc % 9;
+        const bf16* ah = w2h + l32 * 520 + half * 8;
+        const bf16* al = w2l + l32 * 520 + half * 8;
+        const int P0 = (2 * oy) * 20 + 2 * ox + oz;
+        constexpr int D = 3;
+        bf16x8 rah[D], ral[D], rbh[D], rbl[D];
+        auto ld = [&](int s, bf16x8& xah, bf16x8& xal, bf16x8& xbh, bf16x8& xbl) {
+          const int khkw = s >> 1, kh = khkw >> 2, kw = khkw & 3;
+          int pp;   // computed at the step (not hoisted: 32 live offsets otherwise)
+          asm volatile("v_add_u32 %0, %1, %2" : "=v"(pp) : "v"(P0), "i"(kh * 20 + kw));
+          const int ob = a1_off(pp, (s & 1) * 2 + half);
+          xah = *(const bf16x8*)(ah + s * 16);
+          xal = *(const bf16x8*)(al + s * 16);
+          xbh = *(const bf16x8*)(a1h + ob);
+          xbl = *(const bf16x8*)(a1l + ob);
+        };
+#pragma unroll
+        for (int s = 0; s < D; ++s) ld(s, rah[s], ral[s], rbh[s], rbl[s]);
+        f32x16 acc = {};
+#pragma unroll
+        for (int s = 0; s < 32; ++s) {
+          const bf16x8 xah = rah[s % D], xal = ral[s % D], xbh = rbh[s % D], xbl = rbl[s % D];
+          if (s + D < 32) ld(s + D, rah[s % D], ral[s % D], rbh[s % D], rbl[s % D]);
+          __builtin_amdgcn_sched_barrier(0);
+          acc = mfma32_x3(xah, xal, xbh, xbl, acc);
+        }
+        if (p < P2) {
+          bf16* d2 = J.s2 ? J.s2 + ((size_t)f * P2 + p) * 32 : nullptr;
+          bf16* d2l = J.s2 ? J.s2l + ((size_t)f * P2 + p) * 32 : nullptr;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            bf16x4 vh, vl;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int co = 4 * half + 8 * g + e;
+              const float v = fmaxf(acc[4 * g + e] + lb[co], 0.f);
+              vh[e] = (bf16)v;
+              vl[e] = sp_lo(v);
+            }
+            *(bf16x4*)(a2h + p * 40 + 8 * g + 4 * half) = vh;
+            *(bf16x4*)(a2l + p * 40 + 8 * g + 4 * half) = vl;
+            if (d2) {
+              *(bf16x4*)(d2 + 8 * g + 4 * half) = vh;
+              *(bf16x4*)(d2l + 8 * g + 4 * half) = vl;
+            }
+          }
+        }
+      }
+    } else {
+      if (J.s1 != nullptr && !(args.dbg & 64)) {
+        // act1(f) -> channels-last (400, 32) hi / lo: linear LDS chunks, scattered 16-B stores
+        bf16* d1 = J.s1 + (size_t)f * P1 * 32;
+        bf16* d1l = J.s1l + (size_t)f * P1 * 32;
+        for (int i = tid - 192; i < P1 * 4; i += 320) {
+          const int row = i >> 4, pcv = (i & 15) ^ (row & 15);
+          const int P = row * 4 + (pcv >> 2), c = pcv & 3;
+          *(bf16x8*)(d1 + P * 32 + c * 8) = *(const bf16x8*)(a1h + i * 16);
+          *(bf16x8*)(d1l + P * 32 + c * 8) = *(const bf16x8*)(a1l + i * 16);
+        }
+      }
+    }
+    TS2_STAMP(3);
+    lds_sync();
+    TS2_STAMP(4);
+    ++it_dbg;
+    fprev = f;
+    f = fn;
+    row_nx = row_nn;
+  }
+}
+
+static int g_tsp_dbg = 0;
+static long long* g_tsp_trace = nullptr;
+// v2 phase clock stamps of workgroup 0: [wave][frame < 16][5] (loop top, phase A done, barrier,
+// phase B done, barrier), s_memrealtime-free cycle counter
+extern "C" int r2_torso_sp_trace(long long* p) { g_tsp_trace = p; return 0; }
+// timing probes only (tools/sp_micro.py): bit 0 skips conv1, bit 1 conv2, bit 2 conv3;
+// bit 3 runs the v1 kernel
+extern "C" int r2_torso_sp_debug(int bits) { g_tsp_dbg = bits; return 0; }
+
 extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs, int njobs,
                                      int grid, void* stream) {
   if (njobs < 1 || njobs > TS_MAX_JOBS) return -1;
@@ -295,6 +612,8 @@ extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs,
   }
   TSArgs a{};
   a.frames = frames;
+  a.dbg = g_tsp_dbg;
+  a.trace = g_tsp_trace;
   int64_t total = 0;
   for (int i = 0; i < njobs; ++i) total += jobs[TS_JOB_WORDS * i + 1] > 0 ? jobs[TS_JOB_WORDS * i + 1] : 0;
   if (total <= 0) return 0;
@@ -324,8 +643,19 @@ extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs,
   }
   if (wb > nw) return -3;
   if (grid > wb) grid = wb;
-  hipLaunchKernelGGL(torso_fwd_sp_kernel, dim3(grid), dim3(tsp::NT), tsp::LDS_BYTES,
-                     (hipStream_t)stream, a);
+  if (a.dbg & 8) {   // v1 (A/B timing)
+    hipLaunchKernelGGL(torso_fwd_sp_kernel, dim3(grid), dim3(tsp::NT), tsp::LDS_BYTES,
+                       (hipStream_t)stream, a);
+  } else {
+    static bool attr2 = false;
+    if (!attr2) {
+      hipFuncSetAttribute((const void*)torso_fwd_sp2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          tsp2::LDS_BYTES);
+      attr2 = true;
+    }
+    hipLaunchKernelGGL(torso_fwd_sp2_kernel, dim3(grid), dim3(tsp::NT), tsp2::LDS_BYTES,
+                       (hipStream_t)stream, a);
+  }
   R2_CHECK_LAUNCH();
   return 0;
 }

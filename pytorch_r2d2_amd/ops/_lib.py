@@ -57,6 +57,8 @@ _SIGS = {
     "r2_sample_batch": [P, P, P, I, I, U64, P, P, P, P, I, I, I, I, P, P, P, P, P],
     "r2_sample_batch_f32h": [P, P, P, I, I, U64, P, P, P, P, I, I, I, I, P, P, P, P, P],
     "r2_torso_fwd_sp_multi": [P, P, I, I, P],
+    "r2_torso_sp_debug": [I],
+    "r2_torso_sp_trace": [P],
     "r2_torso_bwd_sp": [P, P, I, P, P, P, P, P, P, P, P, P, P, P, P, I, P, P, P, P],
     "r2_torso_grad_reduce": [P, I, P, P, P, P],
     "r2_gather_state": [P, P, I, I, I, I, P, P, P, P],
@@ -100,6 +102,7 @@ _SIGS = {
     "r2_apply_pending": [P, P, I, P, P, P, I, I, F, P, P, P, I, P, P],
     "r2_gemm5": [P, P, I, I, P, I64, P, I, I, P],
     "r2_gemm5_ws_bytes": [P, P, I, I],
+    "r2_gemm5_set_mode": [I],
     "r2_ingest_record": [P, P],
     "r2_ingest_args_bytes": [],
     "r2_stream_create_cumask": [P, I, P],

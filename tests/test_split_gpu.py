@@ -222,3 +222,57 @@ def test_engine_fp32_graph_step_and_seaquest_actions():
     assert torch.equal(rp2.step, rp3.step)
     assert _rel(eng3.master, eng2.master) < 1e-6
     assert eng3.error_word() == 0
+
+
+def test_torso_fwd_sp_v2_bit_identical_to_v1():
+    """torso_fwd_sp2_kernel (frame in LDS, swizzled act1, conv3 on one wave) keeps v1's
+    accumulation order: every output and saved activation plane must match bit for bit, over 4
+    jobs with uneven frame counts (partial last rounds) and activation saves."""
+    import numpy as np
+    from pytorch_r2d2_amd.ops._lib import kernels, ptr, stream_handle
+    k = kernels()
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(7)
+    cap = 3000
+    frames = torch.randint(0, 256, (cap, 4 * 84 * 84), dtype=torch.uint8, device=dev, generator=g)
+    counts = [301, 517, 45, 260]
+    rows = [torch.randint(0, cap, (n,), dtype=torch.int32, device=dev, generator=g) for n in counts]
+
+    def net():
+        w = [_split(torch.randn(32, kk, device=dev, generator=g) * 0.05) for kk in (256, 512, 288)]
+        b = [torch.randn(32, device=dev, generator=g) * 0.1 for _ in range(3)]
+        return w, b
+
+    nets = [net(), net()]
+
+    def run(dbg):
+        outs = []
+        jobs = []
+        for j, n in enumerate(counts):
+            (w, b) = nets[j == 3]
+            X = torch.full((2, n, 1568), 7.0, dtype=torch.bfloat16, device=dev)
+            save = j == 1
+            s1 = torch.zeros(2, n, 400, 32, dtype=torch.bfloat16, device=dev) if save else None
+            s2 = torch.zeros(2, n, 81, 32, dtype=torch.bfloat16, device=dev) if save else None
+            outs.append((X, s1, s2))
+            jobs.append([ptr(rows[j]), n, ptr(w[0][0]), ptr(w[0][1]), ptr(b[0]), ptr(w[1][0]),
+                         ptr(w[1][1]), ptr(b[1]), ptr(w[2][0]), ptr(w[2][1]), ptr(b[2]), ptr(X[0]),
+                         ptr(X[1]), ptr(s1[0]) if save else 0, ptr(s1[1]) if save else 0,
+                         ptr(s2[0]) if save else 0, ptr(s2[1]) if save else 0, 0, 0, 0])
+        arr = np.asarray(jobs, dtype=np.int64)
+        k.r2_torso_sp_debug(dbg)
+        try:
+            n_cus = torch.cuda.get_device_properties(0).multi_processor_count
+            assert k.r2_torso_fwd_sp_multi(ptr(frames), arr.ctypes.data, len(jobs), n_cus,
+                                           stream_handle()) == 0
+            torch.cuda.synchronize()
+        finally:
+            k.r2_torso_sp_debug(0)
+        return outs
+
+    v1, v2 = run(8), run(0)
+    for (a, sa1, sa2), (b, sb1, sb2) in zip(v1, v2):
+        assert torch.equal(a, b)
+        assert not (a == 7.0).any()
+        if sa1 is not None:
+            assert torch.equal(sa1, sb1) and torch.equal(sa2, sb2)
