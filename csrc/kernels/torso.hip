@@ -161,7 +161,7 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(const TFArgs args) {
   if (f >= n_frames) return;
   // ---- prologue: first frame -> LDS (bf16)
   {
-    const size_t row = rows ? (size_t)rows[f] : (size_t)f;
+    const size_t row = rows ? (size_t)ld_uniform_i32(rows, f) : (size_t)f;
     const u32x4* src = (const u32x4*)(frames + row * IN_BYTES);
     for (int c = tid; c < IN_CHUNKS; c += NT) torso_store_chunk(in_bf, c, src[c]);
   }
@@ -171,12 +171,12 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(const TFArgs args) {
 #define TF_TRACE(k) \
   if (dbg && wk == 0 && tid == 0 && it_dbg < 16) dbg[it_dbg * 8 + (k)] = clock64();
   // replay row of the next frame, read one frame ahead so the prefetch never waits on its address
-  int row_nx = f + stride < n_frames ? (rows ? rows[f + stride] : f + stride) : 0;
+  int row_nx = f + stride < n_frames ? (rows ? ld_uniform_i32(rows, f + stride) : f + stride) : 0;
   for (;;) {
     const bool have = f < n_frames;
     const int fn = f + stride;
     const int fnn = fn + stride;
-    const int row_nn = fnn < n_frames ? (rows ? rows[fnn] : fnn) : 0;
+    const int row_nn = fnn < n_frames ? (rows ? ld_uniform_i32(rows, fnn) : fnn) : 0;
     u32x4 pf[PF];
     TF_TRACE(0);
     // =================== phase A: conv1(f) || conv3(f-1)
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(const TFArgs args) {
 __global__ void frames_to_bf16_kernel(const uint8_t* __restrict__ frames, const int* __restrict__ rows,
                                       int n_frames, bf16* __restrict__ out) {
   const int f = blockIdx.y;
-  const size_t row = rows ? (size_t)rows[f] : (size_t)f;
+  const size_t row = rows ? (size_t)ld_uniform_i32(rows, f) : (size_t)f;
   const uint8_t* src = frames + row * torso::IN_BYTES;
   bf16* dst = out + (size_t)f * torso::IN_BYTES;
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < torso::IN_BYTES / 8;
@@ -320,7 +320,7 @@ __global__ void frames_to_bf16_nhwc_kernel(const uint8_t* __restrict__ frames,
                                            const int* __restrict__ rows, int n_frames,
                                            bf16* __restrict__ out) {
   const int f = blockIdx.y;
-  const size_t row = rows ? (size_t)rows[f] : (size_t)f;
+  const size_t row = rows ? (size_t)ld_uniform_i32(rows, f) : (size_t)f;
   const uint8_t* src = frames + row * torso::IN_BYTES;
   bf16x4* dst = (bf16x4*)(out + (size_t)f * torso::IN_BYTES);
   constexpr int PIX = 84 * 84;
@@ -339,7 +339,7 @@ __global__ void frames_gather_nhwc_kernel(const uint8_t* __restrict__ frames, in
                                           const int* __restrict__ rows, int C, int HW, float scale,
                                           bf16* __restrict__ out) {
   const int f = blockIdx.y;
-  const size_t row = rows ? (size_t)rows[f] : (size_t)f;
+  const size_t row = rows ? (size_t)ld_uniform_i32(rows, f) : (size_t)f;
   const uint8_t* src = frames + row * row_bytes;
   bf16* dst = out + (size_t)f * HW * C;
   for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += gridDim.x * blockDim.x)
@@ -354,7 +354,7 @@ __global__ void frames_gather_nhwc4_kernel(const uint8_t* __restrict__ frames, i
                                            const int* __restrict__ rows, int HW, float scale,
                                            bf16* __restrict__ out) {
   const int f = blockIdx.y;
-  const size_t row = rows ? (size_t)rows[f] : (size_t)f;
+  const size_t row = rows ? (size_t)ld_uniform_i32(rows, f) : (size_t)f;
   const uint8_t* src = frames + row * row_bytes;
   bf16* dst = out + (size_t)f * HW * C;
   for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < HW / 4; q += gridDim.x * blockDim.x) {

@@ -161,12 +161,12 @@ __global__ __launch_bounds__(512) void torso_bwd_kernel(const TBArgs a) {
     }
   };
   if (blockIdx.x < a.n) {
-    prefetch_frame(a.rows[blockIdx.x]);
+    prefetch_frame(ld_uniform_i32(a.rows, blockIdx.x));
     prefetch_acts(blockIdx.x);
   }
   // replay row of the frame after next is read one frame ahead, so issuing a prefetch never
   // waits a memory round trip for its own address
-  int row_nx = blockIdx.x + gridDim.x < a.n ? a.rows[blockIdx.x + gridDim.x] : 0;
+  int row_nx = blockIdx.x + gridDim.x < a.n ? ld_uniform_i32(a.rows, blockIdx.x + gridDim.x) : 0;
   __syncthreads();
 
   int it_dbg = 0;
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(512) void torso_bwd_kernel(const TBArgs a) {
     const bf16* fb1 = fb0 + 4 * 84;
 
     // ======== S0: prefetched inputs -> LDS
-    const int row_nn = f + 2 * (int)gridDim.x < a.n ? a.rows[f + 2 * gridDim.x] : 0;
+    const int row_nn = f + 2 * (int)gridDim.x < a.n ? ld_uniform_i32(a.rows, f + 2 * gridDim.x) : 0;
 #pragma unroll
     for (int k = 0; k < PFF; ++k) {
       const int c = tid + k * NT;

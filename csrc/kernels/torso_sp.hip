@@ -120,7 +120,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp_kernel(const TSArgs args) {
     const int fn = f + stride;
     // =================== phase A: conv1(f) || conv3(f-1)
     if (have && !(args.dbg & 1)) {
-      const size_t row = J.rows ? (size_t)J.rows[f] : (size_t)f;
+      const size_t row = J.rows ? (size_t)ld_uniform_i32(J.rows, f) : (size_t)f;
       const __amdgpu_buffer_rsrc_t frs = ts_rsrc(args.frames + row * IN_BYTES, IN_BYTES);
       for (int i = 0; i < t1n; ++i) {
         const int p = (t1b + i) * 32 + l32;
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp_kernel(const TSArgs args) {
       // warm the next frame's lines into L2 / L1 (consumed below, after the act1 copy-out)
       uint32_t wv[2] = {0, 0};
       if (fn < n_frames) {
-        const size_t rn = J.rows ? (size_t)J.rows[fn] : (size_t)fn;
+        const size_t rn = J.rows ? (size_t)ld_uniform_i32(J.rows, fn) : (size_t)fn;
         const uint8_t* fr = args.frames + rn * IN_BYTES;
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -377,12 +377,12 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
     *(bf16x8*)(w3t + pl * 2048 + (r * 32 + c * 8) * 2) = *(const bf16x8*)((pl ? J.w3l : J.w3) + r * 288 + 256 + c * 8);
   }
   {
-    const size_t row = J.rows ? (size_t)J.rows[f] : (size_t)f;
+    const size_t row = J.rows ? (size_t)ld_uniform_i32(J.rows, f) : (size_t)f;
     const u32x4* src = (const u32x4*)(args.frames + row * IN_BYTES);
     for (int c = tid; c < IN_CHUNKS2; c += NT) ((u32x4*)fr)[c] = src[c];
   }
   const int t1b = c_s2_begin[wave], t1n = c_s2_count[wave];
-  int row_nx = f + stride < n_frames ? (J.rows ? J.rows[f + stride] : f + stride) : 0;
+  int row_nx = f + stride < n_frames ? (J.rows ? ld_uniform_i32(J.rows, f + stride) : f + stride) : 0;
   __syncthreads();
 
   int fprev = -1;
@@ -396,7 +396,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
     const bool have = f < n_frames;
     const int fn = f + stride;
     const int fnn = fn + stride;
-    const int row_nn = fnn < n_frames ? (J.rows ? J.rows[fnn] : fnn) : 0;
+    const int row_nn = fnn < n_frames ? (J.rows ? ld_uniform_i32(J.rows, fnn) : fnn) : 0;
     // a per-iteration zero: keeps the lane-constant LDS offsets of the MFMA loops from being
     // hoisted out of the frame loop (32+ VGPRs held across every phase otherwise)
     int oz;
@@ -525,7 +525,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
         const bf16* ah = w2h + l32 * 520 + half * 8;
         const bf16* al = w2l + l32 * 520 + half * 8;
         const int P0 = (2 * oy) * 20 + 2 * ox + oz;
-        constexpr int D = 3;
+        constexpr int D = 2;
         bf16x8 rah[D], ral[D], rbh[D], rbl[D];
         auto ld = [&](int s, bf16x8& xah, bf16x8& xal, bf16x8& xbh, bf16x8& xbl) {
           const int khkw = s >> 1, kh = khkw >> 2, kw = khkw & 3;
@@ -761,22 +761,45 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
   float db1p = 0.f, db2p = 0.f;
 
   u32x4 pfr[PFF], pa1[PF1], pa1l[PF1], pa2, pdx, pdxl, po3;
+  // buffer loads off kernel-argument bases (SGPR descriptors, 32-bit lane offsets): 64-bit VGPR
+  // addresses of these streams were spilled and their reloads waited (vmcnt(0)) on the whole
+  // next-frame prefetch
+  const uint32_t na = (uint32_t)a.n;
+  const __amdgpu_buffer_rsrc_t r_a1 = ts_rsrc(a.act1, na * P1 * 64), r_a1l = ts_rsrc(a.act1l, na * P1 * 64);
+  const __amdgpu_buffer_rsrc_t r_a2 = ts_rsrc(a.act2, na * P2 * 64);
+  const __amdgpu_buffer_rsrc_t r_dx = ts_rsrc(a.dx3, na * 3136), r_dxl = ts_rsrc(a.dx3l, na * 3136);
+  const __amdgpu_buffer_rsrc_t r_o3 = ts_rsrc(a.out3, na * 3136);
   auto prefetch_acts = [&](int f) {
-    const u32x4* s1 = (const u32x4*)(a.act1 + (size_t)f * P1 * 32);
-    const u32x4* s1l = (const u32x4*)(a.act1l + (size_t)f * P1 * 32);
+    const uint32_t o1 = (uint32_t)f * (P1 * 64), o2 = (uint32_t)f * (P2 * 64), o3 = (uint32_t)f * 3136;
 #pragma unroll
     for (int k = 0; k < PF1; ++k) {
       const int c = tid + k * NT;
-      if (c < P1 * 4) { pa1[k] = s1[c]; pa1l[k] = s1l[c]; }
+      if (c < P1 * 4) {
+        pa1[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r_a1, c * 16, o1, 0));
+        pa1l[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r_a1l, c * 16, o1, 0));
+      }
     }
-    if (tid < P2 * 4) pa2 = ((const u32x4*)(a.act2 + (size_t)f * P2 * 32))[tid];
+    if (tid < P2 * 4) pa2 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r_a2, tid * 16, o2, 0));
     if (tid < 196) {
-      pdx = ((const u32x4*)(a.dx3 + (size_t)f * 1568))[tid];
-      pdxl = ((const u32x4*)(a.dx3l + (size_t)f * 1568))[tid];
-      po3 = ((const u32x4*)(a.out3 + (size_t)f * 1568))[tid];
+      pdx = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r_dx, tid * 16, o3, 0));
+      pdxl = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r_dxl, tid * 16, o3, 0));
+      po3 = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r_o3, tid * 16, o3, 0));
     }
   };
-  if (blockIdx.x < a.n) prefetch_acts(blockIdx.x);
+  // frame bytes of frame f: loaded one stage ahead (S3 of the previous frame) so the W3 / W2
+  // operand waits of S1 / S2 (in-order vmcnt) never wait on the frame's HBM fetch
+  auto load_frame = [&](int f) {
+    const __amdgpu_buffer_rsrc_t r_fr = ts_rsrc(a.frames + (size_t)ld_uniform_i32(a.rows, f) * IN_BYTES, IN_BYTES);
+#pragma unroll
+    for (int k = 0; k < PFF; ++k) {
+      const int c = tid + k * NT;
+      if (c < IN_CHUNKS) pfr[k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r_fr, c * 16, 0, 0));
+    }
+  };
+  if (blockIdx.x < a.n) {
+    load_frame(blockIdx.x);
+    prefetch_acts(blockIdx.x);
+  }
   __syncthreads();
 
   for (int f = blockIdx.x; f < a.n; f += gridDim.x) {
@@ -818,14 +841,6 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
         const int o = ((p / 7 + 2) * 11 + p % 7 + 2) * 32 + co;
         g3p[o] = on ? dx[e] : (bf16)0.f;
         g3pl[o] = on ? dxl[e] : (bf16)0.f;
-      }
-    }
-    {
-      const u32x4* src = (const u32x4*)(a.frames + (size_t)a.rows[f] * IN_BYTES);
-#pragma unroll
-      for (int k = 0; k < PFF; ++k) {
-        const int c = tid + k * NT;
-        if (c < IN_CHUNKS) pfr[k] = src[c];
       }
     }
     lds_sync();
@@ -945,6 +960,7 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
     lds_sync();
 
     // ======== S3: dW1 += g1 . im2col(frame), 25 K steps of one 4x4 pixel block each (2 passes)
+    if (f + (int)gridDim.x < a.n) load_frame(f + gridDim.x);
     {
       constexpr int D = 2;
       bf16x8 rah[D], ral[D], rb[D];

@@ -5,3 +5,5 @@ tail -3 gpurun_out/split_tests.txt
 timeout -k 10 200 python bench.py --steps 100 --warmup 10 > gpurun_out/bench_fp32.log 2>&1 || exit 1
 grep metric gpurun_out/bench_fp32.log | cut -c1-300
 bash tools/prof_bench.sh fp32_v2
+timeout -k 10 200 python bench.py --steps 100 --warmup 10 --dtype bf16 > gpurun_out/bench_bf16.log 2>&1 || exit 1
+grep metric gpurun_out/bench_bf16.log | cut -c1-200
