@@ -29,32 +29,53 @@
 // One 512-thread workgroup per CU (151 KB LDS), grid-stride over frames.
 #include "../common.h"
 
-namespace torso {
-constexpr int IN_BYTES = 4 * 84 * 84;   // 28224
-constexpr int IN_CHUNKS = IN_BYTES / 16; // 1764
-constexpr int NT = 512;                  // threads
-constexpr int PF = (IN_CHUNKS + 319) / 320;   // 6 prefetch chunks per thread of waves 3..7
-constexpr int P1 = 400, P2 = 81, P3 = 49;
-constexpr int ACTS = 40;                 // bf16 per pixel row in LDS (32 + 8 pad) = 80 B
-constexpr int W2S = 512 + 8;             // bf16 per conv2 weight row (1040 B)
-constexpr int W3S = 288 + 8;             // bf16 per conv3 weight row (592 B)
-constexpr int S2DS = 72;                 // bf16 per space-to-depth pixel (64 + 8 pad) = 144 B
-constexpr int OFF_IN = 0;                            // frame, bf16 space-to-depth [441][72]
-constexpr int OFF_A1 = OFF_IN + 441 * S2DS * 2;      // 63504
-constexpr int OFF_A2 = OFF_A1 + P1 * ACTS * 2;       // 88448
-constexpr int OFF_W2 = OFF_A2 + P2 * ACTS * 2;       // 94928
-constexpr int OFF_W3 = OFF_W2 + 32 * W2S * 2;        // 128208
-constexpr int OFF_B23 = OFF_W3 + 32 * W3S * 2;      // conv2 / conv3 biases, fp32 [2][32]
-constexpr int LDS_BYTES = OFF_B23 + 64 * 4;          // 154464
-}  // namespace torso
+// Frame geometry of the fused forward (template parameter): CIN uint8 planes of H x W (H, W
+// multiples of 4), Conv(CIN,32,8,s4) -> Conv(32,32,4,s2) -> Conv(32,32,3,s1).  Instantiated for
+// the Atari stack (4x84x84: 20x20 -> 9x9 -> 7x7) and DMLab-30 RGB (3x72x96: 17x23 -> 7x10 -> 5x8).
+template <int CIN_, int H_, int W_>
+struct TGeo {
+  static constexpr int CIN = CIN_, H = H_, W = W_;
+  static constexpr int IN_BYTES = CIN * H * W;
+  static constexpr int IN_CHUNKS = IN_BYTES / 16;
+  static constexpr int NT = 512;                      // threads
+  static constexpr int PF = (IN_CHUNKS + 319) / 320;  // prefetch chunks per thread of waves 3..7
+  static constexpr int H1 = (H - 8) / 4 + 1, W1 = (W - 8) / 4 + 1;
+  static constexpr int H2 = (H1 - 4) / 2 + 1, W2 = (W1 - 4) / 2 + 1;
+  static constexpr int H3 = H2 - 2, W3 = W2 - 2;
+  static constexpr int P1 = H1 * W1, P2 = H2 * W2, P3 = H3 * W3;
+  static constexpr int OUT = 32 * P3;                 // torso features per frame
+  static constexpr int H4 = H / 4, W4 = W / 4;        // space-to-depth image
+  static constexpr int K1S = 4 * CIN;                 // conv1 K steps of 16
+  static constexpr int ACTS = 40;                     // bf16 per pixel row in LDS (32 + 8 pad) = 80 B
+  static constexpr int W2S = 512 + 8;                 // bf16 per conv2 weight row (1040 B)
+  static constexpr int W3S = 288 + 8;                 // bf16 per conv3 weight row (592 B)
+  static constexpr int S2DS = 16 * CIN + 8;           // bf16 per space-to-depth pixel (+8 pad)
+  static constexpr int OFF_IN = 0;                    // frame, bf16 space-to-depth [H4*W4][S2DS]
+  static constexpr int OFF_A1 = OFF_IN + H4 * W4 * S2DS * 2;
+  static constexpr int OFF_A2 = OFF_A1 + P1 * ACTS * 2;
+  static constexpr int OFF_W2 = OFF_A2 + P2 * ACTS * 2;
+  static constexpr int OFF_W3 = OFF_W2 + 32 * W2S * 2;
+  static constexpr int OFF_B23 = OFF_W3 + 32 * W3S * 2;   // conv2 / conv3 biases, fp32 [2][32]
+  static constexpr int LDS_BYTES = OFF_B23 + 64 * 4;
+  static_assert(H % 4 == 0 && W % 4 == 0 && IN_BYTES % 16 == 0, "geometry");
+  static_assert((P1 + 31) / 32 == 13 && (P2 + 31) / 32 == 3 && (P3 + 31) / 32 == 2, "tile deal");
+  static_assert(OFF_A1 % 16 == 0 && LDS_BYTES <= 160 * 1024, "LDS");
+};
+using GeoAtari = TGeo<4, 84, 84>;    // 154464 B LDS
+using GeoDmlab = TGeo<3, 72, 96>;
+namespace torso {   // Atari constants used by the helper kernels below
+constexpr int IN_BYTES = GeoAtari::IN_BYTES;
+}
 
 // 16 uint8 of the CHW frame (chunk c) -> bf16 space-to-depth image (the only u8->bf16
-// conversion of a frame).  Rows are 84 B = 21 dwords, so every dword is 4 consecutive x of one
-// row: (ci, y, X) -> s2d pixel (y/4, X), channels ci*16 + (y%4)*4 + 0..3, one 8-byte store.
+// conversion of a frame).  Every dword is 4 consecutive x of one row: (ci, y, X) -> s2d pixel
+// (y/4, X), channels ci*16 + (y%4)*4 + 0..3, one 8-byte store.
+template <class Gm>
 __device__ __forceinline__ void torso_store_chunk(bf16* s2d, int c, const u32x4& v) {
+  constexpr int RD = Gm::W / 4, PD = Gm::H * RD;   // dwords per row / per plane
   int d = 4 * c;                 // first dword of the chunk
-  int ci = d / 1764, r = d - ci * 1764;
-  int y = r / 21, X = r - y * 21;
+  int ci = d / PD, r = d - ci * PD;
+  int y = r / RD, X = r - y * RD;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const uint32_t w = v[e];
@@ -63,10 +84,10 @@ __device__ __forceinline__ void torso_store_chunk(bf16* s2d, int c, const u32x4&
     o[1] = (bf16)(float)((w >> 8) & 0xff);
     o[2] = (bf16)(float)((w >> 16) & 0xff);
     o[3] = (bf16)(float)(w >> 24);
-    *(bf16x4*)(s2d + ((y >> 2) * 21 + X) * torso::S2DS + ci * 16 + (y & 3) * 4) = o;
-    if (++X == 21) {
+    *(bf16x4*)(s2d + ((y >> 2) * Gm::W4 + X) * Gm::S2DS + ci * 16 + (y & 3) * 4) = o;
+    if (++X == RD) {
       X = 0;
-      if (++y == 84) { y = 0; ++ci; }
+      if (++y == Gm::H) { y = 0; ++ci; }
     }
   }
 }
@@ -96,6 +117,7 @@ struct TFArgs {
   TFJob job[TF_MAX_JOBS];
   int njobs, reserve_xcds, reserve_slots, pad_;
   long long* dbg;
+  long long row_bytes;   // replay row stride (>= the frame's CIN*H*W bytes)
 };
 
 __device__ __forceinline__ int tf_worker(int reserve_xcds, int reserve_slots) {
@@ -107,14 +129,17 @@ __device__ __forceinline__ int tf_worker(int reserve_xcds, int reserve_slots) {
   return keep * 8 + (s - keep) * (8 - reserve_xcds) + (x - reserve_xcds);
 }
 
+template <class Gm>
 __global__ __launch_bounds__(512) void torso_fwd_kernel(const TFArgs args) {
-  using namespace torso;
+  constexpr int NT = Gm::NT, PF = Gm::PF, IN_CHUNKS = Gm::IN_CHUNKS;
+  constexpr int P1 = Gm::P1, P2 = Gm::P2, P3 = Gm::P3, ACTS = Gm::ACTS;
+  constexpr int W2S = Gm::W2S, W3S = Gm::W3S, S2DS = Gm::S2DS, K1S = Gm::K1S;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  bf16* in_bf = (bf16*)(lds + OFF_IN);
-  bf16* act1 = (bf16*)(lds + OFF_A1);
-  bf16* act2 = (bf16*)(lds + OFF_A2);
-  bf16* lw2 = (bf16*)(lds + OFF_W2);
-  bf16* lw3 = (bf16*)(lds + OFF_W3);
+  bf16* in_bf = (bf16*)(lds + Gm::OFF_IN);
+  bf16* act1 = (bf16*)(lds + Gm::OFF_A1);
+  bf16* act2 = (bf16*)(lds + Gm::OFF_A2);
+  bf16* lw2 = (bf16*)(lds + Gm::OFF_W2);
+  bf16* lw3 = (bf16*)(lds + Gm::OFF_W3);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int half = lane >> 5, l32 = lane & 31;
   const int wk = tf_worker(args.reserve_xcds, args.reserve_slots);
@@ -127,6 +152,7 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(const TFArgs args) {
   const int stride = J.wcount;
   if (wk - J.wbegin >= stride) return;
   const uint8_t* __restrict__ frames = args.frames;
+  const long long rb = args.row_bytes;
   const int* __restrict__ rows = J.rows;
   const int n_frames = J.n;
   const bf16* __restrict__ w1 = J.w1; const float* __restrict__ b1 = J.b1;
@@ -146,14 +172,14 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(const TFArgs args) {
     const int r = i / 36, c = i % 36;
     *(bf16x8*)(lw3 + r * W3S + c * 8) = *(const bf16x8*)(w3 + r * 288 + c * 8);
   }
-  bf16x8 wf1[16];
+  bf16x8 wf1[K1S];
 #pragma unroll
-  for (int s = 0; s < 16; ++s) wf1[s] = *(const bf16x8*)(w1 + l32 * 256 + s * 16 + half * 8);
+  for (int s = 0; s < K1S; ++s) wf1[s] = *(const bf16x8*)(w1 + l32 * (16 * K1S) + s * 16 + half * 8);
   float bias1[16];
   const bool conv3_wave = (wave == 2 || wave == 3), conv2_wave = wave < 3;
 #pragma unroll
   for (int r = 0; r < 16; ++r) bias1[r] = b1[(r & 3) + 8 * (r >> 2) + 4 * half];
-  float* lb23 = (float*)(lds + OFF_B23);   // epilogue biases of conv2 / conv3 (LDS broadcast)
+  float* lb23 = (float*)(lds + Gm::OFF_B23);   // epilogue biases of conv2 / conv3 (LDS broadcast)
   if (tid < 64) lb23[tid] = tid < 32 ? b2[tid] : b3[tid - 32];
   const int t1b = c_t1_begin[wave], t1n = c_t1_count[wave];
 
@@ -162,8 +188,8 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(const TFArgs args) {
   // ---- prologue: first frame -> LDS (bf16)
   {
     const size_t row = rows ? (size_t)ld_uniform_i32(rows, f) : (size_t)f;
-    const u32x4* src = (const u32x4*)(frames + row * IN_BYTES);
-    for (int c = tid; c < IN_CHUNKS; c += NT) torso_store_chunk(in_bf, c, src[c]);
+    const u32x4* src = (const u32x4*)(frames + row * rb);
+    for (int c = tid; c < IN_CHUNKS; c += NT) torso_store_chunk<Gm>(in_bf, c, src[c]);
   }
   __syncthreads();
 
@@ -184,7 +210,7 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(const TFArgs args) {
       // waves 3..7 prefetch frame f+stride into registers (lands while the convolutions run);
       // they convert it into LDS during phase B while waves 0..2 run conv2
       if (fn < n_frames && wave >= 3) {
-        const u32x4* src = (const u32x4*)(frames + (size_t)row_nx * IN_BYTES);
+        const u32x4* src = (const u32x4*)(frames + (size_t)row_nx * rb);
 #pragma unroll
         for (int q = 0; q < PF; ++q) {
           const int c = tid - 192 + q * 320;
@@ -195,13 +221,13 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(const TFArgs args) {
         const int pt = t1b + i;
         const int p = pt * 32 + l32;
         const int pc = p < P1 ? p : P1 - 1;
-        const int oy = pc / 20, ox = pc % 20;
-        // K step s: s2d block (by, bx) = (s>>3, (s>>2)&1), channels (s&3)*16 + 8*half .. +8
-        const bf16* base = in_bf + (oy * 21 + ox) * S2DS + half * 8;
+        const int oy = pc / Gm::W1, ox = pc % Gm::W1;
+        // K step s: s2d block (by, bx) = (s / 2CIN, (s / CIN) & 1), channels ci*16 + 8*half .. +8
+        const bf16* base = in_bf + (oy * Gm::W4 + ox) * S2DS + half * 8;
         f32x16 acc = {};
-        mfma_pipe<16, 4>(acc, [&](int s) { return wf1[s]; }, [&](int s) {
-          const int by = s >> 3, bx = (s >> 2) & 1;
-          return *(const bf16x8*)(base + (by * 21 + bx) * S2DS + (s & 3) * 16);
+        mfma_pipe<K1S, 4>(acc, [&](int s) { return wf1[s]; }, [&](int s) {
+          const int by = s / (2 * Gm::CIN), bx = (s / Gm::CIN) & 1, ci = s % Gm::CIN;
+          return *(const bf16x8*)(base + (by * Gm::W4 + bx) * S2DS + ci * 16);
         });
         if (p < P1) {
 #pragma unroll
@@ -218,23 +244,23 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(const TFArgs args) {
       }
     }
     if (fprev >= 0 && conv3_wave) {
-      // conv3(f-1): 2 pixel tiles (49 px), K = 288 = (kh 3, kw 3, ci 32)
+      // conv3(f-1): 2 pixel tiles, K = 288 = (kh 3, kw 3, ci 32)
       const int p = (wave - 2) * 32 + l32;
       const int pc = p < P3 ? p : P3 - 1;
-      const int oy = pc / 7, ox = pc % 7;
+      const int oy = pc / Gm::W3, ox = pc % Gm::W3;
       const bf16* abase = lw3 + l32 * W3S + half * 8;
-      const bf16* bbase = act2 + (oy * 9 + ox) * ACTS + half * 8;
+      const bf16* bbase = act2 + (oy * Gm::W2 + ox) * ACTS + half * 8;
       f32x16 acc = {};
       mfma_pipe<18, 3>(acc, [&](int s) { return *(const bf16x8*)(abase + s * 16); }, [&](int s) {
         const int khkw = s >> 1, kh = khkw / 3, kw = khkw % 3;
-        return *(const bf16x8*)(bbase + (kh * 9 + kw) * ACTS + (s & 1) * 16);
+        return *(const bf16x8*)(bbase + (kh * Gm::W2 + kw) * ACTS + (s & 1) * 16);
       });
       if (p < P3) {
-        bf16* o = out + (size_t)fprev * 1568 + p;
+        bf16* o = out + (size_t)fprev * Gm::OUT + p;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int co = (r & 3) + 8 * (r >> 2) + 4 * half;
-          o[co * 49] = (bf16)fmaxf(acc[r] + lb23[32 + co], 0.f);
+          o[co * P3] = (bf16)fmaxf(acc[r] + lb23[32 + co], 0.f);
         }
       }
     }
@@ -247,13 +273,13 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(const TFArgs args) {
     if (conv2_wave) {
       const int p = wave * 32 + l32;
       const int pc = p < P2 ? p : P2 - 1;
-      const int oy = pc / 9, ox = pc % 9;
+      const int oy = pc / Gm::W2, ox = pc % Gm::W2;
       const bf16* abase = lw2 + l32 * W2S + half * 8;
-      const bf16* bbase = act1 + ((2 * oy) * 20 + 2 * ox) * ACTS + half * 8;
+      const bf16* bbase = act1 + ((2 * oy) * Gm::W1 + 2 * ox) * ACTS + half * 8;
       f32x16 acc = {};
       mfma_pipe<32, 3>(acc, [&](int s) { return *(const bf16x8*)(abase + s * 16); }, [&](int s) {
         const int khkw = s >> 1, kh = khkw >> 2, kw = khkw & 3;
-        return *(const bf16x8*)(bbase + (kh * 20 + kw) * ACTS + (s & 1) * 16);
+        return *(const bf16x8*)(bbase + (kh * Gm::W1 + kw) * ACTS + (s & 1) * 16);
       });
       TF_TRACE(4);
       if (p < P2) {
@@ -285,7 +311,7 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(const TFArgs args) {
 #pragma unroll
       for (int q = 0; q < PF; ++q) {
         const int c = tid - 192 + q * 320;
-        if (c < IN_CHUNKS) torso_store_chunk(in_bf, c, pf[q]);
+        if (c < IN_CHUNKS) torso_store_chunk<Gm>(in_bf, c, pf[q]);
       }
     }
     TF_TRACE(6);
@@ -457,24 +483,39 @@ extern "C" int r2_relu_mask_bf16(const bf16* g, const bf16* act, bf16* out, int6
   return 0;
 }
 
+
 static long long* g_tf_dbg = nullptr;
 extern "C" int r2_torso_fwd_set_debug(long long* p) { g_tf_dbg = p; return 0; }
+
+template <class Gm>
+static void tf_launch(const TFArgs& a, int grid, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute((const void*)torso_fwd_kernel<Gm>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        Gm::LDS_BYTES);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(torso_fwd_kernel<Gm>, dim3(grid), dim3(Gm::NT), Gm::LDS_BYTES, s, a);
+}
 
 // jobs: njobs x 12 int64 {rows, n, w1, b1, w2, b2, w3, b3, out, save1, save2, 0}.
 // grid 0 = one block per CU (256); reserve_slots > 0 (grid must then be 256) keeps the last
 // reserve_slots dispatch slots of XCDs 0..reserve_xcds-1 free (see tf_worker).
-extern "C" int r2_torso_fwd_multi(const uint8_t* frames, const int64_t* jobs, int njobs,
-                                  int grid, int reserve_xcds, int reserve_slots, void* stream) {
+// geom: (cin, h, w) of the frame = 4x84x84 (Atari) or 3x72x96 (DMLab-30); row_bytes: the replay
+// row stride (0 = the frame's bytes).
+extern "C" int r2_torso_fwd_geom(const uint8_t* frames, long long row_bytes, const int64_t* jobs,
+                                 int njobs, int grid, int reserve_xcds, int reserve_slots, int cin,
+                                 int h, int w, void* stream) {
   if (njobs < 1 || njobs > TF_MAX_JOBS) return -1;
   if (reserve_slots < 0 || reserve_slots >= 32 || reserve_xcds < 0 || reserve_xcds > 8) return -2;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute((const void*)torso_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        torso::LDS_BYTES);
-    attr_set = true;
-  }
+  const bool atari = cin == 4 && h == 84 && w == 84, dm = cin == 3 && h == 72 && w == 96;
+  if (!atari && !dm) return -6;
+  const long long fb = (long long)cin * h * w;
+  if (row_bytes <= 0) row_bytes = fb;
+  if (row_bytes < fb || row_bytes % 16) return -7;
   TFArgs a{};
   a.frames = frames;
+  a.row_bytes = row_bytes;
   a.njobs = 0;
   a.reserve_xcds = reserve_xcds;
   a.reserve_slots = reserve_slots;
@@ -509,10 +550,16 @@ extern "C" int r2_torso_fwd_multi(const uint8_t* frames, const int64_t* jobs, in
   }
   if (wb > nw) return -3;   // more jobs than workers
   if (reserve_slots <= 0 && grid > wb) grid = wb;
-  hipLaunchKernelGGL(torso_fwd_kernel, dim3(grid), dim3(torso::NT), torso::LDS_BYTES,
-                     (hipStream_t)stream, a);
+  if (atari) tf_launch<GeoAtari>(a, grid, (hipStream_t)stream);
+  else tf_launch<GeoDmlab>(a, grid, (hipStream_t)stream);
   R2_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int r2_torso_fwd_multi(const uint8_t* frames, const int64_t* jobs, int njobs,
+                                  int grid, int reserve_xcds, int reserve_slots, void* stream) {
+  return r2_torso_fwd_geom(frames, 0, jobs, njobs, grid, reserve_xcds, reserve_slots, 4, 84, 84,
+                           stream);
 }
 
 extern "C" int r2_torso_fwd(const uint8_t* frames, const int* rows, int n_frames,

@@ -33,7 +33,7 @@ from .engine.layout import ParamLayout
 from .engine.replay_hbm import HBMReplay
 from .ops._lib import check, kernels, ptr, stream_handle
 from .ops.gemm import Gemm, gemm
-from .ops.torso_lib import fused_torso_supported, torso_forward_library
+from .ops.torso_lib import fused_torso_fwd_geom, torso_forward_library, torso_fwd_fused
 
 
 _VP = ctypes.c_void_p
@@ -105,7 +105,9 @@ class BatchedActor:
         self.gamma = cfg.learner.gamma
         self.gamma_n = self.gamma ** self.n
         self.layout = ParamLayout(m, cfg.env)
-        self.fused_torso = fused_torso_supported(cfg.env, m)
+        # fused torso forward: Atari 4x84x84 and DMLab-30 3x72x96 (else the library convs)
+        self.fwd_geom = fused_torso_fwd_geom(cfg.env, m) if self.device.type == "cuda" else None
+        self.fused_torso = self.fwd_geom is not None
         total = total_envs or E
         eps = [epsilon_ladder(global_env_offset + i, total, cfg.actor.eps_base, cfg.actor.eps_alpha)
                for i in range(E)]
@@ -208,9 +210,8 @@ class BatchedActor:
                 [[0, E, ptr(w.pk["conv1"]), ptr(w.pk["b1"]), ptr(w.pk["conv2"]), ptr(w.pk["b2"]),
                   ptr(w.pk["conv3"]), ptr(w.pk["b3"]), ptr(self.Xn[key]), 0, 0, 0] for key, w in nets],
                 dtype=np.int64)
-            check(k.r2_torso_fwd_multi(ptr(self.env.frames), self._tjobs.ctypes.data, 2,
-                                       self.n_workers, 0, 0, s),
-                  "torso_fwd_multi")
+            torso_fwd_fused(self.env.frames.reshape(E, -1), self._tjobs, self.fwd_geom,
+                            self.n_workers, s)
         else:
             for key, w in nets:
                 torso_forward_library(self.env.frames.reshape(E, -1), None, L, w.flat, self.cfg.env,

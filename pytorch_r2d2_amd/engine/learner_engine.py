@@ -50,7 +50,8 @@ from ..models.qnet import QNet
 from ..ops._lib import check, kernels, ptr, stream_handle
 from ..ops.gemm import G5_CFGS, Gemm, gemm, gemm_group, gemm_sp, gemm_sp_ws_bytes, group_ws_bytes
 from ..models.qnet import torso_dims
-from ..ops.torso_lib import fused_torso_supported, gather_frames_nhwc, torso_forward_library
+from ..ops.torso_lib import (fused_torso_fwd_geom, fused_torso_supported, gather_frames_nhwc,
+                             torso_forward_library, torso_fwd_fused)
 from .layout import ParamLayout, UNITS
 from .replay_hbm import HBMReplay
 
@@ -222,6 +223,9 @@ class LearnerEngine:
         # kernels cover the Atari geometry (4x84x84 -> 32x20x20 -> 32x9x9 -> 32x7x7), every other
         # geometry (e.g. DMLab RGB 3x72x96) runs the library conv path with the same buffers
         self.fused_torso = fused_torso_supported(cfg.env, cfg.model)
+        # the fused FORWARD kernel also covers DMLab-30 RGB (3x72x96); its backward then runs on
+        # the library convs from the saved activations
+        self.fwd_geom = fused_torso_fwd_geom(cfg.env, cfg.model) if d.type == "cuda" else None
         if sp and not (self.fused_torso and d.type == "cuda" and L.H <= 256
                        and lc.lstm_impl == "persistent" and lc.lstm_handoff == "tagged"):
             raise NotImplementedError(
@@ -590,7 +594,7 @@ class LearnerEngine:
             self._tjobs = np.asarray(jobs, dtype=np.int64)          # kept alive for capture
             check(k.r2_torso_fwd_sp_multi(ptr(rp.frames), self._tjobs.ctypes.data, len(jobs),
                                           self.n_cus, s), "torso_fwd_sp_multi")
-        elif self.fused_torso:
+        elif self.fwd_geom is not None:
             # one launch, workers dealt to the 4 jobs in proportion to their frames: separate
             # launches each ended in a partly idle last round of frames (18.6 us for the 320
             # tail frames alone)
@@ -600,8 +604,7 @@ class LearnerEngine:
                     self._torso_job(pt, rows[self.t_lo_tg * B:], self.X_tg)]
             jobs = [j for j in jobs if j[1] > 0]
             self._tjobs = np.asarray(jobs, dtype=np.int64)          # kept alive for capture
-            check(k.r2_torso_fwd_multi(ptr(rp.frames), self._tjobs.ctypes.data, len(jobs), self.n_cus,
-                                       0, 0, s), "torso_fwd_multi")
+            torso_fwd_fused(rp.frames, self._tjobs, self.fwd_geom, self.n_cus, s)
         else:   # library convs: one call per net over all its frames (bigger, fewer launches)
             torso_forward_library(rp.frames, rows, L, self.master, self.cfg.env, self.cfg.model,
                                   self.X_on, self.act1, self.act2, save_lo=Lb * B)

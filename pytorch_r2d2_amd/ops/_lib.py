@@ -33,6 +33,7 @@ _SIGS = {
     "r2_lstm_bwd": [P, P, P, P, P, P, P, P, P, I, I, I, I, P],
     "r2_torso_fwd": [P, P, I, P, P, P, P, P, P, P, P, P, I, P],
     "r2_torso_fwd_multi": [P, P, I, I, I, I, P],
+    "r2_torso_fwd_geom": [P, I64, P, I, I, I, I, I, I, I, P],
     "r2_frames_to_bf16": [P, P, I, P, P],
     "r2_frames_to_bf16_nhwc": [P, P, I, P, P],
     "r2_frames_gather_nhwc": [P, I64, P, I, I, I, F, P, P],

@@ -15,8 +15,35 @@ from ..config import EnvConfig, ModelConfig
 
 
 def fused_torso_supported(env: EnvConfig, model: ModelConfig) -> bool:
+    """The whole fused torso (forward AND backward kernels): the Atari stack 4x84x84."""
     return (model.torso == "atari" and env.channels_per_frame * env.n_stacks == 4
             and env.frame_h == 84 and env.frame_w == 84 and tuple(model.conv_channels) == (32, 32, 32))
+
+
+# frame geometries instantiated by the fused forward kernel (csrc/kernels/torso.hip TGeo)
+FUSED_FWD_GEOMS = ((4, 84, 84), (3, 72, 96))
+
+
+def fused_torso_fwd_geom(env: EnvConfig, model: ModelConfig):
+    """(cin, h, w) when the fused bf16 torso FORWARD kernel covers this geometry (Atari 4x84x84,
+    DMLab-30 RGB 3x72x96), else None."""
+    g = (env.channels_per_frame * env.n_stacks, env.frame_h, env.frame_w)
+    if model.torso == "atari" and tuple(model.conv_channels) == (32, 32, 32) and g in FUSED_FWD_GEOMS:
+        return g
+    return None
+
+
+def torso_fwd_fused(frames: torch.Tensor, jobs, geom, grid: int, stream=None, reserve_xcds: int = 0,
+                    reserve_slots: int = 0) -> None:
+    """Launch the fused bf16 torso forward (torso.hip r2_torso_fwd_geom) over up to 4 frame-list
+    jobs (rows of the uint8 replay / env frame buffer ``frames``; row stride from the tensor).
+    ``jobs``: an (n, 12) int64 array kept alive by the caller (graph capture)."""
+    from ._lib import check, kernels, ptr, stream_handle
+    cin, h, w = geom
+    check(kernels().r2_torso_fwd_geom(ptr(frames), frames.stride(0) * frames.element_size()
+                                      if frames.dim() > 1 else cin * h * w,
+                                      jobs.ctypes.data, len(jobs), grid, reserve_xcds, reserve_slots,
+                                      cin, h, w, stream or stream_handle()), "torso_fwd_geom")
 
 
 def gather_frames_nhwc(frames: torch.Tensor, rows: Optional[torch.Tensor], cin: int, fh: int,

@@ -17,8 +17,8 @@ def _rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
-def _setup(B=8, H=256, seed=0):
-    cfg = get_config("atari57", **{"model.hidden": H})
+def _setup(B=8, H=256, seed=0, preset="atari57"):
+    cfg = get_config(preset, **{"model.hidden": H})
     torch.manual_seed(seed)
     net = QNet("cpu", cfg.model, cfg.env)
     L = ParamLayout(cfg.model, cfg.env)
@@ -290,6 +290,39 @@ def test_torso_matches_conv_stack():
         assert _rel(out, ref) < 2e-2
         assert _rel(a1.view(n, 20, 20, 32).permute(0, 3, 1, 2), r1) < 2e-2
         assert _rel(a2.view(n, 9, 9, 32).permute(0, 3, 1, 2), r2) < 2e-2
+
+
+def test_torso_dmlab_rgb_matches_conv_stack():
+    """The geometry-templated fused forward on DMLab-30 RGB frames (3x72x96 -> 32x17x23 ->
+    32x7x10 -> 32x5x8) vs the fp32 PyTorch conv stack, with padded replay rows (row stride >
+    frame bytes) and activation saves, several jobs in one launch."""
+    import numpy as np
+    from pytorch_r2d2_amd.ops.torso_lib import torso_fwd_fused
+    cfg, net, L, flat, pk = _setup(preset="dmlab30")
+    n0, n1 = 29, 18
+    fb = 3 * 72 * 96
+    store = torch.randint(0, 256, (60, fb + 64), dtype=torch.uint8, device=DEV)
+    rows = torch.randint(0, 60, (n0 + n1,), dtype=torch.int32, device=DEV)
+    out = torch.zeros(n0 + n1, 1280, dtype=torch.bfloat16, device=DEV)
+    a1 = torch.zeros(n1, 391, 32, dtype=torch.bfloat16, device=DEV)
+    a2 = torch.zeros(n1, 70, 32, dtype=torch.bfloat16, device=DEV)
+    w = [ptr(pk[k]) for k in ("conv1", "b1", "conv2", "b2", "conv3", "b3")]
+    for grid in (256, 7):
+        jobs = np.asarray([[ptr(rows), n0, *w, ptr(out), 0, 0, 0],
+                           [ptr(rows) + 4 * n0, n1, *w, ptr(out) + 2 * 1280 * n0, ptr(a1), ptr(a2), 0]],
+                          dtype=np.int64)
+        out.zero_()
+        torso_fwd_fused(store, jobs, (3, 72, 96), grid)
+        torch.cuda.synchronize()
+        x = store[rows.long(), :fb].view(-1, 3, 72, 96).float() / 255.0
+        with torch.no_grad():
+            v = net.vis_layers
+            r1 = torch.relu(v[0](x))
+            r2 = torch.relu(v[2](r1))
+            ref = torch.relu(v[4](r2)).reshape(n0 + n1, -1)
+        assert _rel(out, ref) < 2e-2
+        assert _rel(a1.view(n1, 17, 23, 32).permute(0, 3, 1, 2), r1[n0:]) < 2e-2
+        assert _rel(a2.view(n1, 7, 10, 32).permute(0, 3, 1, 2), r2[n0:]) < 2e-2
 
 
 def test_dueling_head_fwd_bwd():
