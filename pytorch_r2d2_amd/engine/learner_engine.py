@@ -232,7 +232,7 @@ class LearnerEngine:
                 "compute_dtype=fp32 (split precision) runs the fused Atari torso (4x84x84), hidden "
                 "<= 256 and the tagged persistent LSTM on a GPU; use compute_dtype=bf16 or the torch "
                 "learner (learner_ref.py) for other configurations")
-        if not self.fused_torso and cfg.learner.conv_autotune and d.type == "cuda":
+        if (self.fwd_geom is None or lc.torso_bwd != "fused") and cfg.learner.conv_autotune and d.type == "cuda":
             # library conv path: let MIOpen benchmark its solutions once per shape (find mode);
             # DMLab-30: 463 -> 503 learner steps/s
             torch.backends.cudnn.benchmark = True
@@ -287,8 +287,8 @@ class LearnerEngine:
         self.td_ticket = z(1, dt=torch.int32)           # reset by the kernel's last workgroup
         # fused torso backward: per-workgroup gradient slabs + destination map (allocated here,
         # never lazily: the step must be capturable without warm-up)
-        if self.fused_torso:
-            n_slab = int(kernels().r2_torso_bwd_slab_floats())
+        if self.fwd_geom is not None:
+            n_slab = int(kernels().r2_torso_bwd_slab_floats_geom(*self.fwd_geom))
             self._tb_grid = torso_bwd_grid(Ll * B, self._comm_reserve(), self.n_cus)
             self._tb_slab = z(self._tb_grid * n_slab)
             dst, scale = L.torso_grad_map()
@@ -965,22 +965,25 @@ class LearnerEngine:
                 ptr(pk["conv2_dg"]), ptr(pkl["conv2_dg"]), ptr(self._tb_slab), self._tb_grid,
                 ptr(self._tb_dst), ptr(self._tb_scale), ptr(self.grad), stream_handle()), "torso_bwd_sp")
             return
-        if self.cfg.learner.torso_bwd == "fused" and self.fused_torso:
+        if self.cfg.learner.torso_bwd == "fused" and self.fwd_geom is not None:
             self._backward_torso_fused()
         else:
             self._backward_torso_library()
 
     def _backward_torso_fused(self):
-        """One fused HIP kernel (csrc/kernels/torso_bwd.hip) + slab reduction into self.grad."""
+        """One fused HIP kernel (csrc/kernels/torso_bwd.hip, Atari or DMLab geometry) + slab
+        reduction into self.grad."""
         B, Lb, T = self.B, self.Lb, self.T
         N = self.Ll * B
         pk = self.pk
-        check(kernels().r2_torso_bwd(ptr(self.replay.frames), ptr(self.rows[Lb * B: T * B]), N,
-                                     ptr(self.act1), ptr(self.act2), ptr(self._dX),
-                                     ptr(self.X_on[Lb * B: T * B]), ptr(pk["conv3_dg"]),
-                                     ptr(pk["conv2_dg"]), ptr(self._tb_slab), self._tb_grid,
-                                     ptr(self._tb_dst), ptr(self._tb_scale), ptr(self.grad),
-                                     stream_handle()), "torso_bwd")
+        fr = self.replay.frames
+        check(kernels().r2_torso_bwd_geom(ptr(fr), fr.stride(0) * fr.element_size(),
+                                          ptr(self.rows[Lb * B: T * B]), N,
+                                          ptr(self.act1), ptr(self.act2), ptr(self._dX),
+                                          ptr(self.X_on[Lb * B: T * B]), ptr(pk["conv3_dg"]),
+                                          ptr(pk["conv2_dg"]), ptr(self._tb_slab), self._tb_grid,
+                                          ptr(self._tb_dst), ptr(self._tb_scale), ptr(self.grad),
+                                          *self.fwd_geom, stream_handle()), "torso_bwd")
 
     def _backward_torso_library(self):
         """Conv backward (library kernels) from the activations saved by the torso kernel.

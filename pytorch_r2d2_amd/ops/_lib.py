@@ -73,6 +73,8 @@ _SIGS = {
     "r2_noop_chain": [P, I, I, P],
     "r2_torso_bwd": [P, P, I, P, P, P, P, P, P, P, I, P, P, P, P],
     "r2_torso_bwd_slab_floats": [],
+    "r2_torso_bwd_geom": [P, I64, P, I, P, P, P, P, P, P, P, I, P, P, P, I, I, I, P],
+    "r2_torso_bwd_slab_floats_geom": [I, I, I],
     "r2_gemm": [P, I, P],
     "r2_gemm_set_version": [I],
     "r2_gemm_group": [P, P, I, P, I64, P, I, P],

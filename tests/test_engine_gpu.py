@@ -63,24 +63,36 @@ def test_engine_loss_and_grads_match_reference(mode):
     assert _rel(rp.priority[rows], out["priority"]) < 5e-2
 
 
-def test_engine_dmlab_rgb_library_torso_matches_reference():
-    """DMLab-30 preset (3x72x96 RGB): the generic library conv torso path of the engine."""
+def test_engine_dmlab_rgb_torso_matches_reference():
+    """DMLab-30 preset (3x72x96 RGB): the fused forward kernel instance for this geometry, then
+    BOTH conv backwards from the same forward -- the fused torso_bwd.hip instance and the library
+    (MIOpen) convolution_backward -- vs the fp32 autograd oracle.  bf16 operands put the conv1
+    weight gradient near the 8 % bound for either backward, so the fused one must also stay within
+    1.25x of the library's own error."""
     cfg, rp, eng, net, tgt = _make("shifted", B=8, preset="dmlab30",
                                    **{"replay.burn_in": 4, "replay.learn": 8, "replay.overlap": 6})
-    assert not eng.fused_torso
+    assert not eng.fused_torso and eng.fwd_geom == (3, 72, 96)
     eng._forward_loss()
     eng._backward_core()
-    eng._backward_torso()
+    core = eng.grad.clone()
+    eng._backward_torso_fused()
     torch.cuda.synchronize()
+    g_fused = eng.grad.clone()
+    eng.grad.copy_(core)
+    eng._backward_torso_library()
+    torch.cuda.synchronize()
+    g_lib = eng.grad.clone()
     online = copy.deepcopy(net).to(DEV)
     target = copy.deepcopy(tgt).to(DEV)
     batch = batch_from_hbm(rp, eng.starts, eng.probs, cfg, DEV)
     out = r2d2_loss(online, target, batch, cfg, "shifted")
     out["loss"].backward()
     assert abs(eng.loss.item() - out["loss"].item()) / out["loss"].item() < 3e-2
-    got = eng.layout.views(eng.grad)
+    got_f, got_l = eng.layout.views(g_fused), eng.layout.views(g_lib)
     for name, p in online.named_parameters():
-        assert _rel(got[name], p.grad) < 8e-2, name
+        el, ef = _rel(got_l[name], p.grad), _rel(got_f[name], p.grad)
+        assert el < 8e-2, (name, el)
+        assert ef < max(8e-2, 1.25 * el), (name, ef, el)
 
 
 def test_engine_graph_replay_matches_eager():
@@ -158,8 +170,15 @@ def test_engine_training_reduces_loss_on_fixed_batch():
     assert min(losses[-10:]) < losses[0]
 
 
-def test_fused_torso_backward_matches_library():
-    cfg, rp, eng, net, tgt = _make("shifted", B=16)
+@pytest.mark.parametrize("preset", ["atari57", "dmlab30"])
+def test_fused_torso_backward_matches_library(preset):
+    """The fused torso backward (torso_bwd.hip, Atari 4x84x84 and DMLab-30 3x72x96 instances) vs
+    MIOpen's convolution_backward from the same saved activations."""
+    if preset == "atari57":
+        cfg, rp, eng, net, tgt = _make("shifted", B=16)
+    else:
+        cfg, rp, eng, net, tgt = _make("shifted", B=8, preset="dmlab30",
+                                       **{"replay.burn_in": 4, "replay.learn": 8, "replay.overlap": 6})
     eng._forward_loss()
     eng._backward_core()
     eng.grad.zero_()
