@@ -78,15 +78,15 @@ __device__ __forceinline__ float r2_uniform(uint64_t seed, uint64_t ctr, uint64_
   return (float)(z >> 40) * (1.0f / 16777216.0f);
 }
 
-// Workgroup barrier that orders LDS only.  __syncthreads() also emits s_waitcnt vmcnt(0), which
-// drains every outstanding global load -- including a next-frame register prefetch that is meant to
-// stay in flight across the barrier.  Use this where only LDS traffic must be ordered.
 // a[i] for a wave-uniform index through the scalar (constant) path: s_load + lgkmcnt instead of a
 // vector load whose vmcnt wait would also wait for every older outstanding load / store
 __device__ __forceinline__ int ld_uniform_i32(const int* a, int i) {
   return ((const __attribute__((address_space(4))) int*)a)[i];
 }
 
+// Workgroup barrier that orders LDS only.  __syncthreads() also emits s_waitcnt vmcnt(0), which
+// drains every outstanding global load -- including a next-frame register prefetch that is meant to
+// stay in flight across the barrier.  Use this where only LDS traffic must be ordered.
 __device__ __forceinline__ void lds_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }

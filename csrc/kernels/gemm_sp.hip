@@ -388,8 +388,9 @@ static void g5_kernel_launch(const G5Args& a, hipStream_t s) {
 
 // tile configurations: {BM, BN, BK, NS}
 static const int g5_cfgs[][4] = {{192, 128, 64, 2}, {128, 128, 64, 2}, {256, 128, 32, 3},
-                                 {256, 256, 32, 2}, {256, 64, 64, 2}, {128, 64, 64, 2}};
-static const int g5_ncfg = 6;
+                                 {256, 256, 32, 2}, {256, 64, 64, 2}, {128, 64, 64, 2},
+                                 {128, 128, 32, 4}};
+static const int g5_ncfg = 7;
 
 static int g5_tiles(const GemmProb& p, int bm, int bn) {
   return ((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn);
@@ -469,6 +470,8 @@ extern "C" int r2_gemm5(const int64_t* descs, const int* split, int np, int cfg,
     case 7: g5_kernel_launch<true, 256, 256, 32, 2>(a, s); break;
     case 9: g5_kernel_launch<true, 256, 64, 64, 2>(a, s); break;
     case 11: g5_kernel_launch<true, 128, 64, 64, 2>(a, s); break;
+    case 12: g5_kernel_launch<false, 128, 128, 32, 4>(a, s); break;
+    case 13: g5_kernel_launch<true, 128, 128, 32, 4>(a, s); break;
     default: return -8;
   }
   R2_CHECK_LAUNCH();
