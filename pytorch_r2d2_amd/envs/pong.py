@@ -21,17 +21,22 @@ def _resize_gray(frame: np.ndarray) -> np.ndarray:
         import cv2  # type: ignore
         return cv2.resize(cv2.cvtColor(frame, cv2.COLOR_RGB2GRAY), (84, 84))
     except ImportError:
-        # dependency-free fallback: ITU-R 601 luma + area-average resize
-        g = frame[..., 0] * 0.299 + frame[..., 1] * 0.587 + frame[..., 2] * 0.114
-        h, w = g.shape
-        ys = (np.arange(85) * h / 84).astype(int)
-        xs = (np.arange(85) * w / 84).astype(int)
-        out = np.empty((84, 84), dtype=np.float32)
-        for i in range(84):
-            band = g[ys[i]:max(ys[i + 1], ys[i] + 1)]
-            for j in range(84):
-                out[i, j] = band[:, xs[j]:max(xs[j + 1], xs[j] + 1)].mean()
-        return out
+        return _resize_gray_area(frame)
+
+
+def _resize_gray_area(frame: np.ndarray) -> np.ndarray:
+    """Dependency-free fallback: ITU-R 601 luma + area-average resize to 84x84, vectorised over an
+    integral image (every output cell is the mean of rows [ys[i], ye[i]) x cols [xs[j], xe[j]))."""
+    g = frame[..., 0] * 0.299 + frame[..., 1] * 0.587 + frame[..., 2] * 0.114
+    h, w = g.shape
+    ys = (np.arange(85) * h / 84).astype(int)
+    xs = (np.arange(85) * w / 84).astype(int)
+    y0, y1 = ys[:84], np.maximum(ys[1:], ys[:84] + 1)
+    x0, x1 = xs[:84], np.maximum(xs[1:], xs[:84] + 1)
+    S = np.zeros((h + 1, w + 1), dtype=np.float64)
+    S[1:, 1:] = g.cumsum(0).cumsum(1)
+    tot = S[y1][:, x1] - S[y0][:, x1] - S[y1][:, x0] + S[y0][:, x0]
+    return (tot / ((y1 - y0)[:, None] * (x1 - x0)[None, :])).astype(np.float32)
 
 
 def preprocess(frame: np.ndarray) -> np.ndarray:

@@ -155,3 +155,21 @@ def test_burn_in_blocks_gradient():
     b2.obs[3:5] = 0
     r2d2_loss(online, target, b2, cfg, "shifted")["loss"].backward()
     assert not torch.allclose(g1, online.vis_layers[0].weight.grad)
+
+
+def test_pong_area_resize_fallback_matches_per_cell_mean():
+    """envs/pong.py cv2-free preprocessing: the vectorised integral-image area resize equals the
+    per-cell band mean (the former 7,056-iteration Python loop) on a raw 210x160 RGB frame."""
+    import numpy as np
+    from pytorch_r2d2_amd.envs.pong import _resize_gray_area
+    rng = np.random.default_rng(3)
+    f = rng.integers(0, 256, (210, 160, 3)).astype(np.uint8)
+    g = f[..., 0] * 0.299 + f[..., 1] * 0.587 + f[..., 2] * 0.114
+    ys = (np.arange(85) * 210 / 84).astype(int)
+    xs = (np.arange(85) * 160 / 84).astype(int)
+    ref = np.empty((84, 84), dtype=np.float32)
+    for i in range(84):
+        band = g[ys[i]:max(ys[i + 1], ys[i] + 1)]
+        for j in range(84):
+            ref[i, j] = band[:, xs[j]:max(xs[j + 1], xs[j] + 1)].mean()
+    np.testing.assert_allclose(_resize_gray_area(f), ref, rtol=1e-5, atol=1e-3)
