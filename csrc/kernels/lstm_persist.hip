@@ -1374,6 +1374,9 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
 
 // lo planes handed from r2_lstm_bwd_tag_sp to the shared launcher body (host-side, per call)
 static const bf16* g_bwd_whhT_lo = nullptr;
+// split-precision head-gradient side job operands (r2_lstm_bwd_tag_sp_hg): zr fp32, dz lo plane
+static const float* g_bwd_hg_zr32 = nullptr;
+static const bf16* g_bwd_hg_dz_lo = nullptr;
 static bf16* g_bwd_dgates_lo = nullptr;
 
 extern "C" int r2_lstm_bwd_tag_ring_bytes(int B, int H) {
@@ -1413,7 +1416,7 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
   PTBArgs args{dh_ext, gates, c_seq, c0, whhT, dgates, ring, B, T, t0, ctr, err, MB, xmap, g_pl_slow, 0,
                bias_ws, perm, db1, db2,
                HeadGradArgs{hg_dva, hg_zr, hg_dz, hg_gw2, hg_gb2, hg_gb1, hg_ws, hg_ticket, hg_N, hg_A,
-                            hg_HD, 8, (hg_A + 6) / 7, nullptr, nullptr},
+                            hg_HD, 8, (hg_A + 6) / 7, g_bwd_hg_zr32, g_bwd_hg_dz_lo},
                0};
   args.n_gw = 0; args.gw_wait = 0; args.gx_on = 0; args.n_wtiles = 0;
   int taken = 0, nh = 0;
@@ -1449,7 +1452,9 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
   args.whhT_lo = g_bwd_whhT_lo;
   args.dgates_lo = g_bwd_dgates_lo;
   const bool sp = g_bwd_whhT_lo != nullptr;
-  if (sp && (!args.dgates_lo || H > 256 || taken)) return -11;
+  // split precision: the head-gradient side job (fp32 zr, hi / lo dz) only, no helper GEMMs
+  if (sp && (!args.dgates_lo || H > 256 || (taken & ~1))) return -11;
+  if (sp && args.hg_on && (!args.hg.zr32 || !args.hg.dz_lo)) return -12;
   hipStream_t s = (hipStream_t)stream;   // counters are left zeroed by the previous launch
   dim3 grid(nh ? 256 : (xmap ? 8 * nwg : MB * nwg)), block(320);
 #define R2_BWD_LAUNCH(HH, SPP)                                                                 \
@@ -1492,6 +1497,32 @@ extern "C" int r2_lstm_bwd_tag_sp(const float* dh_ext, const float* gates, const
                                  nullptr, 0, 0, 0, nullptr, nullptr, nullptr, 0, 0, 0, stream);
   g_bwd_whhT_lo = nullptr;
   g_bwd_dgates_lo = nullptr;
+  return rc;
+}
+
+// Split precision with the dueling head's gradient reduction on the launch's idle workgroups
+// (r2_head_grads_sp operands; only when r2_lstm_bwd_tag_hg_ok(B, H, HD)).  Returns the
+// r2_lstm_bwd_tag bit mask: bit 0 set = the head gradients were produced here.
+extern "C" int r2_lstm_bwd_tag_sp_hg(const float* dh_ext, const float* gates, const float* c_seq,
+                                     const float* c0, const bf16* whhT, const bf16* whhT_lo,
+                                     bf16* dgates, bf16* dgates_lo, int B, int T, int t0, int H,
+                                     unsigned* ctr, unsigned* err, void* ring, float* bias_ws,
+                                     const int* perm, float* db1, float* db2, const float* hg_dva,
+                                     const float* hg_zr32, const bf16* hg_dz, const bf16* hg_dz_lo,
+                                     float* hg_gw2, float* hg_gb2, float* hg_gb1, int hg_N, int hg_A,
+                                     int hg_HD, float* hg_ws, unsigned* hg_ticket, void* stream) {
+  if (!whhT_lo || !dgates_lo || !hg_zr32 || !hg_dz_lo) return -5;
+  g_bwd_whhT_lo = whhT_lo;
+  g_bwd_dgates_lo = dgates_lo;
+  g_bwd_hg_zr32 = hg_zr32;
+  g_bwd_hg_dz_lo = hg_dz_lo;
+  const int rc = r2_lstm_bwd_tag(dh_ext, gates, c_seq, c0, whhT, dgates, B, T, t0, H, ctr, err, ring,
+                                 bias_ws, perm, db1, db2, hg_dva, nullptr, hg_dz, hg_gw2, hg_gb2,
+                                 hg_gb1, hg_N, hg_A, hg_HD, hg_ws, hg_ticket, nullptr, 0, 0, 0, stream);
+  g_bwd_whhT_lo = nullptr;
+  g_bwd_dgates_lo = nullptr;
+  g_bwd_hg_zr32 = nullptr;
+  g_bwd_hg_dz_lo = nullptr;
   return rc;
 }
 

@@ -118,6 +118,9 @@ class LearnerConfig:
     # at K splits 4,4,4,1, dh 26 -> 18 us; profiles/r02_gemm_sp_micro_v1.txt) | "multipass"
     sp_gemm: str = "fused"
     sp_group_splits: str = "4,4,4,1"  # K splits of the fused post-BPTT group (dW_ih, dW_hh, dW_head1, dX)
+    # split precision: the dueling head's gradient reduction on the BPTT launch's idle workgroups
+    # (r2_lstm_bwd_tag_sp_hg) instead of its own 28 us launch
+    sp_head_grads_in_bptt: bool = True
     torso_bwd: str = "fused"          # fused (HIP kernel) | library (MIOpen convolution_backward)
     # library conv path (frame geometries without the fused HIP torso, e.g. DMLab): MIOpen find
     # mode (torch.backends.cudnn.benchmark) instead of its immediate-mode heuristics

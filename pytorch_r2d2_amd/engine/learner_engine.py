@@ -715,17 +715,27 @@ class LearnerEngine:
         gw2 = L.span(g, "val.2.weight", "adv.2.weight", (1 + A, HD))
         gb2 = L.span(g, "val.2.bias", "adv.2.bias", (1, 1 + A))
         gb1 = L.span(g, "val.0.bias", "adv.0.bias", (1, 2 * HD))
-        check(k.r2_head_grads_sp(ptr(self.dva), ptr(self.zr_on[:N]), ptr(self.dz), ptr(self.dz_lo),
-                                 ptr(gw2), ptr(gb2), ptr(gb1), N, A, HD, ptr(self.gs_ws),
-                                 ptr(self.gs_ticket), s), "head_grads_sp")
+        hg = [ptr(self.dva), ptr(self.zr_on[:N]), ptr(self.dz), ptr(self.dz_lo), ptr(gw2), ptr(gb2),
+              ptr(gb1), N, A, HD, ptr(self.gs_ws), ptr(self.gs_ticket)]
+        # the head-gradient reduction rides on the BPTT launch's idle workgroups when they suffice
+        # (as in the bf16 engine); otherwise it is its own launch
+        side_hg = (self.cfg.learner.sp_head_grads_in_bptt and self.n_cus >= 256 and A <= 63
+                   and bool(k.r2_lstm_bwd_tag_hg_ok(B, H, HD)))
+        if not side_hg:
+            check(k.r2_head_grads_sp(*hg, s), "head_grads_sp")
         dh = self.dh
         self._gemm_sp("dh", [Gemm(self.dz, pk["head1"], dh, a_lo=self.dz_lo, b_lo=pkl["head1"])])
-        check(k.r2_lstm_bwd_tag_sp(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]), ptr(self.c0["on"]),
-                                   ptr(pk["w_hhT"]), ptr(pkl["w_hhT"]), ptr(self.dgates),
-                                   ptr(self.dgates_lo), B, T, Lb, H, ptr(self.ctr), ptr(self.err),
-                                   ptr(self.ring_b), ptr(self.bias_ws), ptr(self.gate_perm_i32),
-                                   ptr(L.view(g, "lstm.bias_ih")), ptr(L.view(g, "lstm.bias_hh")), s),
-              "lstm_bwd_tag_sp")
+        bptt = [ptr(dh), ptr(self.gates), ptr(self.cseq["on"]), ptr(self.c0["on"]), ptr(pk["w_hhT"]),
+                ptr(pkl["w_hhT"]), ptr(self.dgates), ptr(self.dgates_lo), B, T, Lb, H, ptr(self.ctr),
+                ptr(self.err), ptr(self.ring_b), ptr(self.bias_ws), ptr(self.gate_perm_i32),
+                ptr(L.view(g, "lstm.bias_ih")), ptr(L.view(g, "lstm.bias_hh"))]
+        if side_hg:
+            rc = k.r2_lstm_bwd_tag_sp_hg(*bptt, *hg, s)   # >= 0: bit 0 = head grads done here
+            check(min(rc, 0), "lstm_bwd_tag_sp_hg")
+            if not rc & 1:
+                check(k.r2_head_grads_sp(*hg, s), "head_grads_sp")
+        else:
+            check(k.r2_lstm_bwd_tag_sp(*bptt, s), "lstm_bwd_tag_sp")
         hs, hl = self.hseq["on"], self.hseq_lo["on"]
         h_learn, h_learn_l = hs[Lb:T].reshape(N, H), hl[Lb:T].reshape(N, H)
         if Lb >= 1:

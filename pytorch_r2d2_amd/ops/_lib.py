@@ -48,6 +48,8 @@ _SIGS = {
     "r2_dueling_fwd_multi_f32": [P, I, I, I, P],
     "r2_lstm_fwd_tag_sp": [P, I, I, I, I, P, P, P, P],
     "r2_lstm_bwd_tag_sp": [P, P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P, P, P],
+    "r2_lstm_bwd_tag_sp_hg": [P, P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P, P,
+                              P, P, P, P, P, P, P, I, I, I, P, P, P],
     "r2_tree_sample": [P, P, P, I, I, U64, P, P, P, P],
     "r2_tree_rebuild": [P, P, P, I, P],
     "r2_tree_update": [P, P, P, I, P, P, I, P],
