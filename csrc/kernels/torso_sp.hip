@@ -710,6 +710,7 @@ struct TBSArgs {
   const bf16* w2dg; const bf16* w2dgl;   // (4 phases, 32 ci, 128 = (khi,kwi,co)) hi / lo
   float* slab;
   int n, pad_;
+  long long* trace;   // optional stage clock stamps of workgroup 0 (r2_torso_bwd_sp_trace)
 };
 
 typedef short ts_i16x4 __attribute__((ext_vector_type(4)));
@@ -802,7 +803,12 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
   }
   __syncthreads();
 
+  int it_dbg = 0;
+  long long* tr = (a.trace && blockIdx.x == 0 && lane == 0) ? a.trace + wave * 16 * 7 : nullptr;
+#define TBS_STAMP(k) \
+  if (tr && it_dbg < 16) tr[it_dbg * 7 + (k)] = (long long)__builtin_readcyclecounter();
   for (int f = blockIdx.x; f < a.n; f += gridDim.x) {
+    TBS_STAMP(0);
     int oz;
     asm volatile("s_mov_b32 %0, 0" : "=s"(oz));
     bf16* frb = (bf16*)(lds + R + oz);
@@ -844,6 +850,7 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
       }
     }
     lds_sync();
+    TBS_STAMP(1);
 
     // ======== S1: g2 = convT(g3, W3) * (act2 > 0) on waves 5-7
     if (wave >= 5) {
@@ -884,6 +891,7 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
       }
     }
     lds_sync();
+    TBS_STAMP(2);
 
     // ======== S2: dW2 (tiles wave, wave+8) and dact1 -> g1 (jobs 2w, 2w+1)
     {
@@ -903,27 +911,38 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
         acc2b = mfma32_x3(ah, al, b1h, b1l, acc2b);
       }
     }
+    TBS_STAMP(6);
     {
+      // dact1 -> g1: both of this wave's 32-pixel jobs (phase = wave >> 1) in one pass over K, so
+      // every W2 phase fragment (L2, hi / lo) is fetched once per frame, not once per job
       const int phase = wave >> 1, py = phase >> 1, px = phase & 1;
       const int vb = ((phase * 32 + l32) * 128 + half * 8) * 2;
-#pragma unroll 1
+      int ab[2];
+#pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
         const int mt = (wave & 1) * 2 + jj;
         const int m = mt * 32 + l32, mc = m < 100 ? m : 99;
-        const int ab = ((mc / 10 + 1) * 11 + mc % 10 + 1) * 32 + half * 8;
-        constexpr int D = 3;
-        bf16x8 rbh[D], rbl[D];
+        ab[jj] = ((mc / 10 + 1) * 11 + mc % 10 + 1) * 32 + half * 8;
+      }
+      constexpr int D = 3;
+      bf16x8 rbh[D], rbl[D];
 #pragma unroll
-        for (int s = 0; s < D; ++s) { rbh[s] = ts_bl(w2rs, vb, s * 32); rbl[s] = ts_bl(w2lrs, vb, s * 32); }
-        f32x16 acc = {};
+      for (int s = 0; s < D; ++s) { rbh[s] = ts_bl(w2rs, vb, s * 32); rbl[s] = ts_bl(w2lrs, vb, s * 32); }
+      f32x16 accj[2] = {{}, {}};
 #pragma unroll
-        for (int s = 0; s < 8; ++s) {
-          const bf16x8 bh = rbh[s % D], bl = rbl[s % D];
-          if (s + D < 8) { rbh[s % D] = ts_bl(w2rs, vb, (s + D) * 32); rbl[s % D] = ts_bl(w2lrs, vb, (s + D) * 32); }
-          const int tap = s >> 1;
-          const int o = ab - ((tap >> 1) * 11 + (tap & 1)) * 32 + (s & 1) * 16;
-          acc = mfma32_x3(ts_ld8(g2p + o), ts_ld8(g2pl + o), bh, bl, acc);
-        }
+      for (int s = 0; s < 8; ++s) {
+        const bf16x8 bh = rbh[s % D], bl = rbl[s % D];
+        if (s + D < 8 && !(a.pad_ & 1)) { rbh[s % D] = ts_bl(w2rs, vb, (s + D) * 32); rbl[s % D] = ts_bl(w2lrs, vb, (s + D) * 32); }
+        const int tap = s >> 1;
+        const int o = -((tap >> 1) * 11 + (tap & 1)) * 32 + (s & 1) * 16;
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+          accj[jj] = mfma32_x3(ts_ld8(g2p + ab[jj] + o), ts_ld8(g2pl + ab[jj] + o), bh, bl, accj[jj]);
+      }
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int mt = (wave & 1) * 2 + jj;
+        const f32x16& acc = accj[jj];
         const uint32_t* te = (const uint32_t*)(lds + TE1 + oz) + mt * 32 + half * 16;
         const int moff = (py * 20 + px) * 32 + l32, koff = (4 * py + px) * 32 + l32;
 #pragma unroll
@@ -938,8 +957,10 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
           for (int r = 0; r < 8; ++r) {
             const float v = ((float)mk[r] > 0.f) ? acc[r0 + r] : 0.f;
             const int o = ((e[r] >> 16) & 0x7fff) * 32 + koff;
-            g1h[o] = (bf16)v;
-            g1l[o] = sp_lo(v);
+            if (!(a.pad_ & 2)) {
+              g1h[o] = (bf16)v;
+              g1l[o] = sp_lo(v);
+            }
             db1p += (e[r] >> 31) ? v : 0.f;
           }
         }
@@ -947,6 +968,7 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
     }
     if (f + (int)gridDim.x < a.n) prefetch_acts(f + gridDim.x);
     lds_sync();
+    TBS_STAMP(3);
 
     // ======== S2b: frame -> R (act1 / act2 no longer read)
 #pragma unroll
@@ -958,6 +980,7 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
       }
     }
     lds_sync();
+    TBS_STAMP(4);
 
     // ======== S3: dW1 += g1 . im2col(frame), 25 K steps of one 4x4 pixel block each (2 passes)
     if (f + (int)gridDim.x < a.n) load_frame(f + gridDim.x);
@@ -983,6 +1006,8 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
       }
     }
     lds_sync();
+    TBS_STAMP(5);
+    ++it_dbg;
   }
 
   // ---- epilogue: this workgroup's partial gradients -> slab (dW3 / db3: torso_dw3_sp_kernel)
@@ -1093,6 +1118,13 @@ __global__ __launch_bounds__(512) void torso_dw3_sp_kernel(const TBSArgs a) {
 extern "C" int r2_torso_grad_reduce(const float* slab, int grid, const int* dst, const float* scale,
                                     float* grad, void* stream);
 
+static long long* g_tbs_trace = nullptr;
+static int g_tbs_dbg = 0;   // timing probes: bit 0 W2 fragments not re-fetched, bit 1 no g1 stores
+extern "C" int r2_torso_bwd_sp_debug(int bits) { g_tbs_dbg = bits; return 0; }
+// stage clock stamps of workgroup 0: [wave][frame < 16][7] (loop top, after S0, S1, S2, S2b, S3,
+// S2 dW2 part done)
+extern "C" int r2_torso_bwd_sp_trace(long long* p) { g_tbs_trace = p; return 0; }
+
 // Split-precision torso backward: every activation / gradient operand as hi / lo planes (out3:
 // the torso output's hi plane, a ReLU mask only).  slab: grid x r2_torso_bwd_slab_floats().
 extern "C" int r2_torso_bwd_sp(const uint8_t* frames, const int* rows, int n, const bf16* act1,
@@ -1111,7 +1143,7 @@ extern "C" int r2_torso_bwd_sp(const uint8_t* frames, const int* rows, int n, co
   }
   if (grid <= 0 || grid > n) grid = n < 256 ? n : 256;
   TBSArgs a{frames, rows, act1, act1l, act2, act2l, dx3, dx3l, out3, w3dg, w3dgl, w2dg, w2dgl,
-            slab, n, 0};
+            slab, n, g_tbs_dbg, g_tbs_trace};
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(torso_bwd_sp_kernel, dim3(grid), dim3(tbs::NT), tbs::LDS, s, a);
   hipLaunchKernelGGL(torso_dw3_sp_kernel, dim3(grid), dim3(tbs::NT), 0, s, a);

@@ -62,6 +62,8 @@ _SIGS = {
     "r2_torso_fwd_sp_multi": [P, P, I, I, P],
     "r2_torso_sp_debug": [I],
     "r2_torso_sp_trace": [P],
+    "r2_torso_bwd_sp_trace": [P],
+    "r2_torso_bwd_sp_debug": [I],
     "r2_torso_bwd_sp": [P, P, I, P, P, P, P, P, P, P, P, P, P, P, P, I, P, P, P, P],
     "r2_torso_grad_reduce": [P, I, P, P, P, P],
     "r2_gather_state": [P, P, I, I, I, I, P, P, P, P],
