@@ -52,7 +52,10 @@ struct TGeo {
   static constexpr int S2DS = 16 * CIN + 8;           // bf16 per space-to-depth pixel (+8 pad)
   static constexpr int OFF_IN = 0;                    // frame, bf16 space-to-depth [H4*W4][S2DS]
   static constexpr int OFF_A1 = OFF_IN + H4 * W4 * S2DS * 2;
-  static constexpr int OFF_A2 = OFF_A1 + P1 * ACTS * 2;
+  // act1: 64-B pixel rows, 16-B chunks row-XOR swizzled (tf_a1_off) -- conflict-lighter stride-2
+  // conv2 reads than the 80-B padded rows, and 6.4 KB smaller; act2 keeps the padded rows
+  static constexpr int A1_BYTES = ((P1 + 3) / 4) * 256;
+  static constexpr int OFF_A2 = OFF_A1 + A1_BYTES;
   static constexpr int OFF_W2 = OFF_A2 + P2 * ACTS * 2;
   static constexpr int OFF_W3 = OFF_W2 + 32 * W2S * 2;
   static constexpr int OFF_B23 = OFF_W3 + 32 * W3S * 2;   // conv2 / conv3 biases, fp32 [2][32]
@@ -70,6 +73,16 @@ constexpr int IN_BYTES = GeoAtari::IN_BYTES;
 // 16 uint8 of the CHW frame (chunk c) -> bf16 space-to-depth image (the only u8->bf16
 // conversion of a frame).  Every dword is 4 consecutive x of one row: (ci, y, X) -> s2d pixel
 // (y/4, X), channels ci*16 + (y%4)*4 + 0..3, one 8-byte store.
+// act1 pixel P, 16-byte chunk c (channels 8c .. 8c+7) -> byte offset in the act1 image
+__device__ __forceinline__ int tf_a1_off(int P, int c) {
+  return ((P >> 2) << 8) + (((((P & 3) << 2) | c) ^ ((P >> 2) & 15)) << 4);
+}
+
+// lane -> frame chunk inside each wave's block of 64 chunks: lane l takes chunk (25 l) mod 64, so
+// the 16 lanes of a ds_write_b64 group land on more distinct banks of the space-to-depth image
+// (modelled 8-byte store conflicts: 1328 -> 887 group-cycles per frame, ideal 448)
+__device__ __forceinline__ int tf_chunk(int t) { return (t & ~63) | ((t * 25) & 63); }
+
 template <class Gm>
 __device__ __forceinline__ void torso_store_chunk(bf16* s2d, int c, const u32x4& v) {
   constexpr int RD = Gm::W / 4, PD = Gm::H * RD;   // dwords per row / per plane
@@ -189,7 +202,10 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(const TFArgs args) {
   {
     const size_t row = rows ? (size_t)ld_uniform_i32(rows, f) : (size_t)f;
     const u32x4* src = (const u32x4*)(frames + row * rb);
-    for (int c = tid; c < IN_CHUNKS; c += NT) torso_store_chunk<Gm>(in_bf, c, src[c]);
+    for (int t = tid; t < ((IN_CHUNKS + 63) & ~63); t += NT) {
+      const int c = tf_chunk(t);
+      if (c < IN_CHUNKS) torso_store_chunk<Gm>(in_bf, c, src[c]);
+    }
   }
   __syncthreads();
 
@@ -213,7 +229,7 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(const TFArgs args) {
         const u32x4* src = (const u32x4*)(frames + (size_t)row_nx * rb);
 #pragma unroll
         for (int q = 0; q < PF; ++q) {
-          const int c = tid - 192 + q * 320;
+          const int c = tf_chunk(tid - 192 + q * 320);
           if (c < IN_CHUNKS) pf[q] = src[c];
         }
       }
@@ -238,7 +254,7 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(const TFArgs args) {
               const float x = acc[4 * g + e] * (1.f / 255.f) + bias1[4 * g + e];
               v[e] = (bf16)fmaxf(x, 0.f);
             }
-            *(bf16x4*)(act1 + p * ACTS + 8 * g + 4 * half) = v;
+            *(bf16x4*)((uint8_t*)act1 + tf_a1_off(p, g) + 8 * half) = v;
           }
         }
       }
@@ -275,11 +291,14 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(const TFArgs args) {
       const int pc = p < P2 ? p : P2 - 1;
       const int oy = pc / Gm::W2, ox = pc % Gm::W2;
       const bf16* abase = lw2 + l32 * W2S + half * 8;
-      const bf16* bbase = act1 + ((2 * oy) * Gm::W1 + 2 * ox) * ACTS + half * 8;
+      int oz;
+      asm volatile("v_mov_b32 %0, 0" : "=v"(oz));
+      const int P0 = (2 * oy) * Gm::W1 + 2 * ox + oz;   // (+oz: offsets computed per step, not hoisted)
+      const uint8_t* a1b = (const uint8_t*)act1;
       f32x16 acc = {};
       mfma_pipe<32, 3>(acc, [&](int s) { return *(const bf16x8*)(abase + s * 16); }, [&](int s) {
         const int khkw = s >> 1, kh = khkw >> 2, kw = khkw & 3;
-        return *(const bf16x8*)(bbase + (kh * Gm::W1 + kw) * ACTS + (s & 1) * 16);
+        return *(const bf16x8*)(a1b + tf_a1_off(P0 + kh * Gm::W1 + kw, (s & 1) * 2 + half));
       });
       TF_TRACE(4);
       if (p < P2) {
@@ -300,9 +319,10 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(const TFArgs args) {
       // waves 3..7 copy the channels-last conv1 activations out for the backward pass
       const int t5 = tid - 192;  // 0..319
       bf16* d1 = save1 + (size_t)f * P1 * 32;
-      for (int c = t5; c < P1 * 4; c += 320) {   // 4 chunks of 8 channels per pixel
-        const int px = c >> 2, q = c & 3;
-        *(bf16x8*)(d1 + px * 32 + q * 8) = *(const bf16x8*)(act1 + px * ACTS + q * 8);
+      for (int i = t5; i < P1 * 4; i += 320) {   // linear LDS chunks -> (pixel, chunk)
+        const int row = i >> 4, pcv = (i & 15) ^ (row & 15);
+        const int px = row * 4 + (pcv >> 2), q = pcv & 3;
+        if (px < P1) *(bf16x8*)(d1 + px * 32 + q * 8) = *(const bf16x8*)((const uint8_t*)act1 + i * 16);
       }
     }
     TF_TRACE(5);
@@ -310,7 +330,7 @@ __global__ __launch_bounds__(512) void torso_fwd_kernel(const TFArgs args) {
     if (fn < n_frames && wave >= 3) {
 #pragma unroll
       for (int q = 0; q < PF; ++q) {
-        const int c = tid - 192 + q * 320;
+        const int c = tf_chunk(tid - 192 + q * 320);
         if (c < IN_CHUNKS) torso_store_chunk<Gm>(in_bf, c, pf[q]);
       }
     }
