@@ -198,6 +198,10 @@ struct TdDuelArgs {
   bf16* dz;             // (Tl*B, 2*HD) out (hi plane in split precision)
   float* dva;           // (Tl*B, 1 + A) out
   bf16* dz_lo;          // split precision: lo plane of dz
+  // optional fused head backward to the LSTM output: dh = dz @ W1 for the workgroup's 16 rows
+  const bf16* w1t;      // (256, 2*HD) = W1^T (k contiguous); null = not fused
+  const bf16* w1t_lo;   // split precision: lo plane of W1^T
+  float* dh;            // (Tl*B, 256) out
 };
 
 // SP: zr fp32, dz written as hi / lo planes (split.h).  Actions beyond the MAXA register-resident
@@ -263,6 +267,9 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
 
   const float inv_n = 1.f / (float)n;
   float lsum = 0.f;
+  float dz_v[PER], dz_a[PER];   // pre-mask dz of this row (value / advantage halves) for the fused dh
+#pragma unroll
+  for (int e = 0; e < PER; ++e) { dz_v[e] = 0.f; dz_a[e] = 0.f; }
   if (valid) {
     // argmax_a Q_online(s_{t+n}): first maximum, as td_kernel's sequential scan
     float bv = qa;
@@ -310,6 +317,8 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
         ga += (((k == act) ? g : 0.f) - dmean) * args.w2[(size_t)(1 + k) * HD + lane * PER + e];
       ov[e] = ((float)zv[e] > 0.f) ? gv : 0.f;
       oa[e] = ((float)za[e] > 0.f) ? ga : 0.f;
+      dz_v[e] = gv;
+      dz_a[e] = ga;
     }
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
@@ -322,9 +331,62 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
       }
     }
   }
+  // ---- fused dh = dz @ W1 of the 16 rows (dz staged in LDS; wave w owns dh columns 16w..16w+15,
+  // K = 2HD on v_mfma_f32_16x16x32_bf16, W1^T fragments from L2; 3 passes in split precision)
+  constexpr int KD = 2 * HD, DZS = KD + 8;             // padded LDS rows
+  __shared__ __attribute__((aligned(16))) bf16 dzs[SP ? 2 : 1][NW * DZS];
+  if (args.w1t) {
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const float v0 = valid ? ((float)zv[e] > 0.f ? dz_v[e] : 0.f) : 0.f;
+      const float v1 = valid ? ((float)za[e] > 0.f ? dz_a[e] : 0.f) : 0.f;
+      dzs[0][wave * DZS + lane * PER + e] = (bf16)v0;
+      dzs[0][wave * DZS + HD + lane * PER + e] = (bf16)v1;
+      if constexpr (SP) {
+        dzs[SP ? 1 : 0][wave * DZS + lane * PER + e] = sp_lo(v0);
+        dzs[SP ? 1 : 0][wave * DZS + HD + lane * PER + e] = sp_lo(v1);
+      }
+    }
+  }
   // ---- loss: wave partial (lane 0) -> workgroup partial -> last arriver, fixed order
   if (lane == 0) red[wave] = lsum;
   __syncthreads();
+  if (args.w1t) {
+    const int r16 = lane & 15, kq = 8 * (lane >> 4);
+    const bf16* bt = args.w1t + (size_t)(wave * 16 + r16) * KD + kq;
+    const bf16* btl = SP ? args.w1t_lo + (size_t)(wave * 16 + r16) * KD + kq : nullptr;
+    constexpr int KS = KD / 32, D = 4;
+    bf16x8 rb[D], rbl[D];
+#pragma unroll
+    for (int s = 0; s < D; ++s) {
+      rb[s] = *(const bf16x8*)(bt + 32 * s);
+      if constexpr (SP) rbl[s] = *(const bf16x8*)(btl + 32 * s);
+    }
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const bf16x8 b0 = rb[s % D];
+      bf16x8 b1;
+      if constexpr (SP) b1 = rbl[s % D];
+      if (s + D < KS) {
+        rb[s % D] = *(const bf16x8*)(bt + 32 * (s + D));
+        if constexpr (SP) rbl[s % D] = *(const bf16x8*)(btl + 32 * (s + D));
+      }
+      const bf16x8 a0 = *(const bf16x8*)(&dzs[0][r16 * DZS + 32 * s + kq]);
+      if constexpr (SP) {
+        const bf16x8 a1 = *(const bf16x8*)(&dzs[SP ? 1 : 0][r16 * DZS + 32 * s + kq]);
+        acc = mfma16_x3(a0, a1, b0, b1, acc);
+      } else {
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc, 0, 0, 0);
+      }
+    }
+    // acc[e] = dh[row 4(lane>>4)+e of the workgroup][column 16 wave + (lane & 15)]
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int ri = blockIdx.x * NW + 4 * (lane >> 4) + e;
+      if (ri < n) args.dh[(size_t)ri * 256 + wave * 16 + r16] = acc[e];
+    }
+  }
   if (tid == 0) {
     float v = 0.f;
 #pragma unroll
@@ -364,6 +426,13 @@ static int td_duel_launch(const TdDuelArgs& d, int HD, int grid, hipStream_t s) 
   return 0;
 }
 
+extern "C" int r2_td_duel_dh(const float*, const float*, const float*, const int*, const float*,
+                             const uint8_t*, const float*, const uint8_t*, float*, float*, float*,
+                             float*, float*, const int*, int, int, int, int, int, float, int, float,
+                             float, float, float, float*, unsigned*, const void*, const float*,
+                             bf16*, float*, int, bf16*, const float*, const bf16*, const bf16*,
+                             float*, int, void*);
+
 // zr: bf16 (dz_lo null) or fp32 (split precision: dz_lo = the lo plane of dz)
 extern "C" int r2_td_duel(const float* q_sa, const float* q_arg, const float* q_tgt,
                           const int* starts, const float* probs, const uint8_t* action,
@@ -374,14 +443,33 @@ extern "C" int r2_td_duel(const float* q_sa, const float* q_arg, const float* q_
                           float beta, float* part, unsigned* ticket, const void* zr,
                           const float* w2, bf16* dz, float* dva, int HD, bf16* dz_lo,
                           const float* dp, void* stream) {
+  return r2_td_duel_dh(q_sa, q_arg, q_tgt, starts, probs, action, reward, done, dq, loss, td_abs,
+                       priority, is_w, n_valid, Tl, B, A, burn_in, cap_e, gamma_n, value_rescale,
+                       vr_eps, alpha, prio_eps, beta, part, ticket, zr, w2, dz, dva, HD, dz_lo, dp,
+                       nullptr, nullptr, nullptr, 0, stream);
+}
+
+// + the fused head backward to the LSTM output: dh (Tl*B, H) = dz @ W1 from W1^T (H, 2HD) (and its
+// lo plane in split precision).  H must be 256 (16 waves x 16 columns); w1t = null: not fused.
+extern "C" int r2_td_duel_dh(const float* q_sa, const float* q_arg, const float* q_tgt,
+                             const int* starts, const float* probs, const uint8_t* action,
+                             const float* reward, const uint8_t* done, float* dq, float* loss,
+                             float* td_abs, float* priority, float* is_w, const int* n_valid,
+                             int Tl, int B, int A, int burn_in, int cap_e, float gamma_n,
+                             int value_rescale, float vr_eps, float alpha, float prio_eps,
+                             float beta, float* part, unsigned* ticket, const void* zr,
+                             const float* w2, bf16* dz, float* dva, int HD, bf16* dz_lo,
+                             const float* dp, const bf16* w1t, const bf16* w1t_lo, float* dh, int H,
+                             void* stream) {
   if (B > 256) return -1;
   if (A < 1 || A > 64) return -3;             // one lane per action
   const int grid = (Tl * B + 15) / 16;
   if (grid > 4096) return -2;   // part[] holds one float per workgroup (engine: 4096)
+  if (w1t && (H != 256 || !dh || (dz_lo && !w1t_lo) || (2 * HD) % 32)) return -5;
   TdDuelArgs d{{q_sa, q_arg, q_tgt, starts, probs, action, reward, done, dq, loss, td_abs, priority,
                 is_w, n_valid, part, ticket, Tl, B, A, burn_in, cap_e, gamma_n, vr_eps, alpha,
                 prio_eps, beta, value_rescale, dp},
-               zr, w2, dz, dva, dz_lo};
+               zr, w2, dz, dva, dz_lo, w1t, w1t_lo, dh};
   hipStream_t s = (hipStream_t)stream;
   return dz_lo ? td_duel_launch<true>(d, HD, grid, s) : td_duel_launch<false>(d, HD, grid, s);
 }

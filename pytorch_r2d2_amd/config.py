@@ -112,6 +112,9 @@ class LearnerConfig:
     # ~15 us and a chunk's x-projection GEMM is tile-latency bound; profiles/r01_v9_pipelined.txt)
     fwd_chunks: int = 0
     td_fuse_head_bwd: bool = True     # dueling-head backward inside the TD launch (td_duel_kernel)
+    # ... and the head's input gradient dh = dz @ W1 on that launch's MFMAs (hidden 256): no
+    # separate dh GEMM (hipBLASLt 7-10 us in bf16, 22 us split-precision)
+    td_fuse_dh: bool = True
     dh_gemm: str = "blaslt"           # head backward dh = dz @ W1: blaslt (hipBLASLt) | mfma
     # split precision (compute_dtype fp32) GEMMs: "fused" = gemm_sp.hip (hi / lo planes staged
     # once, 3 MFMAs per fragment pair: x-projection 164 -> 125 us, post-BPTT group 142 -> 106 us

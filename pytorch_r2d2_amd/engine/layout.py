@@ -203,6 +203,10 @@ class ParamLayout:
         whhT = off("lstm.weight_hh") + permr[:, None, :] * H + np.arange(H)[None, :, None]
         add_bf("w_hhT", whhT, (nwg, H, 64))
         add_bf("head1", off("val.0.weight") + np.arange(2 * HD * H), (2 * HD, H))
+        # W1^T (H, 2HD), k contiguous: B operand of the dh = dz @ W1 product fused into the TD
+        # launch (td.hip r2_td_duel_dh)
+        hh, kk = np.meshgrid(np.arange(H), np.arange(2 * HD), indexing="ij")
+        add_bf("head1T", off("val.0.weight") + kk * H + hh, (H, 2 * HD))
         self.bf_numel = cur
         self.bf_index = torch.from_numpy(np.concatenate(bf).astype(np.int32))
 

@@ -180,6 +180,7 @@ class LearnerEngine:
         # data-parallel global prioritized sampling (parallel/sharded_replay.py)
         self.dp_global = bool(world > 1 and process_group is not None and cfg.dist.global_sampling)
         self._duel_done = False       # the TD launch also ran the dueling-head backward
+        self._dh_done = False         # ... and the dh = dz @ W1 product (learner.td_fuse_dh)
         self.graph = None
         self.stats: Dict[str, float] = {}
         self._alloc()
@@ -691,11 +692,18 @@ class LearnerEngine:
         # TD + the dueling head's backward in one launch (td.hip td_duel_kernel): dz / dva of the
         # online learning rows are written right where dL/dQ is known
         self._duel_done = False
+        self._dh_done = False
         if lc.td_fuse_head_bwd:
-            rc_ = k.r2_td_duel(*targs, ptr(self.zr_on[: Ll * B]), ptr(pk["head_w2"]), ptr(self.dz),
-                               ptr(self.dva), L.HD, ptr(self.dz_lo), dp, s)
+            # + dh = dz @ W1 for the BPTT, on the same launch's MFMAs (16 rows per workgroup)
+            fuse_dh = lc.td_fuse_dh and L.H == 256 and self.use_gemm
+            w1t = ptr(pk["head1T"]) if fuse_dh else 0
+            w1t_lo = ptr(self.pk_lo["head1T"]) if fuse_dh and self.sp else 0
+            rc_ = k.r2_td_duel_dh(*targs, ptr(self.zr_on[: Ll * B]), ptr(pk["head_w2"]), ptr(self.dz),
+                                  ptr(self.dva), L.HD, ptr(self.dz_lo), dp, w1t, w1t_lo,
+                                  ptr(self.dh) if fuse_dh else 0, L.H, s)
             if rc_ == 0:
                 self._duel_done = True
+                self._dh_done = fuse_dh
                 return
             if self.sp:
                 check(rc_, "td_duel")
@@ -724,7 +732,8 @@ class LearnerEngine:
         if not side_hg:
             check(k.r2_head_grads_sp(*hg, s), "head_grads_sp")
         dh = self.dh
-        self._gemm_sp("dh", [Gemm(self.dz, pk["head1"], dh, a_lo=self.dz_lo, b_lo=pkl["head1"])])
+        if not self._dh_done:   # else produced by the TD launch
+            self._gemm_sp("dh", [Gemm(self.dz, pk["head1"], dh, a_lo=self.dz_lo, b_lo=pkl["head1"])])
         bptt = [ptr(dh), ptr(self.gates), ptr(self.cseq["on"]), ptr(self.c0["on"]), ptr(pk["w_hhT"]),
                 ptr(pkl["w_hhT"]), ptr(self.dgates), ptr(self.dgates_lo), B, T, Lb, H, ptr(self.ctr),
                 ptr(self.err), ptr(self.ring_b), ptr(self.bias_ws), ptr(self.gate_perm_i32),
@@ -835,8 +844,11 @@ class LearnerEngine:
         if self.use_gemm:
             dh = self.dh
             # a plain 40-tile GEMM (M=2560, N=256, K=512): hipBLASLt runs it in 7.4 us vs 13.1
-            # for the 128x128 MFMA kernel and 18-45 us split-K (tools/dh_split_probe.py)
-            if lc.dh_gemm == "blaslt":
+            # for the 128x128 MFMA kernel and 18-45 us split-K (tools/dh_split_probe.py); by
+            # default it is fused into the TD launch instead (learner.td_fuse_dh)
+            if getattr(self, "_dh_done", False):
+                pass
+            elif lc.dh_gemm == "blaslt":
                 torch.mm(self.dz, pk["head1"], out_dtype=torch.float32, out=dh)   # (N, H) fp32
             else:
                 gemm(Gemm(self.dz, pk["head1"], dh))

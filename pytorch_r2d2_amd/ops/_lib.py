@@ -45,6 +45,8 @@ _SIGS = {
                    P],
     "r2_td_duel": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, F, F, F, F, P, P,
                    P, P, P, P, I, P, P, P],
+    "r2_td_duel_dh": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, I, F, F, F, F, P, P,
+                      P, P, P, P, I, P, P, P, P, P, I, P],
     "r2_dueling_fwd_multi_f32": [P, I, I, I, P],
     "r2_lstm_fwd_tag_sp": [P, I, I, I, I, P, P, P, P],
     "r2_lstm_bwd_tag_sp": [P, P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P, P, P],

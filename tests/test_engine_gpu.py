@@ -245,3 +245,15 @@ def test_engine_bf16_seaquest_18_actions_fused_path():
     for name, p in online.named_parameters():
         r = _rel(got[name], p.grad)
         assert r < 8e-2, f"{name}: rel err {r}"
+
+
+def test_td_fused_dh_matches_gemm():
+    """td.hip r2_td_duel_dh: dh = dz @ W1 on the TD launch's MFMAs (16 rows per workgroup, W1^T
+    from the packed head1T layout) vs the same product from the engine's dz in float64."""
+    cfg, rp, eng, net, tgt = _make("shifted", B=16)
+    eng._forward_loss()
+    torch.cuda.synchronize()
+    assert eng._dh_done
+    N = eng.Ll * eng.B
+    ref = eng.dz[:N].double() @ eng.pk["head1"].double()
+    assert _rel(eng.dh[:N], ref) < 1e-5

@@ -276,3 +276,16 @@ def test_torso_fwd_sp_v2_bit_identical_to_v1():
         assert not (a == 7.0).any()
         if sa1 is not None:
             assert torch.equal(sa1, sb1) and torch.equal(sa2, sb2)
+
+
+def test_td_fused_dh_matches_fp64_split():
+    """Split precision: the fused dh (3 MFMA passes over dz / W1^T hi-lo planes) vs float64 of the
+    same split operands: fp32-accurate."""
+    cfg, rp, eng, net, tgt = _make("fixed")
+    eng._forward_loss()
+    torch.cuda.synchronize()
+    assert eng._dh_done
+    N = eng.Ll * eng.B
+    dz = eng.dz[:N].double() + eng.dz_lo[:N].double()
+    w1 = eng.pk["head1"].double() + eng.pk_lo["head1"].double()
+    assert _rel(eng.dh[:N], dz @ w1) < 2e-5
