@@ -93,6 +93,7 @@ struct G5Args {
   long long slab_base[gm::MAXP];   // first partial slab (BM x BN fp32) of each problem
   int ticket_base[gm::MAXP];
   int np, total;
+  int dbg;   // probe (r2_gemm5_set_mode bits 4-5): 1 = operand staging only, 2 = no staging
   float* ws;
   unsigned* tickets;
 };
@@ -102,12 +103,13 @@ struct G5Args {
 template <bool AK, bool BKM, int BM, int BN, int BK, int NS, bool IL>
 __device__ __forceinline__ void g5_mainloop(const GemmProb& P, int m0, int n0, int kt0, int kt1,
                                             uint8_t* lds, int wave, int lane,
-                                            f32x4 (&acc)[BM / 32][BN / 64]) {
+                                            f32x4 (&acc)[BM / 32][BN / 64], int dbg = 0) {
   constexpr int FM = BM / 32, FN = BN / 64;
   constexpr int OPA = BM * BK * 2, OPB = BN * BK * 2, STB = 2 * (OPA + OPB);
   constexpr int NDMA = 2 * (BM + BN) * BK * 2 / (512 * 16);   // DMA instructions per thread per tile
   const int wr = wave >> 2, wc = wave & 3;
   auto stage = [&](int kt) {
+    if (dbg & 2) return;
     int oz;
     asm volatile("v_mov_b32 %0, 0" : "=v"(oz));
     uint8_t* st = lds + ((kt - kt0) % NS) * STB;
@@ -128,6 +130,7 @@ __device__ __forceinline__ void g5_mainloop(const GemmProb& P, int m0, int n0, i
     else g5_vmwait<0>();
     __builtin_amdgcn_s_barrier();     // tile kt visible; everyone finished reading tile kt-1
     if (kt + NS - 1 < kt1) stage(kt + NS - 1);
+    if (dbg & 1) continue;
     const uint8_t* ah = lds + ((kt - kt0) % NS) * STB;
     const uint8_t* al = ah + OPA;
     const uint8_t* bh = ah + 2 * OPA;
@@ -283,10 +286,10 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const G5Args a) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   if constexpr (BM % 128 == 0) {
-    if (P.a_kmajor) g5_mainloop<true, BKM, BM, BN, BK, NS, IL>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc);
-    else g5_mainloop<false, BKM, BM, BN, BK, NS, IL>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc);
+    if (P.a_kmajor) g5_mainloop<true, BKM, BM, BN, BK, NS, IL>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc, a.dbg);
+    else g5_mainloop<false, BKM, BM, BN, BK, NS, IL>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc, a.dbg);
   } else {
-    g5_mainloop<true, BKM, BM, BN, BK, NS, IL>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc);
+    g5_mainloop<true, BKM, BM, BN, BK, NS, IL>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc, a.dbg);
   }
 
   // ---- epilogue: 64 rows at a time through LDS (row-contiguous, 4 columns per thread)
@@ -366,7 +369,12 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const G5Args a) {
 }
 
 static int g5_il = 1;   // interleaved fragment loads (r2_gemm5_set_mode)
-extern "C" int r2_gemm5_set_mode(int il) { g5_il = il; return 0; }
+static int g5_dbg = 0;  // probe bits (G5Args::dbg)
+extern "C" int r2_gemm5_set_mode(int m) {
+  g5_il = m & 1;
+  g5_dbg = (m >> 4) & 3;
+  return 0;
+}
 
 template <bool BKM, int BM, int BN, int BK, int NS, bool IL>
 static void g5_kernel_launch_il(const G5Args& a, hipStream_t s) {
@@ -404,7 +412,7 @@ extern "C" int r2_gemm5(const int64_t* descs, const int* split, int np, int cfg,
                         long long ws_bytes, unsigned* tickets, int n_tickets, int n_cus, void* stream) {
   if (np < 1 || np > gm::MAXP) return -1;
   G5Args a;
-  a.np = np; a.ws = ws; a.tickets = tickets;
+  a.np = np; a.ws = ws; a.tickets = tickets; a.dbg = g5_dbg;
   int bkm = -1;
   bool all_k = true;
   for (int i = 0; i < np; ++i) {

@@ -97,7 +97,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t pl_rsrc(const void* p, uint32_
 // dispatcher's round-robin placement); otherwise linear (g = b / nwg, j = b % nwg).
 __device__ __forceinline__ bool pl_decode(int xcd_map, int groups, int nwg, int& g, int& j) {
   const int b = blockIdx.x;
-  if (xcd_map) { g = b & 7; j = b >> 3; }
+  if (xcd_map == 2) {   // two groups per XCD: blocks b = 8 l + x, group x + 8 (l / nwg)
+    const int l = b >> 3;
+    g = (b & 7) + 8 * (l / nwg);
+    j = l % nwg;
+  } else if (xcd_map) { g = b & 7; j = b >> 3; }
   else { g = b / nwg; j = b % nwg; }
   return g < groups && j < nwg;
 }
@@ -505,8 +509,14 @@ extern "C" int r2_get_num_cus() { return g_num_cus; }
 static long long* g_pl_dbg = nullptr;
 static int g_pl_slow = 0;
 extern "C" int r2_lstm_persist_set_debug(long long* p) { g_pl_dbg = p; return 0; }
-// testing / diagnostics: 1 = always use the placement-independent sc1 protocol
-extern "C" int r2_lstm_persist_force_slow(int v) { g_pl_slow = v; return 0; }
+static int g_pl_nomap2 = 0;
+// testing / diagnostics: bit 0 = always use the placement-independent sc1 protocol; bit 1 = no
+// two-groups-per-XCD placement in the tagged forward (groups 9..16 spread over every XCD)
+extern "C" int r2_lstm_persist_force_slow(int v) {
+  g_pl_slow = v & 1;
+  g_pl_nomap2 = (v >> 1) & 1;
+  return 0;
+}
 
 // chain_ptrs: n_chains x 9 int64 (same layout as r2_lstm_fwd).  ctr: >= PL_CTR_WORDS (1024) unsigned,
 // err: 1 unsigned.  Both are zeroed here with memset nodes (graph-capturable).
@@ -959,10 +969,16 @@ static int lstm_fwd_tag_launch(const int64_t* chain_ptrs, int words, int n_chain
     if (SP && (!ch.whh_lo || !ch.h_seq_lo)) return -5;
   }
   args.B = B; args.T = T; args.ctr = ctr; args.err = err; args.dbg = g_pl_dbg; args.ring = ring;
-  args.MB = MB; args.groups = groups; args.xcd_map = groups <= 8 && nwg <= 32;
+  // group -> XCD placement (workgroup b runs on XCD b % 8): one group per XCD up to 8 groups,
+  // two per XCD up to 16 (the fixed-target step's 3 chains x 4 batch tiles = 12 groups), so a
+  // group's h hand-off stays in one XCD's L2 (pl_same_xcd: plain stores, L2-hit polls) instead
+  // of crossing the fabric with write-through stores
+  args.MB = MB; args.groups = groups;
+  args.xcd_map = groups <= 8 && nwg <= 32 ? 1 : (groups <= 16 && nwg <= 16 && !g_pl_nomap2 ? 2 : 0);
   args.force_slow = g_pl_slow;
   hipStream_t s = (hipStream_t)stream;   // counters are left zeroed by the previous launch
-  dim3 grid(args.xcd_map ? 8 * nwg : groups * nwg), block(320);   // 4 compute waves + 1 I/O wave
+  const int nblk = args.xcd_map == 1 ? 8 * nwg : args.xcd_map == 2 ? 16 * nwg : groups * nwg;
+  dim3 grid(nblk), block(320);   // 4 compute waves + 1 I/O wave
   const void* fn = H == 64 ? (const void*)lstm_fwd_tag_kernel<64, SP>
                  : H == 128 ? (const void*)lstm_fwd_tag_kernel<128, SP>
                  : H == 256 ? (const void*)lstm_fwd_tag_kernel<256, SP>

@@ -115,6 +115,10 @@ class LearnerConfig:
     # ... and the head's input gradient dh = dz @ W1 on that launch's MFMAs (hidden 256): no
     # separate dh GEMM (hipBLASLt 7-10 us in bf16, 22 us split-precision)
     td_fuse_dh: bool = True
+    # tagged LSTM forward with 9..16 groups (fixed target: 3 chains x 4 batch tiles) placed two
+    # groups per XCD, so every group's h hand-off stays in one XCD's L2 (else spread over all XCDs:
+    # write-through stores, fabric-latency polls)
+    lstm_xcd_pairs: bool = True
     dh_gemm: str = "blaslt"           # head backward dh = dz @ W1: blaslt (hipBLASLt) | mfma
     # split precision (compute_dtype fp32) GEMMs: "fused" = gemm_sp.hip (hi / lo planes staged
     # once, 3 MFMAs per fragment pair: x-projection 164 -> 125 us, post-BPTT group 142 -> 106 us

@@ -136,6 +136,7 @@ class LearnerEngine:
         self.n_cus = int(n_cus) if n_cus else device_cus(d)
         if d.type == "cuda":
             kernels().r2_set_num_cus(self.n_cus)
+            kernels().r2_lstm_persist_force_slow(0 if cfg.learner.lstm_xcd_pairs else 2)
         if init_module is None:
             torch.manual_seed(cfg.seed)
             init_module = QNet("cpu", m, e)

@@ -267,6 +267,59 @@ def test_lstm_tagged_repeated_launches_and_placement(B):
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
 
 
+def test_lstm_tagged_three_chains_two_groups_per_xcd():
+    """The fixed-target step's forward runs 3 chains x 4 batch tiles = 12 groups: placed two per
+    XCD (lstm_persist.hip pl_decode map 2) every group takes the same-XCD hand-off; results are
+    bit-identical to the spread placement and to the sc1 protocol, and match the counter kernel."""
+    B, H, G, T = 64, 256, 1024, 9
+    cfg, net, L, flat, pk = _setup(B, H, seed=5)
+    k = kernels()
+    nw = int(k.r2_lstm_persist_ctr_words())
+    ctr = torch.zeros(nw, dtype=torch.int32, device=DEV)
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+    ring = torch.zeros(k.r2_lstm_tag_ring_bytes(3, B, H) // 4, dtype=torch.int32, device=DEV)
+    xps = [torch.randn(T * B, G, device=DEV) for _ in range(3)]
+    h0s = [(torch.randn(B, H, device=DEV) * 0.3).bfloat16() for _ in range(3)]
+    c0s = [torch.randn(B, H, device=DEV) * 0.3 for _ in range(3)]
+    dbg = torch.zeros(1024, dtype=torch.int64, device=DEV)
+
+    def run(fn_name, mode):
+        k.r2_lstm_persist_force_slow(mode)
+        outs, words = [], []
+        for c in range(3):
+            hs = torch.zeros(T, B, H, dtype=torch.bfloat16, device=DEV)
+            cs = torch.zeros(T, B, H, device=DEV)
+            outs.append((hs, cs))
+            words += [ptr(xps[c]), ptr(pk["w_hh"]), ptr(h0s[c]), ptr(c0s[c]), ptr(hs), ptr(cs), 0, 0, 0]
+        arr = np.asarray(words, dtype=np.int64)
+        dbg.zero_()
+        k.r2_lstm_persist_set_debug(ptr(dbg) if fn_name == "tag" else 0)
+        if fn_name == "tag":
+            rc = k.r2_lstm_fwd_tag(arr.ctypes.data, 3, B, T, H, ptr(ctr), ptr(err), ptr(ring),
+                                   stream_handle())
+        else:
+            rc = k.r2_lstm_fwd_persist(arr.ctypes.data, 3, B, T, H, ptr(ctr), ptr(err),
+                                       stream_handle())
+        torch.cuda.synchronize()
+        k.r2_lstm_persist_set_debug(0)
+        k.r2_lstm_persist_force_slow(0)
+        assert rc == 0 and err.item() == 0
+        return outs, dbg[256:].cpu().clone()
+
+    mapped, d = run("tag", 0)
+    tags = [int(v) for v in d if v >= 1000]
+    assert len(tags) == 12 * (H // UNITS)                      # every recurrence workgroup
+    assert all(v % 10 == 1 for v in tags), "a group missed the same-XCD hand-off"
+    spread, _ = run("tag", 2)
+    sc1, _ = run("tag", 1)
+    ref, _ = run("persist", 0)
+    for c in range(3):
+        for x, y, z in zip(mapped[c], spread[c], sc1[c]):
+            assert torch.equal(x, y) and torch.equal(x, z), c
+        assert _rel(mapped[c][1], ref[c][1]) < 1e-4
+        assert _rel(mapped[c][0].float(), ref[c][0].float()) < 1e-2
+
+
 def test_torso_matches_conv_stack():
     cfg, net, L, flat, pk = _setup()
     n = 37
