@@ -315,9 +315,11 @@ constexpr int OFF_W2L = OFF_W2H + 32 * 520 * 2;            // 125664
 constexpr int OFF_B = OFF_W2L + 32 * 520 * 2;              // 158944: biases conv2, conv3, conv1
 constexpr int OFF_W3T = OFF_B + 96 * 4;                    // 159328: W3[:, 256:288] hi, lo
 constexpr int LDS_BYTES = OFF_W3T + 2 * 32 * 32 * 2;       // 163424
+constexpr int OFF_SC = LDS_BYTES;                          // int8 conv1: row corrections [2][32] int32
+constexpr int LDS_BYTES_I8 = OFF_SC + 2 * 32 * 4;          // 163680
 constexpr int IN_CHUNKS2 = 4 * 84 * 84 / 16;               // 1764
 constexpr int PF = (IN_CHUNKS2 + 319) / 320;               // 6 chunks per prefetch thread
-static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+static_assert(LDS_BYTES <= 160 * 1024 && LDS_BYTES_I8 <= 160 * 1024, "LDS");
 }  // namespace tsp2
 
 // act1 image: pixel P, 16-byte chunk c (channels 8c .. 8c+7) -> byte offset in one plane
@@ -325,9 +327,95 @@ __device__ __forceinline__ int a1_off(int P, int c) {
   return ((P >> 2) << 8) + (((((P & 3) << 2) | c) ^ ((P >> 2) & 15)) << 4);
 }
 
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+typedef short s16x4_t __attribute__((ext_vector_type(4)));
+
+// conv1 on the int8 matrix cores (the default v2 path).  The uint8 frame is exact as int8 after a
+// -128 shift (one XOR per 4 bytes; the conversion to bf16 cost ~12 VALU per 8 bytes and made the
+// conv1 phase issue-bound), and W1 (= hi + lo, the split pair the bf16 path multiplies) becomes
+// three int8 digits under ONE scale s = max|W1| / 127:  W1 ~= s (d0 + d1 / 128 + d2 / 16384),
+// |error| <= s / 32768 (2.4e-7 max|W1|, below the split pair's own rounding).  Products and sums
+// are exact in int32 (|sum| <= 256 * 127 * 255); the shift comes back exactly through the per-row
+// digit sums (x 128), so the only rounding is the final fp32 combine.  v_mfma_i32_16x16x64_i8
+// takes the cycles of the bf16 16x16x32 form at twice the K: 3 digit products per 64 K vs the
+// bf16 path's 2 (hi, lo) per 32 K -- 25 % fewer MFMA cycles and no conversion VALU.
+//
+// Once per workgroup, all 512 threads: 16 weights each (row t / 16, K 16 (t % 16) ..) -> digit
+// images dig[d][32][256] int8 in LDS (the act1 region, free until the first conv1), per-row
+// corrections 128 S0, 128 (128 S1 + S2) of the digit row sums S_d -> sc[2][32] (int32), block max
+// through red[8].  Returns s / 255 (the
+// epilogue's scale).  The caller synchronises, then c1_frags() loads each conv1 lane's fragments.
+__device__ __forceinline__ float c1_digits(const bf16* w1, const bf16* w1l, int tid, uint8_t* dig,
+                                           int* sc, float* red) {
+  const int lane = tid & 63, wave = tid >> 6;
+  const bf16x8 h0 = *(const bf16x8*)(w1 + tid * 16), h1 = *(const bf16x8*)(w1 + tid * 16 + 8);
+  const bf16x8 l0 = *(const bf16x8*)(w1l + tid * 16), l1 = *(const bf16x8*)(w1l + tid * 16 + 8);
+  float w[16];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    w[e] = (float)h0[e] + (float)l0[e];
+    w[8 + e] = (float)h1[e] + (float)l1[e];
+  }
+  float m = 0.f;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) m = fmaxf(m, fabsf(w[e]));
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if (lane == 0) red[wave] = m;
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) m = fmaxf(m, red[i]);
+  const float inv = m > 0.f ? 127.f / m : 0.f;
+  uint32_t pk[3][4] = {};
+  int sum[3] = {0, 0, 0};
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const float q = w[e] * inv;
+    const float d0 = rintf(q), r1 = (q - d0) * 128.f;
+    const float d1 = rintf(r1), d2 = rintf((r1 - d1) * 128.f);
+    const int dd[3] = {(int)d0, (int)d1, (int)d2};
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      sum[d] += dd[d];
+      pk[d][e >> 2] |= ((uint32_t)dd[d] & 0xffu) << (8 * (e & 3));
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    *(u32x4*)(dig + d * 8192 + tid * 16) = u32x4{pk[d][0], pk[d][1], pk[d][2], pk[d][3]};
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) sum[d] += __shfl_xor(sum[d], o, 64);
+  }
+  if ((tid & 15) == 0) {   // row corrections: 128 S0 and 128 (128 S1 + S2) (|.| < 2^29)
+    sc[tid >> 4] = 128 * sum[0];
+    sc[32 + (tid >> 4)] = 128 * (128 * sum[1] + sum[2]);
+  }
+  return m * (1.f / 127.f) * (1.f / 255.f);
+}
+
+// conv1 lane (row l16, k group g): rows 16c + l16 (c = 0, 1), K steps s = 4 KB + g (KB 0..3), 16 K
+// values each (K = 16 s + 4 dy + dx, the bf16 path's order); digit fragment (c, KB, d) -> slot
+// 12 c + 3 KB + d of wfh[0..15] ++ wfl[0..7]
+__device__ __forceinline__ void c1_frags(const uint8_t* dig, int lane, bf16x8 (&wfh)[16],
+                                         bf16x8 (&wfl)[16]) {
+  const int l16 = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const int slot = 12 * c + 3 * kb + d;
+        const bf16x8 v = *(const bf16x8*)(dig + d * 8192 + (16 * c + l16) * 256 + (4 * kb + g) * 16);
+        if (slot < 16) wfh[slot & 15] = v;
+        else wfl[(slot - 16) & 15] = v;
+      }
+}
+
 __constant__ int c_s2_begin[8] = {0, 2, 4, 4, 6, 8, 10, 11};
 __constant__ int c_s2_count[8] = {2, 2, 0, 2, 2, 2, 1, 2};
 
+template <bool I8>
 __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
   using namespace tsp2;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -355,6 +443,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
   if (f >= n_frames) return;
   const bool conv3_wave = wave == 2, conv2_wave = wave < 3, pf_wave = wave >= 3;
   const int t5 = tid - 192;   // prefetch thread index (waves 3..7)
+  const int t7 = tid < 128 ? tid : tid - 64;   // int8 path: prefetch thread index (waves != 2)
 
   // ---- once: W2 hi / lo -> LDS; W1 (conv1 waves) or W3 (wave 2) fragments -> registers; biases;
   //      the first frame -> LDS
@@ -364,12 +453,21 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
     *(bf16x8*)(w2l + r * 520 + c * 8) = *(const bf16x8*)(J.w2l + r * 512 + c * 8);
   }
   bf16x8 wfh[16], wfl[16];
+  float c1_scale = 0.f;
+  if (I8) {   // int8 digits of W1 -> LDS (act1 region) -> conv1 lanes' fragments
+    c1_scale = c1_digits(J.w1, J.w1l, tid, a1h, (int*)(lds + OFF_SC), (float*)(a1h + 3 * 8192));
+    c1_scale = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(c1_scale)));   // SGPR
+    __syncthreads();
+    if (!conv3_wave) c1_frags(a1h, lane, wfh, wfl);
+  }
+  if (!I8 || conv3_wave) {
 #pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    const bf16* ph = conv3_wave ? J.w3 + l32 * 288 + s * 16 + half * 8 : J.w1 + l32 * 256 + s * 16 + half * 8;
-    const bf16* pl = conv3_wave ? J.w3l + l32 * 288 + s * 16 + half * 8 : J.w1l + l32 * 256 + s * 16 + half * 8;
-    wfh[s] = *(const bf16x8*)ph;
-    wfl[s] = *(const bf16x8*)pl;
+    for (int s = 0; s < 16; ++s) {
+      const bf16* ph = conv3_wave ? J.w3 + l32 * 288 + s * 16 + half * 8 : J.w1 + l32 * 256 + s * 16 + half * 8;
+      const bf16* pl = conv3_wave ? J.w3l + l32 * 288 + s * 16 + half * 8 : J.w1l + l32 * 256 + s * 16 + half * 8;
+      wfh[s] = *(const bf16x8*)ph;
+      wfl[s] = *(const bf16x8*)pl;
+    }
   }
   if (tid < 96) lb[tid] = tid < 32 ? J.b2[tid] : tid < 64 ? J.b3[tid - 32] : J.b1[tid - 64];
   if (tid < 256) {   // W3 K columns 256..287, hi then lo: [32 rows][32] bf16 each
@@ -407,11 +505,78 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
       const u32x4* src = (const u32x4*)(args.frames + (size_t)row_nx * IN_BYTES);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int c = tid + NT * q;
-        if (c < IN_CHUNKS2) pf[q] = src[c];
+        const int c = I8 ? t7 + 448 * q : tid + NT * q;
+        if (c < IN_CHUNKS2 && (!I8 || !conv3_wave)) {
+          // int8 path: the 7 conv1 waves prefetch (4 chunks per thread) and park the chunks in
+          // wfl[8..11], which only the conv3 wave uses (W3 K steps 8..11 lo); the conv1 digits
+          // fill slots 0..23
+          if (I8) wfl[8 + q] = __builtin_bit_cast(bf16x8, src[c]);
+          else pf[q] = src[c];
+        }
       }
     }
-    if (have && !(args.dbg & 1)) {
+    if (I8 && have && !(args.dbg & 1)) {
+      // conv1(f) on the int8 matrix cores (c1_digits): per 16-pixel half tile, the 4 K blocks'
+      // frame bytes (4 rows x 4 bytes per lane, -128 by XOR), 3 digits x 2 channel halves of
+      // v_mfma_i32_16x16x64_i8, exact int32 sums
+      const int l16 = lane & 15, gq = lane >> 4;
+      const int* sct = (const int*)(lds + OFF_SC);
+      for (int i = 0; i < t1n; ++i) {
+        // both 16-pixel halves of the tile: half 1's frame bytes load under half 0's MFMAs
+        i32x4_t bx[1][4];
+        auto ldb = [&](int q, i32x4_t (&x)[4]) {
+          const int pc = min((t1b + i) * 32 + 16 * q + l16, P1 - 1);
+          const int oy = pc / 20, ox = pc % 20;
+          const uint8_t* fb = fr + gq * 7056 + 4 * oy * 84 + 4 * ox + oz;
+#pragma unroll
+          for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+            for (int dy = 0; dy < 4; ++dy)
+              x[kb][dy] = (int)(*(const uint32_t*)(fb + (kb >> 1) * 336 + (kb & 1) * 4 + dy * 84) ^ 0x80808080u);
+        };
+#pragma unroll 1
+        for (int q = 0; q < 2; ++q) {
+          ldb(q, bx[0]);
+          const int p = (t1b + i) * 32 + 16 * q + l16;
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {   // channel halves one after the other (12 acc VGPRs)
+            i32x4_t acc[3];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) acc[d] = i32x4_t{0, 0, 0, 0};
+#pragma unroll
+            for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+              for (int d = 0; d < 3; ++d) {
+                const int slot = 12 * c + 3 * kb + d;
+                const i32x4_t a = __builtin_bit_cast(i32x4_t, slot < 16 ? wfh[slot & 15] : wfl[(slot - 16) & 15]);
+                acc[d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bx[0][kb], acc[d], 0, 0, 0);
+              }
+            if (p < P1) {
+              // rows (channels) 16c + 4 gq + e of pixel p.  Digits 1, 2 merge exactly in int32
+              // (|128 i1 + i2| < 2^30); the tables add 128 x the digit row sums (the -128 shift):
+              // sum d (v - 128) + 128 sum d = sum d v
+              const int ch0 = 16 * c + 4 * gq;
+              const i32x4_t k0 = *(const i32x4_t*)(sct + ch0);
+              const i32x4_t k12 = *(const i32x4_t*)(sct + 32 + ch0);
+              bf16x4 vh, vl;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int i0 = acc[0][e] + k0[e];
+                const int i12 = acc[1][e] * 128 + acc[2][e] + k12[e];
+                const float t = fmaf((float)i12, 1.f / 16384.f, (float)i0);
+                const float v = fmaxf(fmaf(t, c1_scale, lb[64 + ch0 + e]), 0.f);
+                vh[e] = (bf16)v;
+                vl[e] = sp_lo(v);
+              }
+              const int o = a1_off(p, 2 * c + (gq >> 1)) + 8 * (gq & 1);
+              *(bf16x4*)(a1h + o) = vh;
+              *(bf16x4*)(a1l + o) = vl;
+            }
+          }
+        }
+      }
+    }
+    if (!I8 && have && !(args.dbg & 1)) {
       for (int i = 0; i < t1n; ++i) {
         const int p = (t1b + i) * 32 + l32;
         const int pc = p < P1 ? p : P1 - 1;
@@ -513,8 +678,9 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
     if (fn < n_frames && !(args.dbg & 16)) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int c = tid + NT * q;
-        if (c < IN_CHUNKS2) ((u32x4*)fr)[c] = pf[q];
+        const int c = I8 ? t7 + 448 * q : tid + NT * q;
+        if (c < IN_CHUNKS2 && (!I8 || !conv3_wave))
+          ((u32x4*)fr)[c] = I8 ? __builtin_bit_cast(u32x4, wfl[8 + q]) : pf[q];
       }
     }
     if (conv2_wave) {
@@ -598,7 +764,7 @@ static long long* g_tsp_trace = nullptr;
 // phase B done, barrier), s_memrealtime-free cycle counter
 extern "C" int r2_torso_sp_trace(long long* p) { g_tsp_trace = p; return 0; }
 // timing probes only (tools/sp_micro.py): bit 0 skips conv1, bit 1 conv2, bit 2 conv3;
-// bit 3 runs the v1 kernel
+// bit 3 runs the v1 kernel; bit 7 runs v2 with the bf16 split conv1 (else int8 digits)
 extern "C" int r2_torso_sp_debug(int bits) { g_tsp_dbg = bits; return 0; }
 
 extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs, int njobs,
@@ -649,12 +815,18 @@ extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs,
   } else {
     static bool attr2 = false;
     if (!attr2) {
-      hipFuncSetAttribute((const void*)torso_fwd_sp2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          tsp2::LDS_BYTES);
+      hipFuncSetAttribute((const void*)torso_fwd_sp2_kernel<false>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, tsp2::LDS_BYTES);
+      hipFuncSetAttribute((const void*)torso_fwd_sp2_kernel<true>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, tsp2::LDS_BYTES_I8);
       attr2 = true;
     }
-    hipLaunchKernelGGL(torso_fwd_sp2_kernel, dim3(grid), dim3(tsp::NT), tsp2::LDS_BYTES,
-                       (hipStream_t)stream, a);
+    if (a.dbg & 128)   // bf16 split conv1 (the previous v2 path)
+      hipLaunchKernelGGL(torso_fwd_sp2_kernel<false>, dim3(grid), dim3(tsp::NT), tsp2::LDS_BYTES,
+                         (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL(torso_fwd_sp2_kernel<true>, dim3(grid), dim3(tsp::NT), tsp2::LDS_BYTES_I8,
+                         (hipStream_t)stream, a);
   }
   R2_CHECK_LAUNCH();
   return 0;

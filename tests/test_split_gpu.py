@@ -225,9 +225,11 @@ def test_engine_fp32_graph_step_and_seaquest_actions():
 
 
 def test_torso_fwd_sp_v2_bit_identical_to_v1():
-    """torso_fwd_sp2_kernel (frame in LDS, swizzled act1, conv3 on one wave) keeps v1's
-    accumulation order: every output and saved activation plane must match bit for bit, over 4
-    jobs with uneven frame counts (partial last rounds) and activation saves."""
+    """torso_fwd_sp2_kernel (frame in LDS, swizzled act1, conv3 on one wave) with its bf16-split
+    conv1 (debug bit 7) keeps v1's accumulation order: every output and saved activation plane
+    must match bit for bit, over 4 jobs with uneven frame counts (partial last rounds) and
+    activation saves.  The default int8-digit conv1 (exact integer sums of W1 = s (d0 + d1/128 +
+    d2/16384)) must agree with it to fp32 accuracy."""
     import numpy as np
     from pytorch_r2d2_amd.ops._lib import kernels, ptr, stream_handle
     k = kernels()
@@ -270,12 +272,15 @@ def test_torso_fwd_sp_v2_bit_identical_to_v1():
             k.r2_torso_sp_debug(0)
         return outs
 
-    v1, v2 = run(8), run(0)
-    for (a, sa1, sa2), (b, sb1, sb2) in zip(v1, v2):
+    v1, v2, v2i = run(8), run(128), run(0)
+    for (a, sa1, sa2), (b, sb1, sb2), (c, sc1, sc2) in zip(v1, v2, v2i):
         assert torch.equal(a, b)
-        assert not (a == 7.0).any()
+        assert not (a == 7.0).any() and not (c == 7.0).any()
+        both = lambda x: x[0].double() + x[1].double()   # noqa: E731
+        assert _rel(both(c), both(a)) < 5e-6
         if sa1 is not None:
             assert torch.equal(sa1, sb1) and torch.equal(sa2, sb2)
+            assert _rel(both(sc1), both(sa1)) < 5e-6 and _rel(both(sc2), both(sa2)) < 5e-6
 
 
 def test_td_fused_dh_matches_fp64_split():

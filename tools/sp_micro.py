@@ -80,7 +80,7 @@ if which in ("torso", "both"):
     if "probe" in sys.argv:
         # phase costs: skip conv1 / conv2 / conv3 (timing only) etc.; variants interleaved over 7
         # rounds, min of the per-round means (single back-to-back timings drift by +-15 %)
-        variants = ((0, "full"), (8, "v1"), (1, "no_conv1"), (2, "no_conv2"), (4, "no_conv3"),
+        variants = ((0, "full"), (128, "bf16_conv1"), (8, "v1"), (1, "no_conv1"), (2, "no_conv2"), (4, "no_conv3"),
                     (7, "none"), (16, "no_frame"), (64, "no_save"), (119, "nothing"))
         best = {}
         for _ in range(7):
