@@ -23,8 +23,11 @@
   optimizer, weight repack, priority write-back + sum-tree repair.
 * Multi-GPU (weak scaling): each rank runs the data-parallel learner on its own replay shard with
   the per-GPU batch fixed; one synchronous optimizer step per iteration over the global batch
-  (64 x N sequences).  ``value`` = optimizer steps/s of the whole job at that global batch;
-  ``sequences_per_sec`` is the aggregate sample throughput.
+  (64 x N sequences).  ``value`` is the WHOLE-JOB aggregate the driver's weak-scaling contract
+  asks for: learner steps/s counted in the BASELINE's unit of work (one B=64 x 80-step batch
+  trained), i.e. optimizer steps/s x N.  At N=1 it is exactly optimizer steps/s; at N>1 the JSON
+  also carries ``optimizer_steps_per_sec`` (synchronous updates/s at global batch 64 x N) and
+  ``sequences_per_sec`` so neither reading is hidden.
 * Timing: W untimed warmup steps, then exactly K steps bracketed by barrier + synchronize on
   both sides; the max over ranks is reported by rank 0 as one JSON line.  The persistent
   kernels' error word is read after the timed loop: a non-zero word fails the run (exit 3).
@@ -144,16 +147,17 @@ def main(argv=None):
     if rank == 0:
         out = {
             "metric": "learner_steps_per_sec",
-            "value": round(opt_steps, 3),
-            "unit": "optimizer steps/s of the whole job (global batch %d x %d-step sequences)"
-                    % (lc.batch_size * world, rc.seq_len),
+            "value": round(opt_steps * world, 3),
+            "unit": ("learner steps/s of the whole job, one step = a %d x %d-step sequence batch "
+                     "(= optimizer steps/s x %d ranks; global batch %d)"
+                     % (lc.batch_size, rc.seq_len, world, lc.batch_size * world)),
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 4),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(opt_steps / base, 3) if base else None,
+            "vs_baseline": round(opt_steps * world / base, 3) if base else None,
             "dtype": lc.compute_dtype,
             "data": data_label(cfg),
             "config": {
