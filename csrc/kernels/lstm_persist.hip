@@ -640,18 +640,30 @@ __device__ __forceinline__ uint32_t pt_pack_bf16x2(float a, float b) {
   return __builtin_bit_cast(uint32_t, v);
 }
 
-// SP (split precision, split.h): h_t travels as {fp32 h[u], tag} granules (one unit each), the
-// consumer splits it into hi / lo LDS images, W_hh hi / lo fragments stay in VGPRs and every
-// product is 3 MFMA passes; h_seq is written as hi / lo planes.
-template <int H, bool SP>
+// SP (split precision, split.h): W_hh hi / lo fragments stay in VGPRs and every product is 3
+// MFMA passes; h_seq is written as hi / lo planes.  h_t travels one of two ways:
+//  * T4 (default): ONE 4-byte word per unit -- fp32 h rounded to 19 explicit mantissa bits with a
+//    4-bit tag in the low nibble, {epoch parity, (t + 1) mod 8}.  Every word is its own granule
+//    (a 4-byte store is single-copy atomic), so the consumer polls 16-B chunks of 4 units and
+//    checks 4 nibbles.  Half the bytes of the 8-byte form (16 KB per workgroup per step, what the
+//    bf16 kernel moves), and no accuracy lost: the consumer splits the rounded value into hi / lo
+//    exactly as before (hi + lo of the full fp32 value is itself only ~2^-17 accurate; the 2^-20
+//    rounding sits below it).  Why 4 bits suffice: a slot read at step t holds either step t-1
+//    (wanted), step t-3 of this launch ((t + 1) mod 8 differs by 2), or -- for t <= 2 only --
+//    the previous launch's step of the same parity, whose epoch parity differs because every
+//    launch of one launch SITE (fixed chain set, one ring, one ctr) advances the epoch by one.
+//    Requirement (the engine keeps it): a ring + ctr pair serves one launch site.
+//  * !T4 (r2_lstm_sp_handoff8(1), A/B probes): {fp32 h[u], 32-bit tag} 8-byte granules.
+template <int H, bool SP, bool T4 = false>
 __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
+  static_assert(!T4 || SP, "T4 is a split-precision hand-off");
   constexpr int G = 4 * H;
   constexpr int NWG = H / PL_UNITS;
   constexpr int KS = H / 32;                  // 16x16x32 k-steps
   constexpr int HS = H + 8;                   // bf16 stride of a staged h row (conflict-free b128)
   constexpr int UG = SP ? 1 : 2;              // hidden units per granule
   constexpr int GR = H / UG;                  // granules per row
-  constexpr int CPR = GR / 2;                 // 16-B chunks (2 granules) per row
+  constexpr int CPR = T4 ? H / 4 : GR / 2;    // 16-B chunks per row (4 units / 2 granules)
   constexpr int CH = PT_ROWS * CPR / 256;     // chunks per compute thread
   constexpr int XS = 20;                      // fp32 stride of a gate-exchange row
   static_assert(CH >= 1 && PT_ROWS * CPR % 256 == 0, "H");
@@ -760,6 +772,10 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
   auto goff = [&](int slot, int r, int p) -> uint32_t {
     return (uint32_t)((((size_t)(chn * 2 + slot) * rows_all + mb * PT_ROWS + r) * GR + p) * 8);
   };
+  // T4: byte offset of unit u's word (same ring, 4 B per unit)
+  auto woff = [&](int slot, int r, int u_) -> uint32_t {
+    return (uint32_t)((((size_t)(chn * 2 + slot) * rows_all + mb * PT_ROWS + r) * H + u_) * 4);
+  };
   // resident W_hh fragments: wave column c (0..15) = gate c>>2 of unit 4*wave + (c&3), i.e.
   // packed row 16*(c>>2) + 4*wave + (c&3) of this workgroup's 64
   bf16x8 wf[KS], wfl[SP ? KS : 1];
@@ -797,7 +813,12 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
       for (int i = 0; i < CH; ++i) {
         const int c = tid + 256 * i, r = c / CPR, cc = c % CPR;
         const int b = min(mb * PT_ROWS + r, B - 1);
-        if constexpr (SP) {   // fp32 h0, units 2cc, 2cc+1
+        if constexpr (T4) {   // fp32 h0, units 4cc .. 4cc+3 (the T4 chunk geometry)
+          const f32x4 x = *(const f32x4*)((const float*)cd.h0 + (size_t)b * H + 4 * cc);
+          *(u32x2*)(hb + r * HS + 4 * cc) = u32x2{pt_pack_bf16x2(x[0], x[1]), pt_pack_bf16x2(x[2], x[3])};
+          *(u32x2*)(hbl + r * HS + 4 * cc) = u32x2{pt_pack_bf16x2(sp_lo(x[0]), sp_lo(x[1])),
+                                                   pt_pack_bf16x2(sp_lo(x[2]), sp_lo(x[3]))};
+        } else if constexpr (SP) {   // fp32 h0, units 2cc, 2cc+1
           const float2 x = *(const float2*)((const float*)cd.h0 + (size_t)b * H + 2 * cc);
           *(uint32_t*)(hb + r * HS + 2 * cc) = pt_pack_bf16x2(x.x, x.y);
           *(uint32_t*)(hbl + r * HS + 2 * cc) = pt_pack_bf16x2(sp_lo(x.x), sp_lo(x.y));
@@ -807,13 +828,17 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
       }
     } else {
       // h_{t-1}: poll the granules themselves (all CH loads in flight, then re-poll stragglers)
-      const unsigned want = (ep << 16) | (unsigned)t;
+      const unsigned want = T4 ? (((ep & 1u) << 3) | ((unsigned)t & 7u)) : ((ep << 16) | (unsigned)t);
       const int slot = (t - 1) & 1;
+      auto ld = [&](int r, int cc) -> u32x4 {   // sc1 poll loads
+        return T4 ? __builtin_amdgcn_raw_buffer_load_b128(rrs, woff(slot, r, 4 * cc), 0, 16)
+                  : __builtin_amdgcn_raw_buffer_load_b128(rrs, goff(slot, r, 2 * cc), 0, 16);
+      };
       u32x4 v[CH];
 #pragma unroll
       for (int i = 0; i < CH; ++i) {
         const int c = tid + 256 * i, r = c / CPR, cc = c % CPR;
-        v[i] = __builtin_amdgcn_raw_buffer_load_b128(rrs, goff(slot, r, 2 * cc), 0, 16);  // sc1
+        v[i] = ld(r, cc);
       }
       // re-poll every stale chunk at once: one round trip per retry round, not one per chunk
       for (unsigned spins = 0;; ++spins) {
@@ -822,7 +847,13 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
 #pragma unroll
         for (int i = 0; i < CH; ++i) {
           const int r = (tid + 256 * i) / CPR;
-          ok[i] = mb * PT_ROWS + r >= B || (v[i][1] == want && v[i][3] == want);
+          bool fresh;
+          if constexpr (T4)
+            fresh = (v[i][0] & 15u) == want && (v[i][1] & 15u) == want && (v[i][2] & 15u) == want &&
+                    (v[i][3] & 15u) == want;
+          else
+            fresh = v[i][1] == want && v[i][3] == want;
+          ok[i] = mb * PT_ROWS + r >= B || fresh;
           all = all && ok[i];
         }
         if (all) break;
@@ -835,13 +866,20 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
 #pragma unroll
         for (int i = 0; i < CH; ++i) {
           const int c = tid + 256 * i, r = c / CPR, cc = c % CPR;
-          if (!ok[i]) v[i] = __builtin_amdgcn_raw_buffer_load_b128(rrs, goff(slot, r, 2 * cc), 0, 16);
+          if (!ok[i]) v[i] = ld(r, cc);
         }
       }
 #pragma unroll
       for (int i = 0; i < CH; ++i) {
         const int c = tid + 256 * i, r = c / CPR, cc = c % CPR;
-        if constexpr (SP) {   // {h[2cc], tag, h[2cc+1], tag} -> hi / lo images
+        if constexpr (T4) {   // 4 tagged words (units 4cc .. 4cc+3) -> hi / lo images
+          float f[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) f[e] = __uint_as_float(v[i][e] & ~15u);
+          *(u32x2*)(hb + r * HS + 4 * cc) = u32x2{pt_pack_bf16x2(f[0], f[1]), pt_pack_bf16x2(f[2], f[3])};
+          *(u32x2*)(hbl + r * HS + 4 * cc) = u32x2{pt_pack_bf16x2(sp_lo(f[0]), sp_lo(f[1])),
+                                                   pt_pack_bf16x2(sp_lo(f[2]), sp_lo(f[3]))};
+        } else if constexpr (SP) {   // {h[2cc], tag, h[2cc+1], tag} -> hi / lo images
           const f32x4 f = __builtin_bit_cast(f32x4, v[i]);
           *(uint32_t*)(hb + r * HS + 2 * cc) = pt_pack_bf16x2(f[0], f[2]);
           *(uint32_t*)(hbl + r * HS + 2 * cc) = pt_pack_bf16x2(sp_lo(f[0]), sp_lo(f[2]));
@@ -895,7 +933,15 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
     creg = sf * creg + si * tg;
     const float hv = so * tanhf_(creg);
     PT_TRACE(3);
-    if constexpr (SP) {
+    if constexpr (T4) {
+      // publish h_t: every unit stores one word, h rounded to 19 mantissa bits | 4-bit tag
+      if (pv) {
+        const uint32_t w = ((__float_as_uint(hv) + 8u) & ~15u) | ((ep & 1u) << 3) | ((unsigned)(t + 1) & 7u);
+        const uint32_t off = woff(t & 1, prow, u);
+        if (fast) __builtin_amdgcn_raw_buffer_store_b32(w, rrs, off, 0, 0);
+        else __builtin_amdgcn_raw_buffer_store_b32(w, rrs, off, 0, 16);
+      }
+    } else if constexpr (SP) {
       // publish h_t: every unit stores {fp32 h[u], tag}
       if (pv) {
         const u32x2 gr = {__float_as_uint(hv), (ep << 16) | (unsigned)(t + 1)};
@@ -944,7 +990,13 @@ extern "C" int r2_lstm_tag_ring_bytes(int n_chains, int B, int H) {
   return n < (1ll << 31) ? (int)n : -1;
 }
 
-// Same chain layout / ctr as r2_lstm_fwd_persist; ring: r2_lstm_tag_ring_bytes bytes, any content.
+// A/B probe switch: 1 = split-precision forward on the 8-byte {h, tag} granules (previous path)
+static int g_pl_sp8 = 0;
+extern "C" int r2_lstm_sp_handoff8(int v) { g_pl_sp8 = v; return 0; }
+
+// Same chain layout / ctr as r2_lstm_fwd_persist; ring: r2_lstm_tag_ring_bytes bytes.  bf16: any
+// content.  Split precision (4-bit tagged words): zero- or (-1)-filled at allocation, and one
+// ring + ctr pair per launch site (a fixed chain set), see lstm_fwd_tag_kernel.
 // Returns -3 when the grid cannot be co-resident at one workgroup per CU (caller falls back).
 template <bool SP>
 static int lstm_fwd_tag_launch(const int64_t* chain_ptrs, int words, int n_chains, int B, int T,
@@ -979,6 +1031,20 @@ static int lstm_fwd_tag_launch(const int64_t* chain_ptrs, int words, int n_chain
   hipStream_t s = (hipStream_t)stream;   // counters are left zeroed by the previous launch
   const int nblk = args.xcd_map == 1 ? 8 * nwg : args.xcd_map == 2 ? 16 * nwg : groups * nwg;
   dim3 grid(nblk), block(320);   // 4 compute waves + 1 I/O wave
+  if (SP && !g_pl_sp8) {   // 4-byte tagged-word hand-off (lstm_fwd_tag_kernel T4)
+#define PT_T4(HH)                                                                              \
+  hipFuncSetAttribute((const void*)lstm_fwd_tag_kernel<HH, true, true>,                       \
+                      hipFuncAttributeMaxDynamicSharedMemorySize, PL_LDS_RESERVE);             \
+  hipLaunchKernelGGL((lstm_fwd_tag_kernel<HH, true, true>), grid, block, PL_LDS_RESERVE, s, args)
+    switch (H) {
+      case 64: PT_T4(64); break;
+      case 128: PT_T4(128); break;
+      default: PT_T4(256); break;
+    }
+#undef PT_T4
+    R2_CHECK_LAUNCH();
+    return 0;
+  }
   const void* fn = H == 64 ? (const void*)lstm_fwd_tag_kernel<64, SP>
                  : H == 128 ? (const void*)lstm_fwd_tag_kernel<128, SP>
                  : H == 256 ? (const void*)lstm_fwd_tag_kernel<256, SP>

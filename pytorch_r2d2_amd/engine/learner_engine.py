@@ -398,13 +398,23 @@ class LearnerEngine:
             d += [ptr(pk_lo["w_hh"]), ptr(hseq_lo)]
         return d
 
-    def _lstm(self, chains, T, t_begin=0):
+    def _lstm(self, chains, T, t_begin=0, site=0):
         k = kernels()
         arr = np.asarray([v for c in chains for v in c], dtype=np.int64)
         if self.sp:
-            self._chain_arr = arr        # kept alive for capture
+            # the split-precision hand-off's 4-bit tags need one ring + ctr pair per launch site
+            # (lstm_persist.hip lstm_fwd_tag_kernel T4): site 1 = the reference mode's nx chain
+            if site == 0:
+                ctr, ring = self.ctr, self.ring
+            else:
+                if not hasattr(self, "_site_bufs"):
+                    z = lambda n: torch.zeros(n, dtype=torch.int32, device=self.device)
+                    self._site_bufs = (z(int(k.r2_lstm_persist_ctr_words())),
+                                       z(max(int(k.r2_lstm_tag_ring_bytes(4, self.B, self.layout.H)), 16) // 4))
+                ctr, ring = self._site_bufs
+            setattr(self, "_chain_arr%d" % site, arr)        # kept alive for capture
             check(k.r2_lstm_fwd_tag_sp(arr.ctypes.data, len(chains), self.B, T, self.layout.H,
-                                       ptr(self.ctr), ptr(self.err), ptr(self.ring), stream_handle()),
+                                       ptr(ctr), ptr(self.err), ptr(ring), stream_handle()),
                   "lstm_fwd_tag_sp")
             return
         if self.cfg.learner.lstm_impl == "persistent" and t_begin == 0:
@@ -650,7 +660,7 @@ class LearnerEngine:
             self.c0["nx"].copy_(self.cseq["on"][T - 1])
             nx = self._chain_desc(xp_on[(n + Lb) * B:], pk, self.h0["nx"], self.c0["nx"],
                                   self.hseq["nx"], self.cseq["nx"], None, 0, pkl, hl.get("nx"))
-            self._lstm([nx], Ll)
+            self._lstm([nx], Ll, site=1)
         self._forward_tail()
 
     def _forward_tail(self):
