@@ -477,7 +477,10 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
   {
     const size_t row = J.rows ? (size_t)ld_uniform_i32(J.rows, f) : (size_t)f;
     const u32x4* src = (const u32x4*)(args.frames + row * IN_BYTES);
-    for (int c = tid; c < IN_CHUNKS2; c += NT) ((u32x4*)fr)[c] = src[c];
+    // int8 conv1 reads the frame as (byte - 128): the shift is applied once here / at the
+    // phase-B store, not per conv1 lane per K step (16 XORs per 16-pixel half tile)
+    const uint32_t sh = I8 ? 0x80808080u : 0u;
+    for (int c = tid; c < IN_CHUNKS2; c += NT) ((u32x4*)fr)[c] = src[c] ^ sh;
   }
   const int t1b = c_s2_begin[wave], t1n = c_s2_count[wave];
   int row_nx = f + stride < n_frames ? (J.rows ? ld_uniform_i32(J.rows, f + stride) : f + stride) : 0;
@@ -532,7 +535,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
           for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
             for (int dy = 0; dy < 4; ++dy)
-              x[kb][dy] = (int)(*(const uint32_t*)(fb + (kb >> 1) * 336 + (kb & 1) * 4 + dy * 84) ^ 0x80808080u);
+              x[kb][dy] = (int)*(const uint32_t*)(fb + (kb >> 1) * 336 + (kb & 1) * 4 + dy * 84);
         };
 #pragma unroll 1
         for (int q = 0; q < 2; ++q) {
@@ -540,9 +543,14 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
           const int p = (t1b + i) * 32 + 16 * q + l16;
 #pragma unroll
           for (int c = 0; c < 2; ++c) {   // channel halves one after the other (12 acc VGPRs)
+            // rows (channels) 16c + 4 gq + e; the -128 shift's row corrections (digit row sums x
+            // 128: sum d (v - 128) + 128 sum d = sum d v) start in the accumulators of digits 0
+            // and 2, so the epilogue merges digits 1, 2 with one shift-add
+            const int ch0 = 16 * c + 4 * gq;
             i32x4_t acc[3];
-#pragma unroll
-            for (int d = 0; d < 3; ++d) acc[d] = i32x4_t{0, 0, 0, 0};
+            acc[0] = *(const i32x4_t*)(sct + ch0);
+            acc[1] = i32x4_t{0, 0, 0, 0};
+            acc[2] = *(const i32x4_t*)(sct + 32 + ch0);
 #pragma unroll
             for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
@@ -552,17 +560,12 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
                 acc[d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bx[0][kb], acc[d], 0, 0, 0);
               }
             if (p < P1) {
-              // rows (channels) 16c + 4 gq + e of pixel p.  Digits 1, 2 merge exactly in int32
-              // (|128 i1 + i2| < 2^30); the tables add 128 x the digit row sums (the -128 shift):
-              // sum d (v - 128) + 128 sum d = sum d v
-              const int ch0 = 16 * c + 4 * gq;
-              const i32x4_t k0 = *(const i32x4_t*)(sct + ch0);
-              const i32x4_t k12 = *(const i32x4_t*)(sct + 32 + ch0);
+              // digits 1, 2 merge exactly in int32 (|128 i1 + i2| < 2^30)
               bf16x4 vh, vl;
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
-                const int i0 = acc[0][e] + k0[e];
-                const int i12 = acc[1][e] * 128 + acc[2][e] + k12[e];
+                const int i0 = acc[0][e];
+                const int i12 = acc[1][e] * 128 + acc[2][e];
                 const float t = fmaf((float)i12, 1.f / 16384.f, (float)i0);
                 const float v = fmaxf(fmaf(t, c1_scale, lb[64 + ch0 + e]), 0.f);
                 vh[e] = (bf16)v;
@@ -680,7 +683,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
       for (int q = 0; q < 4; ++q) {
         const int c = I8 ? t7 + 448 * q : tid + NT * q;
         if (c < IN_CHUNKS2 && (!I8 || !conv3_wave))
-          ((u32x4*)fr)[c] = I8 ? __builtin_bit_cast(u32x4, wfl[8 + q]) : pf[q];
+          ((u32x4*)fr)[c] = I8 ? (__builtin_bit_cast(u32x4, wfl[8 + q]) ^ 0x80808080u) : pf[q];
       }
     }
     if (conv2_wave) {
