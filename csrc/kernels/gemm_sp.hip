@@ -31,16 +31,19 @@ __device__ __forceinline__ int g5_mnswz(int k) { return 2 * ((k & 3) | (((k >> 3
 template <int BK>
 __device__ __forceinline__ int g5_kswz(int r) { return BK == 64 ? ((r >> 1) & 7) : 3 * ((r >> 3) & 1); }
 
-// Stage one R x BK operand plane: R*BK*2/1024 1-KB blocks, dealt evenly over the 8 waves.
+// Stage one R x BK operand plane: R*BK*2/1024 1-KB blocks dealt over the 8 waves (evenly when
+// 8 divides the count; else wave w takes blocks w, w+8, .. -- only legal with 2 stages, whose
+// wait is vmcnt(0): the deeper rings count DMAs per thread).
 template <bool KMAJ, int R, int BK>
 __device__ __forceinline__ void g5_stage(const bf16* X, int ld, int i0, int imax, int k0, int kmax,
                                          uint8_t* tile, int wave, int lane, int oz) {
-  constexpr int NBLK = R * BK * 2 / 1024, PW = NBLK / 8;
-  static_assert(NBLK % 8 == 0, "blocks per wave");
+  constexpr int NBLK = R * BK * 2 / 1024, PW = (NBLK + 7) / 8;
+  constexpr bool EVEN = NBLK % 8 == 0;
   static_assert(KMAJ || R % 128 == 0, "mn-major images are 128-column halves");
 #pragma unroll
   for (int j = 0; j < PW; ++j) {
-    const int blk = wave * PW + j;
+    const int blk = EVEN ? wave * PW + j : wave + 8 * j;
+    if (!EVEN && blk >= NBLK) break;
     int off;
     bool kin;
     if (KMAJ) {
@@ -107,6 +110,8 @@ __device__ __forceinline__ void g5_mainloop(const GemmProb& P, int m0, int n0, i
   constexpr int FM = BM / 32, FN = BN / 64;
   constexpr int OPA = BM * BK * 2, OPB = BN * BK * 2, STB = 2 * (OPA + OPB);
   constexpr int NDMA = 2 * (BM + BN) * BK * 2 / (512 * 16);   // DMA instructions per thread per tile
+  static_assert(NS == 2 || ((BM * BK * 2 / 1024) % 8 == 0 && (BN * BK * 2 / 1024) % 8 == 0),
+                "uneven staging needs the 2-stage ring (vmcnt(0) waits)");
   const int wr = wave >> 2, wc = wave & 3;
   auto stage = [&](int kt) {
     if (dbg & 2) return;
@@ -397,8 +402,8 @@ static void g5_kernel_launch(const G5Args& a, hipStream_t s) {
 // tile configurations: {BM, BN, BK, NS}
 static const int g5_cfgs[][4] = {{192, 128, 64, 2}, {128, 128, 64, 2}, {256, 128, 32, 3},
                                  {256, 256, 32, 2}, {256, 64, 64, 2}, {128, 64, 64, 2},
-                                 {128, 128, 32, 4}};
-static const int g5_ncfg = 7;
+                                 {128, 128, 32, 4}, {192, 256, 32, 2}};
+static const int g5_ncfg = 8;
 
 static int g5_tiles(const GemmProb& p, int bm, int bn) {
   return ((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn);
@@ -480,6 +485,11 @@ extern "C" int r2_gemm5(const int64_t* descs, const int* split, int np, int cfg,
     case 11: g5_kernel_launch<true, 128, 64, 64, 2>(a, s); break;
     case 12: g5_kernel_launch<false, 128, 128, 32, 4>(a, s); break;
     case 13: g5_kernel_launch<true, 128, 128, 32, 4>(a, s); break;
+    // 192 x 256: one round of tiles for the x-projection's 10,560 x 1,024 on 256 CUs (224 items;
+    // 192 x 128 took 2.6 rounds).  Wave tile 96 x 64 -- 20 fragments per 72 MFMAs -- leaves no
+    // VGPRs for the interleaved (double-buffered) fragment loads, so always the plain k-loop
+    case 14: g5_kernel_launch_il<false, 192, 256, 32, 2, false>(a, s); break;
+    case 15: g5_kernel_launch_il<true, 192, 256, 32, 2, false>(a, s); break;
     default: return -8;
   }
   R2_CHECK_LAUNCH();

@@ -98,7 +98,7 @@ def gemm_group(problems: List[Gemm], splits: List[int], ws: torch.Tensor, ticket
 _G5_WS = {}
 # csrc/kernels/gemm_sp.hip g5_cfgs: (BM, BN, BK, stages)
 G5_CFGS = [(192, 128, 64, 2), (128, 128, 64, 2), (256, 128, 32, 3), (256, 256, 32, 2),
-           (256, 64, 64, 2), (128, 64, 64, 2), (128, 128, 32, 4)]
+           (256, 64, 64, 2), (128, 64, 64, 2), (128, 128, 32, 4), (192, 256, 32, 2)]
 
 
 def gemm_sp(problems: List[Gemm], splits: Optional[List[int]] = None, cfg: int = -1,
