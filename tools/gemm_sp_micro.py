@@ -71,8 +71,9 @@ def main():
     ws = torch.zeros(group_ws_bytes(probs, [1, 1, 1, 1]) // 4 + 1, device=DEV)
     tk = torch.zeros(1024, dtype=torch.int32, device=DEV)
     out["group_multipass_us"] = timeit(lambda: gemm_group(probs, [1, 1, 1, 1], ws, tk))
-    for splits in ([1, 1, 1, 1], [2, 2, 2, 1], [3, 2, 2, 1], [4, 4, 4, 1]):
-        for c in (1, 2, 3, -1):
+    for splits in ([1, 1, 1, 1], [2, 2, 2, 1], [3, 2, 2, 1], [3, 3, 3, 1], [4, 4, 4, 1],
+                   [4, 4, 4, 2], [5, 4, 4, 2]):
+        for c in (1, 3, -1):
             key = f"group_fused_{'x'.join(map(str, splits))}_cfg{c}_us"
             out[key] = timeit(lambda: gemm_sp(probs, splits=splits, cfg=c))
     # heads (3 nets' first layers) and dh
