@@ -1122,7 +1122,11 @@ struct PTBArgs {
 
 // SP (split precision, split.h): W_hh^T hi / lo fragments, dgates tile kept as hi / lo images for
 // the partial-dh MFMAs (3 passes) and written as hi / lo planes for the weight-gradient GEMMs.
-template <int H, bool SP>
+// T4 (default, r2_lstm_bwd_handoff8(1) = the 8-byte granules): each partial travels as ONE 4-byte
+// word, fp32 rounded to 19 mantissa bits | 4-bit {epoch parity, (k + 1) mod 8} tag (the forward's
+// T4 scheme, lstm_fwd_tag_kernel): half the ring bytes; a consumer wave gathers 4 units x 4 sources
+// per 16-B load and the 4 waves split the 16 sources (sums in source order, then wave order).
+template <int H, bool SP, bool T4 = false>
 __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   constexpr int G = 4 * H;
   constexpr int NWG = H / PL_UNITS;
@@ -1132,7 +1136,7 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   static_assert(NTW >= 1 && NWG % 2 == 0, "H");
   __shared__ __attribute__((aligned(16))) bf16 dgl[2][PT_ROWS * DS];
   __shared__ __attribute__((aligned(16))) bf16 dgll[2][SP ? PT_ROWS * DS : 8];
-  __shared__ __attribute__((aligned(16))) float red[2][PT_ROWS * PL_UNITS];
+  __shared__ __attribute__((aligned(16))) float red[T4 ? 4 : 2][PT_ROWS * PL_UNITS];
   __shared__ __attribute__((aligned(1024))) float gl[3][PT_ROWS * PL_GCOLS];  // saved gates
   __shared__ __attribute__((aligned(1024))) float cl[3][PT_ROWS * PL_UNITS];  // c_t
   __shared__ __attribute__((aligned(1024))) float cpl[3][PT_ROWS * PL_UNITS]; // c_{t-1}
@@ -1218,6 +1222,9 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   if (fast < 0) return;
   auto goff = [&](int slot, int src, int r, int unit) -> uint32_t {
     return (uint32_t)((((size_t)(slot * NWG + src) * rows_all + mb * PT_ROWS + r) * H + unit) * 8);
+  };
+  auto woff = [&](int slot, int src, int r, int unit) -> uint32_t {   // T4: 4 B per unit
+    return (uint32_t)((((size_t)(slot * NWG + src) * rows_all + mb * PT_ROWS + r) * H + unit) * 4);
   };
 
   if (wave == 4) {
@@ -1305,11 +1312,46 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   // consumer ownership of the partial gather: (row, unit pair) x source half
   const int cmb = tid & 127, cr = cmb >> 3, cp2 = 2 * (cmb & 7), sh = tid >> 7;
   const bool crow_ok = mb * PT_ROWS + cr < B;
+  // T4 ownership: (row, unit quad) x source quarter (= wave)
+  constexpr int SRC4 = NWG / 4;
+  const int cr4 = lane >> 2, cq4 = 4 * (lane & 3), sq = wave;
+  const bool crow4_ok = mb * PT_ROWS + cr4 < B;
   __builtin_amdgcn_s_waitcnt(0);          // drain the one-time loads (see the forward kernel)
 
   for (int k = 0; k < K; ++k) {
     const int t = T - 1 - k;
-    if (k > 0) {
+    if (T4 && k > 0) {
+      const unsigned want = ((ep & 1u) << 3) | ((unsigned)k & 7u);
+      const int slot = (k - 1) & 1;
+      u32x4 v[SRC4];
+#pragma unroll
+      for (int i = 0; i < SRC4; ++i)
+        v[i] = __builtin_amdgcn_raw_buffer_load_b128(rrs, woff(slot, sq * SRC4 + i, cr4, j * PL_UNITS + cq4), 0, 16);
+      for (unsigned spins = 0;; ++spins) {
+        bool all = true;
+        bool ok[SRC4];
+#pragma unroll
+        for (int i = 0; i < SRC4; ++i) {
+          ok[i] = !crow4_ok || ((v[i][0] & 15u) == want && (v[i][1] & 15u) == want &&
+                                (v[i][2] & 15u) == want && (v[i][3] & 15u) == want);
+          all = all && ok[i];
+        }
+        if (all) break;
+        if (spins > PL_SPIN_LIMIT) {
+          __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < SRC4; ++i)
+          if (!ok[i]) v[i] = __builtin_amdgcn_raw_buffer_load_b128(rrs, woff(slot, sq * SRC4 + i, cr4, j * PL_UNITS + cq4), 0, 16);
+      }
+      f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < SRC4; ++i) sum += __builtin_bit_cast(f32x4, v[i] & ~15u);
+      *(f32x4*)(red[T4 ? sq : 0] + cr4 * PL_UNITS + cq4) = sum;
+    } else if (k > 0) {
       const unsigned want = (ep << 16) | (unsigned)k;
       const int slot = (k - 1) & 1;
       u32x4 v[SRCH];
@@ -1350,7 +1392,13 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
     // ---- pointwise (row prow, unit ul)
     const int s3 = k % 3;
     float dh = a.dh_ext ? dhl[s3][prow * PL_UNITS + ul] : 0.f;
-    if (k > 0) dh += red[0][prow * PL_UNITS + ul] + red[1][prow * PL_UNITS + ul];
+    if (k > 0) {
+      if constexpr (T4)
+        dh += ((red[0][prow * PL_UNITS + ul] + red[1][prow * PL_UNITS + ul]) + red[T4 ? 2 : 0][prow * PL_UNITS + ul]) +
+              red[T4 ? 3 : 0][prow * PL_UNITS + ul];
+      else
+        dh += red[0][prow * PL_UNITS + ul] + red[1][prow * PL_UNITS + ul];
+    }
     const float* gq = gl[s3] + prow * PL_GCOLS + ul;
     const float gi = gq[0], gf = gq[16], gg = gq[32], go = gq[48];
     const float ct = cl[s3][prow * PL_UNITS + ul], cpv = cpl[s3][prow * PL_UNITS + ul];
@@ -1406,10 +1454,18 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
         for (int e = 0; e < 4; ++e) {
           const int r = 4 * (lane >> 4) + e;
           if (mb * PT_ROWS + r < B) {
-            const u32x2 gr = {__float_as_uint(acc[e]), tag};
-            const uint32_t off = goff(slot, j, r, n);
-            if (fast) __builtin_amdgcn_raw_buffer_store_b64(gr, rrs, off, 0, 0);
-            else __builtin_amdgcn_raw_buffer_store_b64(gr, rrs, off, 0, 16);
+            if constexpr (T4) {
+              const uint32_t w = ((__float_as_uint(acc[e]) + 8u) & ~15u) | ((ep & 1u) << 3) |
+                                 ((unsigned)(k + 1) & 7u);
+              const uint32_t off = woff(slot, j, r, n);
+              if (fast) __builtin_amdgcn_raw_buffer_store_b32(w, rrs, off, 0, 0);
+              else __builtin_amdgcn_raw_buffer_store_b32(w, rrs, off, 0, 16);
+            } else {
+              const u32x2 gr = {__float_as_uint(acc[e]), tag};
+              const uint32_t off = goff(slot, j, r, n);
+              if (fast) __builtin_amdgcn_raw_buffer_store_b64(gr, rrs, off, 0, 0);
+              else __builtin_amdgcn_raw_buffer_store_b64(gr, rrs, off, 0, 16);
+            }
           }
         }
       }
@@ -1461,13 +1517,18 @@ static const float* g_bwd_hg_zr32 = nullptr;
 static const bf16* g_bwd_hg_dz_lo = nullptr;
 static bf16* g_bwd_dgates_lo = nullptr;
 
+// A/B probe switch: 1 = the BPTT on 8-byte {partial, tag} granules (the previous hand-off)
+static int g_pl_bwd8 = 0;
+extern "C" int r2_lstm_bwd_handoff8(int v) { g_pl_bwd8 = v; return 0; }
+
 extern "C" int r2_lstm_bwd_tag_ring_bytes(int B, int H) {
   const long long n = 2ll * (H / PL_UNITS) * ((B + PT_ROWS - 1) / PT_ROWS) * PT_ROWS * H * 8;
   return n < (1ll << 31) ? (int)n : -1;
 }
 
 // Same operands as r2_lstm_bwd_persist minus the slab; ring: r2_lstm_bwd_tag_ring_bytes bytes,
-// any content.  -3: grid too large for one workgroup per CU (caller falls back).
+// zero- or (-1)-filled at allocation and one ring + ctr per launch site (the 4-bit tags of the
+// T4 hand-off, see lstm_fwd_tag_kernel).  -3: grid too large for one workgroup per CU (caller falls back).
 // 1 when the launch's idle workgroups can take the dueling head's gradient reduction (head
 // width HD): the XCD map leaves (8 - MB) * H/16 workgroups free and the job needs (2HD/64) x 8.
 extern "C" int r2_lstm_bwd_tag_hg_ok(int B, int H, int HD) {
@@ -1539,11 +1600,16 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
   if (sp && args.hg_on && (!args.hg.zr32 || !args.hg.dz_lo)) return -12;
   hipStream_t s = (hipStream_t)stream;   // counters are left zeroed by the previous launch
   dim3 grid(nh ? 256 : (xmap ? 8 * nwg : MB * nwg)), block(320);
+#define R2_BWD_LAUNCH1(HH, SPP, T4)                                                            \
+  do {                                                                                         \
+    hipFuncSetAttribute((const void*)lstm_bwd_tag_kernel<HH, SPP, T4>,                         \
+                        hipFuncAttributeMaxDynamicSharedMemorySize, PL_LDS_RESERVE);           \
+    hipLaunchKernelGGL((lstm_bwd_tag_kernel<HH, SPP, T4>), grid, block, PL_LDS_RESERVE, s, args); \
+  } while (0)
 #define R2_BWD_LAUNCH(HH, SPP)                                                                 \
   do {                                                                                         \
-    hipFuncSetAttribute((const void*)lstm_bwd_tag_kernel<HH, SPP>,                             \
-                        hipFuncAttributeMaxDynamicSharedMemorySize, PL_LDS_RESERVE);           \
-    hipLaunchKernelGGL((lstm_bwd_tag_kernel<HH, SPP>), grid, block, PL_LDS_RESERVE, s, args);  \
+    if (g_pl_bwd8) R2_BWD_LAUNCH1(HH, SPP, false);                                             \
+    else R2_BWD_LAUNCH1(HH, SPP, true);                                                        \
   } while (0)
   if (sp) {
     switch (H) {
@@ -1560,6 +1626,7 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
     }
   }
 #undef R2_BWD_LAUNCH
+#undef R2_BWD_LAUNCH1
   R2_CHECK_LAUNCH();
   return taken;   // bit 0: head grads, 1: weight grads, 2: dX done here
 }

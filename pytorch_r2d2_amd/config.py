@@ -97,6 +97,10 @@ class LearnerConfig:
     # persistent forward hand-off: "tagged" (8-byte {h pair, tag} granules polled directly, 16-row
     # batch tiles; falls back when the grid does not fit) | "counter" (payload + arrival counter)
     lstm_handoff: str = "tagged"
+    # tagged kernels: h (forward, split precision) and the recurrent dh partials (BPTT) as 4-byte
+    # words with a 4-bit tag (lstm_persist.hip T4) -- False = the 8-byte {value, tag} granules
+    # (A/B probes; process-wide kernel switch, set by the engine at construction)
+    lstm_tag_words: bool = True
     # tagged BPTT: GEMMs run beside the recurrence on the launch's helper workgroups
     # ("w" = weight gradients, "x" = dX; comma-separated, "" = none).  Off by default: measured
     # 0.799 ms/step without, 0.860 with "w", 0.987 with "x", 0.942 with both (atari57, 1 GPU) --

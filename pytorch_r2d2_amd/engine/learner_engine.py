@@ -228,6 +228,9 @@ class LearnerEngine:
         # the fused FORWARD kernel also covers DMLab-30 RGB (3x72x96); its backward then runs on
         # the library convs from the saved activations
         self.fwd_geom = fused_torso_fwd_geom(cfg.env, cfg.model) if d.type == "cuda" else None
+        if d.type == "cuda":
+            kernels().r2_lstm_sp_handoff8(0 if lc.lstm_tag_words else 1)
+            kernels().r2_lstm_bwd_handoff8(0 if lc.lstm_tag_words else 1)
         if sp and not (self.fused_torso and d.type == "cuda" and L.H <= 256
                        and lc.lstm_impl == "persistent" and lc.lstm_handoff == "tagged"):
             raise NotImplementedError(

@@ -294,3 +294,66 @@ def test_td_fused_dh_matches_fp64_split():
     dz = eng.dz[:N].double() + eng.dz_lo[:N].double()
     w1 = eng.pk["head1"].double() + eng.pk_lo["head1"].double()
     assert _rel(eng.dh[:N], dz @ w1) < 2e-5
+
+
+@pytest.mark.parametrize("fill", [0, -1])
+def test_lstm_sp_tagged_word_handoff_over_launches(fill):
+    """The split-precision LSTM forward's 4-byte tagged-word hand-off (lstm_persist.hip T4: 4-bit
+    {epoch parity, step} tags) against the 8-byte {h, tag} granule path over 5 consecutive
+    launches on ONE ring + ctr with different inputs each time (stale words of the previous
+    launch must never be taken), on a zero- and a (-1)-filled ring; both vs a float64 recurrence."""
+    import numpy as np
+    from pytorch_r2d2_amd.ops._lib import kernels, ptr, stream_handle
+    k = kernels()
+    H, B, T, NC = 256, 64, 23, 3
+    G = 4 * H
+    g = torch.Generator(device=DEV).manual_seed(3)
+    nwg = H // 16
+    whh = torch.randn(nwg, 64, H, device=DEV, generator=g) * 0.06
+    wh, wl = _split(whh)
+    c0 = torch.randn(B, H, device=DEV, generator=g) * 0.5
+    h0 = torch.randn(B, H, device=DEV, generator=g) * 0.5
+    err = torch.zeros(1, dtype=torch.int32, device=DEV)
+
+    def site():
+        return (torch.zeros(int(k.r2_lstm_persist_ctr_words()), dtype=torch.int32, device=DEV),
+                torch.full((k.r2_lstm_tag_ring_bytes(4, B, H) // 4,), fill, dtype=torch.int32,
+                           device=DEV))
+
+    outs = {}
+    for name, sp8, (ctr, ring) in (("t4", 0, site()), ("g8", 1, site())):
+        res = []
+        for launch in range(5):
+            xp = torch.randn(T * B, G, device=DEV, generator=torch.Generator(device=DEV).manual_seed(launch))
+            bufs, desc = [], []
+            for _ in range(NC):
+                hs = torch.zeros(T, B, H, dtype=torch.bfloat16, device=DEV)
+                hl, cs = torch.zeros_like(hs), torch.zeros(T, B, H, device=DEV)
+                bufs.append((hs, hl, cs))
+                desc += [ptr(xp), ptr(wh), ptr(h0), ptr(c0), ptr(hs), ptr(cs), 0, 0, 0, ptr(wl), ptr(hl)]
+            arr = np.asarray(desc, dtype=np.int64)
+            k.r2_lstm_sp_handoff8(sp8)
+            rc = k.r2_lstm_fwd_tag_sp(arr.ctypes.data, NC, B, T, H, ptr(ctr), ptr(err), ptr(ring),
+                                      stream_handle())
+            k.r2_lstm_sp_handoff8(0)
+            assert rc == 0
+            torch.cuda.synchronize()
+            assert err.item() == 0
+            res.append((xp, bufs))
+        outs[name] = res
+    # float64 recurrence (packed gate layout: workgroup j owns units 16j..16j+15, gate-major rows)
+    W = whh.double().view(nwg, 4, 16, H)                      # [j][gate][unit][k]
+    for (xp, b4), (_, b8) in zip(outs["t4"], outs["g8"]):
+        h, c = h0.double(), c0.double()
+        x = xp.double().view(T, B, nwg, 4, 16)
+        for t in range(T):
+            gt = torch.einsum("bk,jguk->bjgu", h, W) + x[t]
+            i_, f_, gg, o_ = (gt[:, :, q] for q in range(4))
+            c = torch.sigmoid(f_) * c.view(B, nwg, 16) + torch.sigmoid(i_) * torch.tanh(gg)
+            h = torch.sigmoid(o_) * torch.tanh(c)
+            c, h = c.reshape(B, H), h.reshape(B, H)
+            for (hs, hl, cs), (hs8, hl8, cs8) in zip(b4, b8):
+                h4 = hs[t].double() + hl[t].double()
+                assert _rel(h4, h) < 2e-5, t
+                assert _rel(cs[t], c) < 2e-5, t
+                assert (h4 - (hs8[t].double() + hl8[t].double())).abs().max().item() < 5e-5
