@@ -579,23 +579,23 @@ class LearnerEngine:
         from ..parallel.sharded_replay import gather_stats
         gather_stats(self.dp_send, self.world, self.pg, out=self.dp_recv)
 
-    def _forward_rest(self):
+    def _forward_rest(self, tail: bool = True):
+        """Torso, x-projections and recurrent chains; then (``tail``) heads, TD and priorities.
+        DP global sampling needs the all-gathered shard stats only from the TD launch on, so the
+        graphed DP step replays everything before ``_forward_tail`` while the 12-byte all-gather
+        is in flight on its own stream (``step``)."""
         k = kernels()
         s = stream_handle()
         B, T, Tn, Lb, Ll, n = self.B, self.T, self.Tn, self.Lb, self.Ll, self.n
         L, rp, lc = self.layout, self.replay, self.cfg.learner
         H, A = L.H, L.A
         pk, pt = self.pk, self.pk_t
-        if self.dp_global:
-            from ..parallel.sharded_replay import global_is_params
-            global_is_params(self.dp_recv.view(self.world, 3), self.rank, float(self.cfg.replay.beta),
-                             out=self.dp_params)
         rows = self.rows
         if self._chunks is not None:
             self._forward_pipelined()
             xp_on, xp_tg = self.xp_on, self.xp_tg
             self._xp = (xp_on, xp_tg)
-            return self._forward_tail()
+            return self._forward_tail() if tail else None
         # torso: online over all Tn frames (save activations of the learning frames) and target
         if self.sp:
             pkl, ptl = self.pk_lo, self.pk_t_lo
@@ -664,7 +664,8 @@ class LearnerEngine:
             nx = self._chain_desc(xp_on[(n + Lb) * B:], pk, self.h0["nx"], self.c0["nx"],
                                   self.hseq["nx"], self.cseq["nx"], None, 0, pkl, hl.get("nx"))
             self._lstm([nx], Ll, site=1)
-        self._forward_tail()
+        if tail:
+            self._forward_tail()
 
     def _forward_tail(self):
         """Heads, TD loss and priorities (after every recurrent chain has run)."""
@@ -674,6 +675,10 @@ class LearnerEngine:
         L, rp, lc = self.layout, self.replay, self.cfg.learner
         H, A = L.H, L.A
         pk, pt = self.pk, self.pk_t
+        if self.dp_global:   # IS-weight parameters from the all-gathered shard stats
+            from ..parallel.sharded_replay import global_is_params
+            global_is_params(self.dp_recv.view(self.world, 3), self.rank, float(self.cfg.replay.beta),
+                             out=self.dp_params)
         # heads (rows from the first learning step on)
         jobs = [(pk, self.hseq["on"][Lb:].reshape(-1, H), self.z_on, self.q_on, self.zr_on),
                 (pt, self.hseq["tg"][Lb:].reshape(-1, H), self.z_tg, self.q_tg, None)]
@@ -1123,6 +1128,13 @@ class LearnerEngine:
         self._forward_rest()
         self._backward_core()
 
+    def _seg_fwd_head(self):       # DP global sampling: everything before the TD (gather in flight)
+        self._forward_rest(tail=False)
+
+    def _seg_core_tail(self):      # ... and from the heads / TD on (gathered stats joined)
+        self._forward_tail()
+        self._backward_core()
+
     def _seg_torso(self):
         self._backward_torso()
 
@@ -1172,8 +1184,9 @@ class LearnerEngine:
         """Capture the step into HIP graphs.  world == 1: one graph for the whole step.
         world > 1: four graphs (core fwd/bwd | conv bwd | priorities | update) with the two
         bucket all-reduces issued between them on the communication stream; with global
-        sampling the core graph is split after the sampling launch for the 12-byte shard-stats
-        all-gather (five graphs)."""
+        sampling the core graph is split after the sampling launch and again before the heads /
+        TD (six graphs): the 12-byte shard-stats all-gather runs on its own stream beside the
+        torso / x-projection / LSTM graph and is joined before the TD."""
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
@@ -1185,7 +1198,7 @@ class LearnerEngine:
         if self.world > 1:
             segs = [self._seg_core, self._seg_torso, self._seg_prio, self._seg_update]
             if self.dp_global:
-                segs = [self._seg_sample, self._seg_core_rest] + segs[1:]
+                segs = [self._seg_sample, self._seg_fwd_head, self._seg_core_tail] + segs[1:]
         else:
             segs = [lambda: (self._seg_core(), self._seg_torso(), self._seg_tail())]
         pool = None
@@ -1207,9 +1220,18 @@ class LearnerEngine:
         else:
             L = self.layout
             if self.dp_global:
-                g_sample, g_core, g_torso, g_prio, g_update = self.graphs
+                g_sample, g_fwd, g_core, g_torso, g_prio, g_update = self.graphs
                 g_sample.replay()
-                self._gather_dp()
+                # the shard-stats all-gather runs on its own stream beside the torso / LSTM graph
+                main = torch.cuda.current_stream(self.device)
+                if getattr(self, "_gather_stream", None) is None:
+                    self._gather_stream = torch.cuda.Stream(device=self.device)
+                gs = self._gather_stream
+                gs.wait_stream(main)
+                with torch.cuda.stream(gs):
+                    self._gather_dp()
+                g_fwd.replay()
+                main.wait_stream(gs)
             else:
                 g_core, g_torso, g_prio, g_update = self.graphs
             g_core.replay()
