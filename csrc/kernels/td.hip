@@ -1,4 +1,5 @@
 // Fused n-step double-Q TD target / loss / gradient / priority kernel (gfx950).
+#define HEAD_FWD_MAXA 32
 //
 // Reference: learner.py:82-104 computes, over 6 separate PyTorch ops plus a D2H copy and a
 // numpy scatter:
@@ -202,7 +203,62 @@ struct TdDuelArgs {
   const bf16* w1t;      // (256, 2*HD) = W1^T (k contiguous); null = not fused
   const bf16* w1t_lo;   // split precision: lo plane of W1^T
   float* dh;            // (Tl*B, 256) out
+  // optional fused head FORWARD (fixed / reference target modes, where the three Q rows of
+  // transition i are row i of each head): zh = pre-bias layer-1 outputs (ZT) of the online,
+  // online-on-next and target heads; the kernel forms relu(z + b1), the dueling Q rows (the
+  // arithmetic of head.hip dueling_fwd_kernel, bit-identical), writes them to qo[] (optional) and
+  // the online relu'd rows to zr (then an OUTPUT) -- one launch instead of dueling_fwd + td
+  const void* zh[3];
+  const float* b1[2];   // online, target
+  const float* w2t;     // target second layer (1 + A, HD)
+  const float* b2[2];   // online, target
+  float* qo[3];
+  int fuse_fwd;
 };
+
+// head.hip dueling_fwd_kernel for one row on one wave (same order of operations): returns the
+// lane's Q (lane < A); hv / ha = relu(z + b1) of the lane's features.  REGS: the advantage rows
+// below MAXA come from the caller's register copy (static indices only: no scratch)
+template <int HD, typename ZT, int MAXA, bool REGS>
+__device__ __forceinline__ float td_duel_row(const ZT* zrow, const float* b1, const float* w2,
+                                             const float* b2, int A, int lane, float (&hv)[HD / 64],
+                                             float (&ha)[HD / 64], const float (&w2a)[MAXA][HD / 64]) {
+  constexpr int PER = HD / 64;
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int c = lane * PER + e;
+    hv[e] = fmaxf((float)zrow[c] + b1[c], 0.f);
+    ha[e] = fmaxf((float)zrow[HD + c] + b1[HD + c], 0.f);
+  }
+  float v = 0.f;
+#pragma unroll
+  for (int e = 0; e < PER; ++e) v += hv[e] * w2[lane * PER + e];
+  v = wave_sum(v) + b2[0];
+  float amean = 0.f, mine = 0.f;
+  auto act = [&](int a, float s) {
+    s = wave_sum(s) + b2[1 + a];
+    mine = (a == lane) ? s : mine;
+    amean += s;
+  };
+  if constexpr (REGS) {
+#pragma unroll
+    for (int a = 0; a < MAXA; ++a)
+      if (a < A) {
+        float s = 0.f;
+#pragma unroll
+        for (int e = 0; e < PER; ++e) s += ha[e] * w2a[a][e];
+        act(a, s);
+      }
+  }
+  for (int a = REGS ? MAXA : 0; a < A; ++a) {
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < PER; ++e) s += ha[e] * w2[(size_t)(1 + a) * HD + lane * PER + e];
+    act(a, s);
+  }
+  amean /= (float)A;
+  return v + mine - amean;
+}
 
 // SP: zr fp32, dz written as hi / lo planes (split.h).  Actions beyond the MAXA register-resident
 // second-layer rows are read from memory inside the same loop (same order, same bits).
@@ -227,17 +283,9 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
   // chain below (start -> row -> action / reward / done) is the only serial part
   const int start = valid ? a.starts[b] : 0;
   const float NEG = -3.0e38f;
-  const float qa = (valid && lane < a.A) ? a.q_arg[(size_t)i * a.A + lane] : NEG;
-  const float qt = (valid && lane < a.A) ? a.q_tgt[(size_t)i * a.A + lane] : 0.f;
-  const float qs = (valid && lane < a.A) ? a.q_sa[(size_t)i * a.A + lane] : 0.f;
   typedef typename std::conditional<SP, float, bf16>::type ZT;
   ZT zv[PER], za[PER];
   float w2v[PER], w2a[MAXA][PER];
-  if (valid) {
-    const ZT* zrow = (const ZT*)args.zr + (size_t)i * 2 * HD;
-#pragma unroll
-    for (int e = 0; e < PER; ++e) { zv[e] = zrow[lane * PER + e]; za[e] = zrow[HD + lane * PER + e]; }
-  }
 #pragma unroll
   for (int e = 0; e < PER; ++e) w2v[e] = args.w2[lane * PER + e];
 #pragma unroll
@@ -245,6 +293,48 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
 #pragma unroll
     for (int e = 0; e < PER; ++e)
       w2a[k][e] = k < a.A ? args.w2[(size_t)(1 + k) * HD + lane * PER + e] : 0.f;
+  float qa, qt, qs;
+  if (args.fuse_fwd) {
+    // the three heads' dueling forward for row i (online, online-on-next, target)
+    float hv[PER], ha[PER];
+    qs = qa = qt = 0.f;
+    if (valid) {
+#pragma unroll
+      for (int h = 0; h < 3; ++h) {
+        const ZT* zrow = (const ZT*)args.zh[h] + (size_t)i * 2 * HD;
+        const float q = h < 2 ? td_duel_row<HD, ZT, MAXA, true>(zrow, args.b1[0], args.w2, args.b2[0],
+                                                                a.A, lane, hv, ha, w2a)
+                              : td_duel_row<HD, ZT, MAXA, false>(zrow, args.b1[1], args.w2t, args.b2[1],
+                                                                 a.A, lane, hv, ha, w2a);
+        if (args.qo[h] && lane < a.A) args.qo[h][(size_t)i * a.A + lane] = q;
+        if (h == 0) {
+          qs = q;
+          ZT* zo = (ZT*)args.zr + (size_t)i * 2 * HD;
+#pragma unroll
+          for (int e = 0; e < PER; ++e) {
+            zv[e] = (ZT)hv[e];
+            za[e] = (ZT)ha[e];
+            zo[lane * PER + e] = zv[e];
+            zo[HD + lane * PER + e] = za[e];
+          }
+        } else if (h == 1) {
+          qa = q;
+        } else {
+          qt = q;
+        }
+      }
+    }
+    if (!(valid && lane < a.A)) { qa = NEG; qt = 0.f; qs = 0.f; }
+  } else {
+    qa = (valid && lane < a.A) ? a.q_arg[(size_t)i * a.A + lane] : NEG;
+    qt = (valid && lane < a.A) ? a.q_tgt[(size_t)i * a.A + lane] : 0.f;
+    qs = (valid && lane < a.A) ? a.q_sa[(size_t)i * a.A + lane] : 0.f;
+    if (valid) {
+      const ZT* zrow = (const ZT*)args.zr + (size_t)i * 2 * HD;
+#pragma unroll
+      for (int e = 0; e < PER; ++e) { zv[e] = zrow[lane * PER + e]; za[e] = zrow[HD + lane * PER + e]; }
+    }
+  }
   const int row = valid ? ring_row(start, a.burn_in + tl, a.cap_e) : 0;
   const int act = valid ? (int)a.action[row] : 0;
   const float rew = valid ? a.reward[row] : 0.f;
@@ -433,6 +523,18 @@ extern "C" int r2_td_duel_dh(const float*, const float*, const float*, const int
                              bf16*, float*, int, bf16*, const float*, const bf16*, const bf16*,
                              float*, int, void*);
 
+// Head-forward operands of the fused launch (r2_td_duel_fwd_set, consumed by the next
+// r2_td_duel_dh call on this host thread): 12 int64 {z_on, z_nx, z_tg, b1_on, b1_tg, w2_tg,
+// b2_on, b2_tg, q_on, q_nx, q_tg (q outs may be 0)} -- zr of r2_td_duel_dh becomes an output.
+static thread_local int64_t g_td_fwd[12];
+static thread_local bool g_td_fwd_on = false;
+extern "C" int r2_td_duel_fwd_set(const int64_t* fwd) {
+  g_td_fwd_on = fwd != nullptr;
+  if (fwd)
+    for (int k = 0; k < 11; ++k) g_td_fwd[k] = fwd[k];
+  return 0;
+}
+
 // zr: bf16 (dz_lo null) or fp32 (split precision: dz_lo = the lo plane of dz)
 extern "C" int r2_td_duel(const float* q_sa, const float* q_arg, const float* q_tgt,
                           const int* starts, const float* probs, const uint8_t* action,
@@ -470,6 +572,19 @@ extern "C" int r2_td_duel_dh(const float* q_sa, const float* q_arg, const float*
                 is_w, n_valid, part, ticket, Tl, B, A, burn_in, cap_e, gamma_n, vr_eps, alpha,
                 prio_eps, beta, value_rescale, dp},
                zr, w2, dz, dva, dz_lo, w1t, w1t_lo, dh};
+  d.fuse_fwd = 0;
+  if (g_td_fwd_on) {
+    g_td_fwd_on = false;   // one launch per set
+    if (A > HEAD_FWD_MAXA) return -6;
+    for (int k = 0; k < 3; ++k) d.zh[k] = (const void*)g_td_fwd[k];
+    d.b1[0] = (const float*)g_td_fwd[3]; d.b1[1] = (const float*)g_td_fwd[4];
+    d.w2t = (const float*)g_td_fwd[5];
+    d.b2[0] = (const float*)g_td_fwd[6]; d.b2[1] = (const float*)g_td_fwd[7];
+    for (int k = 0; k < 3; ++k) d.qo[k] = (float*)g_td_fwd[8 + k];
+    if (!d.zh[0] || !d.zh[1] || !d.zh[2] || !d.b1[0] || !d.b1[1] || !d.w2t || !d.b2[0] || !d.b2[1])
+      return -7;
+    d.fuse_fwd = 1;
+  }
   hipStream_t s = (hipStream_t)stream;
   return dz_lo ? td_duel_launch<true>(d, HD, grid, s) : td_duel_launch<false>(d, HD, grid, s);
 }

@@ -116,6 +116,9 @@ class LearnerConfig:
     # ~15 us and a chunk's x-projection GEMM is tile-latency bound; profiles/r01_v9_pipelined.txt)
     fwd_chunks: int = 0
     td_fuse_head_bwd: bool = True     # dueling-head backward inside the TD launch (td_duel_kernel)
+    # ... and the heads' dueling FORWARD too (fixed / reference target modes: the TD launch forms
+    # relu(z + b1) and the Q rows of all three heads itself; no separate dueling_fwd launch)
+    td_fuse_head_fwd: bool = True
     # ... and the head's input gradient dh = dz @ W1 on that launch's MFMAs (hidden 256): no
     # separate dh GEMM (hipBLASLt 7-10 us in bf16, 22 us split-precision)
     td_fuse_dh: bool = True

@@ -434,10 +434,10 @@ class LearnerEngine:
             check(k.r2_lstm_fwd(arr.ctypes.data, len(chains), self.B, T, self.layout.H, t_begin,
                                 stream_handle()), "lstm_fwd")
 
-    def _heads(self, jobs, lo=None):
+    def _heads(self, jobs, lo=None, duel: bool = True):
         """jobs: [(pk, h (N,H) bf16, z buffer, q out, zr out or None)].  Layer-1 GEMMs of all heads
-        in one launch, then one dueling kernel per head.  Split precision: ``lo`` = [(pk_lo, h lo
-        plane)] per job; z / zr are fp32."""
+        in one launch, then (``duel``) one dueling kernel for every head.  Split precision: ``lo`` =
+        [(pk_lo, h lo plane)] per job; z / zr are fp32."""
         if self.sp:
             gemm(*[Gemm(h, pk["head1"].t(), zb, a_lo=hl, b_lo=pkl["head1"].t())
                    for (pk, h, zb, _, _), (pkl, hl) in zip(jobs, lo)])
@@ -447,6 +447,11 @@ class LearnerEngine:
             zs = [zb for _, _, zb, _, _ in jobs]
         else:
             zs = [torch.mm(h, pk["head1"].t()) for pk, h, _, _, _ in jobs]
+        self._zs = zs
+        if duel:
+            self._duel_fwd(jobs, zs)
+
+    def _duel_fwd(self, jobs, zs):
         # bias + ReLU + 512 -> 1+A + dueling combine of every head in one launch
         self._djobs = np.asarray([[ptr(z), ptr(pk["head_b1"]), ptr(pk["head_w2"]), ptr(pk["head_b2"]),
                                    ptr(q), ptr(zr), h.shape[0]]
@@ -691,7 +696,11 @@ class LearnerEngine:
             jobs.append((pk, self.hseq["nx"][nx_from:].reshape(-1, H), self.z_nx, self.q_nx, None))
             if self.sp:
                 lo.append((self.pk_lo, self.hseq_lo["nx"][nx_from:].reshape(-1, H)))
-        self._heads(jobs, lo)
+        # fixed / reference modes: the three Q rows of transition i are row i of each head, so the
+        # TD launch can run the dueling forward itself (td.hip td_duel_row)
+        fuse_fwd = (lc.td_fuse_head_bwd and lc.td_fuse_head_fwd and self.mode != "shifted"
+                    and A <= 32 and self.use_gemm)
+        self._heads(jobs, lo, duel=not fuse_fwd)
         if self.mode == "shifted":
             q_sa = self.q_on[: Ll * B]
             q_arg = self.q_on[n * B:(n + Ll) * B]
@@ -717,6 +726,13 @@ class LearnerEngine:
             fuse_dh = lc.td_fuse_dh and L.H == 256 and self.use_gemm
             w1t = ptr(pk["head1T"]) if fuse_dh else 0
             w1t_lo = ptr(self.pk_lo["head1T"]) if fuse_dh and self.sp else 0
+            if fuse_fwd:
+                z_on, z_tg, z_nx = self._zs[0], self._zs[1], self._zs[2]
+                self._fwd_arr = np.asarray(
+                    [ptr(z_on), ptr(z_nx), ptr(z_tg), ptr(pk["head_b1"]), ptr(pt["head_b1"]),
+                     ptr(pt["head_w2"]), ptr(pk["head_b2"]), ptr(pt["head_b2"]), ptr(self.q_on),
+                     ptr(self.q_nx), ptr(self.q_tg), 0], dtype=np.int64)
+                k.r2_td_duel_fwd_set(self._fwd_arr.ctypes.data)
             rc_ = k.r2_td_duel_dh(*targs, ptr(self.zr_on[: Ll * B]), ptr(pk["head_w2"]), ptr(self.dz),
                                   ptr(self.dva), L.HD, ptr(self.dz_lo), dp, w1t, w1t_lo,
                                   ptr(self.dh) if fuse_dh else 0, L.H, s)
@@ -724,6 +740,10 @@ class LearnerEngine:
                 self._duel_done = True
                 self._dh_done = fuse_dh
                 return
+            if fuse_fwd:   # refused on the host before any launch: separate dueling forward
+                k.r2_td_duel_fwd_set(None)
+                self._duel_fwd(jobs, self._zs)
+                fuse_fwd = False
             if self.sp:
                 check(rc_, "td_duel")
         check(k.r2_td_loss(*targs, dp, s), "td_loss")

@@ -94,6 +94,9 @@ _SIGS = {
     "r2_torso_bwd_set_debug": [P],
     "r2_torso_fwd_set_debug": [P],
     "r2_lstm_persist_set_debug": [P],
+    "r2_lstm_sp_handoff8": [I],
+    "r2_lstm_bwd_handoff8": [I],
+    "r2_td_duel_fwd_set": [P],
     "r2_lstm_persist_force_slow": [I],
     "r2_xcc_probe": [P, I, I, I, P],
     "r2_gradsum_ws_floats": [],
