@@ -660,7 +660,11 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
   constexpr int G = 4 * H;
   constexpr int NWG = H / PL_UNITS;
   constexpr int KS = H / 32;                  // 16x16x32 k-steps
-  constexpr int HS = H + 8;                   // bf16 stride of a staged h row (conflict-free b128)
+  // bf16 stride of a staged h row: H + 16 puts consecutive rows 2 bank quads apart (2 mod 16),
+  // the stride at which every ds_read_b128 lane group of the A-fragment reads (rows 0-15 x two
+  // 16-B k halves) hits 16 distinct quads; H + 8 (1 quad) collided in every group (PMC bank
+  // conflict / LDS active 0.56)
+  constexpr int HS = H + 16;
   constexpr int UG = SP ? 1 : 2;              // hidden units per granule
   constexpr int GR = H / UG;                  // granules per row
   constexpr int CPR = T4 ? H / 4 : GR / 2;    // 16-B chunks per row (4 units / 2 granules)
@@ -1131,7 +1135,8 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   constexpr int G = 4 * H;
   constexpr int NWG = H / PL_UNITS;
   constexpr int NTW = H / 64;                 // 16-unit N tiles per wave (4 waves x 16 x NTW = H)
-  constexpr int DS = PL_GCOLS + 8;            // bf16 stride of the dgates tile rows (144 B)
+  constexpr int DS = PL_GCOLS + 16;           // bf16 stride of the dgates tile rows (160 B: 10
+                                              // quads = 2 mod 4, conflict-free b128 fragment reads)
   constexpr int SRCH = NWG / 2;               // sources per consumer half
   static_assert(NTW >= 1 && NWG % 2 == 0, "H");
   __shared__ __attribute__((aligned(16))) bf16 dgl[2][PT_ROWS * DS];
