@@ -640,6 +640,18 @@ __device__ __forceinline__ uint32_t pt_pack_bf16x2(float a, float b) {
   return __builtin_bit_cast(uint32_t, v);
 }
 
+// Staged per-step rows filled by LDS-DMA (16 rows of the x-projection / saved gates, 64 floats;
+// c / dh rows, 16 floats): the DMA writes LDS slots in lane order, so the swizzle is applied
+// through the SOURCE address of each lane -- LDS chunk c of row r holds global chunk c ^ f(r).
+// Without it the pointwise's 4-byte reads (row = lane >> 2, 4 units per wave) hit 4 banks (64-float
+// rows) or 16 (16-float rows).
+__device__ __forceinline__ int pt_swz64(int r, int col) {      // 64-float rows, f(r) = r
+  return r * 64 + ((((col >> 2) ^ r) & 15) << 2) + (col & 3);
+}
+__device__ __forceinline__ int pt_swz16(int r, int col) {      // 16-float rows, f(r) = r >> 2
+  return r * 16 + ((((col >> 2) ^ (r >> 2)) & 3) << 2) + (col & 3);
+}
+
 // SP (split precision, split.h): W_hh hi / lo fragments stay in VGPRs and every product is 3
 // MFMA passes; h_seq is written as hi / lo planes.  h_t travels one of two ways:
 //  * T4 (default): ONE 4-byte word per unit -- fp32 h rounded to 19 explicit mantissa bits with a
@@ -709,9 +721,11 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
       float* dst = xl[t % 3];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
+        // LDS chunk (lane & 15) of row r holds global chunk (lane & 15) ^ r (pt_swz64): the
+        // pointwise reads of 16 rows x 4 units then cover 64 distinct banks
         const int r = 4 * q + (lane >> 4);
         const int b = min(mb * PT_ROWS + r, B - 1);
-        const float* src = cd.xproj + ((size_t)t * B + b) * G + j * PL_GCOLS + 4 * (lane & 15);
+        const float* src = cd.xproj + ((size_t)t * B + b) * G + j * PL_GCOLS + 4 * ((lane & 15) ^ r);
         __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(dst + q * 256),
                                          16, 0, 0);
       }
@@ -905,9 +919,9 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
     }
     float xv[4];
     {
-      const float* xr = xl[t % 3] + prow * PL_GCOLS + ul;
+      const float* xr = xl[t % 3];
 #pragma unroll
-      for (int gi = 0; gi < 4; ++gi) xv[gi] = xr[16 * gi];
+      for (int gi = 0; gi < 4; ++gi) xv[gi] = xr[pt_swz64(prow, ul + 16 * gi)];
     }
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1238,13 +1252,13 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
       const int t = T - 1 - k, tl = t - t0, s = k % 3;
       typedef __attribute__((address_space(3))) void lds_t;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {   // gates: 16 rows x 64 fp32
+      for (int q = 0; q < 4; ++q) {   // gates: 16 rows x 64 fp32, swizzled (pt_swz64)
         const int r = 4 * q + (lane >> 4), b = min(mb * PT_ROWS + r, B - 1);
-        __builtin_amdgcn_global_load_lds(a.gates + ((size_t)tl * B + b) * G + j * PL_GCOLS + 4 * (lane & 15),
+        __builtin_amdgcn_global_load_lds(a.gates + ((size_t)tl * B + b) * G + j * PL_GCOLS + 4 * ((lane & 15) ^ r),
                                          (lds_t*)(gl[s] + q * 256), 16, 0, 0);
       }
-      const int r = lane >> 2, b = min(mb * PT_ROWS + r, B - 1);
-      const size_t hidx = (size_t)b * H + j * PL_UNITS + 4 * (lane & 3);
+      const int r = lane >> 2, b = min(mb * PT_ROWS + r, B - 1);   // 16-float rows (pt_swz16)
+      const size_t hidx = (size_t)b * H + j * PL_UNITS + 4 * ((lane & 3) ^ (r >> 2));
       __builtin_amdgcn_global_load_lds(a.c_seq + (size_t)t * B * H + hidx, (lds_t*)cl[s], 16, 0, 0);
       __builtin_amdgcn_global_load_lds((t == 0 ? a.c0 : a.c_seq + (size_t)(t - 1) * B * H) + hidx,
                                        (lds_t*)cpl[s], 16, 0, 0);
@@ -1396,7 +1410,8 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
     lds_sync();                           // barrier A_k
     // ---- pointwise (row prow, unit ul)
     const int s3 = k % 3;
-    float dh = a.dh_ext ? dhl[s3][prow * PL_UNITS + ul] : 0.f;
+    const int o16 = pt_swz16(prow, ul);
+    float dh = a.dh_ext ? dhl[s3][o16] : 0.f;
     if (k > 0) {
       if constexpr (T4)
         dh += ((red[0][prow * PL_UNITS + ul] + red[1][prow * PL_UNITS + ul]) + red[T4 ? 2 : 0][prow * PL_UNITS + ul]) +
@@ -1404,9 +1419,10 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
       else
         dh += red[0][prow * PL_UNITS + ul] + red[1][prow * PL_UNITS + ul];
     }
-    const float* gq = gl[s3] + prow * PL_GCOLS + ul;
-    const float gi = gq[0], gf = gq[16], gg = gq[32], go = gq[48];
-    const float ct = cl[s3][prow * PL_UNITS + ul], cpv = cpl[s3][prow * PL_UNITS + ul];
+    const float* gq = gl[s3];
+    const float gi = gq[pt_swz64(prow, ul)], gf = gq[pt_swz64(prow, ul + 16)];
+    const float gg = gq[pt_swz64(prow, ul + 32)], go = gq[pt_swz64(prow, ul + 48)];
+    const float ct = cl[s3][o16], cpv = cpl[s3][o16];
     const float tc = tanhf_(ct);
     const float dc = dcr + dh * go * (1.f - tc * tc);
     const float d_o = dh * tc;
