@@ -755,9 +755,9 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int r = 4 * q + (lane >> 4), c4 = lane & 15, b = mb * PT_ROWS + r;
-          if (b < B)
+          if (b < B)   // og rows are chunk-swizzled (pt_swz64)
             *(f32x4*)(cd.gates + ((size_t)(t - cd.save_from) * B + b) * G + j * PL_GCOLS + 4 * c4) =
-                *(const f32x4*)(og[s] + r * PL_GCOLS + 4 * c4);
+                *(const f32x4*)(og[s] + r * PL_GCOLS + (((c4 ^ r) & 15) << 2));
         }
       }
     };
@@ -986,12 +986,12 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
       oh32[s][prow * PL_UNITS + ul] = hv;
       ohs[s][prow * PL_UNITS + ul] = (bf16)hv;
       if constexpr (SP) ohsl[s][prow * PL_UNITS + ul] = sp_lo(hv);
-      if (save_any) {
-        float* gq = og[s] + prow * PL_GCOLS + ul;
-        gq[0] = si;
-        gq[16] = sf;
-        gq[32] = tg;
-        gq[48] = so;
+      if (save_any) {   // swizzled (pt_swz64): a plain 64-float row stride put a wave on one bank
+        float* gq = og[s];
+        gq[pt_swz64(prow, ul)] = si;
+        gq[pt_swz64(prow, ul + 16)] = sf;
+        gq[pt_swz64(prow, ul + 32)] = tg;
+        gq[pt_swz64(prow, ul + 48)] = so;
       }
     }
   }
@@ -1369,7 +1369,7 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
       f32x4 sum = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < SRC4; ++i) sum += __builtin_bit_cast(f32x4, v[i] & ~15u);
-      *(f32x4*)(red[T4 ? sq : 0] + cr4 * PL_UNITS + cq4) = sum;
+      *(f32x4*)(red[T4 ? sq : 0] + pt_swz16(cr4, cq4)) = sum;   // read back at o16
     } else if (k > 0) {
       const unsigned want = (ep << 16) | (unsigned)k;
       const int slot = (k - 1) & 1;
@@ -1414,8 +1414,7 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
     float dh = a.dh_ext ? dhl[s3][o16] : 0.f;
     if (k > 0) {
       if constexpr (T4)
-        dh += ((red[0][prow * PL_UNITS + ul] + red[1][prow * PL_UNITS + ul]) + red[T4 ? 2 : 0][prow * PL_UNITS + ul]) +
-              red[T4 ? 3 : 0][prow * PL_UNITS + ul];
+        dh += ((red[0][o16] + red[1][o16]) + red[T4 ? 2 : 0][o16]) + red[T4 ? 3 : 0][o16];
       else
         dh += red[0][prow * PL_UNITS + ul] + red[1][prow * PL_UNITS + ul];
     }
