@@ -68,7 +68,7 @@ def main(argv=None):
                     help="after the timed run, time each phase of 5 eager steps with HIP events "
                          "(+ roctx ranges) and add them to the JSON line under 'phases_ms'")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
-                    help="config override, e.g. --set learner.fwd_chunks=2 (A/B experiments)")
+                    help="config override, e.g. --set learner.lstm_xcd_pairs=0 (A/B experiments)")
     args = ap.parse_args(argv)
 
     import torch

@@ -138,9 +138,10 @@ __global__ __launch_bounds__(256) void actor_pre_kernel(const ActArgs a) {
   const long long base = (long long)e * a.cap_e, row = base + head;
   // 1. rows about to be overwritten stop being sequence starts (deferred: defer_D rows ahead)
   if (a.defer_D > 0) {
+    // no wrap clears here: the D-ahead clears already invalidated rows cap_e-W+1 .. cap_e-1
+    // before this step, and a clear queued now would share the pending list with this step's
+    // start mark at head-W+1 (the apply kernel runs its entries in no fixed order)
     if (tid == 0) pend_push(a, -2 - (int)(base + (head + a.defer_D) % a.cap_e));
-    if (a.wrap)
-      for (int i = tid; i < a.W - 1; i += blockDim.x) pend_push(a, -2 - (int)(base + a.cap_e - a.W + 1 + i));
   } else {
     if (tid == 0) clear_row(a, row);
     if (a.wrap)

@@ -66,6 +66,13 @@ __device__ bool parse_record(const IngestArgs& a, RecView& v) {
     off += pad64(v.nbytes[f]);
   }
   if (off > a.rec_bytes || v.n < 0) return false;
+  // every field must hold n rows of its declared width (a header whose n exceeds its payload
+  // would make the row scatter read past the record)
+  for (int f = 0; f < ING_FIELDS; ++f) {
+    if (v.code[f] < 0 || v.code[f] > 2 || v.per_row[f] < 1) return false;
+    const long long esz = v.code[f] == 2 ? 4 : 1;
+    if (v.nbytes[f] < v.n * v.per_row[f] * esz) return false;
+  }
   // state uint8 x FB, states fp32 x 2H, 1-byte or fp32 scalars
   if (v.code[0] != 0 || v.per_row[0] != a.FB) return false;
   if (v.code[1] != 2 || v.per_row[1] != a.H2 || v.code[2] != 2 || v.per_row[2] != a.H2) return false;
@@ -137,9 +144,10 @@ __global__ __launch_bounds__(256) void ingest_rows_kernel(const IngestArgs a) {
 
 __global__ void ingest_tail_kernel(const IngestArgs a) {
   if (threadIdx.x != 0) return;
-  const long long* h = reinterpret_cast<const long long*>(a.rec);
-  if (h[0] != ING_MAGIC || h[1] < 0) return;
-  const long long keep = h[1] < a.cap_e ? h[1] : a.cap_e;
+  // the head and the counter advance only for a record the rows kernel accepted (same parse)
+  RecView v;
+  if (!parse_record(a, v)) return;
+  const long long keep = v.n < a.cap_e ? v.n : a.cap_e;
   a.ihead[a.sub] = (a.ihead[a.sub] + keep) % a.cap_e;
   *a.rows_total += keep;
 }

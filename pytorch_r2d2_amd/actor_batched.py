@@ -322,6 +322,11 @@ class BatchedActor:
         both nets, then actor.hip's fused bookkeeping around the device env step."""
         k = kernels()
         s = stream_handle()
+        if self.cfg.actor.reset_state_every_step:   # ablation: memoryless acting
+            for key in ("on", "tg"):
+                self.h_bf[key].zero_()
+                self.h32[key].zero_()
+                self.c[key].zero_()
         self._infer()
         a = self._args(wrap, parity)
         check(k.r2_actor_pre(ctypes.byref(a), s), "actor_pre")

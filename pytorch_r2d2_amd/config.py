@@ -32,6 +32,11 @@ class EnvConfig:
     channels_per_frame: int = 1       # 1 = gray (Atari), 3 = RGB (DMLab)
     n_actions: int = 6                # model.py:35 (Pong)
     episode_len: int = 400            # synthetic env only
+    # synthetic cue task: the rewarded action changes every ``switch`` agent steps; with
+    # ``cue_only_first`` its cue is drawn only on the first frame after a change, so acting well
+    # needs memory (a memoryless policy scores (1/switch + (1 - 1/switch)/A) per step)
+    switch: int = 8
+    cue_only_first: bool = False
     obs_dim: int = 4                  # vector envs (CartPole)
 
 
@@ -101,20 +106,9 @@ class LearnerConfig:
     # words with a 4-bit tag (lstm_persist.hip T4) -- False = the 8-byte {value, tag} granules
     # (A/B probes; process-wide kernel switch, set by the engine at construction)
     lstm_tag_words: bool = True
-    # tagged BPTT: GEMMs run beside the recurrence on the launch's helper workgroups
-    # ("w" = weight gradients, "x" = dX; comma-separated, "" = none).  Off by default: measured
-    # 0.799 ms/step without, 0.860 with "w", 0.987 with "x", 0.942 with both (atari57, 1 GPU) --
-    # a helper's K tiles are paced by the recurrence and each costs more than a BPTT step
-    bptt_helpers: str = ""
     # post-BPTT GEMMs: "group" = weight gradients + dX in one grid (58 us vs 85 separate),
     # "group:a,b,c,d" = with K splits, "separate"
     bwd_gemm: str = "group"
-    # forward pipelining ("shifted" mode, persistent LSTM): the frames are processed in this many
-    # time chunks; the recurrence of chunk c runs on a side stream on CUs the torso leaves free
-    # while the torso + input projection of chunk c+1 run.  0/1 = serial forward (default:
-    # measured 1.146 ms/step at 5 chunks vs 0.993 serial -- each cross-stream graph edge costs
-    # ~15 us and a chunk's x-projection GEMM is tile-latency bound; profiles/r01_v9_pipelined.txt)
-    fwd_chunks: int = 0
     td_fuse_head_bwd: bool = True     # dueling-head backward inside the TD launch (td_duel_kernel)
     # ... and the heads' dueling FORWARD too (fixed / reference target modes: the TD launch forms
     # relu(z + b1) and the Q rows of all three heads itself; no separate dueling_fwd launch)
@@ -126,7 +120,6 @@ class LearnerConfig:
     # groups per XCD, so every group's h hand-off stays in one XCD's L2 (else spread over all XCDs:
     # write-through stores, fabric-latency polls)
     lstm_xcd_pairs: bool = True
-    dh_gemm: str = "blaslt"           # head backward dh = dz @ W1: blaslt (hipBLASLt) | mfma
     # split precision (compute_dtype fp32) GEMMs: "fused" = gemm_sp.hip (hi / lo planes staged
     # once, 3 MFMAs per fragment pair: x-projection 164 -> 125 us, post-BPTT group 142 -> 106 us
     # at K splits 4,4,4,1, dh 26 -> 18 us; profiles/r02_gemm_sp_micro_v1.txt) | "multipass"
@@ -141,6 +134,10 @@ class LearnerConfig:
     conv_autotune: bool = True
     use_graph: bool = True            # capture the whole step in a HIP graph
     save_dir: str = "save"
+    # ablation (tools/learn_check.py): ignore the stored recurrent state of every sampled
+    # sequence (zeros instead of the actor's (h, c)); with burn_in = 0 the learner has no context
+    # from before the sequence start
+    zero_stored_state: bool = False
 
 
 @dataclass
@@ -156,6 +153,9 @@ class ActorConfig:
     # wrap); needs a device env whose step() is capture-safe (VecSyntheticAtari)
     use_graph: bool = True
     return_ring: int = 4096           # device ring of finished-episode returns (drained lazily)
+    # ablation (tools/learn_check.py): reset both nets' LSTM state before every env step -- a
+    # memoryless acting policy (with seq_len 1 and zeroed stored state, a memoryless learner)
+    reset_state_every_step: bool = False
 
 
 @dataclass
@@ -241,7 +241,9 @@ def _pong() -> R2D2Config:
     c = R2D2Config(name="pong")
     c.env = EnvConfig(name="synthetic", n_actions=6)
     c.replay = ReplayConfig(capacity=2_000_000, n_subrings=64)
-    c.learner = LearnerConfig(batch_size=8, target_mode="shifted")
+    # the reference's own game: its precision (fp32) and its 3-chain target structure with Q7
+    # fixed (learner.py:71-93), like the ``reference`` preset
+    c.learner = LearnerConfig(batch_size=8, target_mode="fixed", compute_dtype="fp32")
     c.actor = ActorConfig(n_actors=1, envs_per_actor=64)
     return c
 

@@ -16,8 +16,9 @@ local replay as ONE packed record (``parallel.trajectory.pack_rows``: header + S
    (``csrc/kernels/ingest.hip``: the record is parsed on the device, rows scattered into the
    actor's sub-ring at a device-side write head, start flags / leaves / n_valid updated, changed
    leaves appended to the dirty list),
-4. repairs the sum tree from the dirty list (a full rebuild only for records larger than half
-   the dirty list),
+4. repairs the sum tree from the dirty list -- a full rebuild once the poll's records together
+   could overflow half the dirty list (every record of a poll appends to the same list before
+   the one repair at its end),
 5. releases the ring bytes once the DMA has completed (event query, never a blocking sync on
    the learner stream).
 
@@ -32,7 +33,7 @@ import numpy as np
 import torch
 
 from ..ops._lib import check, kernels, ptr, stream_handle
-from ..parallel.trajectory import ShmTrajectoryReader, header_bytes, record_layout
+from ..parallel.trajectory import ShmTrajectoryReader, header_bytes, validate_record
 
 _VP = ctypes.c_void_p
 
@@ -92,6 +93,7 @@ class HBMIngestor:
         self.rows = 0
         self.records = 0
         self.bytes = 0
+        self.rejected = 0               # records whose header failed validation (dropped)
 
     def _dev_slot(self, nbytes: int) -> torch.Tensor:
         k = self.slot
@@ -124,6 +126,10 @@ class HBMIngestor:
         learner = self.stream if self.stream is not None else torch.cuda.current_stream(self.rp.device)
         rows_here, done = 0, 0
         big = False
+        # dirty entries the poll's records may append before the single repair below: each kept
+        # row can change one leaf; past half the list every later record skips it and the tree
+        # is rebuilt (the kernel drops entries beyond max_dirty without a trace)
+        budget, used = self.rp.max_dirty // 2, 0
         for i, r in enumerate(self.readers):
             if done >= max_records or i in busy:
                 continue
@@ -131,7 +137,12 @@ class HBMIngestor:
             if fr is None:
                 continue
             addr, n = fr
-            n_rows, _ = record_layout(np.frombuffer(ctypes.string_at(addr, header_bytes()), np.uint8))
+            n_rows = validate_record(np.frombuffer(ctypes.string_at(addr, min(n, header_bytes())),
+                                                   np.uint8), n, self.rp.frame_bytes, 2 * self.rp.H)
+            if n_rows is None:          # malformed: dropped before any DMA, never counted
+                r.ring.release()
+                self.rejected += 1
+                continue
             k = self._dev_slot(n)
             dst = self.dev_buf[k]
             if self.registered[i] is not None:
@@ -153,12 +164,13 @@ class HBMIngestor:
             else:
                 self.pin_event.record(self.copy_stream)
             learner.wait_event(ev)
-            use_dirty = min(n_rows, self.rp.cap_e) * 2 <= self.rp.max_dirty
+            kept = min(n_rows, self.rp.cap_e)
+            use_dirty = not big and used + kept <= budget
             big |= not use_dirty
+            used += kept if use_dirty else 0
             a = ingest_args(self.rp, ptr(dst), n, i, use_dirty)
             check(kernels().r2_ingest_record(ctypes.byref(a), _VP(stream_handle(learner))), "ingest")
             self.dev_done[k].record(learner)
-            kept = min(n_rows, self.rp.cap_e)
             rows_here += kept
             done += 1
             self.bytes += n
@@ -169,6 +181,11 @@ class HBMIngestor:
             self.records += done
             self.rp.total_written += rows_here
         return rows_here
+
+    def check_errors(self) -> None:
+        """Raise if the device ingest rejected a record (one D2H read; call at check points)."""
+        if int(self.rp.ingest_err.item()) != 0:
+            raise RuntimeError("device ingest rejected a malformed trajectory record")
 
     def close(self) -> None:
         self._release_done(wait=True)

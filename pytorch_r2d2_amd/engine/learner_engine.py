@@ -15,7 +15,7 @@ priority scatters.  Here a step is:
     head      [val.0;adv.0] GEMM + fused dueling epilogue kernel (every head in one launch)
     td        fused double-Q n-step target / loss / dL/dQ / IS weights / row priorities, with
               the dueling head's backward (dz, dva) in the same launch (td_duel_kernel)
-    backward  dh GEMM (hipBLASLt), persistent BPTT (fused bias-gradient column sums;
+    backward  dh = dz W1 (on the TD launch's MFMAs), persistent BPTT (fused bias-gradient column sums;
               head-gradient reduction on its idle workgroups), weight-gradient + dX GEMMs in
               one grouped launch, fused conv backward from the saved activations
     allreduce (DP) bucket "core" beside the conv backward (which leaves CUs to RCCL), bucket
@@ -54,35 +54,6 @@ from ..ops.torso_lib import (fused_torso_fwd_geom, fused_torso_supported, gather
                              torso_forward_library, torso_fwd_fused)
 from .layout import ParamLayout, UNITS
 from .replay_hbm import HBMReplay
-
-_HAS_MM_DTYPE = None
-
-
-def mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """bf16 x bf16 -> fp32 output library GEMM (hipBLASLt), fallback to bf16 out + cast."""
-    global _HAS_MM_DTYPE
-    if _HAS_MM_DTYPE is not False:
-        try:
-            out = torch.mm(a, b, out_dtype=torch.float32)
-            _HAS_MM_DTYPE = True
-            return out
-        except (RuntimeError, TypeError):
-            _HAS_MM_DTYPE = False
-    return torch.mm(a, b).float()
-
-
-def addmm_f32(bias: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """bias + a @ b with bf16 operands and fp32 output (bias fused into the GEMM epilogue)."""
-    global _HAS_MM_DTYPE
-    if _HAS_MM_DTYPE is not False:
-        try:
-            out = torch.addmm(bias, a, b, out_dtype=torch.float32)
-            _HAS_MM_DTYPE = True
-            return out
-        except (RuntimeError, TypeError):
-            _HAS_MM_DTYPE = False
-    return torch.mm(a, b).float() + bias
-
 
 def device_cus(device) -> int:
     """Multiprocessor (CU) count of ``device`` (256 on a whole MI355X; 256 for CPU tensors)."""
@@ -298,12 +269,16 @@ class LearnerEngine:
             self._tb_slab = z(self._tb_grid * n_slab)
             dst, scale = L.torso_grad_map()
             self._tb_dst, self._tb_scale = dst.to(d), scale.to(d)
-        self.ones_bf = torch.ones(1, Tn * B, dtype=bf16, device=d)
-        self.ones_f32 = torch.ones(1, Tn * B, dtype=f32, device=d)
-        # hand-written MFMA GEMM path (csrc/kernels/gemm.hip): K and the mn-major extents must be
-        # multiples of 8; otherwise the library GEMMs below are used
-        self.use_gemm = (d.type == "cuda" and (Ll * B) % 8 == 0 and D % 8 == 0 and H % 8 == 0
-                         and (2 * HD) % 8 == 0 and G % 8 == 0)
+        # every GEMM of the step is a hand-written MFMA kernel (gemm.hip / gemm_sp.hip): K and the
+        # mn-major extents must be multiples of 8
+        if not ((Ll * B) % 8 == 0 and D % 8 == 0 and H % 8 == 0 and (2 * HD) % 8 == 0 and G % 8 == 0):
+            raise NotImplementedError(
+                f"learn * batch ({Ll}*{B}), the torso width {D}, hidden {H} and head width {2 * HD} "
+                "must be multiples of 8 (MFMA GEMM operands); use the torch learner (learner_ref.py)")
+        self.use_gemm = True
+        if A > 63 or HD % 64 != 0:
+            raise NotImplementedError("the fused head kernels support <= 63 actions and a head "
+                                      "width that is a multiple of 64")
         self.xp_on = z(Tn * B, G)
         self.xp_tg = z(self.X_tg.shape[0], G)
         self.z_on = z(self.Nh, 2 * HD, dt=act_dt)
@@ -311,8 +286,6 @@ class LearnerEngine:
         if mode != "shifted":
             self.z_nx = z(Nnx, 2 * HD, dt=act_dt)
         self.dh = z(Ll * B, H)
-        self._chunks = self._plan_chunks()
-        self._side = torch.cuda.Stream(device=d) if self._chunks is not None else None
         self.dX, self.dX_lo = zsp(Ll * B, D)
         self.gate_perm_i32 = L.gate_perm.to(d, torch.int32)
         self.gs_ws = torch.zeros(int(kernels().r2_gradsum_ws_floats()), dtype=torch.float32, device=d)
@@ -442,11 +415,9 @@ class LearnerEngine:
             gemm(*[Gemm(h, pk["head1"].t(), zb, a_lo=hl, b_lo=pkl["head1"].t())
                    for (pk, h, zb, _, _), (pkl, hl) in zip(jobs, lo)])
             zs = [zb for _, _, zb, _, _ in jobs]
-        elif self.use_gemm:
+        else:
             gemm(*[Gemm(h, pk["head1"].t(), zb) for pk, h, zb, _, _ in jobs])
             zs = [zb for _, _, zb, _, _ in jobs]
-        else:
-            zs = [torch.mm(h, pk["head1"].t()) for pk, h, _, _, _ in jobs]
         self._zs = zs
         if duel:
             self._duel_fwd(jobs, zs)
@@ -459,40 +430,6 @@ class LearnerEngine:
         fn = kernels().r2_dueling_fwd_multi_f32 if self.sp else kernels().r2_dueling_fwd_multi
         check(fn(self._djobs.ctypes.data, len(jobs), self.layout.A, self.layout.HD, stream_handle()),
               "dueling_fwd")
-
-    # ------------------------------------------------------------------ pipelined forward
-    def _plan_chunks(self):
-        """Time-chunk boundaries of the pipelined forward, or None for the serial forward.
-
-        The pipeline: chunk c's torso (both nets, one launch) and input projection (one GEMM
-        launch) run on the main stream; its recurrence (both chains, one persistent launch) runs
-        on a side stream while the torso of chunk c+1 proceeds on the CUs the LSTM does not use
-        (``r2_torso_fwd_multi`` reserve).  Chunk 0 has no LSTM beside it and gets the whole chip,
-        so it is the longest; the last chunk is short because its recurrence is not overlapped.
-        """
-        lc = self.cfg.learner
-        k = int(getattr(lc, "fwd_chunks", 0) or 0)
-        H = self.layout.H
-        groups = 2 * ((self.B + 31) // 32)
-        if (k < 2 or self.mode != "shifted" or lc.lstm_impl != "persistent" or not self.fused_torso
-                or self.n_cus != 256
-                or not self.use_gemm or self.device.type != "cuda" or groups > 8):
-            return None
-        Tc = self.Tc
-        first = max(1, int(round(0.42 * Tc)))
-        rest = Tc - first
-        w = [1.0] * (k - 2) + [0.6]
-        cuts, acc = [0, first], float(first)
-        for wi in w[:-1]:
-            acc += rest * wi / sum(w)
-            cuts.append(int(round(acc)))
-        cuts.append(Tc)
-        cuts = sorted(set(c for c in cuts if 0 <= c <= Tc))
-        if len(cuts) < 3:
-            return None
-        # LSTM placement (lstm_persist.hip): group g on XCD g, H/16 workgroups each
-        self._reserve = (groups, H // UNITS)
-        return cuts
 
     def _torso_job(self, pk, rows, out, save_at=None):
         B = self.B
@@ -517,45 +454,6 @@ class LearnerEngine:
                 ptr(pk["conv2"]), ptr(pkl["conv2"]), ptr(pk["b2"]), ptr(pk["conv3"]),
                 ptr(pkl["conv3"]), ptr(pk["b3"]), ptr(out), ptr(out_lo)] + s + [0, 0, 0]
 
-    def _forward_pipelined(self):
-        k = kernels()
-        B, Lb, T = self.B, self.Lb, self.T
-        pk, pt = self.pk, self.pk_t
-        rows, cuts = self.rows, self._chunks
-        main = torch.cuda.current_stream()
-        side = self._side
-        rx, rs = self._reserve
-        side.wait_stream(main)                      # stored states + row list are ready
-        for c, (t0, t1) in enumerate(zip(cuts[:-1], cuts[1:])):
-            jobs = []
-            # online frames, split where the saved-activation window [Lb, T) begins / ends
-            edges = sorted({t0, t1} | {e for e in (Lb, T) if t0 < e < t1})
-            for a, b in zip(edges[:-1], edges[1:]):
-                save = (a - Lb) if (Lb <= a and b <= T) else None
-                jobs.append(self._torso_job(pk, rows[a * B:b * B], self.X_on[a * B:b * B], save))
-            jobs.append(self._torso_job(pt, rows[t0 * B:t1 * B], self.X_tg[t0 * B:t1 * B]))
-            arr = np.asarray(jobs, dtype=np.int64)
-            check(k.r2_torso_fwd_multi(ptr(self.replay.frames), arr.ctypes.data, len(jobs), 256,
-                                       rx if c > 0 else 0, rs if c > 0 else 0, stream_handle(main)),
-                  "torso_fwd_multi")
-            r0, r1 = t0 * B, t1 * B
-            gemm(Gemm(self.X_on[r0:r1], pk["w_ih"].t(), self.xp_on[r0:r1], bias=self.lstm_b),
-                 Gemm(self.X_tg[r0:r1], pt["w_ih"].t(), self.xp_tg[r0:r1], bias=self.lstm_b_t))
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                chains = []
-                for key, p_, xp in (("on", pk, self.xp_on), ("tg", pt, self.xp_tg)):
-                    h0 = self.h0[key] if t0 == 0 else self.hseq[key][t0 - 1]
-                    c0 = self.c0[key] if t0 == 0 else self.cseq[key][t0 - 1]
-                    gates, save_from = None, 0
-                    if key == "on" and t1 > Lb:
-                        gates = self.gates[max(t0 - Lb, 0):]
-                        save_from = max(Lb - t0, 0)
-                    chains.append(self._chain_desc(xp[r0:], p_, h0, c0, self.hseq[key][t0:],
-                                                   self.cseq[key][t0:], gates, save_from))
-                self._lstm(chains, t1 - t0)
-        main.wait_stream(side)
-
     # ------------------------------------------------------------------ the step
     def _forward_loss(self):
         self._sample()
@@ -574,6 +472,10 @@ class LearnerEngine:
         if self.mode == "fixed":
             states.append((rp.hs_cs, n, self.h0["nx"], self.c0["nx"]))
         rp.sample_batch(B, self.starts, self.probs, self.rows, Tn, states, h_f32=self.sp)
+        if self.cfg.learner.zero_stored_state:     # ablation: no stored recurrent state
+            for _, _, h, c in states:
+                h.zero_()
+                c.zero_()
         if self.dp_global:
             from ..parallel.sharded_replay import local_stats
             root = rp.tree[int(rp.tree_offs[-1]): int(rp.tree_offs[-1]) + 1]
@@ -596,11 +498,6 @@ class LearnerEngine:
         H, A = L.H, L.A
         pk, pt = self.pk, self.pk_t
         rows = self.rows
-        if self._chunks is not None:
-            self._forward_pipelined()
-            xp_on, xp_tg = self.xp_on, self.xp_tg
-            self._xp = (xp_on, xp_tg)
-            return self._forward_tail() if tail else None
         # torso: online over all Tn frames (save activations of the learning frames) and target
         if self.sp:
             pkl, ptl = self.pk_lo, self.pk_t_lo
@@ -638,13 +535,10 @@ class LearnerEngine:
                      b_lo=self.pk_lo["w_ih"].t()),
                 Gemm(self.X_tg, pt["w_ih"].t(), xp_tg, bias=self.lstm_b_t, a_lo=self.X_tg_lo,
                      b_lo=self.pk_t_lo["w_ih"].t())])
-        elif self.use_gemm:
+        else:
             xp_on, xp_tg = self.xp_on, self.xp_tg
             gemm(Gemm(self.X_on, pk["w_ih"].t(), xp_on, bias=self.lstm_b),
                  Gemm(self.X_tg, pt["w_ih"].t(), xp_tg, bias=self.lstm_b_t))
-        else:
-            xp_on = addmm_f32(self.lstm_b, self.X_on, pk["w_ih"].t())
-            xp_tg = addmm_f32(self.lstm_b_t, self.X_tg, pt["w_ih"].t())
         self._xp = (xp_on, xp_tg)
         G = L.G
         hl = self.hseq_lo
@@ -699,7 +593,7 @@ class LearnerEngine:
         # fixed / reference modes: the three Q rows of transition i are row i of each head, so the
         # TD launch can run the dueling forward itself (td.hip td_duel_row)
         fuse_fwd = (lc.td_fuse_head_bwd and lc.td_fuse_head_fwd and self.mode != "shifted"
-                    and A <= 32 and self.use_gemm)
+                    and A <= 32)
         self._heads(jobs, lo, duel=not fuse_fwd)
         if self.mode == "shifted":
             q_sa = self.q_on[: Ll * B]
@@ -723,7 +617,7 @@ class LearnerEngine:
         self._dh_done = False
         if lc.td_fuse_head_bwd:
             # + dh = dz @ W1 for the BPTT, on the same launch's MFMAs (16 rows per workgroup)
-            fuse_dh = lc.td_fuse_dh and L.H == 256 and self.use_gemm
+            fuse_dh = lc.td_fuse_dh and L.H == 256
             w1t = ptr(pk["head1T"]) if fuse_dh else 0
             w1t_lo = ptr(self.pk_lo["head1T"]) if fuse_dh and self.sp else 0
             if fuse_fwd:
@@ -849,99 +743,50 @@ class LearnerEngine:
         H, A, HD, G = L.H, L.A, L.HD, L.G
         N = Ll * B
         zr = self.zr_on[:N]
-        if not getattr(self, "_duel_done", False):      # else fused into the TD launch
+        if not self._duel_done:      # else fused into the TD launch
             check(k.r2_dueling_bwd(ptr(self.dq), ptr(zr), ptr(pk["head_w2"]), ptr(self.dz),
                                    ptr(self.dva), N, A, HD, s), "dueling_bwd")
         g = self.grad
         gw2 = L.span(g, "val.2.weight", "adv.2.weight", (1 + A, HD))
         gb2 = L.span(g, "val.2.bias", "adv.2.bias", (1, 1 + A))
         gb1 = L.span(g, "val.0.bias", "adv.0.bias", (1, 2 * HD))
-        # gradsum.hip head_grads: any head up to 63 actions (Seaquest 18, DMLab 15) in one launch
-        fused_hg = self.use_gemm and A <= 63 and HD % 64 == 0
-        lc = self.cfg.learner
-        # the tagged BPTT kernel's idle workgroups take the head-gradient reduction beside the
-        # recurrence when they are enough; otherwise it runs as its own launch here
-        tagged = lc.lstm_impl == "persistent" and lc.lstm_handoff == "tagged"
-        self._hg_job = None
-        if fused_hg and tagged:
-            self._hg_job = [ptr(self.dva), ptr(zr), ptr(self.dz), ptr(gw2), ptr(gb2), ptr(gb1),
-                            N, A, HD, ptr(self.gs_ws), ptr(self.gs_ticket)]
-        elif fused_hg:
-            # last-layer weight/bias grads and the layer-1 bias grads in one deterministic
-            # column-reduction launch (gradsum.hip), written in place into the flat buffer
-            check(k.r2_head_grads(ptr(self.dva), ptr(zr), ptr(self.dz), ptr(gw2), ptr(gb2),
-                                  ptr(gb1), N, A, HD, ptr(self.gs_ws), ptr(self.gs_ticket), s),
-                  "head_grads")
-        else:
-            g2 = torch.mm(self.dva.t(), zr.float())                      # (1+A, 2HD)
-            gw2[0].copy_(g2[0, :HD])
-            gw2[1:].copy_(g2[1:, HD:])
-            # column sums as GEMVs against a ones row (torch's dim-0 reduce is ~300 us here)
-            torch.mm(self.ones_f32[:, :N], self.dva, out=gb2)
+        # gradsum.hip head_grads (any head up to 63 actions: Seaquest 18, DMLab 15): last-layer
+        # weight / bias grads and the layer-1 bias grads in one deterministic column reduction,
+        # on the tagged BPTT launch's idle workgroups when they are enough, else its own launch
+        self._hg_job = [ptr(self.dva), ptr(zr), ptr(self.dz), ptr(gw2), ptr(gb2), ptr(gb1),
+                        N, A, HD, ptr(self.gs_ws), ptr(self.gs_ticket)]
         h_learn = self.hseq["on"][Lb:T].reshape(N, H)
         gw1 = L.span(g, "val.0.weight", "adv.0.weight", (2 * HD, H))
-        if self.use_gemm:
-            dh = self.dh
-            # a plain 40-tile GEMM (M=2560, N=256, K=512): hipBLASLt runs it in 7.4 us vs 13.1
-            # for the 128x128 MFMA kernel and 18-45 us split-K (tools/dh_split_probe.py); by
-            # default it is fused into the TD launch instead (learner.td_fuse_dh)
-            if getattr(self, "_dh_done", False):
-                pass
-            elif lc.dh_gemm == "blaslt":
-                torch.mm(self.dz, pk["head1"], out_dtype=torch.float32, out=dh)   # (N, H) fp32
-            else:
-                gemm(Gemm(self.dz, pk["head1"], dh))
-        else:
-            gw1.copy_(mm_f32(self.dz.t(), h_learn))
-            dh = mm_f32(self.dz, pk["head1"])                           # (N, H)
-        if not fused_hg:
-            gb1.copy_(mm_f32(self.ones_bf[:, :N], self.dz))
+        dh = self.dh
+        if not self._dh_done:        # else dh = dz W1 ran on the TD launch's MFMAs
+            gemm(Gemm(self.dz, pk["head1"], dh))
         X = self.X_on[Lb * B: T * B]
         if Lb >= 1:
             h_prev = self.hseq["on"][Lb - 1: T - 1].reshape(N, H)
         else:
             h_prev = torch.cat([self.h0["on"][None], self.hseq["on"][: T - 1]]).reshape(N, H)
-        w_jobs = x_job = None
-        if self.use_gemm:
-            # weight gradients straight into the flat buffer; the row map puts the packed gate
-            # order back into torch order (no gather of dgates, no copies)
-            dgT = self.dgates.t()
-            w_jobs = [Gemm(self.dz.t(), h_learn, gw1),
-                      Gemm(dgT, h_prev, L.view(g, "lstm.weight_hh"), crow=self.gate_perm_i32),
-                      Gemm(dgT, X, L.view(g, "lstm.weight_ih"), crow=self.gate_perm_i32)]
-            x_job = Gemm(self.dgates, pk["w_ih"], self.dX)                # (N, D) bf16
-        # tagged BPTT: these GEMMs run on helper workgroups of the same launch, each K / row
-        # tile as soon as the recurrence has stored the dgates it reads
-        helpers = lc.bptt_helpers.split(",")
-        ok = tagged and N % 64 == 0
-        bias_done, taken = self._lstm_bwd(dh, w_jobs if ok and "w" in helpers else None,
-                                          x_job if ok and "x" in helpers else None)
-        if self.use_gemm:
-            splits = self._group_splits(w_jobs, x_job) if not taken & 6 else None
-            if splits:
-                # weight gradients and dX share one grid (gemm_group_kernel), longest K first
-                gemm_group([w_jobs[2], w_jobs[1], w_jobs[0], x_job], splits,
-                           self.gg_ws, self.gg_tickets)
-                taken |= 6
-            if not taken & 2:
-                gemm(w_jobs[2], w_jobs[1], w_jobs[0])
-            # bias grads: column sums of dgates, packed -> torch gate order, into both biases
-            # (fused into the tagged BPTT kernel when it ran)
-            if not bias_done:
-                check(k.r2_colsum_bf16(ptr(self.dgates), N, G, ptr(self.gate_perm_i32),
-                                       ptr(L.view(g, "lstm.bias_ih")), ptr(L.view(g, "lstm.bias_hh")),
-                                       ptr(self.gs_ws), ptr(self.gs_ticket[32:]), s), "colsum")
-            if not taken & 4:
-                gemm(x_job)
-            self._dX = self.dX
+        # weight gradients straight into the flat buffer; the row map puts the packed gate order
+        # back into torch order (no gather of dgates, no copies)
+        dgT = self.dgates.t()
+        w_jobs = [Gemm(self.dz.t(), h_learn, gw1),
+                  Gemm(dgT, h_prev, L.view(g, "lstm.weight_hh"), crow=self.gate_perm_i32),
+                  Gemm(dgT, X, L.view(g, "lstm.weight_ih"), crow=self.gate_perm_i32)]
+        x_job = Gemm(self.dgates, pk["w_ih"], self.dX)                # (N, D) bf16
+        bias_done = self._lstm_bwd(dh)
+        splits = self._group_splits(w_jobs, x_job)
+        if splits:
+            # weight gradients and dX share one grid (gemm_group_kernel), longest K first
+            gemm_group([w_jobs[2], w_jobs[1], w_jobs[0], x_job], splits, self.gg_ws, self.gg_tickets)
         else:
-            dg_o = self.dgates.index_select(1, self.gate_inv)           # original gate order
-            L.view(g, "lstm.weight_ih").copy_(mm_f32(dg_o.t(), X))
-            L.view(g, "lstm.weight_hh").copy_(mm_f32(dg_o.t(), h_prev))
-            db = mm_f32(self.ones_bf[:, :N], dg_o).view(-1)
-            L.view(g, "lstm.bias_ih").copy_(db)
-            L.view(g, "lstm.bias_hh").copy_(db)
-            self._dX = torch.mm(self.dgates, pk["w_ih"])               # (N, D) bf16
+            gemm(w_jobs[2], w_jobs[1], w_jobs[0])
+            gemm(x_job)
+        # bias grads: column sums of dgates, packed -> torch gate order, into both biases (fused
+        # into the tagged BPTT kernel when it ran)
+        if not bias_done:
+            check(k.r2_colsum_bf16(ptr(self.dgates), N, G, ptr(self.gate_perm_i32),
+                                   ptr(L.view(g, "lstm.bias_ih")), ptr(L.view(g, "lstm.bias_hh")),
+                                   ptr(self.gs_ws), ptr(self.gs_ticket[32:]), s), "colsum")
+        self._dX = self.dX
 
     def _group_splits(self, w_jobs, x_job):
         """K splits of the grouped post-BPTT launch ([dW_ih, dW_hh, dW_head1, dX]) or None for
@@ -962,13 +807,10 @@ class LearnerEngine:
             self.gg_tickets = torch.zeros(1024, dtype=torch.int32, device=self.device)
         return splits
 
-    def _lstm_bwd(self, dh: torch.Tensor, w_jobs=None, x_job=None):
-        """BPTT over the learning window: dgates (Ll, B, G) from dh (Ll, B, H).
-
-        Returns (bias_done, taken): bias_done when the kernel also produced the LSTM bias
-        gradients (tagged BPTT, fused column sums); taken = bitmask of the side jobs its helper
-        workgroups ran (1 head grads, 2 the weight-gradient GEMMs ``w_jobs`` =
-        [gw1, dW_hh, dW_ih], 4 the dX GEMM ``x_job``)."""
+    def _lstm_bwd(self, dh: torch.Tensor) -> bool:
+        """BPTT over the learning window: dgates (Ll, B, G) from dh (Ll, B, H), plus the head
+        gradient reduction (``self._hg_job``) on the tagged launch's idle workgroups or on its own.
+        Returns True when the kernel also produced the LSTM bias gradients (tagged BPTT)."""
         k = kernels()
         s = stream_handle()
         B, T, Lb, H, pk = self.B, self.T, self.Lb, self.layout.H, self.pk
@@ -978,21 +820,17 @@ class LearnerEngine:
                     ptr(pk["w_hhT"]), ptr(self.dgates), B, T, Lb, H, ptr(self.ctr), ptr(self.err),
                     ptr(self.ring_b), ptr(self.bias_ws), ptr(self.gate_perm_i32),
                     ptr(L.view(g, "lstm.bias_ih")), ptr(L.view(g, "lstm.bias_hh"))]
-            hg = self._hg_job or [0] * 11
-            descs = [d for j in (w_jobs or []) + ([x_job] if x_job is not None else []) for d in j.desc()]
-            self._gdesc = np.asarray(descs or [0], dtype=np.int64)   # kept alive for capture
-            rc = k.r2_lstm_bwd_tag(*base, *hg, self._gdesc.ctypes.data, len(w_jobs or []),
-                                   0b110 if w_jobs else 0, int(x_job is not None), s)
-            if rc in (-6, -10):   # not enough helper workgroups: recurrence alone
-                rc = k.r2_lstm_bwd_tag(*base, *([0] * 11), 0, 0, 0, 0, s)
+            self._gdesc = np.zeros(1, dtype=np.int64)    # no GEMM side jobs (kept alive for capture)
+            rc = k.r2_lstm_bwd_tag(*base, *self._hg_job, self._gdesc.ctypes.data, 0, 0, 0, s)
+            if rc in (-6, -10):   # not enough idle workgroups for the side job: recurrence alone
+                rc = k.r2_lstm_bwd_tag(*base, *([0] * 11), self._gdesc.ctypes.data, 0, 0, 0, s)
             if rc != -3:          # -3: grid too large for one workgroup per CU
                 if rc < 0:
                     check(rc, "lstm_bwd_tag")
-                if self._hg_job is not None and not rc & 1:
+                if not rc & 1:
                     check(k.r2_head_grads(*self._hg_job, s), "head_grads")
-                return True, rc
-        if self._hg_job is not None:   # the side job did not run: its own launch
-            check(k.r2_head_grads(*self._hg_job, s), "head_grads")
+                return True
+        check(k.r2_head_grads(*self._hg_job, s), "head_grads")
         if lc.lstm_impl == "persistent":
             check(k.r2_lstm_bwd_persist(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]),
                                         ptr(self.c0["on"]), ptr(pk["w_hhT"]), ptr(self.slab_p),
@@ -1003,7 +841,7 @@ class LearnerEngine:
             check(k.r2_lstm_bwd(ptr(dh), ptr(self.gates), ptr(self.cseq["on"]), ptr(self.c0["on"]),
                                 ptr(pk["w_hhT"]), ptr(self.slab0), ptr(self.slab1), ptr(self.dc),
                                 ptr(self.dgates), B, T, Lb, H, s), "lstm_bwd")
-        return False, 0
+        return False
 
     def _relu_mask(self, grad: torch.Tensor, act: torch.Tensor) -> torch.Tensor:
         """grad * (act > 0) for two tensors with the same (channels-last) memory layout."""

@@ -22,9 +22,11 @@ def make_env(cfg, seed: int = 0):
     if e.name == "cartpole":
         return CartPoleEnv(seed=seed, max_steps=e.episode_len)
     if e.name == "dmlab_synth":
-        return DMLabSynthEnv(seed=seed, episode_len=e.episode_len, n_actions=e.n_actions)
+        return DMLabSynthEnv(seed=seed, episode_len=e.episode_len, n_actions=e.n_actions,
+                             switch=e.switch, cue_only_first=e.cue_only_first)
     return SyntheticAtariEnv(seed=seed, episode_len=e.episode_len, n_actions=e.n_actions,
-                             action_repeat=e.action_repeat, n_stacks=e.n_stacks)
+                             action_repeat=e.action_repeat, n_stacks=e.n_stacks, switch=e.switch,
+                             cue_only_first=e.cue_only_first)
 
 
 __all__ = ["PongEnv", "preprocess", "SyntheticAtariEnv", "VecSyntheticAtari", "CartPoleEnv",

@@ -28,8 +28,6 @@ CPU reference the tests check the kernels against.
 """
 from __future__ import annotations
 
-from typing import Tuple
-
 import torch
 import torch.distributed as dist
 
@@ -86,24 +84,4 @@ def dp_is_weights(probs: torch.Tensor, params: torch.Tensor, beta: float) -> tor
 def single_replay_is_weights(p: torch.Tensor, n: float, beta: float) -> torch.Tensor:
     """The single-replay formula w = (N P)^-beta / max (replay over the merged shards)."""
     w = (n * p).clamp_min(1e-30) ** (-beta)
-    return w / w.max()
-
-
-# ---------------------------------------------------------------- legacy helpers (round 1 API)
-def gather_shard_stats(total: torch.Tensor, n_valid: torch.Tensor, world: int, group=None
-                       ) -> Tuple[torch.Tensor, torch.Tensor]:
-    """total, n_valid: 1-element tensors of this shard -> (totals[world], counts[world])."""
-    v = torch.stack([total.reshape(()).float(), n_valid.reshape(()).float()])
-    if world <= 1:
-        return v[:1].clone(), v[1:].clone()
-    out = [torch.zeros_like(v) for _ in range(world)]
-    dist.all_gather(out, v, group=group)
-    allv = torch.stack(out)
-    return allv[:, 0], allv[:, 1]
-
-
-def shard_is_weights(local_probs: torch.Tensor, world: int, n_global: torch.Tensor,
-                     beta: float) -> torch.Tensor:
-    p_global = local_probs / world
-    w = (n_global * p_global).clamp_min(1e-30) ** (-beta)
     return w / w.max()

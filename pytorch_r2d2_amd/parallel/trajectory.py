@@ -57,6 +57,32 @@ def record_layout(buf_head: np.ndarray):
     return n, fields
 
 
+def validate_record(buf_head: np.ndarray, rec_bytes: int, frame_bytes: int, h2: int):
+    """Host mirror of ``parse_record`` (csrc/kernels/ingest.hip): the row count of a record whose
+    header matches the replay schema and whose fields hold all of their rows, else None."""
+    try:
+        head = np.asarray(buf_head[:24], dtype=np.uint8).view(np.int64)
+        if int(head[0]) != MAGIC or int(head[2]) != len(ORDER):
+            return None
+        n, fields = record_layout(buf_head)
+    except ValueError:
+        return None
+    end = max(off + _pad(nb) for _, _, nb, off in fields.values())
+    if n < 0 or end > rec_bytes:
+        return None
+    for code, per_row, nbytes, _ in fields.values():
+        if code not in (0, 1, 2) or per_row < 1 or nbytes < n * per_row * (4 if code == 2 else 1):
+            return None
+    c = {k: v[:2] for k, v in fields.items()}
+    if c["state"] != (0, frame_bytes) or c["hs_cs"] != (2, h2) or c["target_hs_cs"] != (2, h2):
+        return None
+    if any(c[k][0] != 2 for k in ("reward", "priority", "sequence_priority")):
+        return None
+    if c["action"][0] == 2 or c["is_seq_start"][0] == 2:
+        return None
+    return n
+
+
 def header_bytes(k: int = len(ORDER)) -> int:
     return _pad(24 + 24 * k)
 

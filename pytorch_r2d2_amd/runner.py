@@ -60,7 +60,8 @@ def run_native(cfg: R2D2Config, steps: int = 1000, actor_steps_per_update: int =
     env = VecSyntheticAtari(E, dev, seed=cfg.seed + 101 * info.rank, episode_len=cfg.env.episode_len,
                             n_actions=cfg.model.n_actions,
                             n_stacks=cfg.env.channels_per_frame * cfg.env.n_stacks,
-                            shape=(cfg.env.frame_h, cfg.env.frame_w))
+                            shape=(cfg.env.frame_h, cfg.env.frame_w), switch=cfg.env.switch,
+                            cue_only_first=cfg.env.cue_only_first)
     start = 0
     if resume:
         from .utils.checkpoint import load_full_checkpoint, restore_rng
@@ -241,6 +242,7 @@ def run_native_cpu_actors(cfg: R2D2Config, n_actors: int, steps: int = 1000,
                 version += 1
                 weights.publish(eng.master, eng.target, version)
                 eng.check_errors()
+                ingest.check_errors()
             weights.poll()
             if it % log_every == 0 or it == steps:
                 loss = eng.loss_value()
@@ -251,6 +253,7 @@ def run_native_cpu_actors(cfg: R2D2Config, n_actors: int, steps: int = 1000,
                 print("[native-cpu]", rec, flush=True)
         torch.cuda.synchronize(dev)
         eng.check_errors()
+        ingest.check_errors()
     finally:
         sup.stop()
         ingest.close()
@@ -260,6 +263,7 @@ def run_native_cpu_actors(cfg: R2D2Config, n_actors: int, steps: int = 1000,
                wall_s=t_end - t0, ingest_host_s=t_ing,
                learner_steps_per_s=(it / (t_end - t_train0)) if t_train0 and it else 0.0,
                ingest_rows_per_s=ingest.rows / (t_end - t0), weights_version=version,
+               rejected_records=ingest.rejected,
                supervisor=sup.report, zero_copy=[b is not None for b in ingest.registered])
     return out
 

@@ -240,6 +240,37 @@ def test_native_loop_learns_synthetic_cue_task():
     assert rets[-200:].mean() > 3 * random_return, (rets[:200].mean(), rets[-200:].mean())
 
 
+def _memory_task(ablation: str, steps: int):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tools"))
+    from learn_check import make_cfg, memoryless_ceiling, parse
+    from pytorch_r2d2_amd.runner import run_native
+    args = parse(["--memory", "--ablation", ablation, "--steps", str(steps)])
+    cfg = make_cfg(args, "fp32")
+    out = run_native(cfg, steps=steps, log_every=steps, capacity=args.envs * 1000)
+    rets = np.asarray(out["returns"])
+    return rets, memoryless_ceiling(args.episode_len, args.switch, cfg.model.n_actions)
+
+
+def test_recurrent_learner_solves_memory_task():
+    """The cue is drawn only on the first frame after each target switch (env.cue_only_first,
+    switch 8), so a memoryless policy returns at most (1/8 + 7/8 * 1/6) * 64 = 17.3 per episode.
+    The fp32 learner (stored state + burn-in + BPTT over 16 learned steps, the atari57 engine
+    path) must carry the target in its LSTM state: >= 2x that ceiling
+    (profiles/r03_learn_memory_task.txt: 60.4 = 3.5x after 8000 steps)."""
+    rets, ceil = _memory_task("none", 4000)
+    assert len(rets) > 1000
+    assert rets[-300:].mean() >= 2.0 * ceil, (rets[:300].mean(), rets[-300:].mean(), ceil)
+
+
+def test_memoryless_ablation_stays_at_ceiling():
+    """Ablation of the same task: LSTM state reset before every actor step, learner sequences
+    of one step from a zero state -- no memory anywhere, so the return stays near the ceiling."""
+    rets, ceil = _memory_task("memoryless", 4000)
+    assert len(rets) > 1000
+    assert rets[-300:].mean() <= 1.15 * ceil, (rets[-300:].mean(), ceil)
+
+
 @pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
 def test_dp_engine_global_sampling_weights(tmp_path, graph):
     """Different shards per rank: the TD kernel's IS weights are the two-level global ones

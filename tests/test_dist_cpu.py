@@ -86,9 +86,10 @@ def _worker(rank, world, port, outdir):
         got = ch.recv(0, state_shape=(4, 84, 84))
         res["push_ok"] = all(np.array_equal(got[k], m.memory[k]) for k in m.memory)
     # --- shard totals for two-level sampling
-    from pytorch_r2d2_amd.parallel.sharded_replay import gather_shard_stats
-    tot, cnt = gather_shard_stats(torch.tensor([1.0 + rank]), torch.tensor([10 * (rank + 1)]), world)
-    res["shards"] = (tot.tolist(), cnt.tolist())
+    from pytorch_r2d2_amd.parallel.sharded_replay import gather_stats, local_stats
+    st = gather_stats(local_stats(torch.tensor([1.0 + rank]), torch.tensor([10 * (rank + 1)]),
+                                  torch.tensor([0.5])), world)
+    res["shards"] = (st[:, 0].tolist(), st[:, 1].tolist())
     torch.save(res, os.path.join(outdir, f"r{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()

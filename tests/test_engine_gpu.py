@@ -110,27 +110,6 @@ def test_engine_graph_replay_matches_eager():
     assert _rel(rp2.tree, rp.tree) < 1e-5
 
 
-@pytest.mark.parametrize("B", [16, 64])
-def test_pipelined_forward_is_bit_identical_to_serial(B):
-    """Chunked forward (torso/x-projection of chunk c+1 beside the recurrence of chunk c on a
-    side stream, lstm_persist.hip + torso.hip reserve) == the serial forward, bit for bit."""
-    runs = []
-    for chunks in (5, 0):
-        cfg, rp, eng, _, _ = _make("shifted", B=B, **{"learner.fwd_chunks": chunks})
-        assert (eng._chunks is not None) == (chunks > 0)
-        eng._forward_loss()
-        eng._backward_core()
-        eng._backward_torso()
-        torch.cuda.synchronize()
-        runs.append(eng)
-    a, b = runs
-    assert int(a.err.item()) == 0
-    for name in ("X_on", "X_tg", "xp_on", "xp_tg", "gates", "loss", "grad", "act1", "act2"):
-        assert torch.equal(getattr(a, name), getattr(b, name)), name
-    for key in ("on", "tg"):
-        assert torch.equal(a.hseq[key], b.hseq[key]) and torch.equal(a.cseq[key], b.cseq[key]), key
-
-
 def test_engine_resume_from_full_checkpoint(tmp_path):
     from pytorch_r2d2_amd.utils.checkpoint import load_full_checkpoint, save_full_checkpoint
     cfg, rp, eng, net, tgt = _make("shifted", B=8)
@@ -234,7 +213,7 @@ def test_engine_bf16_seaquest_18_actions_fused_path():
         torch.mm = orig
     torch.cuda.synchronize()
     assert eng._duel_done
-    assert not calls or cfg.learner.dh_gemm == "blaslt" and len(calls) == 1, len(calls)
+    assert not calls, len(calls)
     online = copy.deepcopy(net).to(DEV)
     target = copy.deepcopy(tgt).to(DEV)
     batch = batch_from_hbm(rp, eng.starts, eng.probs, cfg, DEV)

@@ -157,6 +157,48 @@ def test_engine_fp32_matches_fp64_oracle(mode):
     assert _rel(rp.priority[rows].cpu(), out["priority"]) < max(1e-4, 2 * p32)
 
 
+def test_engine_fp32_matches_fp64_oracle_at_bench_shape():
+    """The benched step itself (atari57: B=64, burn-in 40 + learn 40, n=5, fixed target) against
+    the float64 truth: the 12 LSTM groups (3 chains x 4 batch tiles) placed two per XCD, the
+    85-step tagged T4 hand-offs (the 4-bit tags wrap 5 times per launch), the 192x256 split GEMM
+    tiles, the full-chip torso grids.  Same bounds as the reduced-shape test; then 5 replays of
+    the captured graph with the persistent kernels' error word still 0."""
+    over = {"replay.burn_in": 40, "replay.learn": 40, "replay.overlap": 40, "replay.n_step": 5,
+            "replay.capacity": 64000}
+    cfg, rp, eng, net, tgt = _make("fixed", B=64, **over)
+    assert (eng.B, eng.Lb, eng.Ll, eng.n, eng.Tn) == (64, 40, 40, 5, 85)
+    rp.fill_synthetic(episode_len=200, seed=5)
+    eng._forward_loss()
+    eng._backward_core()
+    eng._backward_torso()
+    torch.cuda.synchronize()
+    assert eng.error_word() == 0
+    online, out = _oracle64(rp, eng, net, tgt, cfg, "fixed")
+    on32, out32 = _oracle(rp, eng, net, tgt, cfg, "fixed", torch.float32)
+    l64 = out["loss"].item()
+    lrel = abs(eng.loss.item() - l64) / l64
+    lrel32 = abs(out32["loss"].item() - l64) / l64
+    assert lrel < max(1e-4, 2 * lrel32), (lrel, lrel32)
+    got = eng.layout.views(eng.grad)
+    g32 = dict(on32.named_parameters())
+    errs = {n: (_rel(got[n].cpu(), p.grad), _rel(g32[n].grad, p.grad)) for n, p in online.named_parameters()}
+    assert len(errs) == 18
+    bad = {k: v for k, v in errs.items() if v[0] > max(1e-4, 2 * v[1])}
+    assert not bad, errs
+    Lb, T = cfg.replay.burn_in, cfg.replay.seq_len
+    s = eng.starts.long()
+    base = s - s % rp.cap_e
+    rows = base[None] + (s[None] - base[None] + torch.arange(Lb, T, device=DEV)[:, None]) % rp.cap_e
+    p32 = _rel(out32["priority"], out["priority"])
+    assert _rel(rp.priority[rows].cpu(), out["priority"]) < max(1e-4, 2 * p32)
+    eng.capture(warmup=1)
+    for _ in range(5):
+        eng.step()
+    torch.cuda.synchronize()
+    assert eng.error_word() == 0
+    assert torch.isfinite(eng.master).all() and torch.isfinite(eng.loss).all()
+
+
 def test_engine_fp32_forward_activations():
     """Torso features, x-projection, recurrent states and Q values of the fp32 engine vs float64:
     <= 2e-5 relative (bf16: ~3e-3)."""

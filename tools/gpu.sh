@@ -1,0 +1,77 @@
+#!/bin/bash
+# One parametrised driver for every GPU-box job (run through gpurun from the repo root).  Each
+# GPU step runs under its own time limit and the first failure ends the script.
+#
+#   tools/gpu.sh smoke                          __graft_entry__.smoke()
+#   tools/gpu.sh test [pytest args...]          GPU test suite (default: tests -m gpu)
+#   tools/gpu.sh bench [N] [bench args...]      N x bench.py --steps 300 (default N=3), one line each
+#   tools/gpu.sh ab KEY=V[,KEY=V] ...           bench.py under override sets (same box A/B)
+#   tools/gpu.sh prof TAG [bench args...]       rocprofv3 kernel trace + step breakdown
+#   tools/gpu.sh pmc TAG [filters...]           PMC passes over the bench step (kernel trace only)
+#   tools/gpu.sh learn [learn_check args...]    tools/learn_check.py
+#
+# Output goes under gpurun_out/ (merged back by gpurun); summaries worth keeping are copied into
+# profiles/ by hand.
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+cmd=${1:-test}; shift || true
+
+fail() { echo "FAIL: $1"; [ -f "$2" ] && tail -30 "$2"; exit 1; }
+
+case "$cmd" in
+  smoke)
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 \
+      || fail smoke gpurun_out/smoke.log
+    echo "smoke ok" ;;
+  test)
+    args=("$@"); [ ${#args[@]} -eq 0 ] && args=(tests -m gpu)
+    timeout -k 10 1000 python -u -m pytest -x -q --timeout 120 --timeout-method thread "${args[@]}" \
+      > gpurun_out/pytest_gpu.txt 2>&1 || fail pytest gpurun_out/pytest_gpu.txt
+    tail -2 gpurun_out/pytest_gpu.txt ;;
+  bench)
+    n=${1:-3}; shift || true
+    for i in $(seq 1 "$n"); do
+      timeout -k 10 180 python bench.py --steps 300 --warmup 30 "$@" > gpurun_out/bench_$i.log 2>&1 \
+        || fail "bench $i" gpurun_out/bench_$i.log
+      grep -h '^{' gpurun_out/bench_$i.log | python -c \
+        "import sys,json; d=json.loads(sys.stdin.read()); print(d['config'].get('preset'), d['value'], d['ms_per_step'])"
+    done ;;
+  ab)
+    for v in "$@"; do
+      sets=(); IFS=, read -ra kvs <<< "$v"; for kv in "${kvs[@]}"; do [ -n "$kv" ] && sets+=(--set "$kv"); done
+      timeout -k 10 180 python bench.py --steps 300 --warmup 30 "${sets[@]}" > gpurun_out/ab.log 2>&1 \
+        || fail "ab [$v]" gpurun_out/ab.log
+      echo "[$v] $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab.log)"
+    done ;;
+  prof)
+    tag=$1; shift
+    rm -rf gpurun_out/prof_$tag
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$tag -- \
+      python bench.py --steps 20 --warmup 10 "$@" > gpurun_out/prof_$tag.log 2>&1 || fail "prof $tag" gpurun_out/prof_$tag.log
+    grep -h '^{' gpurun_out/prof_$tag.log | cut -c1-120
+    python tools/step_breakdown.py "gpurun_out/prof_$tag/*/*kernel_trace.csv" gpurun_out/$tag.txt 5 > /dev/null
+    head -30 gpurun_out/$tag.txt ;;
+  pmc)
+    tag=$1; shift
+    filters=("$@"); [ ${#filters[@]} -eq 0 ] && filters=(torso lstm gemm td_duel rmsprop)
+    mkdir -p gpurun_out/pmc_$tag
+    i=0
+    for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS" \
+               "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_ACTIVE_INST_LDS" \
+               "SQ_INSTS_VALU SQ_INSTS_VALU_MFMA_BF16 SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU" \
+               "SQ_INSTS_VMEM_RD SQ_INSTS_LDS_STORE SQ_INSTS_LDS_LOAD SQ_WAIT_INST_ANY" \
+               "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum"; do
+      i=$((i+1))
+      timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d gpurun_out/pmc_$tag/p$i -- \
+        python bench.py --steps 3 --warmup 2 > gpurun_out/pmc_$tag/p$i.log 2>&1 || fail "pmc pass $i" gpurun_out/pmc_$tag/p$i.log
+    done
+    python tools/pmc_summary.py "gpurun_out/pmc_$tag/p*/**/*counter_collection.csv" "${filters[@]}" \
+      > gpurun_out/pmc_$tag/summary.txt
+    head -60 gpurun_out/pmc_$tag/summary.txt ;;
+  learn)
+    timeout -k 10 300 python -u tools/learn_check.py "$@" > gpurun_out/learn.log 2>&1 || fail learn gpurun_out/learn.log
+    grep -h '^{' gpurun_out/learn.log ;;
+  *)
+    echo "unknown command $cmd"; exit 2 ;;
+esac
