@@ -131,6 +131,73 @@ def test_shm_ring_ingestor_dma_into_hbm():
         ing.close()
 
 
+def test_ingest_poll_dirty_budget_spans_all_records():
+    """One poll ingests one record per ring and repairs the tree once: the records' dirty
+    entries share one list.  4 rings x 40 rows that are all sequence starts = 160 entries on a
+    128-entry list -- each record alone fits, together they would overflow (entries past the list
+    are dropped and the tree keeps stale sums); the poll must fall back to a full rebuild."""
+    from pytorch_r2d2_amd.engine.ingest import HBMIngestor
+    from pytorch_r2d2_amd.parallel.trajectory import ShmTrajectoryWriter
+    cfg = _small_cfg()
+    rp = HBMReplay(cfg, DEV, capacity=4 * 200, n_subrings=4)
+    rp.max_dirty = 128
+    rp.dirty = rp.dirty[:128]
+    names = [f"/r2d2_gd_{uuid.uuid4().hex[:6]}_{i}" for i in range(4)]
+    ing = HBMIngestor(rp, names, ring_bytes=16 << 20)
+    try:
+        writers = [ShmTrajectoryWriter(n, 16 << 20) for n in names]
+        for i, w in enumerate(writers):
+            m = _record(40, 50 + i)
+            m["is_seq_start"][:] = 1
+            m["sequence_priority"][:] = np.random.default_rng(i).random(40) + 0.5
+            w.push(m)
+        assert ing.poll() == 160
+        ing._release_done(wait=True)
+        torch.cuda.synchronize()
+        assert int(rp.n_valid.item()) == 160
+        _tree_consistent(rp)
+    finally:
+        ing.close()
+
+
+def test_ingestor_drops_malformed_records_uncounted():
+    """A record whose header does not match the schema, or whose n exceeds its payload, is
+    dropped on the host before any DMA (not counted as ingested); a forged header that reaches
+    the device kernel is rejected there without advancing the write head or the row counter."""
+    from pytorch_r2d2_amd.engine.ingest import HBMIngestor
+    from pytorch_r2d2_amd.parallel.trajectory import ShmTrajectoryWriter, pack_rows
+    cfg = _small_cfg()
+    rp = HBMReplay(cfg, DEV, capacity=2 * 200, n_subrings=2)
+    names = [f"/r2d2_gm_{uuid.uuid4().hex[:6]}_{i}" for i in range(2)]
+    ing = HBMIngestor(rp, names, ring_bytes=16 << 20)
+    try:
+        w = [ShmTrajectoryWriter(n, 16 << 20) for n in names]
+        bad = _record(30, 7)
+        bad["hs_cs"] = bad["hs_cs"][:, :100].copy()
+        w[0].push(bad)
+        good = _record(30, 8)
+        w[1].push(good)
+        assert ing.poll() == 30
+        ing._release_done(wait=True)
+        torch.cuda.synchronize()
+        assert ing.rejected == 1 and ing.records == 1 and ing.rows == 30
+        _check_replay_rows(rp, good, 1, 0)
+        ing.check_errors()
+    finally:
+        ing.close()
+    # device side: n in the header larger than the fields hold
+    buf = pack_rows(_record(20, 9))
+    buf[8:16] = np.asarray([5000], dtype=np.int64).view(np.uint8)
+    dev = torch.empty(buf.size + 64, dtype=torch.uint8, device=DEV)
+    off = (-dev.data_ptr()) % 64
+    dev[off: off + buf.size].copy_(torch.from_numpy(buf))
+    head0, tot0 = rp.ihead.clone(), rp.rows_total_d.clone()
+    rp.ingest_device_record(dev[off: off + buf.size], None, 0)
+    torch.cuda.synchronize()
+    assert int(rp.ingest_err.item()) & 1
+    assert torch.equal(rp.ihead, head0) and torch.equal(rp.rows_total_d, tot0)
+
+
 def test_cu_masked_streams_partition_the_chip():
     from pytorch_r2d2_amd.parallel.placement import split_chip
     sa, sl, na, nl = split_chip(DEV, 4)
