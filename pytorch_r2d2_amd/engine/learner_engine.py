@@ -151,6 +151,19 @@ class LearnerEngine:
         self.steps_done = 0
         # data-parallel global prioritized sampling (parallel/sharded_replay.py)
         self.dp_global = bool(world > 1 and process_group is not None and cfg.dist.global_sampling)
+        if self.dp_global and self.device.type == "cuda":
+            # the 12-byte shard-stats all-gather runs on a side stream beside the torso / LSTM
+            # graph segment.  It cannot starve the persistent forward: it depends on no kernel of
+            # this step, so its RCCL workgroups finish once the peers reach the same collective;
+            # and the forward's grid (one workgroup per CU, every member co-resident) must still
+            # leave comm_reserve_cus CUs for them so the LSTM never waits for their exit
+            chains = 2 if cfg.learner.target_mode == "shifted" else 3
+            lstm_wgs = chains * -(-cfg.learner.batch_size // 16) * (cfg.model.hidden // UNITS)
+            if lstm_wgs > self.n_cus - int(cfg.dist.comm_reserve_cus):
+                raise ValueError(
+                    f"DP global sampling: the persistent LSTM forward needs {lstm_wgs} co-resident "
+                    f"workgroups, more than {self.n_cus} CUs minus dist.comm_reserve_cus="
+                    f"{cfg.dist.comm_reserve_cus} left beside the shard-stats all-gather")
         self._duel_done = False       # the TD launch also ran the dueling-head backward
         self._dh_done = False         # ... and the dh = dz @ W1 product (learner.td_fuse_dh)
         self.graph = None
@@ -1100,6 +1113,15 @@ class LearnerEngine:
             self._sync().finish()
             g_update.replay()
         self.steps_done += 1
+
+    def dp_imbalance(self) -> float:
+        """W * sum_k (S_k / S)^2 of the last step's gathered shard totals: the variance inflation
+        of the fixed-B shard-ratio sampling over one merged replay (parallel/sharded_replay.py;
+        1.0 = balanced shards).  One D2H read; 1.0 without DP global sampling."""
+        if not self.dp_global:
+            return 1.0
+        from ..parallel.sharded_replay import imbalance_factor
+        return float(imbalance_factor(self.dp_recv.view(self.world, 3)))
 
     def loss_value(self) -> float:
         return float(self.loss.item())

@@ -85,3 +85,52 @@ def single_replay_is_weights(p: torch.Tensor, n: float, beta: float) -> torch.Te
     """The single-replay formula w = (N P)^-beta / max (replay over the merged shards)."""
     w = (n * p).clamp_min(1e-30) ** (-beta)
     return w / w.max()
+
+
+# ---------------------------------------------------------------- variance of the two-level scheme
+# Why not per-shard counts drawn by multinomial (SURVEY §5.8)?  Those would give every step the
+# exact distribution of one merged replay, but a rank's batch size would change every step: the
+# graphed step needs a static B, and a shard asked for more than B sequences cannot serve them.
+# The shard-ratio weights keep B fixed and stay unbiased (the chi-square test pins that); what they
+# cost is variance.  For a per-sequence quantity f with within-shard variance V_k and shard means
+# mu_k (mu the global mean, s_k = S_k / S):
+#
+#     Var(local + ratio)  = (1/B) sum_k s_k^2 V_k
+#     Var(merged replay)  = 1/(W B) [sum_k s_k V_k + sum_k s_k (mu_k - mu)^2]
+#
+# With equal within-shard variances the ratio is at most W sum_k s_k^2 (``imbalance_factor``): 1
+# for balanced shards, 1 + W sum_k (s_k - 1/W)^2 in general; the between-shard term, which local
+# sampling removes (it is stratified over shards), only lowers it.  Co-located actor groups feed
+# the shards symmetrically, so s_k ~ 1/W: e.g. +-10 % shard totals at W = 8 cost ~1 % variance.
+# ``mc_estimator_variance`` measures all of this (tests/test_sharded_sampling_cpu.py,
+# tools/dp_sampling_variance.py -> profiles/r03_dp_sampling_variance.txt).
+def imbalance_factor(stats: torch.Tensor) -> torch.Tensor:
+    """W * sum_k (S_k / S)^2 from the gathered (W, 3) shard stats (>= 1; 1 = balanced)."""
+    s = stats[:, 0] / stats[:, 0].sum().clamp_min(1e-30)
+    return stats.shape[0] * (s * s).sum()
+
+
+def mc_estimator_variance(priorities, values, B: int, trials: int = 4000, seed: int = 0):
+    """Monte-Carlo variance of three estimators of E_P[f] (P proportional to priority over the
+    union of the shards): ``merged`` (W*B draws from the merged replay), ``multinomial`` (shard
+    counts ~ Multinomial(W*B, s), then within-shard draws) and ``local_ratio`` (B draws per shard
+    with the shard-ratio weight W s_k -- what the engine does).  priorities / values: lists of
+    per-shard numpy arrays.  Returns {name: (mean, variance)} and the true mean."""
+    import numpy as np
+    g = np.random.default_rng(seed)
+    W = len(priorities)
+    S = np.asarray([p.sum() for p in priorities])
+    s = S / S.sum()
+    allp = np.concatenate(priorities) / S.sum()
+    allf = np.concatenate(values)
+    mu = float((allp * allf).sum())
+    q = [p / p.sum() for p in priorities]
+    est = {"merged": [], "multinomial": [], "local_ratio": []}
+    for _ in range(trials):
+        est["merged"].append(allf[g.choice(len(allf), W * B, p=allp)].mean())
+        c = g.multinomial(W * B, s)
+        est["multinomial"].append(np.concatenate(
+            [values[k][g.choice(len(q[k]), c[k], p=q[k])] for k in range(W)]).mean())
+        est["local_ratio"].append(sum(W * s[k] * values[k][g.choice(len(q[k]), B, p=q[k])].sum()
+                                      for k in range(W)) / (W * B))
+    return {k: (float(np.mean(v)), float(np.var(v))) for k, v in est.items()}, mu

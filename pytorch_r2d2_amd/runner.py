@@ -125,7 +125,7 @@ def run_native(cfg: R2D2Config, steps: int = 1000, actor_steps_per_update: int =
             rec = dict(step=it + 1, loss=loss, replay_rows=replay.size,
                        n_valid=int(replay.n_valid.item()), env_steps=actor.env_steps,
                        mean_return=float(np.mean(rets)) if rets else None,
-                       learner_steps_per_s=(it + 1) / el,
+                       learner_steps_per_s=(it + 1) / el, dp_imbalance=eng.dp_imbalance(),
                        env_steps_per_s=(actor.env_steps - env0) / el)
             if mlog:
                 mlog.log("native", **rec)

@@ -107,3 +107,22 @@ def test_two_level_sampling_matches_merged_replay(tmp_path, world):
     assert res["chi2_raw"] > 10 * crit and res["tv_raw"] > 0.05, res
     assert res["tv"] < 0.03, res
     assert res["is_err"] < 1e-5, res
+
+
+def test_local_ratio_sampling_variance_matches_imbalance_factor():
+    """The fixed-B shard-ratio scheme's only cost vs one merged replay is variance, and it is the
+    shard imbalance factor W sum s_k^2 (parallel/sharded_replay.py): ~1 for balanced shards,
+    1.34 at +-90 % shard totals; unbiased throughout (profiles/r03_dp_sampling_variance.txt)."""
+    from pytorch_r2d2_amd.parallel.sharded_replay import imbalance_factor, mc_estimator_variance
+    W, M, B, trials = 4, 128, 16, 3000
+    for spread in (0.0, 0.9):
+        g = np.random.default_rng(3)
+        scale = 1 + spread * np.linspace(-1, 1, W)
+        pr = [(g.random(M) + 0.05) * scale[k] for k in range(W)]
+        fv = [g.normal(size=M) for _ in range(W)]
+        res, mu = mc_estimator_variance(pr, fv, B, trials=trials, seed=5)
+        imb = float(imbalance_factor(torch.tensor([[p.sum(), M, 0.0] for p in pr])))
+        ratio = res["local_ratio"][1] / res["merged"][1]
+        assert abs(ratio - imb) < 0.12 * imb, (spread, ratio, imb)
+        z = (res["local_ratio"][0] - mu) / np.sqrt(res["local_ratio"][1] / trials)
+        assert abs(z) < 4.0, z
