@@ -40,6 +40,11 @@ struct IngestArgs {
   int* count;
   int max_dirty;
   int FB, H2, cap_e;
+  int rows_per_sub;         // > 0: rows i*rps .. (i+1)*rps - 1 go to sub-ring sub + i (an actor
+                            // rank's E env windows in one record); 0: every row to sub-ring sub
+  int W;                    // rows a sequence touches (T + n): the W - 1 positions in front of
+                            // each written range lose their starts (their windows now run into
+                            // new data; a record's own starts keep their windows inside it)
 };
 
 struct RecView {
@@ -87,7 +92,19 @@ __device__ __forceinline__ float scalar_at(const uint8_t* base, int code, long l
   return (float)base[i];
 }
 
-__global__ __launch_bounds__(256) void ingest_rows_kernel(const IngestArgs a) {
+__device__ __forceinline__ void ingest_clear(const IngestArgs& a, long long row) {
+  if (a.is_start[row] || a.leaves[row] != 0.f) {
+    if (a.is_start[row]) atomicSub(a.n_valid, 1);
+    a.is_start[row] = 0;
+    a.leaves[row] = 0.f;
+    if (a.dirty) {
+      const int slot = atomicAdd(a.count, 1);
+      if (slot < a.max_dirty) a.dirty[slot] = (int)row;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void ingest_rows_kernel(const IngestArgs a, int grid_rows) {
   RecView v;
   const bool ok = parse_record(a, v);
   const int tid = threadIdx.x;
@@ -95,12 +112,33 @@ __global__ __launch_bounds__(256) void ingest_rows_kernel(const IngestArgs a) {
     if (blockIdx.x == 0 && tid == 0) atomicOr(a.err, 1u);
     return;
   }
-  const long long keep = v.n < a.cap_e ? v.n : a.cap_e;
-  const long long i = blockIdx.x;
-  if (i >= keep) return;
-  const long long src = v.n - keep + i;                 // only the newest cap_e rows survive
-  const long long head = a.ihead[a.sub];
-  const long long row = (long long)a.sub * a.cap_e + (head + i) % a.cap_e;
+  if ((int)blockIdx.x >= grid_rows) {
+    // the W - 1 positions in front of each written range (disjoint from every written row:
+    // rows per sub-ring + W - 1 <= cap_e, checked by the launcher)
+    if (tid != 0) return;
+    const int q = (int)blockIdx.x - grid_rows, wm = a.W > 1 ? a.W - 1 : 1;
+    const int sub = a.sub + q / wm, k = q % wm + 1;
+    if (a.rows_per_sub > 0 && (long long)(q / wm) >= v.n / a.rows_per_sub) return;
+    const long long pos = ((a.ihead[sub] - k) % a.cap_e + a.cap_e) % a.cap_e;
+    ingest_clear(a, (long long)sub * a.cap_e + pos);
+    return;
+  }
+  long long src, row;
+  if (a.rows_per_sub > 0) {   // env-major windows: one per sub-ring, rows_per_sub <= cap_e
+    const long long i = blockIdx.x;
+    if (i >= v.n) return;
+    const int sub = a.sub + (int)(i / a.rows_per_sub);
+    const long long j = i % a.rows_per_sub;
+    src = i;
+    row = (long long)sub * a.cap_e + (a.ihead[sub] + j) % a.cap_e;
+  } else {
+    const long long keep = v.n < a.cap_e ? v.n : a.cap_e;
+    const long long i = blockIdx.x;
+    if (i >= keep) return;
+    src = v.n - keep + i;                                // only the newest cap_e rows survive
+    const long long head = a.ihead[a.sub];
+    row = (long long)a.sub * a.cap_e + (head + i) % a.cap_e;
+  }
   // frames: 16-byte vectors (fields are 64-byte aligned; FB % 16 == 0 for every frame geometry)
   {
     const uint8_t* s = a.rec + v.off[0] + src * a.FB;
@@ -147,6 +185,12 @@ __global__ void ingest_tail_kernel(const IngestArgs a) {
   // the head and the counter advance only for a record the rows kernel accepted (same parse)
   RecView v;
   if (!parse_record(a, v)) return;
+  if (a.rows_per_sub > 0) {
+    const int nsub = (int)(v.n / a.rows_per_sub);
+    for (int q = 0; q < nsub; ++q) a.ihead[a.sub + q] = (a.ihead[a.sub + q] + a.rows_per_sub) % a.cap_e;
+    *a.rows_total += v.n;
+    return;
+  }
   const long long keep = v.n < a.cap_e ? v.n : a.cap_e;
   a.ihead[a.sub] = (a.ihead[a.sub] + keep) % a.cap_e;
   *a.rows_total += keep;
@@ -154,13 +198,77 @@ __global__ void ingest_tail_kernel(const IngestArgs a) {
 
 extern "C" int r2_ingest_args_bytes() { return (int)sizeof(IngestArgs); }
 
+// ---------------------------------------------------------------------------------------------
+// The producer side of a device record: an actor rank's replay rows [h0, h0 + K) of each of its E
+// sub-rings (ring-wrapped), env-major, into a record whose header the caller wrote once (fixed
+// E, K: a constant layout).  Only the starts whose whole window lies inside the record are kept
+// (start_from <= j < start_to): consecutive windows overlap by W - 1 rows, so every sequence is
+// shipped exactly once and the learner never samples a window it has not fully received.  Replaces the host-side pack_rows of the RCCL trajectory channel:
+// the rows never leave device memory on either side of the send.
+struct PackArgs {
+  const uint8_t* frames; const float* hs_cs; const float* ths_cs; const uint8_t* action;
+  const float* reward; const uint8_t* done; const float* priority; const uint8_t* is_start;
+  const float* leaves;
+  uint8_t* rec;
+  long long off[ING_FIELDS];   // byte offset of every field in the record
+  long long h0;                // first ring position (same for every sub-ring: lockstep envs)
+  int E, K, cap_e, FB, H2;     // K rows per env window
+  int start_from, start_to;    // starts kept only for window rows j in [start_from, start_to)
+  int pad_;
+};
+
+__global__ __launch_bounds__(256) void pack_rows_kernel(const PackArgs a) {
+  const int i = blockIdx.x;                // record row (env-major)
+  const int e = i / a.K, j = i % a.K;
+  const long long row = (long long)e * a.cap_e + (a.h0 + j) % a.cap_e;
+  const int tid = threadIdx.x;
+  {
+    const u32x4* s = reinterpret_cast<const u32x4*>(a.frames + row * a.FB);
+    u32x4* d = reinterpret_cast<u32x4*>(a.rec + a.off[0] + (long long)i * a.FB);
+    for (int k = tid; k < a.FB / 16; k += blockDim.x) d[k] = s[k];
+  }
+  {
+    float* d1 = reinterpret_cast<float*>(a.rec + a.off[1]) + (long long)i * a.H2;
+    float* d2 = reinterpret_cast<float*>(a.rec + a.off[2]) + (long long)i * a.H2;
+    for (int k = tid; k < a.H2; k += blockDim.x) {
+      d1[k] = a.hs_cs[row * a.H2 + k];
+      d2[k] = a.ths_cs[row * a.H2 + k];
+    }
+  }
+  if (tid != 0) return;
+  a.rec[a.off[3] + i] = a.action[row];                                // int8 (A <= 127)
+  reinterpret_cast<float*>(a.rec + a.off[4])[i] = a.reward[row];
+  reinterpret_cast<float*>(a.rec + a.off[5])[i] = a.done[row] ? 1.f : 0.f;
+  a.rec[a.off[6] + i] = 0;                                           // stack_count
+  reinterpret_cast<float*>(a.rec + a.off[7])[i] = a.priority[row];
+  const bool st = a.is_start[row] && j >= a.start_from && j < a.start_to;
+  reinterpret_cast<float*>(a.rec + a.off[8])[i] = st ? a.leaves[row] : 0.f;
+  a.rec[a.off[9] + i] = st ? 1 : 0;
+}
+
+extern "C" int r2_pack_args_bytes() { return (int)sizeof(PackArgs); }
+
+extern "C" int r2_pack_rows(const PackArgs* a, void* stream) {
+  if (!a->rec || a->E <= 0 || a->K <= 0 || a->K > a->cap_e || (a->FB & 15) || a->H2 <= 0) return -1;
+  if ((reinterpret_cast<uintptr_t>(a->rec) & 63) != 0) return -2;
+  hipLaunchKernelGGL(pack_rows_kernel, dim3(a->E * a->K), dim3(256), 0, (hipStream_t)stream, *a);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
 // One record -> one sub-ring.  max_rows bounds the grid (rows kept = min(n, cap_e) <= max_rows is
 // the caller's contract: it knows the record length, and rows / record >= FB bytes each).
 extern "C" int r2_ingest_record(const IngestArgs* a, void* stream) {
   if (!a->rec || a->max_rows <= 0 || a->cap_e <= 0 || a->FB <= 0 || a->H2 <= 0) return -1;
   if ((reinterpret_cast<uintptr_t>(a->rec) & 63) != 0) return -2;
-  const int grid = a->max_rows < a->cap_e ? a->max_rows : a->cap_e;
-  hipLaunchKernelGGL(ingest_rows_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, *a);
+  const int rps = a->rows_per_sub;
+  const int W = a->W > 1 ? a->W : 1;
+  if (rps > 0 && rps + W - 1 > a->cap_e) return -3;
+  const int grid = rps > 0 ? a->max_rows : (a->max_rows < a->cap_e ? a->max_rows : a->cap_e);
+  // clear blocks: W - 1 per sub-ring the record may write
+  const int nsub = rps > 0 ? (grid + rps - 1) / rps : 1;
+  const int nclr = W > 1 ? nsub * (W - 1) : 0;
+  hipLaunchKernelGGL(ingest_rows_kernel, dim3(grid + nclr), dim3(256), 0, (hipStream_t)stream, *a, grid);
   hipLaunchKernelGGL(ingest_tail_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, *a);
   R2_CHECK_LAUNCH();
   return 0;

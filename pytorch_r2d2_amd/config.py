@@ -172,6 +172,14 @@ class DistConfig:
     # globally proportional prioritized sampling over the ranks' replay shards
     # (parallel/sharded_replay.py: one 12-byte all-gather per step, shard-ratio loss weights)
     global_sampling: bool = True
+    # split topology (parallel/actor_ranks.py, runner.run_split): the last ``actor_ranks`` ranks
+    # run actor groups only and feed the learner ranks over RCCL; per round every actor rank takes
+    # ``push_rows`` env steps and ships one record, every learner rank trains
+    # ``learner_steps_per_round`` steps; weights are broadcast every ``publish_rounds`` rounds
+    actor_ranks: int = 0
+    push_rows: int = 32
+    learner_steps_per_round: int = 1
+    publish_rounds: int = 8
 
 
 @dataclass

@@ -45,10 +45,11 @@ class IngestArgs(ctypes.Structure):
         (n, _VP) for n in ("ihead", "rows_total", "err", "frames", "hs_cs", "ths_cs", "action",
                            "reward", "done", "priority", "is_start", "leaves", "n_valid", "dirty",
                            "count")] + [
-        (n, ctypes.c_int) for n in ("max_dirty", "FB", "H2", "cap_e")]
+        (n, ctypes.c_int) for n in ("max_dirty", "FB", "H2", "cap_e", "rows_per_sub", "W")]
 
 
-def ingest_args(replay, rec: int, rec_bytes: int, sub: int, use_dirty: bool) -> IngestArgs:
+def ingest_args(replay, rec: int, rec_bytes: int, sub: int, use_dirty: bool,
+                rows_per_sub: int = 0) -> IngestArgs:
     if ctypes.sizeof(IngestArgs) != kernels().r2_ingest_args_bytes():
         raise RuntimeError("IngestArgs layout differs from csrc/kernels/ingest.hip")
     rp = replay
@@ -63,6 +64,10 @@ def ingest_args(replay, rec: int, rec_bytes: int, sub: int, use_dirty: bool) -> 
         setattr(a, name, ptr(t))
     a.dirty = ptr(rp.dirty) if use_dirty else 0
     a.max_dirty, a.FB, a.H2, a.cap_e = rp.max_dirty, rp.frame_bytes, 2 * rp.H, rp.cap_e
+    a.rows_per_sub = int(rows_per_sub)
+    a.W = int(replay.cfg.replay.seq_len + replay.cfg.replay.n_step)
+    if rows_per_sub > 0:   # env-major windows: every row of the record is kept
+        a.max_rows = int(rec_bytes // max(rp.frame_bytes, 1) + 1)
     return a
 
 
@@ -164,14 +169,15 @@ class HBMIngestor:
             else:
                 self.pin_event.record(self.copy_stream)
             learner.wait_event(ev)
-            kept = min(n_rows, self.rp.cap_e)
+            # + the W - 1 start clears in front of the record's range
+            kept = min(n_rows, self.rp.cap_e) + self.rp.cfg.replay.seq_len + self.rp.cfg.replay.n_step
             use_dirty = not big and used + kept <= budget
             big |= not use_dirty
             used += kept if use_dirty else 0
             a = ingest_args(self.rp, ptr(dst), n, i, use_dirty)
             check(kernels().r2_ingest_record(ctypes.byref(a), _VP(stream_handle(learner))), "ingest")
             self.dev_done[k].record(learner)
-            rows_here += kept
+            rows_here += min(n_rows, self.rp.cap_e)
             done += 1
             self.bytes += n
         if done:

@@ -11,12 +11,26 @@ approaches 1.
 ``SyntheticAtariEnv`` is the numpy single-env version with the PongEnv API
 (step -> (state float32 (4,84,84)/255, reward, done, info), reset -> state).
 ``VecSyntheticAtari`` runs E envs on a torch device and writes uint8 frames into a
-preallocated (E, 4*84*84) buffer -- the batched GPU actor's input.
+preallocated (E, 4*84*84) buffer -- the batched GPU actor's input.  On a GPU one env step of all
+E envs is ONE kernel (csrc/kernels/env.hip: dynamics + render, counter-hash RNG, graph-safe);
+the torch-op version below it serves CPU tensors.
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 import torch
+
+_VP = ctypes.c_void_p
+
+
+class EnvArgs(ctypes.Structure):
+    """Mirror of ``struct EnvArgs`` (csrc/kernels/env.hip); size checked against the .so."""
+    _fields_ = [(n, _VP) for n in ("action", "t", "target", "k", "ep_return", "reward", "done",
+                                   "finished", "frames")] + [
+        ("seed", ctypes.c_ulonglong)] + [
+        (n, ctypes.c_int) for n in ("E", "A", "C", "H", "W", "episode_len", "sw", "cue_only_first")]
 
 
 class SyntheticAtariEnv:
@@ -103,6 +117,15 @@ class VecSyntheticAtari:
         # (A, W) mask of each action's column band
         self._bands = (col[None, :] // band) == torch.arange(n_actions, device=d)[:, None]
         self._bands &= col[None, :] < band * n_actions
+        # fused device step (csrc/kernels/env.hip): its state / output buffers are persistent, so
+        # a captured actor graph replays it in place
+        self._k = torch.zeros(n_envs, dtype=torch.int64, device=d)
+        self._reward = torch.zeros(n_envs, dtype=torch.float32, device=d)
+        self._done = torch.zeros(n_envs, dtype=torch.bool, device=d)
+        self._finished = torch.zeros(n_envs, dtype=torch.float32, device=d)
+        self._act = torch.zeros(n_envs, dtype=torch.int64, device=d)
+        self._seed = (int(seed) * 0x9E3779B97F4A7C15 + 0x51ED27) & ((1 << 64) - 1)
+        self.fused = self.device.type == "cuda"
 
     def _render(self):
         E = self.E
@@ -125,10 +148,32 @@ class VecSyntheticAtari:
         self._render()
         return self.frames
 
+    def _step_fused(self, actions: torch.Tensor):
+        from ..ops._lib import check, kernels, stream_handle
+        k = kernels()
+        if ctypes.sizeof(EnvArgs) != k.r2_env_args_bytes():
+            raise RuntimeError("EnvArgs layout differs from csrc/kernels/env.hip")
+        act = actions
+        if act.dtype != torch.int64 or not act.is_contiguous():
+            self._act.copy_(actions.reshape(-1))
+            act = self._act
+        a = EnvArgs()
+        for name, t in (("action", act), ("t", self.t), ("target", self.target), ("k", self._k),
+                        ("ep_return", self.ep_return), ("reward", self._reward), ("done", self._done),
+                        ("finished", self._finished), ("frames", self.frames)):
+            setattr(a, name, t.data_ptr())
+        a.seed = self._seed
+        a.E, a.A, a.C, a.H, a.W = self.E, self.A, self.C, self.h, self.w
+        a.episode_len, a.sw, a.cue_only_first = self.episode_len, self.switch, int(self.cue_only_first)
+        check(k.r2_synth_env_step(ctypes.byref(a), _VP(stream_handle())), "synth_env_step")
+        return self._reward, self._done, self._finished
+
     def step(self, actions: torch.Tensor):
         """actions (E,) int on device -> (reward (E,) f32, done (E,) bool, finished_returns).
 
         Envs whose episode ended are reset in place (their new first frame is rendered)."""
+        if self.fused:
+            return self._step_fused(actions)
         reward = (actions.long() == self.target).float()
         self.ep_return += reward
         self.t += 1

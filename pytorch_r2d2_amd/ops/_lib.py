@@ -117,6 +117,10 @@ _SIGS = {
     "r2_gemm5_set_mode": [I],
     "r2_ingest_record": [P, P],
     "r2_ingest_args_bytes": [],
+    "r2_env_args_bytes": [],
+    "r2_pack_args_bytes": [],
+    "r2_pack_rows": [P, P],
+    "r2_synth_env_step": [P, P],
     "r2_stream_create_cumask": [P, I, P],
     "r2_stream_get_cumask": [P, P, I],
     "r2_stream_destroy": [P],

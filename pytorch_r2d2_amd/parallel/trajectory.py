@@ -83,6 +83,29 @@ def validate_record(buf_head: np.ndarray, rec_bytes: int, frame_bytes: int, h2: 
     return n
 
 
+def record_spec(n_rows: int, frame_bytes: int, h2: int):
+    """The record layout ``pack_rows`` produces for ``n_rows`` rows of the replay schema (uint8
+    frames, fp32 [h|c] x 2, int8 action / stack count, fp32 reward / done / priorities, uint8
+    start flag) without
+    materialising the rows: (header uint8 array, byte offset of every field, total bytes).  The
+    device pack kernel (csrc/kernels/ingest.hip pack_rows_kernel) fills the fields of a buffer
+    whose header was written once from this."""
+    # the reference's dtypes (replay_memory.py:76-87): action int8, done fp32
+    spec = [(0, frame_bytes, 1), (2, h2, 4), (2, h2, 4), (1, 1, 1), (2, 1, 4), (2, 1, 4), (1, 1, 1),
+            (2, 1, 4), (2, 1, 4), (0, 1, 1)]
+    meta, offs = [], []
+    off = header_bytes()
+    for code, per_row, esz in spec:
+        nb = n_rows * per_row * esz
+        meta += [code, per_row, nb]
+        offs.append(off)
+        off += _pad(nb)
+    hdr = np.zeros(header_bytes(), dtype=np.uint8)
+    h = np.asarray([MAGIC, n_rows, len(ORDER)] + meta, dtype=np.int64).view(np.uint8)
+    hdr[: h.size] = h
+    return hdr, offs, off
+
+
 def header_bytes(k: int = len(ORDER)) -> int:
     return _pad(24 + 24 * k)
 
@@ -168,8 +191,10 @@ class RcclTrajectoryChannel:
         self.device = torch.device(device)
         self.group = group
 
-    def send(self, mem: Dict[str, np.ndarray], dst: int) -> None:
-        buf = torch.from_numpy(pack_rows(mem)).to(self.device)
+    def send(self, rec, dst: int) -> None:
+        """``rec``: a packed record already in device memory (actor ranks: the pack kernel, see
+        ``parallel.actor_ranks``), or a row dict (tools / tests: packed on the host)."""
+        buf = rec if isinstance(rec, torch.Tensor) else torch.from_numpy(pack_rows(rec)).to(self.device)
         size = torch.tensor([buf.numel()], dtype=torch.int64, device=self.device)
         dist.send(size, dst, group=self.group)
         dist.send(buf, dst, group=self.group)

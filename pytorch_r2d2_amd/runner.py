@@ -8,6 +8,8 @@
 ``run_compat``  -- the reference topology (main.py:10-33): a learner process + N single-env
                    actor processes, Manager-dict weights, file transport (fixed, tensor-only),
                    under the ``Supervisor`` (restarts crashed actors).
+``run_split``   -- learner ranks + actor-only ranks: device-packed trajectory records over RCCL
+                   send/recv, weights broadcast from learner rank 0 (parallel/actor_ranks.py).
 ``run_inproc``  -- single process, CPU or GPU, host replay + torch learner + single-env actors
                    stepping inline (the CartPole plumbing config, tests).
 """
@@ -157,6 +159,126 @@ def run_native(cfg: R2D2Config, steps: int = 1000, actor_steps_per_update: int =
     for s_ in (s_act, s_learn):
         if s_ is not None:
             s_.close()
+    return out
+
+
+def run_split(cfg: R2D2Config, rounds: int = 200, actor_ranks: Optional[int] = None,
+              capacity: Optional[int] = None, log_every: int = 50, use_graph: bool = True,
+              backend: str = "auto") -> Dict:
+    """Split topology (parallel/actor_ranks.py): learner ranks 0 .. L-1 (data parallel), actor
+    ranks L .. W-1 (``BatchedActor`` groups only).  Per round: every actor rank takes
+    ``dist.push_rows`` env steps and sends one device-packed record to its learner; every learner
+    receives, ingests, then (once every learner shard holds a batch of sequences) trains
+    ``dist.learner_steps_per_round`` steps; every ``dist.publish_rounds`` rounds learner 0
+    broadcasts its weights to the actor ranks.  Returns per-role throughput."""
+    import torch.distributed as dist
+
+    from .actor_batched import BatchedActor, PackedWeights
+    from .engine.layout import ParamLayout
+    from .engine.learner_engine import LearnerEngine
+    from .engine.replay_hbm import HBMReplay
+    from .envs.synthetic import VecSyntheticAtari
+    from .parallel.actor_ranks import (TrajectoryPusher, TrajectoryReceiver, broadcast_weights,
+                                       split_roles)
+    from .parallel.dist import init_distributed
+    from .parallel.weights import WeightPublisher
+    from .utils.faults import Liveness
+
+    info = init_distributed(backend=backend)
+    dev = info.device
+    A = int(actor_ranks if actor_ranks is not None else cfg.dist.actor_ranks)
+    learners, actors, feeds = split_roles(info.world, A)
+    dc, rc = cfg.dist, cfg.replay
+    E, K = cfg.actor.envs_per_actor, int(dc.push_rows)
+    W = rc.seq_len + rc.n_step
+    # every rank creates the same groups in the same order
+    g_learn = dist.new_group(learners) if len(learners) > 1 else None
+    g_bcast = dist.new_group([learners[0]] + actors)
+    torch.manual_seed(cfg.seed)
+    L = ParamLayout(cfg.model, cfg.env)
+    live = Liveness("learner" if info.rank in learners else "actor", info.rank, None)
+    out = {"rank": info.rank, "role": "learner" if info.rank in learners else "actor",
+           "rounds": rounds, "world": info.world, "actor_ranks": A}
+    P = max(1, int(dc.publish_rounds))
+    version = 0
+    if info.rank in learners:
+        mine = [a for a in actors if feeds[a] == info.rank]
+        n_sub = max(1, E * len(mine))
+        cap = capacity or cfg.replay.capacity
+        replay = HBMReplay(cfg, dev, capacity=max(cap // n_sub, 2 * (K + W)) * n_sub, n_subrings=n_sub)
+        eng = LearnerEngine(cfg, replay, dev, rank=learners.index(info.rank), world=len(learners),
+                            process_group=g_learn)
+        recv = TrajectoryReceiver(replay, mine, E, K)
+        pub = WeightPublisher(L.padded, dev, src_rank=learners[0], group=g_bcast) \
+            if info.rank == learners[0] else None
+        if pub is not None:
+            broadcast_weights(pub, eng, version)
+        steps, t_train, captured = 0, None, False
+        warm = torch.zeros(1, dtype=torch.float32, device=dev)
+        for r in range(rounds):
+            live.tick(r)
+            recv.recv_all()
+            if not captured:
+                # every learner shard must hold a batch of sequences before any of them steps
+                # (the DP step's collectives need all learner ranks in it)
+                warm.fill_(float(replay.n_valid.item() >= cfg.learner.batch_size))
+                if g_learn is not None:
+                    dist.all_reduce(warm, op=dist.ReduceOp.MIN, group=g_learn)
+                if warm.item() > 0:
+                    if use_graph and cfg.learner.use_graph:
+                        eng.capture(warmup=1)
+                    captured = True
+                    torch.cuda.synchronize(dev)
+                    t_train = time.perf_counter()
+            if captured:
+                for _ in range(int(dc.learner_steps_per_round)):
+                    eng.step()
+                    steps += 1
+            if pub is not None and (r + 1) % P == 0:
+                version += 1
+                broadcast_weights(pub, eng, version)
+            if info.rank == learners[0] and log_every and (r + 1) % log_every == 0 and captured:
+                print(f"[split] round {r + 1} learner steps {steps} loss {eng.loss_value():.4f} "
+                      f"rows {recv.rows}", flush=True)
+        torch.cuda.synchronize(dev)
+        eng.check_errors()
+        el = time.perf_counter() - t_train if t_train else 0.0
+        out.update(learner_steps=steps, learner_steps_per_s=steps / el if el > 0 else 0.0,
+                   rows_ingested=recv.rows, records=recv.records, weights_version=version,
+                   n_valid=int(replay.n_valid.item()), final_loss=eng.loss_value() if steps else None,
+                   engine=eng, replay=replay)
+    else:
+        cap_e = max(2 * (K + W), 512)
+        replay = HBMReplay(cfg, dev, capacity=cap_e * E, n_subrings=E)
+        w_on, w_tg = PackedWeights(L, dev), PackedWeights(L, dev)
+        pub = WeightPublisher(L.padded, dev, src_rank=learners[0], group=g_bcast)
+        broadcast_weights(pub, None, version, (w_on, w_tg))
+        env = VecSyntheticAtari(E, dev, seed=cfg.seed + 101 * info.rank, episode_len=cfg.env.episode_len,
+                                n_actions=cfg.model.n_actions,
+                                n_stacks=cfg.env.channels_per_frame * cfg.env.n_stacks,
+                                shape=(cfg.env.frame_h, cfg.env.frame_w), switch=cfg.env.switch,
+                                cue_only_first=cfg.env.cue_only_first)
+        idx = actors.index(info.rank)
+        actor = BatchedActor(cfg, replay, env, w_on, w_tg, global_env_offset=idx * E,
+                             total_envs=A * E, seed=cfg.seed + info.rank)
+        if use_graph and cfg.actor.use_graph and actor.can_capture:
+            actor.capture(warmup=0)
+        push = TrajectoryPusher(replay, K, feeds[info.rank])
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for r in range(rounds):
+            live.tick(r)
+            for _ in range(K):
+                actor.step()
+            push.push(r)
+            if (r + 1) % P == 0:
+                version += 1
+                broadcast_weights(pub, None, version, (w_on, w_tg))
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        out.update(env_steps=actor.env_steps, env_steps_per_s=actor.env_steps / el,
+                   windows=push.windows, weights_version=w_on.version,
+                   returns=list(actor.finished_returns))
     return out
 
 

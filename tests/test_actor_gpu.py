@@ -291,3 +291,44 @@ def test_dp_engine_global_sampling_weights(tmp_path, graph):
         torch.testing.assert_close(r[k]["is_w"], dp_is_weights(r[k]["probs"], params, r[k]["beta"]),
                                    rtol=2e-6, atol=1e-7)
     assert max(float(r[k]["is_w"].max()) for k in range(2)) == pytest.approx(1.0, rel=1e-6)
+
+
+@pytest.mark.parametrize("cue_only_first", [False, True])
+def test_fused_synthetic_env_step_dynamics(cue_only_first):
+    """csrc/kernels/env.hip (one launch per step of all E envs) against the env's rules: reward =
+    (action == target before the step), episode counter / auto-reset / finished returns, targets
+    redrawn only on switch steps, and the rendered observation: the target's column band at 220
+    exactly when the cue is shown, noise in 0..47 everywhere else."""
+    E, A, ep, sw = 32, 6, 19, 4
+    env = VecSyntheticAtari(E, DEV, seed=5, episode_len=ep, n_actions=A, switch=sw,
+                            cue_only_first=cue_only_first)
+    assert env.fused
+    env.reset_all()
+    g = torch.Generator(device=DEV).manual_seed(1)
+    ret = torch.zeros(E, device=DEV)
+    band = 84 // A
+    cols = torch.arange(84, device=DEV)
+    for _ in range(3 * ep):
+        t0, tgt0 = env.t.clone(), env.target.clone()
+        act = torch.randint(0, A, (E,), device=DEV, generator=g)
+        r, d, f = env.step(act)
+        exp_r = (act == tgt0).float()
+        assert torch.equal(r, exp_r)
+        t1 = t0 + 1
+        assert torch.equal(d, t1 >= ep)
+        ret += exp_r
+        fin = torch.where(d, ret, torch.full_like(ret, float("nan")))
+        assert torch.equal(torch.isnan(f), torch.isnan(fin)) and torch.equal(f[d], fin[d])
+        ret[d] = 0
+        assert torch.equal(env.t, torch.where(d, torch.zeros_like(t1), t1))
+        keep = (t1 % sw) != 0
+        assert torch.equal(env.target[keep], tgt0[keep])
+        assert int(env.target.min()) >= 0 and int(env.target.max()) < A
+        fr = env.frames.view(E, 4, 84, 84)
+        in_band = (cols[None, :] // band == env.target[:, None]) & (cols[None, :] < band * A)   # (E, W)
+        show = torch.ones(E, dtype=torch.bool, device=DEV) if not cue_only_first else (env.t % sw) == 0
+        m = (in_band & show[:, None])[:, None, None, :].expand_as(fr)
+        assert bool((fr[m] == 220).all())
+        assert int(fr[~m].max()) <= 47
+    noise = env.frames.view(E, 4, 84, 84).float()
+    assert 20.0 < float(noise[noise <= 47].mean()) < 27.0

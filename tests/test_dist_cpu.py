@@ -138,3 +138,53 @@ def test_torso_bwd_grid_leaves_cus_for_the_allreduce():
             g = torso_bwd_grid(n, r)
             assert 1 <= g <= min(n, 256 - r if r else 256)
             assert -(-n // g) == -(-n // min(n, 256 - r))   # same per-workgroup frame count
+
+
+def test_split_roles_and_record_spec_match_pack_rows():
+    import numpy as np
+    from pytorch_r2d2_amd.parallel.actor_ranks import split_roles
+    from pytorch_r2d2_amd.parallel.trajectory import pack_rows, record_layout, record_spec
+    from pytorch_r2d2_amd.replay.memory import ReplayMemory
+    assert split_roles(8, 6) == ([0, 1], [2, 3, 4, 5, 6, 7], {2: 0, 3: 1, 4: 0, 5: 1, 6: 0, 7: 1})
+    with pytest.raises(ValueError):
+        split_roles(2, 2)
+    rm = ReplayMemory(13, 8, 3, (84, 84), 256, 4, 4, obs_shape=(4, 84, 84))
+    buf = pack_rows(rm.memory)
+    hdr, offs, total = record_spec(13, 4 * 84 * 84, 512)
+    assert total == buf.size and np.array_equal(buf[: hdr.size], hdr)
+    assert [f[3] for f in record_layout(buf)[1].values()] == offs
+
+
+def _bcast_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from pytorch_r2d2_amd.parallel.actor_ranks import split_roles
+    from pytorch_r2d2_amd.parallel.dist import init_distributed
+    from pytorch_r2d2_amd.parallel.weights import WeightPublisher
+    init_distributed(backend="gloo", device_type="cpu")
+    learners, actors, _ = split_roles(world, 2)
+    g_learn = dist.new_group(learners) if len(learners) > 1 else None   # same order on all ranks
+    g_b = dist.new_group([learners[0]] + actors)
+    got = []
+    if rank in [learners[0]] + actors:
+        pub = WeightPublisher(10, "cpu", src_rank=learners[0], group=g_b)
+        for v in range(3):
+            w = torch.full((10,), float(v + 1)) if rank == learners[0] else None
+            pub.publish(w, None if w is None else -w, v)
+            on, tg, ver = pub.current()
+            got.append((on.clone(), tg.clone(), ver))
+    torch.save(got, os.path.join(outdir, f"b{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_weight_broadcast_over_actor_rank_group(tmp_path):
+    """WeightPublisher on the split topology's {learner 0} + actor-ranks group (gloo, world 4:
+    2 learner ranks, 2 actor ranks): versioned, every actor rank sees learner 0's weights, learner
+    rank 1 is not in the group."""
+    tmp.spawn(_bcast_worker, args=(4, _free_port(), str(tmp_path)), nprocs=4, join=True)
+    r = {k: torch.load(os.path.join(tmp_path, f"b{k}.pt"), weights_only=True) for k in range(4)}
+    assert r[1] == []
+    for k in (2, 3):
+        for v, (on, tg, ver) in enumerate(r[k]):
+            assert ver == v and torch.equal(on, torch.full((10,), float(v + 1))) and torch.equal(tg, -on)

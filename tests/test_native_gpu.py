@@ -42,8 +42,15 @@ def _record(n, seed, T=10, H=256):
     return m
 
 
-def _check_replay_rows(rp, m, sub, head):
+def _check_replay_rows(rp, m, sub, head, cleared_tail=0):
+    """``cleared_tail``: the last rows of a record followed by another record in the same sub-ring
+    lost their starts (ingest.hip: a window running into the next record's rows is invalid)."""
     n = m["state"].shape[0]
+    if cleared_tail:
+        m = dict(m)
+        st = m["is_seq_start"].copy()
+        st[n - cleared_tail:] = 0
+        m["is_seq_start"] = st
     rows = sub * rp.cap_e + (head + np.arange(n)) % rp.cap_e
     r = torch.as_tensor(rows, device=DEV)
     np.testing.assert_array_equal(rp.frames[r].cpu().numpy(), m["state"].reshape(n, -1))
@@ -118,10 +125,11 @@ def test_shm_ring_ingestor_dma_into_hbm():
             ing._release_done(wait=True)
         torch.cuda.synchronize()
         assert total == sum(m["state"].shape[0] for ms in recs.values() for m in ms)
+        W = cfg.replay.seq_len + cfg.replay.n_step
         for i in range(3):
             head = 0
-            for m in recs[i]:
-                _check_replay_rows(rp, m, i, head)
+            for j, m in enumerate(recs[i]):
+                _check_replay_rows(rp, m, i, head, cleared_tail=(W - 1) if j + 1 < len(recs[i]) else 0)
                 head += m["state"].shape[0]
         _tree_consistent(rp)
         assert all(ws.ring.used() >= 0 for ws in writers)
@@ -406,3 +414,97 @@ def test_td_row_priorities_last_write_wins(fused):
     ref[rows.reshape(-1)] = ((ad + 1e-6) ** 0.9).reshape(-1)
     np.testing.assert_allclose(outs[0].numpy(), ref, rtol=1e-6)
     assert torch.equal(outs[0], outs[1])
+
+
+def test_actor_rank_window_pack_and_env_major_ingest():
+    """Split topology data path without the network: an actor group's replay windows packed on the
+    device (pack_rows_kernel: K + W - 1 rows per env, only starts whose window lies inside the
+    record) and scattered env-major into a learner replay: every row bit-identical, every learner
+    start a start of the actor with its whole window received, each actor sequence shipped
+    exactly once, the tree consistent."""
+    import ctypes as C
+    from pytorch_r2d2_amd.actor_batched import BatchedActor, PackedWeights
+    from pytorch_r2d2_amd.engine.ingest import ingest_args
+    from pytorch_r2d2_amd.engine.layout import ParamLayout
+    from pytorch_r2d2_amd.envs.synthetic import VecSyntheticAtari
+    from pytorch_r2d2_amd.models import QNet
+    from pytorch_r2d2_amd.ops._lib import ptr, stream_handle
+    from pytorch_r2d2_amd.parallel.actor_ranks import TrajectoryPusher
+    cfg = _small_cfg()
+    E, K = 4, 16
+    W = cfg.replay.seq_len + cfg.replay.n_step
+    act_rp = HBMReplay(cfg, DEV, capacity=E * 128, n_subrings=E)
+    L = ParamLayout(cfg.model, cfg.env)
+    w = PackedWeights(L, DEV)
+    torch.manual_seed(0)
+    w.load(QNet("cpu", cfg.model, cfg.env).state_dict())
+    env = VecSyntheticAtari(E, DEV, seed=9, episode_len=23)
+    actor = BatchedActor(cfg, act_rp, env, w, w, seed=2)
+    push = TrajectoryPusher(act_rp, K, dst=0)
+    R = push.R
+    lrn = HBMReplay(cfg, DEV, capacity=E * 300, n_subrings=E)
+    shipped_starts = 0
+    for c in range(12):
+        for _ in range(K):
+            actor.step()
+        rec = push.pack(c)
+        torch.cuda.synchronize()
+        h_act = (c * K - (W - 1)) % act_rp.cap_e
+        a_rows = (torch.arange(E, device=DEV)[:, None] * act_rp.cap_e
+                  + (h_act + torch.arange(R, device=DEV)[None, :]) % act_rp.cap_e).reshape(-1)
+        h_lrn = lrn.ihead.clone()
+        a = ingest_args(lrn, ptr(rec), push.nbytes, 0, True, rows_per_sub=R)
+        assert kernels().r2_ingest_record(C.byref(a), C.c_void_p(stream_handle())) == 0
+        lrn.repair_after_ingest()
+        torch.cuda.synchronize()
+        l_rows = (torch.arange(E, device=DEV)[:, None] * lrn.cap_e
+                  + (h_lrn[:, None] + torch.arange(R, device=DEV)[None, :]) % lrn.cap_e).reshape(-1)
+        for name in ("frames", "hs_cs", "target_hs_cs", "action", "reward", "done", "priority"):
+            assert torch.equal(getattr(lrn, name)[l_rows], getattr(act_rp, name)[a_rows]), (c, name)
+        j = torch.arange(R, device=DEV).repeat(E)
+        keep = (j < K) & (j >= (W - 1 if c == 0 else 0))
+        exp = act_rp.is_start[a_rows].bool() & keep
+        assert torch.equal(lrn.is_start[l_rows].bool(), exp), c
+        assert torch.equal(lrn.tree[l_rows], torch.where(exp, act_rp.tree[a_rows], 0.0)), c
+        shipped_starts += int(exp.sum())
+        assert int(lrn.ihead[0]) == (c + 1) * R % lrn.cap_e
+    _tree_consistent(lrn)
+    assert shipped_starts > 20 and int(lrn.ingest_err.item()) == 0
+
+
+def _split_worker(rank, world, port, outdir):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0")
+    from pytorch_r2d2_amd.runner import run_split
+    cfg = _small_cfg(**{"actor.envs_per_actor": 8, "dist.push_rows": 16, "dist.publish_rounds": 4,
+                        "learner.publish_interval": 4, "env.episode_len": 30})
+    out = run_split(cfg, rounds=16, actor_ranks=world - 1, capacity=8 * 600, backend="gloo",
+                    log_every=0)
+    keep = {k: v for k, v in out.items() if isinstance(v, (int, float, str)) or v is None}
+    if out["role"] == "learner":
+        keep["master"] = out["engine"].master.detach().cpu()
+    torch.save(keep, os.path.join(outdir, f"split{rank}.pt"))
+    import torch.distributed as dist
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_split_topology_actor_rank_feeds_learner_rank(tmp_path):
+    """run_split with 1 learner rank + 1 actor rank sharing this GPU (gloo staging): 16 rounds of
+    device-packed windows -> learner ingest -> training, weights broadcast every 4 rounds."""
+    import socket
+    import torch.multiprocessing as tmp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    tmp.spawn(_split_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    lr = torch.load(tmp_path / "split0.pt", weights_only=True)
+    ac = torch.load(tmp_path / "split1.pt", weights_only=True)
+    assert lr["role"] == "learner" and ac["role"] == "actor"
+    assert ac["windows"] == 16 and lr["records"] == 16
+    assert lr["rows_ingested"] == 16 * 8 * (16 + 12)     # rounds x E x (K + W - 1)
+    assert lr["learner_steps"] > 0 and lr["n_valid"] > 0
+    assert ac["weights_version"] == lr["weights_version"] == 4
+    assert torch.isfinite(lr["master"]).all()
