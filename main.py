@@ -49,6 +49,10 @@ def build_parser():
                    help="native: GPU actor group and learner run simultaneously on disjoint CUs")
     p.add_argument("--actor-cus-per-xcd", type=int, default=4)
     p.add_argument("--actor-steps", type=int, default=1, help="native: env steps per learner step")
+    p.add_argument("--actor-ranks", type=int, default=0,
+                   help="native under torchrun: the last N ranks run GPU actor groups only and feed "
+                        "the learner ranks (split topology, parallel/actor_ranks.py)")
+    p.add_argument("--rounds", type=int, default=200, help="split topology: actor push rounds")
     return p
 
 
@@ -60,7 +64,11 @@ def run(argv=None):
     if args.env:
         overrides["env.name"] = args.env
     cfg = get_config(preset, **overrides)
-    if args.mode == "native" and args.cpu_actors > 0:
+    if args.mode == "native" and args.actor_ranks > 0:
+        from pytorch_r2d2_amd.runner import run_split
+        out = run_split(cfg, rounds=args.rounds, actor_ranks=args.actor_ranks, capacity=args.capacity)
+        out = {k: v for k, v in out.items() if k not in ("engine", "replay")}
+    elif args.mode == "native" and args.cpu_actors > 0:
         from pytorch_r2d2_amd.runner import run_native_cpu_actors
         out = run_native_cpu_actors(cfg, args.cpu_actors, steps=args.steps or 1000,
                                     capacity=args.capacity, metrics_path=args.metrics)

@@ -46,6 +46,10 @@ def actor_process(actor_id, n_actors, shared_dict, device="cuda:0", cfg: Optiona
     shared-memory weight slot (seqlock); without them the reference file / Manager-dict transport."""
     if isinstance(device, str) and device.startswith("cuda") and not torch.cuda.is_available():
         device = "cpu"
+    if str(device) == "cpu":
+        # one intra-op thread per CPU actor process by default: N actors x the machine's cores
+        # threads each would oversubscribe the host many times over
+        torch.set_num_threads(int(os.environ.get("R2D2_ACTOR_THREADS", "1")))
     actor = Actor(actor_id, n_actors, shared_dict, device, cfg=cfg, memory_path=memory_path, seed=seed)
     if shm_ring:
         from .parallel.trajectory import ShmTrajectoryWriter

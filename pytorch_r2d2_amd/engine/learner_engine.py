@@ -51,7 +51,8 @@ from ..ops._lib import check, kernels, ptr, stream_handle
 from ..ops.gemm import G5_CFGS, Gemm, gemm, gemm_group, gemm_sp, gemm_sp_ws_bytes, group_ws_bytes
 from ..models.qnet import torso_dims
 from ..ops.torso_lib import (fused_torso_fwd_geom, fused_torso_supported, gather_frames_nhwc,
-                             torso_forward_library, torso_fwd_fused)
+                             torso_backward_library_sp, torso_forward_library,
+                             torso_forward_library_sp, torso_fwd_fused)
 from .layout import ParamLayout, UNITS
 from .replay_hbm import HBMReplay
 
@@ -215,13 +216,19 @@ class LearnerEngine:
         if d.type == "cuda":
             kernels().r2_lstm_sp_handoff8(0 if lc.lstm_tag_words else 1)
             kernels().r2_lstm_bwd_handoff8(0 if lc.lstm_tag_words else 1)
-        if sp and not (self.fused_torso and d.type == "cuda" and L.H <= 256
+        if sp and not (cfg.model.torso == "atari" and d.type == "cuda" and L.H <= 256
                        and lc.lstm_impl == "persistent" and lc.lstm_handoff == "tagged"):
             raise NotImplementedError(
-                "compute_dtype=fp32 (split precision) runs the fused Atari torso (4x84x84), hidden "
-                "<= 256 and the tagged persistent LSTM on a GPU; use compute_dtype=bf16 or the torch "
-                "learner (learner_ref.py) for other configurations")
-        if (self.fwd_geom is None or lc.torso_bwd != "fused") and cfg.learner.conv_autotune and d.type == "cuda":
+                "compute_dtype=fp32 (split precision) runs the conv torso, hidden <= 256 and the "
+                "tagged persistent LSTM on a GPU; use compute_dtype=bf16 or the torch learner "
+                "(learner_ref.py) for other configurations")
+        # fp32 on a frame geometry the fused split torso (torso_sp.hip, Atari 4x84x84) does not
+        # cover, e.g. DMLab-30 RGB: IEEE fp32 library convs feeding the same split planes
+        self.sp_lib = sp and not self.fused_torso
+        if self.sp_lib:
+            torch.backends.cudnn.allow_tf32 = False     # the convs must stay IEEE fp32
+        if (self.fwd_geom is None or lc.torso_bwd != "fused" or self.sp_lib) \
+                and cfg.learner.conv_autotune and d.type == "cuda":
             # library conv path: let MIOpen benchmark its solutions once per shape (find mode);
             # DMLab-30: 463 -> 503 learner steps/s
             torch.backends.cudnn.benchmark = True
@@ -229,8 +236,12 @@ class LearnerEngine:
             cin, dims, _ = torso_dims(cfg.env, cfg.model)
             c1, c2, _c3 = cfg.model.conv_channels
             self.tdims = (cin, dims)
-            self.act1, self.act1_lo = zsp(Ll * B, dims[0][0] * dims[0][1], c1)
-            self.act2, self.act2_lo = zsp(Ll * B, dims[1][0] * dims[1][1], c2)
+            if self.sp_lib:     # fp32 activations for the library backward
+                self.act1, self.act1_lo = z(Ll * B, dims[0][0] * dims[0][1], c1), None
+                self.act2, self.act2_lo = z(Ll * B, dims[1][0] * dims[1][1], c2), None
+            else:
+                self.act1, self.act1_lo = zsp(Ll * B, dims[0][0] * dims[0][1], c1)
+                self.act2, self.act2_lo = zsp(Ll * B, dims[1][0] * dims[1][1], c2)
             self.frames_bf = z(Ll * B, cfg.env.frame_h * cfg.env.frame_w * cin, dt=bf16)
         self.h0 = {k: z(B, H, dt=act_dt) for k in ("on", "tg", "nx")}
         self.c0 = {k: z(B, H) for k in ("on", "tg", "nx")}
@@ -512,7 +523,13 @@ class LearnerEngine:
         pk, pt = self.pk, self.pk_t
         rows = self.rows
         # torso: online over all Tn frames (save activations of the learning frames) and target
-        if self.sp:
+        if self.sp_lib:
+            env, mc = self.cfg.env, self.cfg.model
+            torso_forward_library_sp(rp.frames, rows, L, self.master, env, mc, self.X_on,
+                                     self.X_on_lo, self.act1, self.act2, save_lo=Lb * B)
+            torso_forward_library_sp(rp.frames, rows[self.t_lo_tg * B:], L, self.target, env, mc,
+                                     self.X_tg, self.X_tg_lo)
+        elif self.sp:
             pkl, ptl = self.pk_lo, self.pk_t_lo
             Xo, Xol, Xt, Xtl = self.X_on, self.X_on_lo, self.X_tg, self.X_tg_lo
             jobs = [self._torso_job_sp(pk, pkl, rows[: Lb * B], Xo[: Lb * B], Xol[: Lb * B]),
@@ -867,6 +884,13 @@ class LearnerEngine:
         return grad * (act > 0)
 
     def _backward_torso(self):
+        if self.sp_lib:
+            B, Lb, T = self.B, self.Lb, self.T
+            torso_backward_library_sp(self.replay.frames, self.rows[Lb * B: T * B], self.layout,
+                                      self.master, self.cfg.env, self.cfg.model, self.tdims[1],
+                                      self.dX, self.dX_lo, self.X_on[Lb * B: T * B], self.act1,
+                                      self.act2, self.grad)
+            return
         if self.sp:
             B, Lb, T = self.B, self.Lb, self.T
             pk, pkl = self.pk, self.pk_lo

@@ -109,3 +109,60 @@ def torso_forward_library(frames: torch.Tensor, rows: Optional[torch.Tensor], la
         if act is not None:
             m = min(act.shape[0], n - save_lo)
             act[:m].copy_(y[save_lo:save_lo + m].permute(0, 2, 3, 1).reshape(m, -1, y.shape[1]))
+
+
+def torso_forward_library_sp(frames: torch.Tensor, rows: Optional[torch.Tensor], layout,
+                             flat: torch.Tensor, env: EnvConfig, model: ModelConfig,
+                             out: torch.Tensor, out_lo: torch.Tensor,
+                             act1: Optional[torch.Tensor] = None, act2: Optional[torch.Tensor] = None,
+                             save_lo: int = 0):
+    """fp32 (compute_dtype "fp32") library torso for geometries the split-precision fused kernel
+    (torso_sp.hip, Atari 4x84x84 only) does not cover, e.g. DMLab-30 RGB 3x72x96: IEEE fp32 convs
+    (MIOpen, channels-last), the features written as the (hi, lo) bf16 planes every split GEMM of
+    the step reads (out + out_lo == the fp32 value to 2^-16 relative), the conv1 / conv2
+    activations of frames [save_lo, ...) saved in fp32 for ``torso_backward_library_sp``."""
+    cin = env.channels_per_frame * env.n_stacks
+    x = gather_frames_nhwc(frames, rows, cin, env.frame_h, env.frame_w).float()  # exact 0..255
+    n = x.shape[0]
+    v = lambda k: layout.view(flat, k)
+    y1 = F.conv2d(x, v("vis_layers.0.weight") * (1.0 / 255), v("vis_layers.0.bias"), stride=4).relu_()
+    y2 = F.conv2d(y1, v("vis_layers.2.weight"), v("vis_layers.2.bias"), stride=2).relu_()
+    y3 = F.conv2d(y2, v("vis_layers.4.weight"), v("vis_layers.4.bias"), stride=1).relu_()
+    y = y3.contiguous().view(n, -1)                            # torch (C,H,W) flatten order
+    hi = y.to(torch.bfloat16)
+    out.copy_(hi)
+    out_lo.copy_(y - hi.float())
+    for act, a in ((act1, y1), (act2, y2)):
+        if act is not None:
+            m = min(act.shape[0], n - save_lo)
+            act[:m].copy_(a[save_lo:save_lo + m].permute(0, 2, 3, 1).reshape(m, -1, a.shape[1]))
+
+
+def torso_backward_library_sp(frames: torch.Tensor, rows: torch.Tensor, layout, flat: torch.Tensor,
+                              env: EnvConfig, model: ModelConfig, dims, dX: torch.Tensor,
+                              dX_lo: torch.Tensor, X: torch.Tensor, act1: torch.Tensor,
+                              act2: torch.Tensor, grad: torch.Tensor) -> None:
+    """fp32 conv-torso backward of ``torso_forward_library_sp``: dX = hi + lo planes, ReLU masks
+    from the saved activations (X: the forward's hi plane, > 0 exactly where the fp32 value is),
+    IEEE fp32 ``convolution_backward``; the six torso gradients written into ``grad``."""
+    cin = env.channels_per_frame * env.n_stacks
+    c1, c2, c3 = model.conv_channels
+    (h1, w1), (h2, w2), (h3, w3) = dims
+    N = dX.shape[0]
+    cl = torch.channels_last
+    g3 = ((dX.float() + dX_lo.float()) * (X > 0)).view(N, c3, h3, w3).contiguous(memory_format=cl)
+    a2 = act2.view(N, h2, w2, c2).permute(0, 3, 1, 2)
+    a1 = act1.view(N, h1, w1, c1).permute(0, 3, 1, 2)
+    v = lambda k: layout.view(flat, k)
+    cb = torch.ops.aten.convolution_backward
+    d2, dw3, db3 = cb(g3, a2, v("vis_layers.4.weight"), [c3], [1, 1], [0, 0], [1, 1], False,
+                      [0, 0], 1, [True, True, True])
+    d1, dw2, db2 = cb(d2 * (a2 > 0), a1, v("vis_layers.2.weight"), [c2], [2, 2], [0, 0], [1, 1],
+                      False, [0, 0], 1, [True, True, True])
+    x = gather_frames_nhwc(frames, rows, cin, env.frame_h, env.frame_w).float()
+    _, dw1, db1 = cb(d1 * (a1 > 0), x, v("vis_layers.0.weight"), [c1], [4, 4], [0, 0], [1, 1],
+                     False, [0, 0], 1, [False, True, True])
+    for k, t in (("vis_layers.4.weight", dw3), ("vis_layers.4.bias", db3),
+                 ("vis_layers.2.weight", dw2), ("vis_layers.2.bias", db2),
+                 ("vis_layers.0.weight", dw1 * (1.0 / 255)), ("vis_layers.0.bias", db1)):
+        layout.view(grad, k).copy_(t)

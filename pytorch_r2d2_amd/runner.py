@@ -385,6 +385,8 @@ def run_native_cpu_actors(cfg: R2D2Config, n_actors: int, steps: int = 1000,
                wall_s=t_end - t0, ingest_host_s=t_ing,
                learner_steps_per_s=(it / (t_end - t_train0)) if t_train0 and it else 0.0,
                ingest_rows_per_s=ingest.rows / (t_end - t0), weights_version=version,
+               # every ingested row is one CPU env step (the actors' aggregate env throughput)
+               cpu_env_steps_per_s=ingest.rows / (t_end - t0),
                rejected_records=ingest.rejected,
                supervisor=sup.report, zero_copy=[b is not None for b in ingest.registered])
     return out

@@ -9,6 +9,10 @@ processes) or programmatically, as ``;``-separated specs:
     push:<id>:drop=<prob>             drop a trajectory push with probability p
     weights:<id>:stale=<n>            ignore the first n weight publications
 
+Add ``once=1`` to a crash / hang rule (``actor:3:crash_at=500,once=1``) to fire it only in the
+process's first incarnation: the supervisor exports ``R2D2_INCARNATION`` (its restart count) to
+every child, so the restarted actor runs on instead of failing at the same step again.
+
 Roles call ``faults().check(role, id, step)`` / ``faults().drop(role, id)``; with no spec the
 calls are a dict lookup.
 """
@@ -39,6 +43,8 @@ class FaultPlan:
     def check(self, role: str, rid: int, step: int) -> None:
         r = self._r(role, rid)
         if not r:
+            return
+        if r.get("once") and int(os.environ.get("R2D2_INCARNATION", "0")) > 0:
             return
         if "crash_at" in r and step >= r["crash_at"]:
             os._exit(EXIT_CODE)

@@ -48,8 +48,9 @@ class RoleSpec:
     max_restarts: int = 3
 
 
-def _child_entry(target, args, kwargs, beat: Beat):
+def _child_entry(target, args, kwargs, beat: Beat, incarnation: int = 0):
     import inspect
+    os.environ["R2D2_INCARNATION"] = str(incarnation)    # read by utils/faults.py once-rules
     beat(0, 1)
     kwargs = dict(kwargs)
     try:
@@ -74,7 +75,8 @@ class Supervisor:
     def _start(self, i: int):
         r = self.roles[i]
         beat = Beat(self.table_name, len(self.roles), i)
-        p = self.ctx.Process(target=_child_entry, args=(r.target, r.args, r.kwargs, beat),
+        p = self.ctx.Process(target=_child_entry, args=(r.target, r.args, r.kwargs, beat,
+                                                               self.report[r.name]["restarts"]),
                              name=r.name, daemon=False)
         p.start()
         self.procs[i] = p

@@ -225,3 +225,13 @@ def test_supervisor_restarts_crashed_actor_and_kills_stalled(monkeypatch):
     assert rep["actor0"]["restarts"] == 2
     assert 17 in rep["actor0"]["exitcodes"]
     assert rep["actor1"]["stalls"] >= 1
+
+
+def test_once_fault_fires_in_first_incarnation_only(monkeypatch):
+    """``once=1``: the restarted actor (R2D2_INCARNATION=1) runs past the crash step to a clean
+    exit; the supervisor reports one restart and the exit codes [17, 0]."""
+    from pytorch_r2d2_amd.utils.supervisor import RoleSpec, Supervisor
+    monkeypatch.setenv("R2D2_FAULTS", "actor:0:crash_at=20,once=1")
+    sup = Supervisor([RoleSpec("actor0", _crashy, (0,), max_restarts=3)], poll_s=0.05)
+    rep = sup.run(timeout_s=60)
+    assert rep["actor0"]["restarts"] == 1 and rep["actor0"]["exitcodes"] == [17, 0], rep

@@ -124,15 +124,18 @@ def _oracle64(rp, eng, net, tgt, cfg, mode):
     return _oracle(rp, eng, net, tgt, cfg, mode, torch.float64)
 
 
-@pytest.mark.parametrize("mode", ["fixed", "shifted", "reference"])
-def test_engine_fp32_matches_fp64_oracle(mode):
+@pytest.mark.parametrize("mode,preset", [("fixed", "atari57"), ("shifted", "atari57"),
+                                         ("reference", "atari57"), ("fixed", "dmlab30")])
+def test_engine_fp32_matches_fp64_oracle(mode, preset):
     """The fp32 (split-precision) learner step against the float64 truth, with plain fp32 PyTorch
     as the yardstick.  With random-init nets the TD error is a small difference of two Q values,
     so every fp32 implementation's gradient error is amplified: fp32 PyTorch itself lands 1e-4 ..
     5e-4 off float64 on these tensors (tools/sp_oracle_calib.py, CPU and GPU alike).  The engine
     must be within 1e-4 of the truth or no worse than 2x fp32 PyTorch, on the loss, all 18
-    gradients and the replay priorities; its forward activations are ~5e-6 off (test below)."""
-    cfg, rp, eng, net, tgt = _make(mode)
+    gradients and the replay priorities; its forward activations are ~5e-6 off (test below).
+    dmlab30 (RGB 3x72x96): the fp32 library torso (ops/torso_lib.py) feeding the split planes."""
+    cfg, rp, eng, net, tgt = _make(mode, preset=preset)
+    assert eng.sp_lib == (preset == "dmlab30")
     eng._forward_loss()
     eng._backward_core()
     eng._backward_torso()
@@ -155,6 +158,12 @@ def test_engine_fp32_matches_fp64_oracle(mode):
     rows = base[None] + (s[None] - base[None] + torch.arange(Lb, T, device=DEV)[:, None]) % rp.cap_e
     p32 = _rel(out32["priority"], out["priority"])
     assert _rel(rp.priority[rows].cpu(), out["priority"]) < max(1e-4, 2 * p32)
+    if preset == "dmlab30":     # the library convs inside the captured step
+        eng.capture(warmup=1)
+        for _ in range(3):
+            eng.step()
+        torch.cuda.synchronize()
+        assert eng.error_word() == 0 and torch.isfinite(eng.master).all()
 
 
 def test_engine_fp32_matches_fp64_oracle_at_bench_shape():
