@@ -163,10 +163,20 @@ def test_inproc_cartpole_learns():
     weights, stored state, on the CPU): 4 in-process actors + the fp32 torch learner.  A random
     policy balances ~20 steps; after 1800 learner steps the mean return of the last 20 episodes
     must be >= 150 (seeds 0 / 1 measured 206 at 1500 / 275 at 1800 steps, ~70 s on 8 CPUs)."""
+    import random
     from pytorch_r2d2_amd.runner import run_inproc
+    # every RNG and the intra-op thread count pinned: the outcome must not depend on which tests
+    # ran before in the same process
     torch.manual_seed(0)
-    cfg = get_config("cartpole")
-    out = run_inproc(cfg, steps=1800, n_actors=4, actor_steps_per_update=4, log_every=300)
+    np.random.seed(0)
+    random.seed(0)
+    nt = torch.get_num_threads()
+    torch.set_num_threads(4)
+    try:
+        cfg = get_config("cartpole")
+        out = run_inproc(cfg, steps=1800, n_actors=4, actor_steps_per_update=4, log_every=300)
+    finally:
+        torch.set_num_threads(nt)
     rets = out["returns"]
     assert len(rets) >= 40 and all(np.isfinite(out["losses"]))
     assert np.mean(rets[-20:]) >= 150, (np.mean(rets[:20]), np.mean(rets[-20:]))
