@@ -14,6 +14,13 @@
 //   ingest_tail_kernel  advances the sub-ring's device write head and the rows counter
 //
 // No host work besides the launch: the write head lives on the device.
+//
+// Every sub-ring holds ONE producer's stream, written contiguously, so no start outside the
+// written rows can go stale: the rows just behind the write head are that stream's newest rows
+// (the starts there run on into the rows written now, their true continuation), every row ahead
+// of it is untouched old data.  Producers keep each start's window inside the stream they have
+// shipped: an actor rank ships overlapping windows (pack_rows_kernel below), a CPU actor whole
+// episodes (its last sequence's n-step tail past the episode end is masked by `done`).
 #include "../common.h"
 
 #define ING_FIELDS 10   // state hs_cs target_hs_cs action reward done stack_count priority seqprio start
@@ -42,9 +49,6 @@ struct IngestArgs {
   int FB, H2, cap_e;
   int rows_per_sub;         // > 0: rows i*rps .. (i+1)*rps - 1 go to sub-ring sub + i (an actor
                             // rank's E env windows in one record); 0: every row to sub-ring sub
-  int W;                    // rows a sequence touches (T + n): the W - 1 positions in front of
-                            // each written range lose their starts (their windows now run into
-                            // new data; a record's own starts keep their windows inside it)
 };
 
 struct RecView {
@@ -92,35 +96,12 @@ __device__ __forceinline__ float scalar_at(const uint8_t* base, int code, long l
   return (float)base[i];
 }
 
-__device__ __forceinline__ void ingest_clear(const IngestArgs& a, long long row) {
-  if (a.is_start[row] || a.leaves[row] != 0.f) {
-    if (a.is_start[row]) atomicSub(a.n_valid, 1);
-    a.is_start[row] = 0;
-    a.leaves[row] = 0.f;
-    if (a.dirty) {
-      const int slot = atomicAdd(a.count, 1);
-      if (slot < a.max_dirty) a.dirty[slot] = (int)row;
-    }
-  }
-}
-
-__global__ __launch_bounds__(256) void ingest_rows_kernel(const IngestArgs a, int grid_rows) {
+__global__ __launch_bounds__(256) void ingest_rows_kernel(const IngestArgs a) {
   RecView v;
   const bool ok = parse_record(a, v);
   const int tid = threadIdx.x;
   if (!ok) {
     if (blockIdx.x == 0 && tid == 0) atomicOr(a.err, 1u);
-    return;
-  }
-  if ((int)blockIdx.x >= grid_rows) {
-    // the W - 1 positions in front of each written range (disjoint from every written row:
-    // rows per sub-ring + W - 1 <= cap_e, checked by the launcher)
-    if (tid != 0) return;
-    const int q = (int)blockIdx.x - grid_rows, wm = a.W > 1 ? a.W - 1 : 1;
-    const int sub = a.sub + q / wm, k = q % wm + 1;
-    if (a.rows_per_sub > 0 && (long long)(q / wm) >= v.n / a.rows_per_sub) return;
-    const long long pos = ((a.ihead[sub] - k) % a.cap_e + a.cap_e) % a.cap_e;
-    ingest_clear(a, (long long)sub * a.cap_e + pos);
     return;
   }
   long long src, row;
@@ -262,13 +243,9 @@ extern "C" int r2_ingest_record(const IngestArgs* a, void* stream) {
   if (!a->rec || a->max_rows <= 0 || a->cap_e <= 0 || a->FB <= 0 || a->H2 <= 0) return -1;
   if ((reinterpret_cast<uintptr_t>(a->rec) & 63) != 0) return -2;
   const int rps = a->rows_per_sub;
-  const int W = a->W > 1 ? a->W : 1;
-  if (rps > 0 && rps + W - 1 > a->cap_e) return -3;
+  if (rps > a->cap_e) return -3;
   const int grid = rps > 0 ? a->max_rows : (a->max_rows < a->cap_e ? a->max_rows : a->cap_e);
-  // clear blocks: W - 1 per sub-ring the record may write
-  const int nsub = rps > 0 ? (grid + rps - 1) / rps : 1;
-  const int nclr = W > 1 ? nsub * (W - 1) : 0;
-  hipLaunchKernelGGL(ingest_rows_kernel, dim3(grid + nclr), dim3(256), 0, (hipStream_t)stream, *a, grid);
+  hipLaunchKernelGGL(ingest_rows_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, *a);
   hipLaunchKernelGGL(ingest_tail_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, *a);
   R2_CHECK_LAUNCH();
   return 0;

@@ -45,7 +45,7 @@ class IngestArgs(ctypes.Structure):
         (n, _VP) for n in ("ihead", "rows_total", "err", "frames", "hs_cs", "ths_cs", "action",
                            "reward", "done", "priority", "is_start", "leaves", "n_valid", "dirty",
                            "count")] + [
-        (n, ctypes.c_int) for n in ("max_dirty", "FB", "H2", "cap_e", "rows_per_sub", "W")]
+        (n, ctypes.c_int) for n in ("max_dirty", "FB", "H2", "cap_e", "rows_per_sub")]
 
 
 def ingest_args(replay, rec: int, rec_bytes: int, sub: int, use_dirty: bool,
@@ -65,7 +65,6 @@ def ingest_args(replay, rec: int, rec_bytes: int, sub: int, use_dirty: bool,
     a.dirty = ptr(rp.dirty) if use_dirty else 0
     a.max_dirty, a.FB, a.H2, a.cap_e = rp.max_dirty, rp.frame_bytes, 2 * rp.H, rp.cap_e
     a.rows_per_sub = int(rows_per_sub)
-    a.W = int(replay.cfg.replay.seq_len + replay.cfg.replay.n_step)
     if rows_per_sub > 0:   # env-major windows: every row of the record is kept
         a.max_rows = int(rec_bytes // max(rp.frame_bytes, 1) + 1)
     return a
@@ -169,8 +168,7 @@ class HBMIngestor:
             else:
                 self.pin_event.record(self.copy_stream)
             learner.wait_event(ev)
-            # + the W - 1 start clears in front of the record's range
-            kept = min(n_rows, self.rp.cap_e) + self.rp.cfg.replay.seq_len + self.rp.cfg.replay.n_step
+            kept = min(n_rows, self.rp.cap_e)
             use_dirty = not big and used + kept <= budget
             big |= not use_dirty
             used += kept if use_dirty else 0

@@ -263,8 +263,7 @@ class HBMReplay:
         from ..parallel.trajectory import record_layout
         from .ingest import ingest_args
         n = record_layout(head)[0] if head is not None else 0
-        W = self.cfg.replay.seq_len + self.cfg.replay.n_step
-        use_dirty = head is not None and (min(n, self.cap_e) + W) * 2 <= self.max_dirty
+        use_dirty = head is not None and min(n, self.cap_e) * 2 <= self.max_dirty
         a = ingest_args(self, ptr(rec), rec.numel(), subring, use_dirty)
         import ctypes
         check(kernels().r2_ingest_record(ctypes.byref(a), ctypes.c_void_p(stream_handle())), "ingest")

@@ -118,11 +118,13 @@ def torso_forward_library_sp(frames: torch.Tensor, rows: Optional[torch.Tensor],
                              save_lo: int = 0):
     """fp32 (compute_dtype "fp32") library torso for geometries the split-precision fused kernel
     (torso_sp.hip, Atari 4x84x84 only) does not cover, e.g. DMLab-30 RGB 3x72x96: IEEE fp32 convs
-    (MIOpen, channels-last), the features written as the (hi, lo) bf16 planes every split GEMM of
+    (MIOpen, NCHW), the features written as the (hi, lo) bf16 planes every split GEMM of
     the step reads (out + out_lo == the fp32 value to 2^-16 relative), the conv1 / conv2
     activations of frames [save_lo, ...) saved in fp32 for ``torso_backward_library_sp``."""
     cin = env.channels_per_frame * env.n_stacks
-    x = gather_frames_nhwc(frames, rows, cin, env.frame_h, env.frame_w).float()  # exact 0..255
+    # NCHW-contiguous fp32 throughout: MIOpen's most mature fp32 path (its NHWC fp32 backward
+    # aborted the process on gfx950)
+    x = gather_frames_nhwc(frames, rows, cin, env.frame_h, env.frame_w).float().contiguous()
     n = x.shape[0]
     v = lambda k: layout.view(flat, k)
     y1 = F.conv2d(x, v("vis_layers.0.weight") * (1.0 / 255), v("vis_layers.0.bias"), stride=4).relu_()
@@ -149,17 +151,16 @@ def torso_backward_library_sp(frames: torch.Tensor, rows: torch.Tensor, layout, 
     c1, c2, c3 = model.conv_channels
     (h1, w1), (h2, w2), (h3, w3) = dims
     N = dX.shape[0]
-    cl = torch.channels_last
-    g3 = ((dX.float() + dX_lo.float()) * (X > 0)).view(N, c3, h3, w3).contiguous(memory_format=cl)
-    a2 = act2.view(N, h2, w2, c2).permute(0, 3, 1, 2)
-    a1 = act1.view(N, h1, w1, c1).permute(0, 3, 1, 2)
+    g3 = ((dX.float() + dX_lo.float()) * (X > 0)).view(N, c3, h3, w3)
+    a2 = act2.view(N, h2, w2, c2).permute(0, 3, 1, 2).contiguous()
+    a1 = act1.view(N, h1, w1, c1).permute(0, 3, 1, 2).contiguous()
     v = lambda k: layout.view(flat, k)
     cb = torch.ops.aten.convolution_backward
     d2, dw3, db3 = cb(g3, a2, v("vis_layers.4.weight"), [c3], [1, 1], [0, 0], [1, 1], False,
                       [0, 0], 1, [True, True, True])
     d1, dw2, db2 = cb(d2 * (a2 > 0), a1, v("vis_layers.2.weight"), [c2], [2, 2], [0, 0], [1, 1],
                       False, [0, 0], 1, [True, True, True])
-    x = gather_frames_nhwc(frames, rows, cin, env.frame_h, env.frame_w).float()
+    x = gather_frames_nhwc(frames, rows, cin, env.frame_h, env.frame_w).float().contiguous()
     _, dw1, db1 = cb(d1 * (a1 > 0), x, v("vis_layers.0.weight"), [c1], [4, 4], [0, 0], [1, 1],
                      False, [0, 0], 1, [False, True, True])
     for k, t in (("vis_layers.4.weight", dw3), ("vis_layers.4.bias", db3),

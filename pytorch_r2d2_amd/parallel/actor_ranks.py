@@ -14,7 +14,7 @@ process per GPU, torchrun):
   window lies inside the record are kept) with the device pack kernel
   (``csrc/kernels/ingest.hip`` pack_rows_kernel) and sends the fixed-size record with one RCCL
   send; the learner receives it into device memory and scatters it into that actor's E sub-rings
-  (env-major ingest; the W - 1 positions in front of each written range lose their starts);
+  (env-major ingest);
 * weights: every ``publish_rounds`` rounds learner rank 0 broadcasts master + target over the
   {learner 0} + actor-ranks group (``WeightPublisher``: one 2 x 8 MB RCCL broadcast); the actors
   re-pack them between env steps.
@@ -139,7 +139,7 @@ class TrajectoryReceiver:
         from ..engine.ingest import ingest_args
         rp = self.rp
         rows_rec = self.E * self.R
-        # the dirty list takes every record's rows + start clears; past half of it, rebuild
+        # the dirty list takes every record's rows; past half of it, rebuild
         budget, used, big = rp.max_dirty // 2, 0, False
         for i, src in enumerate(self.srcs):
             if self.host is not None:
@@ -147,7 +147,7 @@ class TrajectoryReceiver:
                 self.recs[i].copy_(self.host[i], non_blocking=True)
             else:
                 dist.recv(self.recs[i], src, group=self.group)
-            need = rows_rec + self.E * self.W
+            need = rows_rec
             use_dirty = not big and used + need <= budget
             big |= not use_dirty
             used += need if use_dirty else 0

@@ -42,15 +42,8 @@ def _record(n, seed, T=10, H=256):
     return m
 
 
-def _check_replay_rows(rp, m, sub, head, cleared_tail=0):
-    """``cleared_tail``: the last rows of a record followed by another record in the same sub-ring
-    lost their starts (ingest.hip: a window running into the next record's rows is invalid)."""
+def _check_replay_rows(rp, m, sub, head):
     n = m["state"].shape[0]
-    if cleared_tail:
-        m = dict(m)
-        st = m["is_seq_start"].copy()
-        st[n - cleared_tail:] = 0
-        m["is_seq_start"] = st
     rows = sub * rp.cap_e + (head + np.arange(n)) % rp.cap_e
     r = torch.as_tensor(rows, device=DEV)
     np.testing.assert_array_equal(rp.frames[r].cpu().numpy(), m["state"].reshape(n, -1))
@@ -125,11 +118,10 @@ def test_shm_ring_ingestor_dma_into_hbm():
             ing._release_done(wait=True)
         torch.cuda.synchronize()
         assert total == sum(m["state"].shape[0] for ms in recs.values() for m in ms)
-        W = cfg.replay.seq_len + cfg.replay.n_step
         for i in range(3):
             head = 0
-            for j, m in enumerate(recs[i]):
-                _check_replay_rows(rp, m, i, head, cleared_tail=(W - 1) if j + 1 < len(recs[i]) else 0)
+            for m in recs[i]:
+                _check_replay_rows(rp, m, i, head)
                 head += m["state"].shape[0]
         _tree_consistent(rp)
         assert all(ws.ring.used() >= 0 for ws in writers)
