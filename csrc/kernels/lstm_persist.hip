@@ -503,8 +503,38 @@ __global__ __launch_bounds__(256) void lstm_bwd_persist_kernel(const PBwdArgs a)
 // CUs of the device (set by the engine from hipDeviceProp_t::multiProcessorCount): every
 // persistent grid must be co-resident at one workgroup per CU
 static int g_num_cus = 256;
-extern "C" int r2_set_num_cus(int n) { if (n > 0) g_num_cus = n; return 0; }
+// CUs of each XCD the engine's stream may use (a CU-masked learner stream beside an actor group,
+// parallel/placement.py): the XCD-placed grids below (block b -> XCD b % 8) need their groups'
+// blocks co-resident on their own XCD
+static int g_xcd_cus[8] = {32, 32, 32, 32, 32, 32, 32, 32};
+extern "C" int r2_set_num_cus(int n) {
+  if (n > 0) {
+    g_num_cus = n;
+    for (int x = 0; x < 8; ++x) g_xcd_cus[x] = n / 8;     // an even split unless told otherwise
+  }
+  return 0;
+}
+extern "C" int r2_set_xcd_cus(const int* c) {
+  int n = 0;
+  for (int x = 0; x < 8; ++x) n += c[x];
+  if (n <= 0) return -1;
+  for (int x = 0; x < 8; ++x) g_xcd_cus[x] = c[x];
+  g_num_cus = n;
+  return 0;
+}
 extern "C" int r2_get_num_cus() { return g_num_cus; }
+
+// do the recurrence groups of an XCD-mapped grid fit their XCDs?  map 1: group x on XCD x;
+// map 2: groups x and x + 8 on XCD x; ``full``: the whole XCD must be free (a group's XCD also
+// hosts helper workgroups that take part in the launch)
+static bool pl_xcd_fit(int xcd_map, int groups, int nwg, bool full = false) {
+  for (int x = 0; x < 8; ++x) {
+    const int n = (x < groups ? 1 : 0) + (xcd_map == 2 && x + 8 < groups ? 1 : 0);
+    if (n == 0) continue;
+    if (n * nwg > g_xcd_cus[x] || (full && g_xcd_cus[x] < 32)) return false;
+  }
+  return true;
+}
 
 static long long* g_pl_dbg = nullptr;
 static int g_pl_slow = 0;
@@ -537,7 +567,8 @@ extern "C" int r2_lstm_fwd_persist(const int64_t* chain_ptrs, int n_chains, int 
   }
   const int groups = n_chains * MB, nwg = H / PL_UNITS;
   args.B = B; args.T = T; args.ctr = ctr; args.err = err; args.dbg = g_pl_dbg;
-  args.MB = MB; args.groups = groups; args.xcd_map = groups <= 8 && nwg <= 32; args.force_slow = g_pl_slow;
+  args.MB = MB; args.groups = groups; args.xcd_map = groups <= 8 && nwg <= 32 && pl_xcd_fit(1, groups, nwg);
+  args.force_slow = g_pl_slow;
   hipStream_t s = (hipStream_t)stream;
   hipMemsetAsync(ctr, 0, PL_CTR_WORDS * sizeof(unsigned), s);
   dim3 grid(args.xcd_map ? 8 * nwg : groups * nwg), block(256);
@@ -567,7 +598,7 @@ extern "C" int r2_lstm_bwd_persist(const float* dh_ext, const float* gates, cons
   if ((H / PL_UNITS) * MB > g_num_cus || MB > 8) return -3;
   if ((size_t)2 * (H / PL_UNITS) * B * H * 4 >= (1ull << 32)) return -4;
   const int nwg = H / PL_UNITS;
-  const int xmap = MB <= 8 && nwg <= 32;
+  const int xmap = MB <= 8 && nwg <= 32 && pl_xcd_fit(1, MB, nwg);
   PBwdArgs a{dh_ext, gates, c_seq, c0, whhT, slab, dgates, B, T, t0, ctr, err, MB, xmap, g_pl_slow};
   hipStream_t s = (hipStream_t)stream;
   hipMemsetAsync(ctr, 0, PL_CTR_WORDS * sizeof(unsigned), s);
@@ -1045,6 +1076,7 @@ static int lstm_fwd_tag_launch(const int64_t* chain_ptrs, int words, int n_chain
   // of crossing the fabric with write-through stores
   args.MB = MB; args.groups = groups;
   args.xcd_map = groups <= 8 && nwg <= 32 ? 1 : (groups <= 16 && nwg <= 16 && !g_pl_nomap2 ? 2 : 0);
+  if (args.xcd_map && !pl_xcd_fit(args.xcd_map, groups, nwg)) args.xcd_map = 0;
   args.force_slow = g_pl_slow;
   hipStream_t s = (hipStream_t)stream;   // counters are left zeroed by the previous launch
   const int nblk = args.xcd_map == 1 ? 8 * nwg : args.xcd_map == 2 ? 16 * nwg : groups * nwg;
@@ -1553,7 +1585,7 @@ extern "C" int r2_lstm_bwd_tag_ring_bytes(int B, int H) {
 // width HD): the XCD map leaves (8 - MB) * H/16 workgroups free and the job needs (2HD/64) x 8.
 extern "C" int r2_lstm_bwd_tag_hg_ok(int B, int H, int HD) {
   const int MB = (B + PT_ROWS - 1) / PT_ROWS, nwg = H / PL_UNITS;
-  const bool xmap = MB <= 8 && nwg <= 32;
+  const bool xmap = MB <= 8 && nwg <= 32 && pl_xcd_fit(1, MB, nwg, true);
   return (xmap && HD % 64 == 0 && (8 - MB) * nwg >= ((2 * HD + 63) / 64) * 8) ? 1 : 0;
 }
 
@@ -1574,7 +1606,7 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
   if (MB * nwg > g_num_cus || MB > PL_MAX_GROUPS) return -3;
   if ((size_t)T * B * (size_t)(4 * H) * 4 >= (1ull << 32) || r2_lstm_bwd_tag_ring_bytes(B, H) < 0 ||
       T - t0 >= 65535) return -4;
-  const int xmap = MB <= 8 && nwg <= 32;
+  const int xmap = MB <= 8 && nwg <= 32 && pl_xcd_fit(1, MB, nwg);
   if (bias_ws && (!perm || !db1)) return -1;
   PTBArgs args{dh_ext, gates, c_seq, c0, whhT, dgates, ring, B, T, t0, ctr, err, MB, xmap, g_pl_slow, 0,
                bias_ws, perm, db1, db2,
@@ -1585,7 +1617,7 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
   int taken = 0, nh = 0;
   if (hg_dva || n_gw > 0 || gx_on) {
     // helpers: every block of the 8 x 32 grid outside the recurrence's groups
-    if (!xmap || nwg > 32 || T - t0 > PT_ITER_MAX || g_num_cus < 256) return -6;
+    if (!xmap || nwg > 32 || T - t0 > PT_ITER_MAX || !pl_xcd_fit(1, MB, nwg, true)) return -6;
     nh = 8 * 32 - MB * nwg;
     int nw = 0, nx = 0;
     if (n_gw < 0 || n_gw > 3) return -7;

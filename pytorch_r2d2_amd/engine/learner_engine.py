@@ -40,7 +40,8 @@ target_mode (config.learner.target_mode):
 """
 from __future__ import annotations
 
-from typing import Dict, Optional
+import ctypes
+from typing import Dict, List, Optional
 
 import numpy as np
 import torch
@@ -89,7 +90,7 @@ class LearnerEngine:
 
     def __init__(self, cfg: R2D2Config, replay: HBMReplay, device="cuda", rank: int = 0,
                  world: int = 1, process_group=None, init_module: Optional[QNet] = None,
-                 n_cus: Optional[int] = None):
+                 n_cus: Optional[int] = None, xcd_cus: Optional[List[int]] = None):
         self.cfg = cfg
         self.device = torch.device(device)
         self.replay = replay
@@ -108,6 +109,9 @@ class LearnerEngine:
         self.n_cus = int(n_cus) if n_cus else device_cus(d)
         if d.type == "cuda":
             kernels().r2_set_num_cus(self.n_cus)
+            if xcd_cus is not None:     # a CU mask that is not an even split over the XCDs
+                arr = (ctypes.c_int * 8)(*xcd_cus)
+                kernels().r2_set_xcd_cus(arr)
             kernels().r2_lstm_persist_force_slow(0 if cfg.learner.lstm_xcd_pairs else 2)
         if init_module is None:
             torch.manual_seed(cfg.seed)
@@ -690,7 +694,7 @@ class LearnerEngine:
               ptr(gb1), N, A, HD, ptr(self.gs_ws), ptr(self.gs_ticket)]
         # the head-gradient reduction rides on the BPTT launch's idle workgroups when they suffice
         # (as in the bf16 engine); otherwise it is its own launch
-        side_hg = (self.cfg.learner.sp_head_grads_in_bptt and self.n_cus >= 256 and A <= 63
+        side_hg = (self.cfg.learner.sp_head_grads_in_bptt and A <= 63
                    and bool(k.r2_lstm_bwd_tag_hg_ok(B, H, HD)))
         if not side_hg:
             check(k.r2_head_grads_sp(*hg, s), "head_grads_sp")

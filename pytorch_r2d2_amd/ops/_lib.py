@@ -28,6 +28,7 @@ F = ctypes.c_float
 _SIGS = {
     "r2_abi_version": [],
     "r2_set_num_cus": [I],
+    "r2_set_xcd_cus": [P],
     "r2_get_num_cus": [],
     "r2_lstm_fwd": [P, I, I, I, I, I, P],
     "r2_lstm_bwd": [P, P, P, P, P, P, P, P, P, I, I, I, I, P],

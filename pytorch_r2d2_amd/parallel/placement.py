@@ -25,7 +25,9 @@ N_XCD = 8
 
 def cu_mask_words(n_cus: int, per_xcd: int, first: bool, n_xcd: int = N_XCD) -> List[int]:
     """32-bit mask words: ``first`` -> the ``per_xcd * n_xcd`` CUs of bits [0, per_xcd*n_xcd),
-    else the complement (every remaining CU)."""
+    else the complement (every remaining CU).  Every XCD must keep at least one CU in a mask: an
+    XCD with none set runs the stream on ALL of its CUs (measured, tests/test_native_gpu.py
+    partition test history: a mask of 8 CUs on XCDs 4-7 only ran on 32 CUs of XCDs 0-3 too)."""
     if n_cus % n_xcd or not 0 < per_xcd < n_cus // n_xcd:
         raise ValueError(f"cannot give {per_xcd} CUs per XCD out of {n_cus} CUs / {n_xcd} XCDs")
     cut = per_xcd * n_xcd
@@ -34,6 +36,15 @@ def cu_mask_words(n_cus: int, per_xcd: int, first: bool, n_xcd: int = N_XCD) -> 
     for b in bits:
         words[b // 32] |= 1 << (b % 32)
     return words
+
+
+def xcd_counts(words: List[int], n_cus: int, n_xcd: int = N_XCD) -> List[int]:
+    """CUs per XCD selected by a mask."""
+    c = [0] * n_xcd
+    for b in range(n_cus):
+        if words[b // 32] >> (b % 32) & 1:
+            c[b % n_xcd] += 1
+    return c
 
 
 class MaskedStream:
@@ -64,13 +75,16 @@ class MaskedStream:
 
 
 def split_chip(device, actor_cus_per_xcd: int = 4
-               ) -> Tuple[Optional[MaskedStream], Optional[MaskedStream], int, int]:
-    """(actor stream, learner stream, actor CUs, learner CUs).  ``actor_cus_per_xcd`` <= 0: no
-    partition (two ordinary streams sharing the chip; returns None streams)."""
+               ) -> Tuple[Optional[MaskedStream], Optional[MaskedStream], int, int, Optional[List[int]]]:
+    """(actor stream, learner stream, actor CUs, learner CUs, learner CUs per XCD).
+    ``actor_cus_per_xcd`` <= 0: no partition (two ordinary streams sharing the chip; returns None
+    streams): the learner keeps all 256 CUs for its placement and the actor's short kernels fill
+    whatever CUs are idle at the moment -- safe because they never wait on the learner, so a
+    persistent learner block that finds its CU taken only waits for an actor workgroup to end."""
     d = torch.device(device)
     n = int(torch.cuda.get_device_properties(d).multi_processor_count)
     if actor_cus_per_xcd <= 0:
-        return None, None, n, n
+        return None, None, n, n, None
     a = MaskedStream(cu_mask_words(n, actor_cus_per_xcd, True), d)
     lr = MaskedStream(cu_mask_words(n, actor_cus_per_xcd, False), d)
-    return a, lr, a.n_cus, lr.n_cus
+    return a, lr, a.n_cus, lr.n_cus, xcd_counts(lr.words, n)

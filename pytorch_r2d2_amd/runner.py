@@ -49,16 +49,16 @@ def run_native(cfg: R2D2Config, steps: int = 1000, actor_steps_per_update: int =
     E = cfg.actor.envs_per_actor
     torch.manual_seed(cfg.seed)
     s_act = s_learn = None
-    n_cus_learner = None
+    n_cus_learner = xcd_cus = None
     n_cus_actor = 256
     if concurrent and dev.type == "cuda" and actor_cus_per_xcd > 0:
         from .parallel.placement import split_chip
-        s_act, s_learn, n_cus_actor, n_cus_learner = split_chip(dev, actor_cus_per_xcd)
+        s_act, s_learn, n_cus_actor, n_cus_learner, xcd_cus = split_chip(dev, actor_cus_per_xcd)
     replay = HBMReplay(cfg, dev, capacity=capacity or cfg.replay.capacity, n_subrings=E)
     import torch.distributed as dist
     eng = LearnerEngine(cfg, replay, dev, rank=info.rank, world=info.world,
                         process_group=dist.group.WORLD if info.world > 1 else None,
-                        n_cus=n_cus_learner)
+                        n_cus=n_cus_learner, xcd_cus=xcd_cus)
     env = VecSyntheticAtari(E, dev, seed=cfg.seed + 101 * info.rank, episode_len=cfg.env.episode_len,
                             n_actions=cfg.model.n_actions,
                             n_stacks=cfg.env.channels_per_frame * cfg.env.n_stacks,

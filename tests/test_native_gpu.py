@@ -200,9 +200,11 @@ def test_ingestor_drops_malformed_records_uncounted():
 
 def test_cu_masked_streams_partition_the_chip():
     from pytorch_r2d2_amd.parallel.placement import split_chip
-    sa, sl, na, nl = split_chip(DEV, 4)
+    sa, sl, na, nl, per_l = split_chip(DEV, 4)
+    want = {"actor": [4] * 8, "learner": [28] * 8}
     try:
         assert na == 32 and nl == torch.cuda.get_device_properties(0).multi_processor_count - 32
+        assert per_l == want["learner"]
         k = kernels()
         seen = {}
         for name, s in (("actor", sa), ("learner", sl)):
@@ -220,7 +222,7 @@ def test_cu_masked_streams_partition_the_chip():
             cus = {(int(x), (int(h) >> 8) & 15, (int(h) >> 13) & 7) for x, h in v}
             seen[name] = cus
             per = np.bincount([c[0] for c in cus], minlength=8)
-            assert len(per) == 8 and (per == (4 if name == "actor" else 28)).all(), (name, per)
+            assert list(per) == want[name], (name, per)
         assert not (seen["actor"] & seen["learner"])
     finally:
         sa.close()
@@ -238,7 +240,7 @@ def _concurrent_setup(E=16, cap_e=512, M=2, masked=True, **over):
     sa = sl = None
     na, nl = 256, None
     if masked:
-        sa, sl, na, nl = split_chip(DEV, 4)
+        sa, sl, na, nl, _ = split_chip(DEV, 4)
     rp = HBMReplay(cfg, DEV, capacity=E * cap_e, n_subrings=E)
     eng = LearnerEngine(cfg, rp, DEV, n_cus=nl)
     env = VecSyntheticAtari(E, DEV, seed=3, episode_len=37, n_actions=cfg.model.n_actions)
@@ -254,8 +256,9 @@ def _concurrent_setup(E=16, cap_e=512, M=2, masked=True, **over):
     return cfg, rp, eng, actor, drv, (sa, sl)
 
 
-def test_concurrent_driver_never_samples_rows_being_written():
-    cfg, rp, eng, actor, drv, streams = _concurrent_setup()
+@pytest.mark.parametrize("masked", [True, False], ids=["cu_masked", "shared_chip"])
+def test_concurrent_driver_never_samples_rows_being_written(masked):
+    cfg, rp, eng, actor, drv, streams = _concurrent_setup(masked=masked)
     B, Tn = cfg.learner.batch_size, cfg.replay.seq_len + cfg.replay.n_step
     R = 120
     hist = torch.zeros(R, B, dtype=torch.int32, device=DEV)
@@ -300,15 +303,15 @@ def test_run_native_concurrent_and_serial_train():
     from pytorch_r2d2_amd.runner import run_native
     cfg = _small_cfg(**{"actor.envs_per_actor": 32, "learner.publish_interval": 10})
     outs = {}
-    for conc in (False, True):
+    for mode, conc, k in (("serial", False, 0), ("masked", True, 4), ("shared", True, 0)):
         out = run_native(cfg, steps=60, actor_steps_per_update=2, warmup_rows=32 * 120,
-                         capacity=32 * 600, log_every=30, concurrent=conc, check_every=20)
+                         capacity=32 * 600, log_every=30, concurrent=conc, actor_cus_per_xcd=k,
+                         check_every=20)
         assert all(np.isfinite(out["losses"]))
-        outs[conc] = out
-        print("concurrent" if conc else "serial", {k: out[k] for k in
-              ("learner_steps_per_s", "env_steps_per_s", "learner_cus")})
-    assert outs[True]["learner_cus"] < outs[False]["learner_cus"]
-    assert outs[True]["weights_version"] == 6
+        outs[mode] = out
+        print(mode, {k: out[k] for k in ("learner_steps_per_s", "env_steps_per_s", "learner_cus")})
+    assert outs["masked"]["learner_cus"] < outs["serial"]["learner_cus"] == outs["shared"]["learner_cus"]
+    assert outs["masked"]["weights_version"] == outs["shared"]["weights_version"] == 6
 
 
 @pytest.mark.slow

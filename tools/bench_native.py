@@ -40,6 +40,7 @@ def main():
                          capacity=cap, log_every=10 ** 9, concurrent=(mode == "concurrent"),
                          actor_cus_per_xcd=a.actor_cus_per_xcd, check_every=100)
         rec = {"mode": mode, "preset": a.preset, "envs": E, "actor_steps_per_learner_step": a.actor_steps,
+               "actor_cus_per_xcd": a.actor_cus_per_xcd,
                "learner_steps_per_s": round(out["learner_steps_per_s"], 1),
                "env_steps_per_s": round(out["env_steps_per_s"], 1),
                "learner_cus": out["learner_cus"], "dtype": cfg.learner.compute_dtype,

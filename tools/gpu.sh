@@ -9,6 +9,7 @@
 #   tools/gpu.sh prof TAG [bench args...]       rocprofv3 kernel trace + step breakdown
 #   tools/gpu.sh pmc TAG [filters...]           PMC passes over the bench step (kernel trace only)
 #   tools/gpu.sh learn [learn_check args...]    tools/learn_check.py
+#   tools/gpu.sh native [bench_native args...]  actor + learner loop (serial / concurrent)
 #
 # Output goes under gpurun_out/ (merged back by gpurun); summaries worth keeping are copied into
 # profiles/ by hand.
@@ -72,6 +73,10 @@ case "$cmd" in
   learn)
     timeout -k 10 300 python -u tools/learn_check.py "$@" > gpurun_out/learn.log 2>&1 || fail learn gpurun_out/learn.log
     grep -h '^{' gpurun_out/learn.log ;;
+  native)
+    timeout -k 10 240 python -u tools/bench_native.py "$@" >> gpurun_out/native.log 2>&1 \
+      || fail native gpurun_out/native.log
+    grep -h '^{' gpurun_out/native.log | tail -n 2 ;;
   *)
     echo "unknown command $cmd"; exit 2 ;;
 esac
