@@ -47,7 +47,8 @@ def build_parser():
                    help="native: N CPU actor processes feeding the GPU learner (instead of GPU actors)")
     p.add_argument("--concurrent", action="store_true",
                    help="native: GPU actor group and learner run simultaneously on disjoint CUs")
-    p.add_argument("--actor-cus-per-xcd", type=int, default=4)
+    p.add_argument("--actor-cus-per-xcd", type=int, default=0,
+                   help="concurrent: CUs per XCD reserved for the actor group (0: share the chip)")
     p.add_argument("--actor-steps", type=int, default=1, help="native: env steps per learner step")
     p.add_argument("--actor-ranks", type=int, default=0,
                    help="native under torchrun: the last N ranks run GPU actor groups only and feed "
@@ -72,7 +73,9 @@ def run(argv=None):
         from pytorch_r2d2_amd.runner import run_native_cpu_actors
         out = run_native_cpu_actors(cfg, args.cpu_actors, steps=args.steps or 1000,
                                     capacity=args.capacity, metrics_path=args.metrics)
-        out.pop("supervisor", None)
+        sup = out.pop("supervisor", None) or {}
+        out["restarts"] = {k: v["restarts"] for k, v in sup.items() if v["restarts"]}
+        out["exitcodes"] = {k: v["exitcodes"] for k, v in sup.items() if v["exitcodes"]}
     elif args.mode == "native":
         from pytorch_r2d2_amd.runner import run_native
         out = run_native(cfg, steps=args.steps or 1000, metrics_path=args.metrics,

@@ -5,9 +5,12 @@ Reference: actors and the learner are separate processes running at the same tim
 (``learner.py:109-110``) and actors pull them every 5 episodes (``actor.py:134-135``).  On the
 native path both roles live in one process per GPU and run SIMULTANEOUSLY on disjoint CU sets:
 
-* the actor group's stream and the learner's stream are CU-masked (``parallel/placement.py``:
-  ``k`` CUs of every XCD for the actor, the other ``32 - k`` for the learner, whose persistent
-  kernels are sized to its own CU count);
+* the two roles get their own streams, either sharing the whole chip (the default: the actor's
+  short kernels fill CUs the learner leaves idle, e.g. the 64 outside the persistent LSTM
+  forward's 192, and never wait on the learner, so a learner workgroup that finds its CU taken
+  waits at most for one actor workgroup) or CU-masked (``parallel/placement.py``: ``k`` CUs of
+  every XCD for the actor, the other ``32 - k`` for the learner, whose persistent kernels are
+  placed for its own per-XCD CU counts);
 * the host issues *rounds*: ``M`` actor env steps (graph replays) on the actor stream and one
   learner step on the learner stream.  Actor round ``r`` waits for learner step ``r - 1``; learner
   step ``r`` waits for actor round ``r - 1``.  Each role therefore overlaps the other's next
@@ -37,7 +40,7 @@ from ..ops._lib import check, kernels, ptr, stream_handle
 class ConcurrentDriver:
     def __init__(self, engine, actor, steps_per_round: int = 2, publish_interval: Optional[int] = None,
                  lookahead: Optional[int] = None, actor_stream=None, learner_stream=None,
-                 capture: bool = True):
+                 capture: bool = True, learner_priority: int = 0):
         from ..actor_batched import PackedWeights
         self.eng, self.actor = engine, actor
         self.rp = rp = actor.replay
@@ -66,7 +69,10 @@ class ConcurrentDriver:
         self.version = 0
         self._repack = False
         self.s_act = actor_stream if actor_stream is not None else torch.cuda.Stream(device=dev)
-        self.s_learn = learner_stream if learner_stream is not None else torch.cuda.Stream(device=dev)
+        # shared chip (no CU masks): ``learner_priority`` -1 puts the learner's stream on a
+        # high-priority queue, so its workgroups win free CUs over the actor's
+        self.s_learn = learner_stream if learner_stream is not None else \
+            torch.cuda.Stream(device=dev, priority=int(learner_priority))
         self.ev_act = [torch.cuda.Event(), torch.cuda.Event()]
         self.ev_learn = torch.cuda.Event()
         self.rounds = 0

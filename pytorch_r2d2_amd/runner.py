@@ -29,7 +29,8 @@ def run_native(cfg: R2D2Config, steps: int = 1000, actor_steps_per_update: int =
                warmup_rows: Optional[int] = None, metrics_path: Optional[str] = None,
                checkpoint_dir: Optional[str] = None, log_every: int = 100, use_graph: bool = True,
                capacity: Optional[int] = None, resume: Optional[str] = None,
-               concurrent: bool = False, actor_cus_per_xcd: int = 4, beat=None,
+               concurrent: bool = False, actor_cus_per_xcd: int = 0, learner_priority: int = 0,
+               beat=None,
                check_every: int = 200, on_step=None) -> Dict:
     """``concurrent``: actor group and learner run simultaneously on disjoint CU sets
     (engine/concurrent.py; ``actor_steps_per_update`` env steps per learner step), else they
@@ -97,7 +98,8 @@ def run_native(cfg: R2D2Config, steps: int = 1000, actor_steps_per_update: int =
         drv = ConcurrentDriver(eng, actor, steps_per_round=actor_steps_per_update,
                                actor_stream=s_act.stream if s_act else None,
                                learner_stream=s_learn.stream if s_learn else None,
-                               capture=use_graph and cfg.actor.use_graph and actor.can_capture)
+                               capture=use_graph and cfg.actor.use_graph and actor.can_capture,
+                               learner_priority=learner_priority)
         if on_step is not None:
             drv.on_learner_step = on_step
     elif use_graph and cfg.actor.use_graph and actor.can_capture:
@@ -387,7 +389,7 @@ def run_native_cpu_actors(cfg: R2D2Config, n_actors: int, steps: int = 1000,
                ingest_rows_per_s=ingest.rows / (t_end - t0), weights_version=version,
                # every ingested row is one CPU env step (the actors' aggregate env throughput)
                cpu_env_steps_per_s=ingest.rows / (t_end - t0),
-               rejected_records=ingest.rejected,
+               rejected_records=ingest.rejected, kernel_error_word=eng.error_word(),
                supervisor=sup.report, zero_copy=[b is not None for b in ingest.registered])
     return out
 

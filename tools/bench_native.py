@@ -24,7 +24,8 @@ def main():
     ap.add_argument("--actor-steps", type=int, default=1)
     ap.add_argument("--envs", type=int, default=None)
     ap.add_argument("--capacity", type=int, default=None)
-    ap.add_argument("--actor-cus-per-xcd", type=int, default=4)
+    ap.add_argument("--actor-cus-per-xcd", type=int, default=0)
+    ap.add_argument("--learner-priority", type=int, default=0)
     ap.add_argument("--modes", default="serial,concurrent")
     ap.add_argument("--set", nargs="*", default=[])
     a = ap.parse_args()
@@ -38,9 +39,10 @@ def main():
     for mode in a.modes.split(","):
         out = run_native(cfg, steps=a.steps, actor_steps_per_update=a.actor_steps, warmup_rows=warm,
                          capacity=cap, log_every=10 ** 9, concurrent=(mode == "concurrent"),
-                         actor_cus_per_xcd=a.actor_cus_per_xcd, check_every=100)
+                         actor_cus_per_xcd=a.actor_cus_per_xcd, learner_priority=a.learner_priority,
+                         check_every=100)
         rec = {"mode": mode, "preset": a.preset, "envs": E, "actor_steps_per_learner_step": a.actor_steps,
-               "actor_cus_per_xcd": a.actor_cus_per_xcd,
+               "actor_cus_per_xcd": a.actor_cus_per_xcd, "learner_priority": a.learner_priority,
                "learner_steps_per_s": round(out["learner_steps_per_s"], 1),
                "env_steps_per_s": round(out["env_steps_per_s"], 1),
                "learner_cus": out["learner_cus"], "dtype": cfg.learner.compute_dtype,

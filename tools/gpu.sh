@@ -10,6 +10,8 @@
 #   tools/gpu.sh pmc TAG [filters...]           PMC passes over the bench step (kernel trace only)
 #   tools/gpu.sh learn [learn_check args...]    tools/learn_check.py
 #   tools/gpu.sh native [bench_native args...]  actor + learner loop (serial / concurrent)
+#   tools/gpu.sh cfg2 [N] [steps]               main.py --cpu-actors N with an injected actor crash
+#   tools/gpu.sh dp [N] [bench args...]         N-rank DP bench rehearsal sharing the one GPU
 #
 # Output goes under gpurun_out/ (merged back by gpurun); summaries worth keeping are copied into
 # profiles/ by hand.
@@ -73,6 +75,21 @@ case "$cmd" in
   learn)
     timeout -k 10 300 python -u tools/learn_check.py "$@" > gpurun_out/learn.log 2>&1 || fail learn gpurun_out/learn.log
     grep -h '^{' gpurun_out/learn.log ;;
+  cfg2)
+    # BASELINE config 2: one GPU learner fed by N CPU actor processes (default 16), one injected
+    # actor crash (restarted by the supervisor), metrics JSONL
+    n=${1:-16}; steps=${2:-3000}
+    R2D2_FAULTS="actor:3:crash_at=300,once=1" timeout -k 10 900 python -u main.py --mode native \
+      --config pong --cpu-actors "$n" --steps "$steps" --metrics gpurun_out/cfg2_metrics.jsonl \
+      > gpurun_out/cfg2.log 2>&1 || fail cfg2 gpurun_out/cfg2.log
+    tail -n 3 gpurun_out/cfg2.log ;;
+  dp)
+    # multi-rank rehearsal on one GPU (gloo, ranks share the card): N ranks (default 4)
+    n=${1:-4}; shift || true
+    R2D2_BENCH_SHARED=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 \
+      --nproc-per-node "$n" --master-addr 127.0.0.1 --master-port 29531 bench.py --steps 20 \
+      --warmup 5 --capacity 200000 "$@" > gpurun_out/dp.log 2>&1 || fail dp gpurun_out/dp.log
+    grep -h '^{' gpurun_out/dp.log ;;
   native)
     timeout -k 10 240 python -u tools/bench_native.py "$@" >> gpurun_out/native.log 2>&1 \
       || fail native gpurun_out/native.log
