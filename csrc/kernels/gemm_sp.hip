@@ -34,15 +34,15 @@ __device__ __forceinline__ int g5_kswz(int r) { return BK == 64 ? ((r >> 1) & 7)
 // Stage one R x BK operand plane: R*BK*2/1024 1-KB blocks dealt over the 8 waves (evenly when
 // 8 divides the count; else wave w takes blocks w, w+8, .. -- only legal with 2 stages, whose
 // wait is vmcnt(0): the deeper rings count DMAs per thread).
-template <bool KMAJ, int R, int BK>
+template <bool KMAJ, int R, int BK, int NW = 8>
 __device__ __forceinline__ void g5_stage(const bf16* X, int ld, int i0, int imax, int k0, int kmax,
                                          uint8_t* tile, int wave, int lane, int oz) {
-  constexpr int NBLK = R * BK * 2 / 1024, PW = (NBLK + 7) / 8;
-  constexpr bool EVEN = NBLK % 8 == 0;
+  constexpr int NBLK = R * BK * 2 / 1024, PW = (NBLK + NW - 1) / NW;
+  constexpr bool EVEN = NBLK % NW == 0;
   static_assert(KMAJ || R % 128 == 0, "mn-major images are 128-column halves");
 #pragma unroll
   for (int j = 0; j < PW; ++j) {
-    const int blk = EVEN ? wave * PW + j : wave + 8 * j;
+    const int blk = EVEN ? wave * PW + j : wave + NW * j;
     if (!EVEN && blk >= NBLK) break;
     int off;
     bool kin;
@@ -373,10 +373,230 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const G5Args a) {
   }
 }
 
+// ============================================================================================
+// gemm6: the split GEMM for k-major A and B without split-K (the x-projection of both nets,
+// 10,560 x 1,024 x 1,568) on ONE wave per SIMD with register double-buffered fragments.
+// gemm5's 8-wave 192 x 256 tile (wave tile 96 x 64: 96 accumulator + 80 fragment registers) has
+// no registers for a second fragment set, so after every K tile's barrier both waves of a SIMD
+// read their fragments from LDS at the same moment and only then issue their MFMAs: the pipe
+// idles through the read burst (PMC: MFMA ~42 % busy, waves waiting 35 % of their cycles).  Here
+// 4 waves of 96 x 128 hold 192 accumulator registers and two 28-fragment sets (224), within the
+// 512 a lone wave on its SIMD may use, and read tile k+1's fragments between tile k's 144 MFMAs
+// (one ds_read_b128 per ~5 MFMAs).  Per K tile of 32: stage ring of 2 x 56 KB (A / B hi and lo
+// by global_load_lds, gemm5's bank swizzles); the DMA of tile k+2 is issued right after the
+// barrier that retires tile k's LDS buffer, so it has one tile of MFMAs to land.
+__device__ __forceinline__ void g6_dma(const bf16* src, uint8_t* dst) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+}
+
+// interleave N fragment reads (issued first in program order) with the pass's M MFMAs
+template <int N, int M>
+__device__ __forceinline__ void g6_mix() {
+  if constexpr (N > 0) {
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, M / N, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, M - N * (M / N), 0);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int BM, int BN, int NW>
+__global__ __launch_bounds__(NW * 64)
+void gemm6_kernel(const G5Args a) {
+  constexpr int BK = 32, WC = NW / 2;                 // waves: 2 rows x WC columns
+  constexpr int FM = BM / 32, FN = BN / (16 * WC);    // 16 x 16 fragments of the (BM/2) x (BN/WC) wave tile
+  constexpr int OPA = BM * BK * 2, OPB = BN * BK * 2, STB = 2 * (OPA + OPB);
+  extern __shared__ __attribute__((aligned(1024))) uint8_t lds6[];
+  int bid;
+  {
+    const int b = blockIdx.x, x = b & 7, qn = a.total >> 3, r = a.total & 7;
+    bid = (x < r ? x * (qn + 1) : r * (qn + 1) + (x - r) * qn) + (b >> 3);
+  }
+  int pi = 0;
+#pragma unroll
+  for (int i = 1; i < gm::MAXP; ++i)
+    if (i < a.np && bid >= a.item_base[i]) pi = i;
+  const GemmProb& P = a.p[pi];
+  const int tile = bid - a.item_base[pi];
+  const int tm = tile / P.tiles_n, tn = tile % P.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = (P.K + BK - 1) / BK;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave / WC, wc = wave % WC;
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // staging: this thread's 1-KB blocks of each plane (gemm5's k-major layout: 16 rows x 4
+  // swizzled 16-B chunks per block) as element offsets fixed for the whole K loop (K % 32 == 0,
+  // checked by the launcher: no K tail); a tile adds k0.  hi and lo planes share the offsets.
+  constexpr int NBA = BM * BK * 2 / 1024, NBB = BN * BK * 2 / 1024;   // 1-KB blocks per plane
+  constexpr int PA = (NBA + NW - 1) / NW, PB = (NBB + NW - 1) / NW;       // block w + NW j
+  uint32_t offa[PA], offb[PB];
+  {
+    const int rr = lane >> 2, cp = lane & 3;
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+      const int row = (wave + NW * j) * 16 + rr;
+      offa[j] = (uint32_t)(min(m0 + row, P.M - 1) * P.lda + (cp ^ g5_kswz<BK>(row)) * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      const int row = (wave + NW * j) * 16 + rr;
+      offb[j] = (uint32_t)(min(n0 + row, P.N - 1) * P.ldb + (cp ^ g5_kswz<BK>(row)) * 8);
+    }
+  }
+  auto stage = [&](int kt) {
+    uint8_t* st = lds6 + (kt & 1) * STB;
+    const uint32_t k0 = (uint32_t)(kt * BK);
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+      if (NBA % NW == 0 || wave + NW * j < NBA) {
+        uint8_t* d = st + (wave + NW * j) * 1024;
+        g6_dma(P.A + (offa[j] + k0), d);
+        g6_dma(P.A_lo + (offa[j] + k0), d + OPA);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      if (NBB % NW == 0 || wave + NW * j < NBB) {
+        uint8_t* d = st + 2 * OPA + (wave + NW * j) * 1024;
+        g6_dma(P.B + (offb[j] + k0), d);
+        g6_dma(P.B_lo + (offb[j] + k0), d + OPB);
+      }
+    }
+  };
+  // fragment (rows i0 .. i0+15, k-major, BK 32) of this lane: row i0 + l16, chunk g ^ swz(row),
+  // and swz depends only on bit 3 of the row, i.e. on l16: one lane offset + a constant per fragment
+  const int l16f = lane & 15, gf = lane >> 4;
+  int foff = l16f * (BK * 2) + ((gf ^ g5_kswz<BK>(l16f)) * 16);
+  asm volatile("" : "+v"(foff));
+  auto frag = [&](const uint8_t* plane, int i0) {
+    return *(const bf16x8*)(plane + foff + i0 * (BK * 2));
+  };
+  auto planes = [&](int buf, const uint8_t*& ah, const uint8_t*& al, const uint8_t*& bh,
+                    const uint8_t*& bl) {
+    ah = lds6 + buf * STB;
+    al = ah + OPA;
+    bh = ah + 2 * OPA;
+    bl = bh + OPB;
+  };
+  // One register set per plane, each refilled with the next K tile's fragments in the pass after
+  // its last use.  Pass order per tile: A hi.B lo, A hi.B hi, A lo.B hi -- the only order whose
+  // last pass frees the operands the next tile's first pass does NOT need: B lo refills during
+  // pass 2, A hi during pass 3, A lo and B hi during the next tile's pass 1.  112 fragment + 192
+  // accumulator registers (an MFMA's A / B operands must sit in the 256 VGPRs).  The single
+  // barrier per tile follows pass 1 (the last reads of this tile's LDS buffer): tile k+1 has
+  // landed, and tile k+2's DMA into this buffer gets three passes to land.
+  bf16x8 ahi[FM], alo[FM], bhi[FN], blo[FN];
+  auto ldA = [&](bf16x8 (&f)[FM], const uint8_t* pl) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i) f[i] = frag(pl, wr * (BM / 2) + 16 * i);
+  };
+  auto ldB = [&](bf16x8 (&f)[FN], const uint8_t* pl) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) f[j] = frag(pl, wc * (BN / WC) + 16 * j);
+  };
+  auto step = [&](int kt, int buf, bool more) {
+    const uint8_t *cah, *cal, *cbh, *cbl, *nah, *nal, *nbh, *nbl;
+    planes(buf, cah, cal, cbh, cbl);
+    planes(buf ^ 1, nah, nal, nbh, nbl);
+    // pass 1: A hi x B lo; this tile's A lo / B hi arrive
+    ldA(alo, cal);
+    ldB(bhi, cbh);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = g5_mfma(ahi[i], blo[j], acc[i][j]);
+    g6_mix<FM + FN, FM * FN>();
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();          // tile kt+1 visible; this tile's buffer read out
+    if (kt + 2 < nk) stage(kt + 2);
+    // pass 2: A hi x B hi; B lo <- tile kt+1
+    if (more) ldB(blo, nbl);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = g5_mfma(ahi[i], bhi[j], acc[i][j]);
+    if (more) g6_mix<FN, FM * FN>(); else g6_mix<0, FM * FN>();
+    // pass 3: A lo x B hi; A hi <- tile kt+1
+    if (more) ldA(ahi, nah);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = g5_mfma(alo[i], bhi[j], acc[i][j]);
+    if (more) g6_mix<FM, FM * FN>(); else g6_mix<0, FM * FN>();
+  };
+  if (nk > 0) {
+    stage(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (nk > 1) stage(1);
+    const uint8_t *pah, *pal, *pbh, *pbl;
+    planes(0, pah, pal, pbh, pbl);
+    ldA(ahi, pah);
+    ldB(blo, pbl);
+  }
+  for (int kt = 0; kt + 1 < nk; ++kt) step(kt, kt & 1, true);
+  if (nk > 0) step(nk - 1, (nk - 1) & 1, false);
+
+  // ---- epilogue: 64 rows at a time through LDS (row-contiguous, 4 columns per thread)
+  // acc[i][j][e] = tile[wr*(BM/2) + 16i + 4(l>>4) + e][wc*(BN/2) + 16j + (l&15)]
+  constexpr int LS = BN + 16;
+  float* L = (float*)lds6;
+  const int l16 = lane & 15, g = lane >> 4;
+  const bool vec = ((uintptr_t)P.C % 16 == 0) && (P.ldc % 4 == 0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int p = 0; p < FM / 2; ++p) {
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          L[(wr * 32 + ii * 16 + 4 * g + e) * LS + wc * (BN / WC) + 16 * j + l16] = acc[2 * p + ii][j][e];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#pragma unroll 2
+    for (int q = tid; q < 64 * (BN / 4); q += NW * 64) {
+      const int lr = q / (BN / 4), cc = (q % (BN / 4)) * 4;
+      const int row = m0 + (lr >> 5) * (BM / 2) + 32 * p + (lr & 31);
+      const int col = n0 + cc;
+      if (row >= P.M || col >= P.N) continue;
+      g5_emit(P, row, col, *(const f32x4*)(L + lr * LS + cc), vec);
+    }
+  }
+}
+
+static int g6_off = 0;   // r2_gemm5_set_mode bit 2: keep the x-projection on gemm5
+
+static int g6_nw4 = 0;  // r2_gemm5_set_mode bit 3: the 4-wave (one per SIMD) variant
+
+template <int BM, int BN, int NW>
+static void g6_kernel_launch(const G5Args& a, hipStream_t s) {
+  constexpr int LDS = 2 * 2 * (BM + BN) * 32 * 2;
+  static_assert(LDS <= 160 * 1024 && 64 * (BN + 16) * 4 <= LDS, "LDS");
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)gemm6_kernel<BM, BN, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL((gemm6_kernel<BM, BN, NW>), dim3(a.total), dim3(NW * 64), LDS, s, a);
+}
+
 static int g5_il = 1;   // interleaved fragment loads (r2_gemm5_set_mode)
 static int g5_dbg = 0;  // probe bits (G5Args::dbg)
 extern "C" int r2_gemm5_set_mode(int m) {
   g5_il = m & 1;
+  g6_off = (m >> 2) & 1;
+  g6_nw4 = (m >> 3) & 1;
   g5_dbg = (m >> 4) & 3;
   return 0;
 }
@@ -472,6 +692,16 @@ extern "C" int r2_gemm5(const int64_t* descs, const int* split, int np, int cfg,
   a.total = items;
   if (slabs * bm * bn * 4 > ws_bytes || tks > n_tickets) return -7;
   hipStream_t s = (hipStream_t)stream;
+  bool nosplit = true;
+  for (int i = 0; i < np; ++i) nosplit = nosplit && a.split[i] == 1;
+  bool k32 = true;
+  for (int i = 0; i < np; ++i) k32 = k32 && a.p[i].K % 32 == 0;
+  if (cfg == 7 && bkm && all_k && nosplit && k32 && !g6_off && !a.dbg) {
+    if (g6_nw4) g6_kernel_launch<192, 256, 4>(a, s);
+    else g6_kernel_launch<192, 256, 8>(a, s);
+    R2_CHECK_LAUNCH();
+    return cfg;
+  }
   switch (cfg * 2 + bkm) {
     case 0: g5_kernel_launch<false, 192, 128, 64, 2>(a, s); break;
     case 1: g5_kernel_launch<true, 192, 128, 64, 2>(a, s); break;

@@ -113,6 +113,7 @@ class LearnerEngine:
                 arr = (ctypes.c_int * 8)(*xcd_cus)
                 kernels().r2_set_xcd_cus(arr)
             kernels().r2_lstm_persist_force_slow(0 if cfg.learner.lstm_xcd_pairs else 2)
+            kernels().r2_gemm5_set_mode(1 | (0 if cfg.learner.sp_gemm6 else 4))
         if init_module is None:
             torch.manual_seed(cfg.seed)
             init_module = QNet("cpu", m, e)
