@@ -259,45 +259,18 @@ __device__ __forceinline__ void g5_emit(const GemmProb& P, int row, int col, f32
   }
 }
 
-template <bool BKM, int BM, int BN, int BK, int NS, bool IL>
-__global__ __launch_bounds__(512) void gemm5_kernel(const G5Args a) {
+// Epilogue of an 8-wave (2 x 4) tile, shared by gemm5 and gemm6: the BM x BN accumulators pass
+// through LDS 64 rows at a time (row-contiguous, 4 columns per thread); with a K split, the
+// partial tile goes write-through to the workspace and the tile's last arriver sums the splits
+// in split order (bit-reproducible) and runs the epilogue.
+template <int BM, int BN>
+__device__ __forceinline__ void g5_epilogue(const G5Args& a, const GemmProb& P, int pi, int tile,
+                                            int ksp, int S, int m0, int n0,
+                                            const f32x4 (&acc)[BM / 32][BN / 64], uint8_t* lds5,
+                                            int tid, int wave, int lane) {
   constexpr int FM = BM / 32, FN = BN / 64;
-  extern __shared__ __attribute__((aligned(1024))) uint8_t lds5[];
-  // the split-K arrival flag lives past the epilogue's staging rows (static LDS would push the
-  // (192, 128) tile past 160 KB)
-  int& last = *(int*)(lds5 + 64 * (BN + 16) * 4);
-  int bid;
-  {
-    const int b = blockIdx.x, x = b & 7, qn = a.total >> 3, r = a.total & 7;
-    bid = (x < r ? x * (qn + 1) : r * (qn + 1) + (x - r) * qn) + (b >> 3);
-  }
-  int pi = 0;
-#pragma unroll
-  for (int i = 1; i < gm::MAXP; ++i)
-    if (i < a.np && bid >= a.item_base[i]) pi = i;
-  const GemmProb& P = a.p[pi];
-  const int S = a.split[pi];
-  const int item = bid - a.item_base[pi];
-  const int tile = item / S, ksp = item % S;
-  const int tm = tile / P.tiles_n, tn = tile % P.tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int nk = (P.K + BK - 1) / BK, per = (nk + S - 1) / S;
-  const int kt0 = min(nk, ksp * per), kt1 = min(nk, kt0 + per);
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wr = wave >> 2, wc = wave & 3;
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (BM % 128 == 0) {
-    if (P.a_kmajor) g5_mainloop<true, BKM, BM, BN, BK, NS, IL>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc, a.dbg);
-    else g5_mainloop<false, BKM, BM, BN, BK, NS, IL>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc, a.dbg);
-  } else {
-    g5_mainloop<true, BKM, BM, BN, BK, NS, IL>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc, a.dbg);
-  }
-
-  // ---- epilogue: 64 rows at a time through LDS (row-contiguous, 4 columns per thread)
+  int& last = *(int*)(lds5 + 64 * (BN + 16) * 4);
   // acc[i][j][e] = tile[wr*(BM/2) + 16i + 4(l>>4) + e][wc*(BN/4) + 16j + (l&15)]
   constexpr int LS = BN + 16;
   constexpr int NP = FM / 2;                // 32 rows per wave row per pass -> 64 rows per pass
@@ -373,18 +346,57 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const G5Args a) {
   }
 }
 
+template <bool BKM, int BM, int BN, int BK, int NS, bool IL>
+__global__ __launch_bounds__(512) void gemm5_kernel(const G5Args a) {
+  constexpr int FM = BM / 32, FN = BN / 64;
+  extern __shared__ __attribute__((aligned(1024))) uint8_t lds5[];
+  int bid;
+  {
+    const int b = blockIdx.x, x = b & 7, qn = a.total >> 3, r = a.total & 7;
+    bid = (x < r ? x * (qn + 1) : r * (qn + 1) + (x - r) * qn) + (b >> 3);
+  }
+  int pi = 0;
+#pragma unroll
+  for (int i = 1; i < gm::MAXP; ++i)
+    if (i < a.np && bid >= a.item_base[i]) pi = i;
+  const GemmProb& P = a.p[pi];
+  const int S = a.split[pi];
+  const int item = bid - a.item_base[pi];
+  const int tile = item / S, ksp = item % S;
+  const int tm = tile / P.tiles_n, tn = tile % P.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = (P.K + BK - 1) / BK, per = (nk + S - 1) / S;
+  const int kt0 = min(nk, ksp * per), kt1 = min(nk, kt0 + per);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wr = wave >> 2, wc = wave & 3;
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (BM % 128 == 0) {
+    if (P.a_kmajor) g5_mainloop<true, BKM, BM, BN, BK, NS, IL>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc, a.dbg);
+    else g5_mainloop<false, BKM, BM, BN, BK, NS, IL>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc, a.dbg);
+  } else {
+    g5_mainloop<true, BKM, BM, BN, BK, NS, IL>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc, a.dbg);
+  }
+
+  g5_epilogue<BM, BN>(a, P, pi, tile, ksp, S, m0, n0, acc, lds5, tid, wave, lane);
+}
+
 // ============================================================================================
-// gemm6: the split GEMM for k-major A and B without split-K (the x-projection of both nets,
-// 10,560 x 1,024 x 1,568) on ONE wave per SIMD with register double-buffered fragments.
-// gemm5's 8-wave 192 x 256 tile (wave tile 96 x 64: 96 accumulator + 80 fragment registers) has
-// no registers for a second fragment set, so after every K tile's barrier both waves of a SIMD
-// read their fragments from LDS at the same moment and only then issue their MFMAs: the pipe
-// idles through the read burst (PMC: MFMA ~42 % busy, waves waiting 35 % of their cycles).  Here
-// 4 waves of 96 x 128 hold 192 accumulator registers and two 28-fragment sets (224), within the
-// 512 a lone wave on its SIMD may use, and read tile k+1's fragments between tile k's 144 MFMAs
-// (one ds_read_b128 per ~5 MFMAs).  Per K tile of 32: stage ring of 2 x 56 KB (A / B hi and lo
-// by global_load_lds, gemm5's bank swizzles); the DMA of tile k+2 is issued right after the
-// barrier that retires tile k's LDS buffer, so it has one tile of MFMAs to land.
+// gemm6: the split GEMM mainloop with the fragment registers refilled between the three product
+// passes.  gemm5 reads all of a K step's fragments (A / B hi and lo) and then issues its MFMAs;
+// with two waves per SIMD released together by the per-tile barrier, both read LDS at the same
+// moment and the MFMA pipe idles through the read burst (PMC: ~42 % busy, waves waiting 35 %).
+// Here every K step runs its products as three passes over all FM x FN accumulators in the order
+// A hi.B lo, A hi.B hi, A lo.B hi -- the only order whose last pass frees the operands the next
+// step's first pass does not need -- and each plane's registers take the next step's fragments
+// in the pass after their last use (B lo during pass 2, A hi during pass 3, A lo and B hi during
+// the next step's pass 1), so fragment reads always overlap MFMAs without a second register set.
+// The one barrier per LDS tile follows pass 1 of its last K step (the tile's last LDS reads): the
+// next tile has landed, and the DMA of the tile after it refills this buffer with a whole tile
+// of MFMAs to land.  Same 8-wave 2 x 4 layout, staging and epilogue (split-K included) as gemm5.
 __device__ __forceinline__ void g6_dma(const bf16* src, uint8_t* dst) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
@@ -403,42 +415,21 @@ __device__ __forceinline__ void g6_mix() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int BM, int BN, int NW>
-__global__ __launch_bounds__(NW * 64)
-void gemm6_kernel(const G5Args a) {
-  constexpr int BK = 32, WC = NW / 2;                 // waves: 2 rows x WC columns
-  constexpr int FM = BM / 32, FN = BN / (16 * WC);    // 16 x 16 fragments of the (BM/2) x (BN/WC) wave tile
+template <bool AK, bool BKM, int BM, int BN, int BK>
+__device__ __forceinline__ void g6_mainloop(const GemmProb& P, int m0, int n0, int kt0, int kt1,
+                                            uint8_t* lds6, int wave, int lane,
+                                            f32x4 (&acc)[BM / 32][BN / 64]) {
+  constexpr int NW = 8, KS = BK / 32;
+  constexpr int FM = BM / 32, FN = BN / 64;
   constexpr int OPA = BM * BK * 2, OPB = BN * BK * 2, STB = 2 * (OPA + OPB);
-  extern __shared__ __attribute__((aligned(1024))) uint8_t lds6[];
-  int bid;
-  {
-    const int b = blockIdx.x, x = b & 7, qn = a.total >> 3, r = a.total & 7;
-    bid = (x < r ? x * (qn + 1) : r * (qn + 1) + (x - r) * qn) + (b >> 3);
-  }
-  int pi = 0;
-#pragma unroll
-  for (int i = 1; i < gm::MAXP; ++i)
-    if (i < a.np && bid >= a.item_base[i]) pi = i;
-  const GemmProb& P = a.p[pi];
-  const int tile = bid - a.item_base[pi];
-  const int tm = tile / P.tiles_n, tn = tile % P.tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int nk = (P.K + BK - 1) / BK;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int wr = wave / WC, wc = wave % WC;
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // staging: this thread's 1-KB blocks of each plane (gemm5's k-major layout: 16 rows x 4
-  // swizzled 16-B chunks per block) as element offsets fixed for the whole K loop (K % 32 == 0,
-  // checked by the launcher: no K tail); a tile adds k0.  hi and lo planes share the offsets.
-  constexpr int NBA = BM * BK * 2 / 1024, NBB = BN * BK * 2 / 1024;   // 1-KB blocks per plane
-  constexpr int PA = (NBA + NW - 1) / NW, PB = (NBB + NW - 1) / NW;       // block w + NW j
-  uint32_t offa[PA], offb[PB];
-  {
+  const int wr = wave >> 2, wc = wave & 3;
+  // both operands k-major, no K tail (the x-projection): each thread's 1-KB staging blocks as
+  // element offsets fixed for the whole K loop (a tile adds k0); else gemm5's generic staging
+  constexpr bool FAST = AK && BKM && BK == 32;
+  constexpr int NBA = BM * BK * 2 / 1024, NBB = BN * BK * 2 / 1024;
+  constexpr int PA = (NBA + NW - 1) / NW, PB = (NBB + NW - 1) / NW;
+  uint32_t offa[FAST ? PA : 1], offb[FAST ? PB : 1];
+  if constexpr (FAST) {
     const int rr = lane >> 2, cp = lane & 3;
 #pragma unroll
     for (int j = 0; j < PA; ++j) {
@@ -452,143 +443,142 @@ void gemm6_kernel(const G5Args a) {
     }
   }
   auto stage = [&](int kt) {
-    uint8_t* st = lds6 + (kt & 1) * STB;
-    const uint32_t k0 = (uint32_t)(kt * BK);
+    uint8_t* st = lds6 + ((kt - kt0) & 1) * STB;
+    if constexpr (FAST) {
+      const uint32_t k0 = (uint32_t)(kt * BK);
 #pragma unroll
-    for (int j = 0; j < PA; ++j) {
-      if (NBA % NW == 0 || wave + NW * j < NBA) {
-        uint8_t* d = st + (wave + NW * j) * 1024;
-        g6_dma(P.A + (offa[j] + k0), d);
-        g6_dma(P.A_lo + (offa[j] + k0), d + OPA);
+      for (int j = 0; j < PA; ++j) {
+        if (NBA % NW == 0 || wave + NW * j < NBA) {
+          uint8_t* d = st + (wave + NW * j) * 1024;
+          g6_dma(P.A + (offa[j] + k0), d);
+          g6_dma(P.A_lo + (offa[j] + k0), d + OPA);
+        }
       }
-    }
 #pragma unroll
-    for (int j = 0; j < PB; ++j) {
-      if (NBB % NW == 0 || wave + NW * j < NBB) {
-        uint8_t* d = st + 2 * OPA + (wave + NW * j) * 1024;
-        g6_dma(P.B + (offb[j] + k0), d);
-        g6_dma(P.B_lo + (offb[j] + k0), d + OPB);
+      for (int j = 0; j < PB; ++j) {
+        if (NBB % NW == 0 || wave + NW * j < NBB) {
+          uint8_t* d = st + 2 * OPA + (wave + NW * j) * 1024;
+          g6_dma(P.B + (offb[j] + k0), d);
+          g6_dma(P.B_lo + (offb[j] + k0), d + OPB);
+        }
       }
+    } else {
+      int oz;
+      asm volatile("v_mov_b32 %0, 0" : "=v"(oz));
+      const int k0 = kt * BK;
+      g5_stage<AK, BM, BK>(P.A, P.lda, m0, P.M, k0, P.K, st, wave, lane, oz);
+      g5_stage<AK, BM, BK>(P.A_lo, P.lda, m0, P.M, k0, P.K, st + OPA, wave, lane, oz);
+      g5_stage<BKM, BN, BK>(P.B, P.ldb, n0, P.N, k0, P.K, st + 2 * OPA, wave, lane, oz);
+      g5_stage<BKM, BN, BK>(P.B_lo, P.ldb, n0, P.N, k0, P.K, st + 2 * OPA + OPB, wave, lane, oz);
     }
   };
-  // fragment (rows i0 .. i0+15, k-major, BK 32) of this lane: row i0 + l16, chunk g ^ swz(row),
-  // and swz depends only on bit 3 of the row, i.e. on l16: one lane offset + a constant per fragment
-  const int l16f = lane & 15, gf = lane >> 4;
-  int foff = l16f * (BK * 2) + ((gf ^ g5_kswz<BK>(l16f)) * 16);
-  asm volatile("" : "+v"(foff));
-  auto frag = [&](const uint8_t* plane, int i0) {
-    return *(const bf16x8*)(plane + foff + i0 * (BK * 2));
-  };
-  auto planes = [&](int buf, const uint8_t*& ah, const uint8_t*& al, const uint8_t*& bh,
-                    const uint8_t*& bl) {
-    ah = lds6 + buf * STB;
-    al = ah + OPA;
-    bh = ah + 2 * OPA;
-    bl = bh + OPB;
-  };
-  // One register set per plane, each refilled with the next K tile's fragments in the pass after
-  // its last use.  Pass order per tile: A hi.B lo, A hi.B hi, A lo.B hi -- the only order whose
-  // last pass frees the operands the next tile's first pass does NOT need: B lo refills during
-  // pass 2, A hi during pass 3, A lo and B hi during the next tile's pass 1.  112 fragment + 192
-  // accumulator registers (an MFMA's A / B operands must sit in the 256 VGPRs).  The single
-  // barrier per tile follows pass 1 (the last reads of this tile's LDS buffer): tile k+1 has
-  // landed, and tile k+2's DMA into this buffer gets three passes to land.
   bf16x8 ahi[FM], alo[FM], bhi[FN], blo[FN];
-  auto ldA = [&](bf16x8 (&f)[FM], const uint8_t* pl) {
+  // K step q = (LDS tile kt, step ks of it); its planes in buffer (kt - kt0) & 1
+  auto ldA = [&](bf16x8 (&f)[FM], int kt, int ks, int plane) {
+    const uint8_t* pl = lds6 + ((kt - kt0) & 1) * STB + plane * OPA;
 #pragma unroll
-    for (int i = 0; i < FM; ++i) f[i] = frag(pl, wr * (BM / 2) + 16 * i);
+    for (int i = 0; i < FM; ++i) f[i] = g5_frag<AK, BK>(pl, wr * (BM / 2) + 16 * i, ks, lane);
   };
-  auto ldB = [&](bf16x8 (&f)[FN], const uint8_t* pl) {
+  auto ldB = [&](bf16x8 (&f)[FN], int kt, int ks, int plane) {
+    const uint8_t* pl = lds6 + ((kt - kt0) & 1) * STB + 2 * OPA + plane * OPB;
 #pragma unroll
-    for (int j = 0; j < FN; ++j) f[j] = frag(pl, wc * (BN / WC) + 16 * j);
+    for (int j = 0; j < FN; ++j) f[j] = g5_frag<BKM, BK>(pl, wc * (BN / 4) + 16 * j, ks, lane);
   };
-  auto step = [&](int kt, int buf, bool more) {
-    const uint8_t *cah, *cal, *cbh, *cbl, *nah, *nal, *nbh, *nbl;
-    planes(buf, cah, cal, cbh, cbl);
-    planes(buf ^ 1, nah, nal, nbh, nbl);
-    // pass 1: A hi x B lo; this tile's A lo / B hi arrive
-    ldA(alo, cal);
-    ldB(bhi, cbh);
+  auto step = [&](int kt, int ks, bool more) {
+    // the next K step: same tile, or the first step of the next one
+    const int nkt = ks + 1 < KS ? kt : kt + 1, nks = ks + 1 < KS ? ks + 1 : 0;
+    // pass 1: A hi x B lo; this step's A lo / B hi arrive
+    ldA(alo, kt, ks, 1);
+    ldB(bhi, kt, ks, 0);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = g5_mfma(ahi[i], blo[j], acc[i][j]);
     g6_mix<FM + FN, FM * FN>();
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();          // tile kt+1 visible; this tile's buffer read out
-    if (kt + 2 < nk) stage(kt + 2);
-    // pass 2: A hi x B hi; B lo <- tile kt+1
-    if (more) ldB(blo, nbl);
+    if (ks == KS - 1) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // tile kt+1 landed; kt read
+      __builtin_amdgcn_s_barrier();        // every wave: tile kt+1 visible, tile kt's buffer free
+      if (kt + 2 < kt1) stage(kt + 2);
+    }
+    // pass 2: A hi x B hi; B lo <- the next step's
+    if (more) ldB(blo, nkt, nks, 1);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = g5_mfma(ahi[i], bhi[j], acc[i][j]);
     if (more) g6_mix<FN, FM * FN>(); else g6_mix<0, FM * FN>();
-    // pass 3: A lo x B hi; A hi <- tile kt+1
-    if (more) ldA(ahi, nah);
+    // pass 3: A lo x B hi; A hi <- the next step's
+    if (more) ldA(ahi, nkt, nks, 0);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = g5_mfma(alo[i], bhi[j], acc[i][j]);
     if (more) g6_mix<FM, FM * FN>(); else g6_mix<0, FM * FN>();
   };
-  if (nk > 0) {
-    stage(0);
+  if (kt0 < kt1) {
+    stage(kt0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (nk > 1) stage(1);
-    const uint8_t *pah, *pal, *pbh, *pbl;
-    planes(0, pah, pal, pbh, pbl);
-    ldA(ahi, pah);
-    ldB(blo, pbl);
-  }
-  for (int kt = 0; kt + 1 < nk; ++kt) step(kt, kt & 1, true);
-  if (nk > 0) step(nk - 1, (nk - 1) & 1, false);
-
-  // ---- epilogue: 64 rows at a time through LDS (row-contiguous, 4 columns per thread)
-  // acc[i][j][e] = tile[wr*(BM/2) + 16i + 4(l>>4) + e][wc*(BN/2) + 16j + (l&15)]
-  constexpr int LS = BN + 16;
-  float* L = (float*)lds6;
-  const int l16 = lane & 15, g = lane >> 4;
-  const bool vec = ((uintptr_t)P.C % 16 == 0) && (P.ldc % 4 == 0);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int p = 0; p < FM / 2; ++p) {
-    __builtin_amdgcn_s_barrier();
-#pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          L[(wr * 32 + ii * 16 + 4 * g + e) * LS + wc * (BN / WC) + 16 * j + l16] = acc[2 * p + ii][j][e];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-#pragma unroll 2
-    for (int q = tid; q < 64 * (BN / 4); q += NW * 64) {
-      const int lr = q / (BN / 4), cc = (q % (BN / 4)) * 4;
-      const int row = m0 + (lr >> 5) * (BM / 2) + 32 * p + (lr & 31);
-      const int col = n0 + cc;
-      if (row >= P.M || col >= P.N) continue;
-      g5_emit(P, row, col, *(const f32x4*)(L + lr * LS + cc), vec);
-    }
+    if (kt0 + 1 < kt1) stage(kt0 + 1);
+    ldA(ahi, kt0, 0, 0);
+    ldB(blo, kt0, 0, 1);
+    const int nq = (kt1 - kt0) * KS;
+    for (int q = 0; q + 1 < nq; ++q) step(kt0 + q / KS, q % KS, true);
+    step(kt1 - 1, KS - 1, false);
   }
 }
 
-static int g6_off = 0;   // r2_gemm5_set_mode bit 2: keep the x-projection on gemm5
+template <bool BKM, int BM, int BN, int BK>
+__global__ __launch_bounds__(512) void gemm6_kernel(const G5Args a) {
+  constexpr int FM = BM / 32, FN = BN / 64;           // 16 x 16 fragments of the (BM/2) x (BN/4) wave tile
+  extern __shared__ __attribute__((aligned(1024))) uint8_t lds6[];
+  int bid;
+  {
+    const int b = blockIdx.x, x = b & 7, qn = a.total >> 3, r = a.total & 7;
+    bid = (x < r ? x * (qn + 1) : r * (qn + 1) + (x - r) * qn) + (b >> 3);
+  }
+  int pi = 0;
+#pragma unroll
+  for (int i = 1; i < gm::MAXP; ++i)
+    if (i < a.np && bid >= a.item_base[i]) pi = i;
+  const GemmProb& P = a.p[pi];
+  const int S = a.split[pi];
+  const int item = bid - a.item_base[pi];
+  const int tile = item / S, ksp = item % S;
+  const int tm = tile / P.tiles_n, tn = tile % P.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = (P.K + BK - 1) / BK, per = (nk + S - 1) / S;
+  const int kt0 = min(nk, ksp * per), kt1 = min(nk, kt0 + per);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (BM % 128 == 0) {
+    if (P.a_kmajor) g6_mainloop<true, BKM, BM, BN, BK>(P, m0, n0, kt0, kt1, lds6, wave, lane, acc);
+    else g6_mainloop<false, BKM, BM, BN, BK>(P, m0, n0, kt0, kt1, lds6, wave, lane, acc);
+  } else {
+    g6_mainloop<true, BKM, BM, BN, BK>(P, m0, n0, kt0, kt1, lds6, wave, lane, acc);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();            // every wave past its last LDS read before the epilogue
+  g5_epilogue<BM, BN>(a, P, pi, tile, ksp, S, m0, n0, acc, lds6, tid, wave, lane);
+}
 
-static int g6_nw4 = 0;  // r2_gemm5_set_mode bit 3: the 4-wave (one per SIMD) variant
+static int g6_off = 0;   // r2_gemm5_set_mode bit 2: every launch on gemm5
 
-template <int BM, int BN, int NW>
+template <bool BKM, int BM, int BN, int BK>
 static void g6_kernel_launch(const G5Args& a, hipStream_t s) {
-  constexpr int LDS = 2 * 2 * (BM + BN) * 32 * 2;
-  static_assert(LDS <= 160 * 1024 && 64 * (BN + 16) * 4 <= LDS, "LDS");
+  constexpr int LDS = 2 * 2 * (BM + BN) * BK * 2;
+  static_assert(LDS <= 160 * 1024 && 64 * (BN + 16) * 4 + 4 <= LDS, "LDS");
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)gemm6_kernel<BM, BN, NW>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    hipFuncSetAttribute((const void*)gemm6_kernel<BKM, BM, BN, BK>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm6_kernel<BM, BN, NW>), dim3(a.total), dim3(NW * 64), LDS, s, a);
+  hipLaunchKernelGGL((gemm6_kernel<BKM, BM, BN, BK>), dim3(a.total), dim3(512), LDS, s, a);
 }
 
 static int g5_il = 1;   // interleaved fragment loads (r2_gemm5_set_mode)
@@ -596,7 +586,6 @@ static int g5_dbg = 0;  // probe bits (G5Args::dbg)
 extern "C" int r2_gemm5_set_mode(int m) {
   g5_il = m & 1;
   g6_off = (m >> 2) & 1;
-  g6_nw4 = (m >> 3) & 1;
   g5_dbg = (m >> 4) & 3;
   return 0;
 }
@@ -692,13 +681,28 @@ extern "C" int r2_gemm5(const int64_t* descs, const int* split, int np, int cfg,
   a.total = items;
   if (slabs * bm * bn * 4 > ws_bytes || tks > n_tickets) return -7;
   hipStream_t s = (hipStream_t)stream;
-  bool nosplit = true;
-  for (int i = 0; i < np; ++i) nosplit = nosplit && a.split[i] == 1;
+  // gemm6 (refilled fragment registers) for every configuration; gemm5 under r2_gemm5_set_mode
+  // bit 2 or the probe bits.  gemm6's fast staging (k-major A and B, BK 32) has no K tail.
   bool k32 = true;
   for (int i = 0; i < np; ++i) k32 = k32 && a.p[i].K % 32 == 0;
-  if (cfg == 7 && bkm && all_k && nosplit && k32 && !g6_off && !a.dbg) {
-    if (g6_nw4) g6_kernel_launch<192, 256, 4>(a, s);
-    else g6_kernel_launch<192, 256, 8>(a, s);
+  if (!g6_off && !a.dbg && (k32 || !(bkm && all_k))) {
+    switch (cfg * 2 + bkm) {
+      case 0: g6_kernel_launch<false, 192, 128, 64>(a, s); break;
+      case 1: g6_kernel_launch<true, 192, 128, 64>(a, s); break;
+      case 2: g6_kernel_launch<false, 128, 128, 64>(a, s); break;
+      case 3: g6_kernel_launch<true, 128, 128, 64>(a, s); break;
+      case 4: g6_kernel_launch<false, 256, 128, 32>(a, s); break;
+      case 5: g6_kernel_launch<true, 256, 128, 32>(a, s); break;
+      case 6: g6_kernel_launch<false, 256, 256, 32>(a, s); break;
+      case 7: g6_kernel_launch<true, 256, 256, 32>(a, s); break;
+      case 9: g6_kernel_launch<true, 256, 64, 64>(a, s); break;
+      case 11: g6_kernel_launch<true, 128, 64, 64>(a, s); break;
+      case 12: g6_kernel_launch<false, 128, 128, 32>(a, s); break;
+      case 13: g6_kernel_launch<true, 128, 128, 32>(a, s); break;
+      case 14: g6_kernel_launch<false, 192, 256, 32>(a, s); break;
+      case 15: g6_kernel_launch<true, 192, 256, 32>(a, s); break;
+      default: return -8;
+    }
     R2_CHECK_LAUNCH();
     return cfg;
   }

@@ -125,8 +125,9 @@ class LearnerConfig:
     # at K splits 4,4,4,1, dh 26 -> 18 us; profiles/r02_gemm_sp_micro_v1.txt) | "multipass"
     sp_gemm: str = "fused"
     sp_group_splits: str = "4,4,4,1"  # K splits of the fused post-BPTT group (dW_ih, dW_hh, dW_head1, dX)
-    # x-projection on gemm6 (gemm_sp.hip: the fragment planes refilled between the three product
-    # passes, one barrier per K tile): 115-129 -> 102-110 us, tools/gemm6_probe.py
+    # split GEMMs on gemm6 (gemm_sp.hip: the fragment planes refilled between the three product
+    # passes, one barrier per LDS tile; the heads' layer-1 GEMMs join the one-pass kernel too):
+    # x-projection 115-129 -> 102-110 us, tools/gemm6_probe.py
     sp_gemm6: bool = True
     # split precision: the dueling head's gradient reduction on the BPTT launch's idle workgroups
     # (r2_lstm_bwd_tag_sp_hg) instead of its own 28 us launch

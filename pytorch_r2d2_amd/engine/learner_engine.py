@@ -441,8 +441,12 @@ class LearnerEngine:
         in one launch, then (``duel``) one dueling kernel for every head.  Split precision: ``lo`` =
         [(pk_lo, h lo plane)] per job; z / zr are fp32."""
         if self.sp:
-            gemm(*[Gemm(h, pk["head1"].t(), zb, a_lo=hl, b_lo=pkl["head1"].t())
-                   for (pk, h, zb, _, _), (pkl, hl) in zip(jobs, lo)])
+            probs = [Gemm(h, pk["head1"].t(), zb, a_lo=hl, b_lo=pkl["head1"].t())
+                     for (pk, h, zb, _, _), (pkl, hl) in zip(jobs, lo)]
+            if self.cfg.learner.sp_gemm6 and self.cfg.learner.sp_gemm == "fused":
+                self._gemm_sp("heads", probs)     # one-pass split kernel (gemm6)
+            else:
+                gemm(*probs)
             zs = [zb for _, _, zb, _, _ in jobs]
         else:
             gemm(*[Gemm(h, pk["head1"].t(), zb) for pk, h, zb, _, _ in jobs])
