@@ -67,6 +67,10 @@ def main(argv=None):
     ap.add_argument("--profile-phases", action="store_true",
                     help="after the timed run, time each phase of 5 eager steps with HIP events "
                          "(+ roctx ranges) and add them to the JSON line under 'phases_ms'")
+    ap.add_argument("--force-dp", action="store_true",
+                    help="rehearsal under torchrun at ONE rank: the data-parallel step (segmented "
+                         "graphs, RCCL all-reduces on the comm stream, CU reservation, shard-stats "
+                         "all-gather) with one-rank collectives; labelled in 'parallelism'")
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="config override, e.g. --set learner.lstm_xcd_pairs=0 (A/B experiments)")
     args = ap.parse_args(argv)
@@ -87,7 +91,8 @@ def main(argv=None):
     shared = os.environ.get("R2D2_BENCH_SHARED") == "1"
     if shared:
         local = local % torch.cuda.device_count()
-    if world > 1:
+    use_pg = world > 1 or args.force_dp
+    if use_pg:
         torch.cuda.set_device(local)
         if shared:
             dist.init_process_group("gloo")
@@ -99,6 +104,8 @@ def main(argv=None):
     # one model seed for every rank (the engine also broadcasts rank 0's weights); the replay
     # contents differ per rank (their own shard)
     overrides = {"seed": 1234}
+    if args.force_dp:
+        overrides["dist.force_dp"] = True
     if args.target_mode:
         overrides["learner.target_mode"] = args.target_mode
     if args.dtype:
@@ -111,20 +118,20 @@ def main(argv=None):
     replay = HBMReplay(cfg, device, capacity=cap)
     replay.fill_synthetic(episode_len=400, seed=rank)
     eng = LearnerEngine(cfg, replay, device, rank=rank, world=world,
-                        process_group=dist.group.WORLD if world > 1 else None)
+                        process_group=dist.group.WORLD if use_pg else None)
     use_graph = cfg.learner.use_graph and not args.no_graph
     if use_graph:
         eng.capture(warmup=2)
     for _ in range(args.warmup):
         eng.step()
-    if world > 1:
+    if use_pg:
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         eng.step()
     torch.cuda.synchronize(device)
-    if world > 1:
+    if use_pg:
         dist.barrier()
     dt = time.perf_counter() - t0
     err = eng.error_word()
@@ -173,7 +180,8 @@ def main(argv=None):
                 "matmul": ("bf16x3 split (fp32 accumulate, fp32 state/storage)"
                            if lc.compute_dtype == "fp32" else "bf16 operands, fp32 accumulate"),
                 "replay_rows_per_gpu": replay.capacity,
-                "parallelism": "dp%d" % world + ("-shared-gpu-gloo-rehearsal" if shared else ""),
+                "parallelism": "dp%d" % world + ("-shared-gpu-gloo-rehearsal" if shared else "")
+                               + ("-forced-dp-rehearsal" if args.force_dp and world == 1 else ""),
                 "hip_graph": bool(use_graph),
             },
             "optimizer_steps_per_sec": round(opt_steps, 3),
@@ -185,7 +193,7 @@ def main(argv=None):
         if phases is not None:
             out["phases_ms"] = phases
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
     if err:
         print(f"bench: persistent-kernel error word {err:#x} (hand-off spin timed out)",

@@ -182,6 +182,11 @@ class DistConfig:
     # ``learner_steps_per_round`` steps; weights are broadcast every ``publish_rounds`` rounds
     actor_ranks: int = 0
     push_rows: int = 32
+    # rehearsal: run the data-parallel step machinery (segmented graphs, bucketed RCCL
+    # all-reduces on the comm stream, CU reservation, the shard-stats all-gather) at world 1
+    # (bench.py --force-dp under torchrun): the collectives are one-rank no-ops, the code path is
+    # the N-GPU one
+    force_dp: bool = False
     learner_steps_per_round: int = 1
     publish_rounds: int = 8
 

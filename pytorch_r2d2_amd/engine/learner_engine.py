@@ -84,7 +84,7 @@ def torso_bwd_grid(n_frames: int, reserve_cus: int = 0, n_cus: int = 256) -> int
 class LearnerEngine:
     def _comm_reserve(self) -> int:
         dc = self.cfg.dist
-        if self.world > 1 and dc.overlap_allreduce and self.device.type == "cuda":
+        if self.dp and dc.overlap_allreduce and self.device.type == "cuda":
             return int(dc.comm_reserve_cus)
         return 0
 
@@ -95,6 +95,8 @@ class LearnerEngine:
         self.device = torch.device(device)
         self.replay = replay
         self.rank, self.world, self.pg = rank, world, process_group
+        # data-parallel step machinery: world > 1, or forced at world 1 (dist.force_dp rehearsal)
+        self.dp = bool(process_group is not None and (world > 1 or cfg.dist.force_dp))
         m, e, rc, lc = cfg.model, cfg.env, cfg.replay, cfg.learner
         if m.torso != "atari":
             raise NotImplementedError("the HIP engine runs the conv torso (Atari / DMLab frames); "
@@ -156,7 +158,7 @@ class LearnerEngine:
         self.clip_buf = torch.zeros(1, dtype=torch.float32, device=d)
         self.steps_done = 0
         # data-parallel global prioritized sampling (parallel/sharded_replay.py)
-        self.dp_global = bool(world > 1 and process_group is not None and cfg.dist.global_sampling)
+        self.dp_global = bool(self.dp and cfg.dist.global_sampling)
         if self.dp_global and self.device.type == "cuda":
             # the 12-byte shard-stats all-gather runs on a side stream beside the torso / LSTM
             # graph segment.  It cannot starve the persistent forward: it depends on no kernel of
@@ -517,7 +519,7 @@ class LearnerEngine:
     def _gather_dp(self):
         """The step's one extra collective (DP global sampling): 3 floats per rank."""
         from ..parallel.sharded_replay import gather_stats
-        gather_stats(self.dp_send, self.world, self.pg, out=self.dp_recv)
+        gather_stats(self.dp_send, self.world, self.pg, out=self.dp_recv, force=self.dp)
 
     def _forward_rest(self, tail: bool = True):
         """Torso, x-projections and recurrent chains; then (``tail``) heads, TD and priorities.
@@ -741,7 +743,7 @@ class LearnerEngine:
         x_job = Gemm(self.dgates, pk["w_ih"], self.dX, a_lo=self.dgates_lo, b_lo=pkl["w_ih"],
                      c_lo=self.dX_lo)
         if self.cfg.learner.sp_gemm == "fused":
-            splits = [int(v) for v in self.cfg.learner.sp_group_splits.split(",")]
+            splits = [int(v) for v in self.cfg.learner.sp_group_splits.replace(":", ",").split(",")]
             self._gemm_sp("group", [w_jobs[2], w_jobs[1], w_jobs[0], x_job], splits)
             self._dX = self.dX
             return
@@ -1016,7 +1018,7 @@ class LearnerEngine:
         if getattr(self, "_gsync", None) is None:
             from ..parallel.grad_sync import GradSync
             self._gsync = GradSync(self.grad, self.world, self.pg, self.cfg.dist.grad_dtype,
-                                   use_stream=self.cfg.dist.overlap_allreduce)
+                                   use_stream=self.cfg.dist.overlap_allreduce, force=self.dp)
         return self._gsync
 
     def _seg_core(self):
@@ -1065,11 +1067,11 @@ class LearnerEngine:
             self._forward_loss()      # (DP global sampling: includes the stats all-gather)
         with ph("backward_core"):
             self._backward_core()
-        if self.world > 1:   # core bucket all-reduce overlaps the conv backward
+        if self.dp:   # core bucket all-reduce overlaps the conv backward
             self._sync().start(0, L.torso_offset)
         with ph("backward_torso"):
             self._seg_torso()
-        if self.world > 1:   # torso bucket all-reduce overlaps the priority tail
+        if self.dp:   # torso bucket all-reduce overlaps the priority tail
             self._sync().start(L.torso_offset, L.padded)
             with ph("priorities"):
                 self._seg_prio()
@@ -1099,7 +1101,7 @@ class LearnerEngine:
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         self.graphs = []
-        if self.world > 1:
+        if self.dp:
             segs = [self._seg_core, self._seg_torso, self._seg_prio, self._seg_update]
             if self.dp_global:
                 segs = [self._seg_sample, self._seg_fwd_head, self._seg_core_tail] + segs[1:]
@@ -1119,7 +1121,7 @@ class LearnerEngine:
         if not self.graph:
             self.step_eager()
             return
-        if self.world <= 1:
+        if not self.dp:
             self.graphs[0].replay()
         else:
             L = self.layout

@@ -26,9 +26,10 @@ import torch.distributed as dist
 
 class GradSync:
     def __init__(self, grad: torch.Tensor, world: int, group=None, dtype: str = "fp32",
-                 use_stream: bool = True):
+                 use_stream: bool = True, force: bool = False):
         self.grad = grad
         self.world = world
+        self.force = force            # issue the collectives at world 1 too (dist.force_dp)
         self.group = group
         self.dtype = dtype
         self.cuda = grad.is_cuda
@@ -37,7 +38,7 @@ class GradSync:
         self._bufs = {}
 
     def start(self, lo: int, hi: int) -> None:
-        if self.world <= 1 or hi <= lo:
+        if (self.world <= 1 and not self.force) or hi <= lo:
             return
         view = self.grad[lo:hi]
         if self.stream is None:

@@ -43,12 +43,13 @@ def local_stats(total: torch.Tensor, n_valid: torch.Tensor, probs: torch.Tensor,
     return v
 
 
-def gather_stats(local: torch.Tensor, world: int, group=None, out: torch.Tensor = None
-                 ) -> torch.Tensor:
-    """(world, 3) all-gathered shard stats (a 12-byte message per rank)."""
+def gather_stats(local: torch.Tensor, world: int, group=None, out: torch.Tensor = None,
+                 force: bool = False) -> torch.Tensor:
+    """(world, 3) all-gathered shard stats (a 12-byte message per rank).  ``force``: run the
+    collective at world 1 too (dist.force_dp rehearsal)."""
     if out is None:
         out = torch.empty(world * 3, dtype=local.dtype, device=local.device)
-    if world <= 1:
+    if world <= 1 and not (force and group is not None):
         out.copy_(local.reshape(-1))
     else:
         dist.all_gather_into_tensor(out, local.reshape(-1), group=group)

@@ -332,3 +332,43 @@ def test_fused_synthetic_env_step_dynamics(cue_only_first):
         assert int(fr[~m].max()) <= 47
     noise = env.frames.view(E, 4, 84, 84).float()
     assert 20.0 < float(noise[noise <= 47].mean()) < 27.0
+
+
+def _force_dp_worker(rank, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                      LOCAL_RANK="0")
+    import torch.distributed as dist
+    from pytorch_r2d2_amd.engine.learner_engine import LearnerEngine
+    dist.init_process_group("nccl", device_id=torch.device(DEV))
+    out = {}
+    for force in (True, False):
+        cfg = get_config("atari57", **{"learner.batch_size": 8, "replay.burn_in": 4,
+                                       "replay.learn": 4, "replay.overlap": 4, "seed": 11,
+                                       "learner.use_graph": False, "dist.force_dp": force})
+        rp = HBMReplay(cfg, DEV, capacity=8 * 200, n_subrings=8)
+        rp.fill_synthetic(episode_len=50, seed=0)
+        torch.manual_seed(5)
+        eng = LearnerEngine(cfg, rp, DEV, process_group=dist.group.WORLD if force else None,
+                            init_module=QNet("cpu", cfg.model, cfg.env))
+        assert eng.dp == force and eng.dp_global == force
+        eng.capture(warmup=1)
+        assert len(eng.graphs) == (6 if force else 1)
+        for _ in range(3):
+            eng.step()
+        torch.cuda.synchronize()
+        assert eng.error_word() == 0
+        out[force] = {"master": eng.master.cpu(), "loss": eng.loss_value()}
+    torch.save(out, os.path.join(outdir, "force_dp.pt"))
+    dist.destroy_process_group()
+
+
+def test_forced_dp_step_over_rccl_matches_plain_step(tmp_path):
+    """The N-GPU step machinery at ONE rank over RCCL (dist.force_dp): six graph segments, the
+    bucketed all-reduces on the comm stream and the shard-stats all-gather as one-rank
+    collectives -- the same trajectory as the plain single-graph step (what the 8-GPU run uses,
+    exercised on the real backend instead of gloo)."""
+    import torch.multiprocessing as tmp
+    tmp.spawn(_force_dp_worker, args=(_free_port(), str(tmp_path)), nprocs=1, join=True)
+    r = torch.load(tmp_path / "force_dp.pt", weights_only=True)
+    torch.testing.assert_close(r[True]["master"], r[False]["master"], rtol=0, atol=1e-6)
+    assert abs(r[True]["loss"] - r[False]["loss"]) <= 1e-5 * max(1.0, abs(r[False]["loss"]))
