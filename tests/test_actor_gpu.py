@@ -339,7 +339,7 @@ def _force_dp_worker(rank, port, outdir):
                       LOCAL_RANK="0")
     import torch.distributed as dist
     from pytorch_r2d2_amd.engine.learner_engine import LearnerEngine
-    dist.init_process_group("nccl", device_id=torch.device(DEV))
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
     out = {}
     for force in (True, False):
         cfg = get_config("atari57", **{"learner.batch_size": 8, "replay.burn_in": 4,
