@@ -187,6 +187,9 @@ class DistConfig:
     # (bench.py --force-dp under torchrun): the collectives are one-rank no-ops, the code path is
     # the N-GPU one
     force_dp: bool = False
+    # capture the DP step as ONE graph, the RCCL collectives included (side-stream fork / join
+    # edges), instead of 4-6 segment graphs with the collectives issued between them
+    graph_collectives: bool = False
     learner_steps_per_round: int = 1
     publish_rounds: int = 8
 

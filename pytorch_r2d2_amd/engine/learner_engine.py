@@ -512,9 +512,13 @@ class LearnerEngine:
                 h.zero_()
                 c.zero_()
         if self.dp_global:
-            from ..parallel.sharded_replay import local_stats
             root = rp.tree[int(rp.tree_offs[-1]): int(rp.tree_offs[-1]) + 1]
-            local_stats(root, rp.n_valid, self.probs, out=self.dp_send)
+            if self.device.type == "cuda":     # one launch (dp_stats.hip)
+                check(kernels().r2_dp_local_stats(ptr(root), ptr(rp.n_valid), ptr(self.probs), B,
+                                                  ptr(self.dp_send), stream_handle()), "dp_local_stats")
+            else:
+                from ..parallel.sharded_replay import local_stats
+                local_stats(root, rp.n_valid, self.probs, out=self.dp_send)
 
     def _gather_dp(self):
         """The step's one extra collective (DP global sampling): 3 floats per rank."""
@@ -616,9 +620,14 @@ class LearnerEngine:
         H, A = L.H, L.A
         pk, pt = self.pk, self.pk_t
         if self.dp_global:   # IS-weight parameters from the all-gathered shard stats
-            from ..parallel.sharded_replay import global_is_params
-            global_is_params(self.dp_recv.view(self.world, 3), self.rank, float(self.cfg.replay.beta),
-                             out=self.dp_params)
+            if self.device.type == "cuda":     # one launch (dp_stats.hip)
+                check(kernels().r2_dp_is_params(ptr(self.dp_recv), self.world, self.rank,
+                                                float(self.cfg.replay.beta), ptr(self.dp_params),
+                                                stream_handle()), "dp_is_params")
+            else:
+                from ..parallel.sharded_replay import global_is_params
+                global_is_params(self.dp_recv.view(self.world, 3), self.rank,
+                                 float(self.cfg.replay.beta), out=self.dp_params)
         # heads (rows from the first learning step on)
         jobs = [(pk, self.hseq["on"][Lb:].reshape(-1, H), self.z_on, self.q_on, self.zr_on),
                 (pt, self.hseq["tg"][Lb:].reshape(-1, H), self.z_tg, self.q_tg, None)]
@@ -1101,6 +1110,19 @@ class LearnerEngine:
         torch.cuda.current_stream(self.device).wait_stream(s)
         torch.cuda.synchronize(self.device)
         self.graphs = []
+        self._one_dp_graph = False
+        if self.dp and self.cfg.dist.graph_collectives:
+            # the whole DP step in ONE graph: the bucket all-reduces and the shard-stats
+            # all-gather are captured on their side streams (fork / join as graph edges), so the
+            # ~15 us gap of every segment boundary disappears
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._dp_step_body()
+            self.graphs.append(g)
+            self._one_dp_graph = True
+            torch.cuda.synchronize(self.device)
+            self.graph = True
+            return
         if self.dp:
             segs = [self._seg_core, self._seg_torso, self._seg_prio, self._seg_update]
             if self.dp_global:
@@ -1117,11 +1139,37 @@ class LearnerEngine:
         torch.cuda.synchronize(self.device)
         self.graph = True
 
+    def _dp_step_body(self):
+        """The DP step as stream operations (capturable): segments in order, the collectives on
+        their side streams with event fork / join -- what ``step`` issues between the segment
+        graphs."""
+        L = self.layout
+        if self.dp_global:
+            self._seg_sample()
+            main = torch.cuda.current_stream(self.device)
+            if getattr(self, "_gather_stream", None) is None:
+                self._gather_stream = torch.cuda.Stream(device=self.device)
+            gs = self._gather_stream
+            gs.wait_stream(main)
+            with torch.cuda.stream(gs):
+                self._gather_dp()
+            self._seg_fwd_head()
+            main.wait_stream(gs)
+            self._seg_core_tail()
+        else:
+            self._seg_core()
+        self._sync().start(0, L.torso_offset)
+        self._seg_torso()
+        self._sync().start(L.torso_offset, L.padded)
+        self._seg_prio()
+        self._sync().finish()
+        self._seg_update()
+
     def step(self):
         if not self.graph:
             self.step_eager()
             return
-        if not self.dp:
+        if not self.dp or getattr(self, "_one_dp_graph", False):
             self.graphs[0].replay()
         else:
             L = self.layout

@@ -29,6 +29,8 @@ _SIGS = {
     "r2_abi_version": [],
     "r2_set_num_cus": [I],
     "r2_set_xcd_cus": [P],
+    "r2_dp_local_stats": [P, P, P, I, P, P],
+    "r2_dp_is_params": [P, I, I, F, P, P],
     "r2_get_num_cus": [],
     "r2_lstm_fwd": [P, I, I, I, I, I, P],
     "r2_lstm_bwd": [P, P, P, P, P, P, P, P, P, I, I, I, I, P],

@@ -341,10 +341,11 @@ def _force_dp_worker(rank, port, outdir):
     from pytorch_r2d2_amd.engine.learner_engine import LearnerEngine
     dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
     out = {}
-    for force in (True, False):
+    for force, one in ((True, False), (True, True), (False, False)):
         cfg = get_config("atari57", **{"learner.batch_size": 8, "replay.burn_in": 4,
                                        "replay.learn": 4, "replay.overlap": 4, "seed": 11,
-                                       "learner.use_graph": False, "dist.force_dp": force})
+                                       "learner.use_graph": False, "dist.force_dp": force,
+                                       "dist.graph_collectives": one})
         rp = HBMReplay(cfg, DEV, capacity=8 * 200, n_subrings=8)
         rp.fill_synthetic(episode_len=50, seed=0)
         torch.manual_seed(5)
@@ -352,12 +353,12 @@ def _force_dp_worker(rank, port, outdir):
                             init_module=QNet("cpu", cfg.model, cfg.env))
         assert eng.dp == force and eng.dp_global == force
         eng.capture(warmup=1)
-        assert len(eng.graphs) == (6 if force else 1)
+        assert len(eng.graphs) == (6 if force and not one else 1)
         for _ in range(3):
             eng.step()
         torch.cuda.synchronize()
         assert eng.error_word() == 0
-        out[force] = {"master": eng.master.cpu(), "loss": eng.loss_value()}
+        out[(force, one)] = {"master": eng.master.cpu(), "loss": eng.loss_value()}
     torch.save(out, os.path.join(outdir, "force_dp.pt"))
     dist.destroy_process_group()
 
@@ -370,5 +371,7 @@ def test_forced_dp_step_over_rccl_matches_plain_step(tmp_path):
     import torch.multiprocessing as tmp
     tmp.spawn(_force_dp_worker, args=(_free_port(), str(tmp_path)), nprocs=1, join=True)
     r = torch.load(tmp_path / "force_dp.pt", weights_only=True)
-    torch.testing.assert_close(r[True]["master"], r[False]["master"], rtol=0, atol=1e-6)
-    assert abs(r[True]["loss"] - r[False]["loss"]) <= 1e-5 * max(1.0, abs(r[False]["loss"]))
+    plain = r[(False, False)]
+    for key in ((True, False), (True, True)):     # segmented graphs; one graph, RCCL captured
+        torch.testing.assert_close(r[key]["master"], plain["master"], rtol=0, atol=1e-6)
+        assert abs(r[key]["loss"] - plain["loss"]) <= 1e-5 * max(1.0, abs(plain["loss"]))
