@@ -188,8 +188,10 @@ class DistConfig:
     # the N-GPU one
     force_dp: bool = False
     # capture the DP step as ONE graph, the RCCL collectives included (side-stream fork / join
-    # edges), instead of 4-6 segment graphs with the collectives issued between them
-    graph_collectives: bool = False
+    # edges), instead of 4-6 segment graphs with the collectives issued between them: the DP
+    # machinery's overhead at one forced rank 1.180 -> 1.122 ms against 1.102 for the plain step
+    # (tools/dp_overhead_ab.sh, profiles/r03_force_dp_ab.txt)
+    graph_collectives: bool = True
     learner_steps_per_round: int = 1
     publish_rounds: int = 8
 
