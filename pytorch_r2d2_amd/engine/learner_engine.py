@@ -1111,7 +1111,7 @@ class LearnerEngine:
         torch.cuda.synchronize(self.device)
         self.graphs = []
         self._one_dp_graph = False
-        if self.dp and self.cfg.dist.graph_collectives:
+        if self.dp and self.cfg.dist.graph_collectives and self._pg_backend() == "nccl":
             # the whole DP step in ONE graph: the bucket all-reduces and the shard-stats
             # all-gather are captured on their side streams (fork / join as graph edges), so the
             # ~15 us gap of every segment boundary disappears
@@ -1138,6 +1138,15 @@ class LearnerEngine:
             self.graphs.append(g)
         torch.cuda.synchronize(self.device)
         self.graph = True
+
+    def _pg_backend(self) -> str:
+        """Backend of the DP process group (only RCCL collectives can be graph-captured; gloo
+        ones -- CPU tests, ranks sharing a GPU -- stay between segment graphs)."""
+        import torch.distributed as dist
+        try:
+            return str(dist.get_backend(self.pg))
+        except (RuntimeError, ValueError):
+            return ""
 
     def _dp_step_body(self):
         """The DP step as stream operations (capturable): segments in order, the collectives on
