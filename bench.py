@@ -183,8 +183,8 @@ def main(argv=None):
                 "parallelism": "dp%d" % world + ("-shared-gpu-gloo-rehearsal" if shared else "")
                                + ("-forced-dp-rehearsal" if args.force_dp and world == 1 else ""),
                 "hip_graph": bool(use_graph),
-                "dp_graph": ("one graph, RCCL captured" if cfg.dist.graph_collectives
-                             else "segmented") if eng.dp else None,
+                "dp_graph": ("one graph, RCCL captured" if getattr(eng, "_one_dp_graph", False)
+                             else "segment graphs") if eng.dp else None,
             },
             "optimizer_steps_per_sec": round(opt_steps, 3),
             "sequences_per_sec": round(opt_steps * lc.batch_size * world, 1),
