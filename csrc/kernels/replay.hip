@@ -178,7 +178,7 @@ __global__ void tree_update_level_kernel(float* __restrict__ tree, TreeGeom g, i
 __global__ void tree_update_tail_kernel(float* __restrict__ tree, TreeGeom g,
                                         const int* __restrict__ dirty, int* __restrict__ count,
                                         int max_dirty, unsigned* __restrict__ ticket,
-                                        int64_t* __restrict__ step) {
+                                        int64_t* __restrict__ step, int reset_count) {
   __shared__ int last;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int n = min(*count, max_dirty);
@@ -215,10 +215,8 @@ __global__ void tree_update_tail_kernel(float* __restrict__ tree, TreeGeom g,
   }
   if (threadIdx.x == 0) {
     *ticket = 0u;
-    if (step) {
-      *step += 1;
-      *count = 0;
-    }
+    if (step) *step += 1;
+    if (reset_count) *count = 0;
   }
 }
 
@@ -390,8 +388,8 @@ __global__ void gather_state_kernel(const float* __restrict__ hs_cs, const int* 
 // ---- end of learner step: bump the device step counter, reset the dirty list
 __global__ void step_end_kernel(int64_t* step, int* count) {
   if (threadIdx.x == 0) {
-    *step += 1;
-    *count = 0;
+    if (step) *step += 1;
+    if (count) *count = 0;
   }
 }
 
@@ -489,9 +487,9 @@ extern "C" int r2_tree_update(float* tree, const int64_t* offs, const int64_t* s
 // Level 0 as its own launch, then level 1 with every upper level (and, given `step`, the step
 // counter + dirty-list reset) folded into one launch (tree_update_tail_kernel).  ticket: one
 // zeroed uint, reset by the kernel.  -3: the tree is too shallow or too wide for the fold.
-extern "C" int r2_tree_update_fused(float* tree, const int64_t* offs, const int64_t* sizes,
-                                    int levels, const int* dirty, int* count, int max_dirty,
-                                    unsigned* ticket, int64_t* step, void* stream) {
+static int tree_update_fused(float* tree, const int64_t* offs, const int64_t* sizes, int levels,
+                             const int* dirty, int* count, int max_dirty, unsigned* ticket,
+                             int64_t* step, int reset_count, void* stream) {
   if (levels < 4 || levels > TREE_MAX_LEVELS) return -3;
   for (int l = 3; l < levels; ++l)
     if (sizes[l - 1] > 64 * 64) return -3;
@@ -505,9 +503,26 @@ extern "C" int r2_tree_update_fused(float* tree, const int64_t* offs, const int6
   // atomics on one address serialise); 64 x 4 waves cover a learner step's dirty list in a pass
   const int nbt = nb < 64 ? nb : 64;
   hipLaunchKernelGGL(tree_update_tail_kernel, dim3(nbt), dim3(256), 0, (hipStream_t)stream,
-                     tree, g, dirty, count, max_dirty, ticket, step);
+                     tree, g, dirty, count, max_dirty, ticket, step, reset_count);
   R2_CHECK_LAUNCH();
   return 0;
+}
+
+// step: non-null = the learner step's end (step counter + 1 and the dirty-list reset)
+extern "C" int r2_tree_update_fused(float* tree, const int64_t* offs, const int64_t* sizes,
+                                    int levels, const int* dirty, int* count, int max_dirty,
+                                    unsigned* ticket, int64_t* step, void* stream) {
+  return tree_update_fused(tree, offs, sizes, levels, dirty, count, max_dirty, ticket, step,
+                           step != nullptr, stream);
+}
+
+// the dirty-list reset without the step counter (the priority tail on a side stream: the
+// counter is advanced on the main stream after the optimizer's target-sync read, r2_step_inc)
+extern "C" int r2_tree_update_fused_reset(float* tree, const int64_t* offs, const int64_t* sizes,
+                                          int levels, const int* dirty, int* count, int max_dirty,
+                                          unsigned* ticket, void* stream) {
+  return tree_update_fused(tree, offs, sizes, levels, dirty, count, max_dirty, ticket, nullptr, 1,
+                           stream);
 }
 
 extern "C" int r2_seqprio_refresh(const int* starts, int B, const uint8_t* is_start,

@@ -862,9 +862,9 @@ constexpr int G2PL = G2P + 122 * 32 * 2;
 constexpr int G1H = G2PL + 122 * 32 * 2;                  // g1 hi, lo: [406][32] each
 constexpr int G1L = G1H + 406 * 32 * 2;
 constexpr int TBL2 = G1L + 406 * 32 * 2;                  // dW2 gather offsets int2 [12][64]
-constexpr int TE1 = TBL2 + 12 * 64 * 8;
-constexpr int TE2 = TE1 + 128 * 4;
-constexpr int LDS = TE2 + 96 * 4;                         // 146560
+constexpr int LDS = TBL2 + 12 * 64 * 8;                   // 145664
+// S0 / S1: W3 hi / lo staged in the g1 region (free until S2), rows of W3S bf16
+constexpr int W3S = 296, W3PL = 19 * 1024;                // 32 x 592 B per plane, padded to 19 KB
 constexpr int G2_TRASH = 121, G1_TRASH = 400;
 constexpr int PF1 = (P1 * 4 + NT - 1) / NT;               // act1 chunks per thread per plane (4)
 constexpr int PFF = (IN_CHUNKS + NT - 1) / NT;            // frame chunks per thread (4)
@@ -905,7 +905,7 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
 
-  // ---- once: zero the bordered gradient images, the gather / epilogue tables (as torso_bwd.hip)
+  // ---- once: zero the bordered gradient images, the dW2 gather table (as torso_bwd.hip)
   for (int i = tid; i < (G1H - G3P) / 16; i += NT) ((u32x4*)(lds + G3P))[i] = u32x4{0, 0, 0, 0};
   for (int i = tid; i < 12 * 64; i += NT) {
     const int sr = i >> 6, l = i & 63, sS = sr >> 1, r = sr & 1;
@@ -914,27 +914,11 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
     const int arow = P < P2 ? (Pc / 9 + 1) * 11 + Pc % 9 + 1 : 0;
     ((int2*)(lds + TBL2))[i] = make_int2(arow * 32 + cb, ((2 * (Pc / 9)) * 20 + 2 * (Pc % 9)) * 32 + cb);
   }
-  for (int i = tid; i < 128 + 96; i += NT) {
-    const int j = i < 128 ? i : i - 128, mt = j >> 5, h = (j >> 4) & 1, r = j & 15;
-    const int m = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-    uint32_t e;
-    if (i < 128) {
-      const int mv = m < 100 ? m : 99, ay = mv / 10, bx = mv % 10;
-      const int kb = 16 * (5 * (ay >> 1) + (bx >> 1)) + 8 * (ay & 1) + 2 * (bx & 1);
-      e = (uint32_t)((2 * ay) * 20 + 2 * bx) | (uint32_t)(m < 100 ? kb : G1_TRASH) << 16 |
-          (uint32_t)(m < 100) << 31;
-    } else {
-      const int qv = m < P2 ? m : P2 - 1;
-      e = (uint32_t)qv | (uint32_t)(m < P2 ? (qv / 9 + 1) * 11 + qv % 9 + 1 : G2_TRASH) << 16 |
-          (uint32_t)(m < P2) << 31;
-    }
-    ((uint32_t*)(lds + TE1))[i] = e;
-  }
-  const __amdgpu_buffer_rsrc_t w3rs = ts_rsrc(a.w3dg, 32 * 288 * 2), w3lrs = ts_rsrc(a.w3dgl, 32 * 288 * 2);
   const __amdgpu_buffer_rsrc_t w2rs = ts_rsrc(a.w2dg, 4 * 32 * 128 * 2), w2lrs = ts_rsrc(a.w2dgl, 4 * 32 * 128 * 2);
 
   f32x16 acc1 = {}, acc2a = {}, acc2b = {};
-  float db1p = 0.f, db2p = 0.f;
+  float db1v[16] = {};   // db1 partials: this lane's channel quads (dact1 epilogue layout)
+  float db2p = 0.f;
 
   u32x4 pfr[PFF], pa1[PF1], pa1l[PF1], pa2, pdx, pdxl, po3;
   // buffer loads off kernel-argument bases (SGPR descriptors, 32-bit lane offsets): 64-bit VGPR
@@ -1005,7 +989,16 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
     const bf16* fb0 = frb + (wave >> 1) * 7056 + kh1 * 84 + 4 * (pp & 1) + (4 * (2 * half)) * 84 + 4 * q;
     const bf16* fb1 = fb0 + 4 * 84;
 
-    // ======== S0: prefetched activations / gradients -> LDS; this frame's bytes start loading
+    // ======== S0: prefetched activations / gradients -> LDS; W3 hi / lo -> the g1 region by
+    // LDS-DMA (1 KB per wave-instruction, 38 of them: chunk j of a plane = row j / 37, 16-byte
+    // column min(j % 37, 35); the 37th column is the row pad)
+    for (int i = wave; i < 38; i += 8) {
+      const int pl = i >= 19, blk = i - 19 * pl, j = blk * 64 + lane;
+      const int r = j / 37, c = min(j - 37 * r, 35);
+      const bf16* src = (pl ? a.w3dgl : a.w3dg) + (j < 32 * 37 ? r * 288 + c * 8 : 0);
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(lds + G1H + pl * W3PL + blk * 1024),
+                                       16, 0, 0);
+    }
 #pragma unroll
     for (int k = 0; k < PF1; ++k) {
       const int c = tid + k * NT;
@@ -1024,45 +1017,53 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
         g3pl[o] = on ? dxl[e] : (bf16)0.f;
       }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the W3 DMA (and older loads) landed
     lds_sync();
     TBS_STAMP(1);
 
-    // ======== S1: g2 = convT(g3, W3) * (act2 > 0) on waves 5-7
-    if (wave >= 5) {
-      const int mt = wave - 5;
-      const int qq0 = mt * 32 + l32, qc = qq0 < P2 ? qq0 : P2 - 1;
-      const int ab = (((qc / 9) + 2) * 11 + qc % 9 + 2) * 32 + half * 8;
-      const int vb = (l32 * 288 + half * 8) * 2;
-      constexpr int D = 3;
-      bf16x8 rbh[D], rbl[D];
+    // ======== S1: g2 = convT(g3, W3) * (act2 > 0): waves 0-5, one 16-pixel tile each, both
+    // 16-channel halves (v_mfma_f32_16x16x32_bf16, K step = one 3x3 tap x 32 channels), A = W3
+    // from LDS, B = g3; transposed output (lane = pixel, 4 consecutive channels per accumulator):
+    // one 8-byte mask read and hi / lo store per channel quad
+    if (wave < 6) {
+      const int l16 = lane_f & 15, kg = lane_f >> 4;
+      const int qv = wave * 16 + l16, qc = qv < P2 ? qv : P2 - 1;
+      const int gb = ((qc / 9 + 2) * 11 + qc % 9 + 2) * 32 + kg * 8;
+      const bf16* w3h = (const bf16*)(lds + G1H + oz) + l16 * W3S + 8 * kg;
+      const bf16* w3l = w3h + W3PL / 2;
+      f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-      for (int s = 0; s < D; ++s) { rbh[s] = ts_bl(w3rs, vb, s * 32); rbl[s] = ts_bl(w3lrs, vb, s * 32); }
-      f32x16 acc = {};
+      for (int t = 0; t < 9; ++t) {
+        const int o = gb - ((t / 3) * 11 + t % 3) * 32;
+        const bf16x8 bh = ts_ld8(g3p + o), bl = ts_ld8(g3pl + o);
 #pragma unroll
-      for (int s = 0; s < 18; ++s) {
-        const bf16x8 bh = rbh[s % D], bl = rbl[s % D];
-        if (s + D < 18) { rbh[s % D] = ts_bl(w3rs, vb, (s + D) * 32); rbl[s % D] = ts_bl(w3lrs, vb, (s + D) * 32); }
-        const int khkw = s >> 1;
-        const int o = ab - ((khkw / 3) * 11 + khkw % 3) * 32 + (s & 1) * 16;
-        acc = mfma32_x3(ts_ld8(g3p + o), ts_ld8(g3pl + o), bh, bl, acc);
+        for (int ch = 0; ch < 2; ++ch)
+          acc[ch] = mfma16_x3(ts_ld8(w3h + ch * 16 * W3S + 32 * t), ts_ld8(w3l + ch * 16 * W3S + 32 * t),
+                              bh, bl, acc[ch]);
       }
-      const uint32_t* te = (const uint32_t*)(lds + TE2 + oz) + mt * 32 + half * 16;
+      const int row = qv < P2 ? (qc / 9 + 1) * 11 + qc % 9 + 1 : G2_TRASH;
+      float db[8];
 #pragma unroll
-      for (int r0 = 0; r0 < 16; r0 += 8) {
-        uint32_t e[8];
-        bf16 mk[8];
+      for (int ch = 0; ch < 2; ++ch) {
+        const int c0 = 16 * ch + 4 * kg;
+        const bf16x4 mk = *(const bf16x4*)(a2 + qc * 32 + c0);
+        bf16x4 vh, vl;
 #pragma unroll
-        for (int r = 0; r < 8; ++r) e[r] = te[r0 + r];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) mk[r] = a2[(e[r] & 0xffff) * 32 + l32];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const float v = ((float)mk[r] > 0.f) ? acc[r0 + r] : 0.f;
-          const int o = ((e[r] >> 16) & 0x7fff) * 32 + l32;
-          g2p[o] = (bf16)v;
-          g2pl[o] = sp_lo(v);
-          db2p += (e[r] >> 31) ? v : 0.f;
+        for (int e = 0; e < 4; ++e) {
+          const float v = (float)mk[e] > 0.f ? acc[ch][e] : 0.f;
+          vh[e] = (bf16)v;
+          vl[e] = sp_lo(v);
+          db[4 * ch + e] = qv < P2 ? v : 0.f;
         }
+        *(bf16x4*)(g2p + row * 32 + c0) = vh;
+        *(bf16x4*)(g2pl + row * 32 + c0) = vl;
+      }
+      // db2: sum over the tile's 16 pixel lanes; lane l16 = i < 8 keeps channel quad value i
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int o2 = 1; o2 < 16; o2 <<= 1) db[i] += __shfl_xor(db[i], o2, 64);
+        db2p += l16 == i ? db[i] : 0.f;
       }
     }
     lds_sync();
@@ -1089,7 +1090,12 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
     TBS_STAMP(6);
     {
       // dact1 -> g1: both of this wave's 32-pixel jobs (phase = wave >> 1) in one pass over K, so
-      // every W2 phase fragment (L2, hi / lo) is fetched once per frame, not once per job
+      // every W2 phase fragment (L2, hi / lo) is fetched once per frame, not once per job.
+      // Transposed product (A = W2 phase slice, B = g2 pixels): lane l32 owns one act1 pixel and
+      // each accumulator quad 4 consecutive channels, so the epilogue is one pixel's mask row read
+      // and one 8-byte hi / lo store per quad (vs 16 scattered 2-byte stores and mask reads per
+      // lane with the pixel-row layout: ~16k cycles per frame against 1.5k of MFMA).  g1 rows keep
+      // S3's 4x4-block order; the 8-byte channel chunk c of row R sits at c ^ ((R >> 1) & 7).
       const int phase = wave >> 1, py = phase >> 1, px = phase & 1;
       const int vb = ((phase * 32 + l32) * 128 + half * 8) * 2;
       int ab[2];
@@ -1107,37 +1113,37 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
         const bf16x8 bh = rbh[s % D], bl = rbl[s % D];
-        if (s + D < 8 && !(a.pad_ & 1)) { rbh[s % D] = ts_bl(w2rs, vb, (s + D) * 32); rbl[s % D] = ts_bl(w2lrs, vb, (s + D) * 32); }
+        if (s + D < 8) { rbh[s % D] = ts_bl(w2rs, vb, (s + D) * 32); rbl[s % D] = ts_bl(w2lrs, vb, (s + D) * 32); }
         const int tap = s >> 1;
         const int o = -((tap >> 1) * 11 + (tap & 1)) * 32 + (s & 1) * 16;
 #pragma unroll
         for (int jj = 0; jj < 2; ++jj)
-          accj[jj] = mfma32_x3(ts_ld8(g2p + ab[jj] + o), ts_ld8(g2pl + ab[jj] + o), bh, bl, accj[jj]);
+          accj[jj] = mfma32_x3(bh, bl, ts_ld8(g2p + ab[jj] + o), ts_ld8(g2pl + ab[jj] + o), accj[jj]);
       }
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
         const int mt = (wave & 1) * 2 + jj;
-        const f32x16& acc = accj[jj];
-        const uint32_t* te = (const uint32_t*)(lds + TE1 + oz) + mt * 32 + half * 16;
-        const int moff = (py * 20 + px) * 32 + l32, koff = (4 * py + px) * 32 + l32;
+        const int m = mt * 32 + l32, mc = m < 100 ? m : 99;
+        const int ay = mc / 10, bx = mc % 10;
+        const int P = (2 * ay + py) * 20 + 2 * bx + px;                 // act1 pixel
+        const int row = m < 100 ? 16 * (5 * (ay >> 1) + (bx >> 1)) + 8 * (ay & 1) + 2 * (bx & 1) +
+                                  4 * py + px : G1_TRASH;
+        const int sw = (row >> 1) & 7;
+        const float keep = m < 100 ? 1.f : 0.f;
 #pragma unroll
-        for (int r0 = 0; r0 < 16; r0 += 8) {
-          uint32_t e[8];
-          bf16 mk[8];
+        for (int g = 0; g < 4; ++g) {
+          const bf16x4 mk = *(const bf16x4*)(a1 + P * 32 + 8 * g + 4 * half);
+          bf16x4 vh, vl;
 #pragma unroll
-          for (int r = 0; r < 8; ++r) e[r] = te[r0 + r];
-#pragma unroll
-          for (int r = 0; r < 8; ++r) mk[r] = a1[(e[r] & 0xffff) * 32 + moff];
-#pragma unroll
-          for (int r = 0; r < 8; ++r) {
-            const float v = ((float)mk[r] > 0.f) ? acc[r0 + r] : 0.f;
-            const int o = ((e[r] >> 16) & 0x7fff) * 32 + koff;
-            if (!(a.pad_ & 2)) {
-              g1h[o] = (bf16)v;
-              g1l[o] = sp_lo(v);
-            }
-            db1p += (e[r] >> 31) ? v : 0.f;
+          for (int e = 0; e < 4; ++e) {
+            const float v = (float)mk[e] > 0.f ? accj[jj][4 * g + e] : 0.f;
+            vh[e] = (bf16)v;
+            vl[e] = sp_lo(v);
+            db1v[4 * g + e] = fmaf(v, keep, db1v[4 * g + e]);
           }
+          const int o = row * 32 + (((2 * g + half) ^ sw) << 2);
+          *(bf16x4*)(g1h + o) = vh;
+          *(bf16x4*)(g1l + o) = vl;
         }
       }
     }
@@ -1162,11 +1168,14 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
     {
       constexpr int D = 2;
       bf16x8 rah[D], ral[D], rb[D];
+      // g1 rows 16 s + 8 half + q and + 4: their chunk swizzles ((R >> 1) & 7) do not depend on s
+      const int c4 = colb >> 2;
+      const int g0 = (8 * half + q) * 32 + ((c4 ^ ((4 * half + (q >> 1)) & 7)) << 2);
+      const int g4 = (8 * half + q + 4) * 32 + ((c4 ^ ((4 * half + 2 + (q >> 1)) & 7)) << 2);
       auto ld = [&](int s, bf16x8& xah, bf16x8& xal, bf16x8& xb) {
-        const int r0 = (16 * s + 8 * half + q) * 32 + colb;
         const int blk = (16 * (s / 5)) * 84 + 16 * (s % 5);
-        xah = ts_tr8(g1h + r0, g1h + r0 + 4 * 32);
-        xal = ts_tr8(g1l + r0, g1l + r0 + 4 * 32);
+        xah = ts_tr8(g1h + 512 * s + g0, g1h + 512 * s + g4);
+        xal = ts_tr8(g1l + 512 * s + g0, g1l + 512 * s + g4);
         xb = ts_tr8(fb0 + blk, fb1 + blk);
       };
 #pragma unroll
@@ -1196,14 +1205,27 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
     sl[OFF_W2 + co * 512 + (wave + 8) * 32 + l32] = acc2b[r];
   }
   float* red = (float*)(lds + G1H);
-  red[tid] = db1p;
-  red[512 + tid] = wave >= 5 ? db2p : 0.f;
+  // db1: lane partials of channels 8 (r >> 2) + 4 half + (r & 3), summed over the 32 pixel lanes
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float v = db1v[r];
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, 64);
+    if (l32 == 0) red[wave * 32 + 8 * (r >> 2) + 4 * half + (r & 3)] = v;
+  }
+  red[512 + tid] = wave < 6 ? db2p : 0.f;
   __syncthreads();
   if (tid < 64) {
     const int part = tid >> 5, c = tid & 31;
     float v = 0.f;
+    if (part == 0) {
 #pragma unroll
-    for (int w = 0; w < 8; ++w) v += red[part * 512 + w * 64 + c] + red[part * 512 + w * 64 + 32 + c];
+      for (int w = 0; w < 8; ++w) v += red[w * 32 + c];
+    } else {   // channel c = 16 ch + 4 kg + e at lane 16 kg + 4 ch + e
+      const int ln = 16 * ((c >> 2) & 3) + 4 * (c >> 4) + (c & 3);
+#pragma unroll
+      for (int w = 0; w < 6; ++w) v += red[512 + w * 64 + ln];
+    }
     sl[OFF_B + tid] = v;
   }
 }

@@ -132,7 +132,13 @@ class LearnerConfig:
     # split precision: the dueling head's gradient reduction on the BPTT launch's idle workgroups
     # (r2_lstm_bwd_tag_sp_hg) instead of its own 28 us launch
     sp_head_grads_in_bptt: bool = True
-    torso_bwd: str = "fused"          # fused (HIP kernel) | library (MIOpen convolution_backward)
+    # single-GPU step: the priority refresh + tree repair (they need only the TD's priorities) run
+    # on a side stream beside the BPTT, whose persistent launch leaves most CUs idle; the step
+    # counter follows the optimizer update on the main stream.  Off: the 16 us tail does leave the
+    # critical path, but the two-queue graph pays it back at the graph boundary (same-box A/B
+    # 0.9987 / 0.9984 / 1.0017 vs 0.9995 / 1.0001 / 1.0017 ms, profiles/r03_prio_side_stream_ab.txt)
+    prio_side_stream: bool = False
+    torso_bwd: str = "fused"         # fused (HIP kernel) | library (MIOpen convolution_backward)
     # library conv path (frame geometries without the fused HIP torso, e.g. DMLab): MIOpen find
     # mode (torch.backends.cudnn.benchmark) instead of its immediate-mode heuristics
     conv_autotune: bool = True

@@ -1057,6 +1057,47 @@ class LearnerEngine:
         self._update()
         self._priorities()
 
+    def _single_body(self, timer=None):
+        """The world == 1 step as stream operations (eager or captured).  With
+        ``learner.prio_side_stream`` the priority refresh + tree repair (they read only the TD's
+        priorities and the sampled starts) run on a side stream beside the BPTT, whose persistent
+        launch occupies 64 of the chip's CUs: the main stream records an event after the TD and
+        issues its own launches first (so the graph keeps the critical path on the launch's queue),
+        the side stream waits on that event, its tree tail resets the dirty list, and the step
+        counter is advanced on the main stream after the optimizer / target-sync launches read it.
+        The side stream is joined at the very end (no launch waits on it inside the step)."""
+        import contextlib
+        ph = timer.phase if timer is not None else (lambda name: contextlib.nullcontext())
+        side = self.cfg.learner.prio_side_stream and self.device.type == "cuda"
+        with ph("forward+td"):
+            self._forward_loss()
+        if side:
+            main = torch.cuda.current_stream(self.device)
+            if getattr(self, "_prio_stream", None) is None:
+                self._prio_stream = torch.cuda.Stream(device=self.device)
+                self._prio_event = torch.cuda.Event()
+            ps = self._prio_stream
+            self._prio_event.record(main)
+        with ph("backward_core"):
+            self._backward_core()
+        with ph("backward_torso"):
+            self._seg_torso()
+        with ph("update"):
+            self._update()
+        if side:
+            self.replay.step_inc()
+            ps.wait_event(self._prio_event)
+            with torch.cuda.stream(ps):
+                rp = self.replay
+                rp.refresh_sequences(self.starts, self.B, self.Lb, self.T)
+                if not (self.cfg.replay.fused_tree_tail and rp.update_tree_and_reset_dirty()):
+                    rp.update_tree()
+                    rp.reset_dirty()
+            main.wait_stream(ps)
+        else:
+            with ph("priorities"):
+                self._priorities()
+
     # DP (world > 1): the priority refresh + tree repair need only the forward's TD errors, so
     # they run while the torso bucket is all-reduced; the update and the step counter follow
     def _seg_prio(self):
@@ -1072,27 +1113,24 @@ class LearnerEngine:
         import contextlib
         L = self.layout
         ph = timer.phase if timer is not None else (lambda name: contextlib.nullcontext())
+        if not self.dp:
+            self._single_body(timer)
+            self.steps_done += 1
+            return
         with ph("forward+td"):
             self._forward_loss()      # (DP global sampling: includes the stats all-gather)
         with ph("backward_core"):
             self._backward_core()
-        if self.dp:   # core bucket all-reduce overlaps the conv backward
-            self._sync().start(0, L.torso_offset)
+        self._sync().start(0, L.torso_offset)        # core bucket: overlaps the conv backward
         with ph("backward_torso"):
             self._seg_torso()
-        if self.dp:   # torso bucket all-reduce overlaps the priority tail
-            self._sync().start(L.torso_offset, L.padded)
-            with ph("priorities"):
-                self._seg_prio()
-            with ph("allreduce_wait"):
-                self._sync().finish()
-            with ph("update"):
-                self._seg_update()
-        else:
-            with ph("update"):
-                self._update()
-            with ph("priorities"):
-                self._priorities()
+        self._sync().start(L.torso_offset, L.padded)  # torso bucket: overlaps the priority tail
+        with ph("priorities"):
+            self._seg_prio()
+        with ph("allreduce_wait"):
+            self._sync().finish()
+        with ph("update"):
+            self._seg_update()
         self.steps_done += 1
 
     def capture(self, warmup: int = 2):
@@ -1128,7 +1166,7 @@ class LearnerEngine:
             if self.dp_global:
                 segs = [self._seg_sample, self._seg_fwd_head, self._seg_core_tail] + segs[1:]
         else:
-            segs = [lambda: (self._seg_core(), self._seg_torso(), self._seg_tail())]
+            segs = [self._single_body]
         pool = None
         for fn in segs:
             g = torch.cuda.CUDAGraph()

@@ -172,6 +172,30 @@ class HBMReplay:
         check(rc, "tree_update_fused")
         return True
 
+    def update_tree_and_reset_dirty(self, stream=None) -> bool:
+        """The fused tree repair with the dirty-list reset but NOT the step counter (the priority
+        tail on a side stream; the counter follows on the main stream, ``step_inc``).  False
+        (nothing launched) when the tree shape does not allow the fold."""
+        if self.tree_ticket is None:
+            if self.tree.device.type != "cuda":
+                return False
+            self.tree_ticket = torch.zeros(1, dtype=torch.int32, device=self.tree.device)
+        rc = kernels().r2_tree_update_fused_reset(
+            ptr(self.tree), self.tree_offs.ctypes.data, self.tree_sizes.ctypes.data,
+            self.tree_levels, ptr(self.dirty), ptr(self.dirty_count), self.max_dirty,
+            ptr(self.tree_ticket), self._ts(stream))
+        if rc == -3:
+            return False
+        check(rc, "tree_update_fused_reset")
+        return True
+
+    def reset_dirty(self, stream=None) -> None:
+        check(kernels().r2_step_end(0, ptr(self.dirty_count), self._ts(stream)), "reset_dirty")
+
+    def step_inc(self, stream=None) -> None:
+        """Step counter + 1 only (the dirty list is reset by the side-stream tree tail)."""
+        check(kernels().r2_step_end(ptr(self.step), 0, self._ts(stream)), "step_inc")
+
     def refresh_sequences(self, starts: torch.Tensor, B: int, upd_lo: int, upd_hi: int,
                           stream=None) -> None:
         rc = self.cfg.replay

@@ -59,6 +59,7 @@ _SIGS = {
     "r2_tree_rebuild": [P, P, P, I, P],
     "r2_tree_update": [P, P, P, I, P, P, I, P],
     "r2_tree_update_fused": [P, P, P, I, P, P, I, P, P, P],
+    "r2_tree_update_fused_reset": [P, P, P, I, P, P, I, P, P],
     "r2_seqprio_refresh": [P, I, P, P, P, I, I, I, I, F, P, P, I, P],
     "r2_mark_starts": [P, P, I, P, P, P, I, I, F, P, P, P, I, P],
     "r2_make_rows": [P, I, I, I, I, P, P],

@@ -11,6 +11,9 @@ def main(path_glob, out=None, last=1, marker=('step_end', 'tree_update_tail')):
     rows = list(csv.DictReader(open(paths[0])))
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
     marks = (marker,) if isinstance(marker, str) else marker
+    # the first marker present in the trace ends a step (step_end_kernel when the tree repair
+    # runs on the side stream, the fused tree tail otherwise)
+    marks = [m for m in marks if any(m in r['Kernel_Name'] for r in rows)][:1]
     ends = [i for i, r in enumerate(rows) if any(m in r['Kernel_Name'] for m in marks)]
     a, b = ends[-1 - last] + 1, ends[-1] + 1
     st = rows[a:b]
