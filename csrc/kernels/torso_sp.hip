@@ -900,6 +900,14 @@ __device__ __forceinline__ bf16x8 ts_bl(const __amdgpu_buffer_rsrc_t r, int v, i
   return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, v, s, 0));
 }
 
+// Every [rows][32] bf16 image of the backward (act1, act2, g3, g2) keeps its 16-byte channel chunk
+// c of row r at chunk c ^ ((r >> 2) & 3): 16 lanes on 16 consecutive rows at one chunk (the b128 /
+// b64 reads and stores of the transposed products, the pixel-row gathers) hit 16 distinct bank
+// groups instead of 4 (64-byte rows).  Element offset of (row r, channel e):
+__device__ __forceinline__ int tb_sw(int r, int e) {
+  return r * 32 + ((((e >> 3) ^ (r >> 2)) & 3) << 3) + (e & 7);
+}
+
 __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
   using namespace tbs;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -912,7 +920,7 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
     const int h = l >> 5, qq = (l >> 2) & 3, cb = 16 * ((l >> 4) & 1) + 4 * (l & 3);
     const int P = 16 * sS + 8 * h + 4 * r + qq, Pc = P < P2 ? P : P2 - 1;
     const int arow = P < P2 ? (Pc / 9 + 1) * 11 + Pc % 9 + 1 : 0;
-    ((int2*)(lds + TBL2))[i] = make_int2(arow * 32 + cb, ((2 * (Pc / 9)) * 20 + 2 * (Pc % 9)) * 32 + cb);
+    ((int2*)(lds + TBL2))[i] = make_int2(tb_sw(arow, cb), (2 * (Pc / 9)) * 20 + 2 * (Pc % 9));
   }
   const __amdgpu_buffer_rsrc_t w2rs = ts_rsrc(a.w2dg, 4 * 32 * 128 * 2), w2lrs = ts_rsrc(a.w2dgl, 4 * 32 * 128 * 2);
 
@@ -1002,9 +1010,10 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
 #pragma unroll
     for (int k = 0; k < PF1; ++k) {
       const int c = tid + k * NT;
-      if (c < P1 * 4) { ((u32x4*)a1)[c] = pa1[k]; ((u32x4*)a1lo)[c] = pa1l[k]; }
+      const int cs = (c & ~3) | ((c ^ (c >> 4)) & 3);   // tb_sw at chunk granularity
+      if (c < P1 * 4) { ((u32x4*)a1)[cs] = pa1[k]; ((u32x4*)a1lo)[cs] = pa1l[k]; }
     }
-    if (tid < P2 * 4) ((u32x4*)a2)[tid] = pa2;
+    if (tid < P2 * 4) ((u32x4*)a2)[(tid & ~3) | ((tid ^ (tid >> 4)) & 3)] = pa2;
     if (tid < 196) {
       const bf16x8 dx = __builtin_bit_cast(bf16x8, pdx), dxl = __builtin_bit_cast(bf16x8, pdxl);
       const bf16x8 o3 = __builtin_bit_cast(bf16x8, po3);
@@ -1012,7 +1021,7 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
       for (int e = 0; e < 8; ++e) {
         const int i = tid * 8 + e, co = i / P3, p = i % P3;
         const bool on = (float)o3[e] > 0.f;
-        const int o = ((p / 7 + 2) * 11 + p % 7 + 2) * 32 + co;
+        const int o = tb_sw((p / 7 + 2) * 11 + p % 7 + 2, co);
         g3p[o] = on ? dx[e] : (bf16)0.f;
         g3pl[o] = on ? dxl[e] : (bf16)0.f;
       }
@@ -1028,13 +1037,13 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
     if (wave < 6) {
       const int l16 = lane_f & 15, kg = lane_f >> 4;
       const int qv = wave * 16 + l16, qc = qv < P2 ? qv : P2 - 1;
-      const int gb = ((qc / 9 + 2) * 11 + qc % 9 + 2) * 32 + kg * 8;
+      const int gr = (qc / 9 + 2) * 11 + qc % 9 + 2;
       const bf16* w3h = (const bf16*)(lds + G1H + oz) + l16 * W3S + 8 * kg;
       const bf16* w3l = w3h + W3PL / 2;
       f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        const int o = gb - ((t / 3) * 11 + t % 3) * 32;
+        const int o = tb_sw(gr - ((t / 3) * 11 + t % 3), 8 * kg);
         const bf16x8 bh = ts_ld8(g3p + o), bl = ts_ld8(g3pl + o);
 #pragma unroll
         for (int ch = 0; ch < 2; ++ch)
@@ -1046,7 +1055,7 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
 #pragma unroll
       for (int ch = 0; ch < 2; ++ch) {
         const int c0 = 16 * ch + 4 * kg;
-        const bf16x4 mk = *(const bf16x4*)(a2 + qc * 32 + c0);
+        const bf16x4 mk = *(const bf16x4*)(a2 + tb_sw(qc, c0));
         bf16x4 vh, vl;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1055,8 +1064,8 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
           vl[e] = sp_lo(v);
           db[4 * ch + e] = qv < P2 ? v : 0.f;
         }
-        *(bf16x4*)(g2p + row * 32 + c0) = vh;
-        *(bf16x4*)(g2pl + row * 32 + c0) = vl;
+        *(bf16x4*)(g2p + tb_sw(row, c0)) = vh;
+        *(bf16x4*)(g2pl + tb_sw(row, c0)) = vl;
       }
       // db2: sum over the tile's 16 pixel lanes; lane l16 = i < 8 keeps channel quad value i
 #pragma unroll
@@ -1072,17 +1081,19 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
     // ======== S2: dW2 (tiles wave, wave+8) and dact1 -> g1 (jobs 2w, 2w+1)
     {
       const int nt = wave;
-      const bf16* bh = a1 + ((nt >> 2) * 20 + (nt & 3)) * 32;
-      const bf16* bl = a1lo + ((nt >> 2) * 20 + (nt & 3)) * 32;
+      const int pb = (nt >> 2) * 20 + (nt & 3);   // act1 pixel of this tile's (kh, kw)
+      const int cbl = 16 * ((lane_f >> 4) & 1) + 4 * (lane_f & 3);
       const int2* tl = tbl2 + lane_f;
 #pragma unroll
       for (int s = 0; s < 6; ++s) {
         const int x0 = tl[(2 * s) * 64].x, x1 = tl[(2 * s + 1) * 64].x;
         const int y0 = tl[(2 * s) * 64].y, y1 = tl[(2 * s + 1) * 64].y;
         const bf16x8 ah = ts_tr8(g2p + x0, g2p + x1), al = ts_tr8(g2pl + x0, g2pl + x1);
-        const bf16x8 b0h = ts_tr8(bh + y0, bh + y1), b0l = ts_tr8(bl + y0, bl + y1);
-        const bf16x8 b1h = ts_tr8(bh + 40 * 32 + y0, bh + 40 * 32 + y1);
-        const bf16x8 b1l = ts_tr8(bl + 40 * 32 + y0, bl + 40 * 32 + y1);
+        const int u0 = tb_sw(pb + y0, cbl), u1 = tb_sw(pb + y1, cbl);
+        const int v0 = tb_sw(pb + 40 + y0, cbl), v1 = tb_sw(pb + 40 + y1, cbl);
+        const bf16x8 b0h = ts_tr8(a1 + u0, a1 + u1), b0l = ts_tr8(a1lo + u0, a1lo + u1);
+        const bf16x8 b1h = ts_tr8(a1 + v0, a1 + v1);
+        const bf16x8 b1l = ts_tr8(a1lo + v0, a1lo + v1);
         acc2a = mfma32_x3(ah, al, b0h, b0l, acc2a);
         acc2b = mfma32_x3(ah, al, b1h, b1l, acc2b);
       }
@@ -1103,7 +1114,7 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
       for (int jj = 0; jj < 2; ++jj) {
         const int mt = (wave & 1) * 2 + jj;
         const int m = mt * 32 + l32, mc = m < 100 ? m : 99;
-        ab[jj] = ((mc / 10 + 1) * 11 + mc % 10 + 1) * 32 + half * 8;
+        ab[jj] = (mc / 10 + 1) * 11 + mc % 10 + 1;   // g2 bordered row of tap (0, 0)
       }
       constexpr int D = 3;
       bf16x8 rbh[D], rbl[D];
@@ -1115,10 +1126,12 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
         const bf16x8 bh = rbh[s % D], bl = rbl[s % D];
         if (s + D < 8) { rbh[s % D] = ts_bl(w2rs, vb, (s + D) * 32); rbl[s % D] = ts_bl(w2lrs, vb, (s + D) * 32); }
         const int tap = s >> 1;
-        const int o = -((tap >> 1) * 11 + (tap & 1)) * 32 + (s & 1) * 16;
+        const int dr = (tap >> 1) * 11 + (tap & 1), e0 = (s & 1) * 16 + half * 8;
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-          accj[jj] = mfma32_x3(bh, bl, ts_ld8(g2p + ab[jj] + o), ts_ld8(g2pl + ab[jj] + o), accj[jj]);
+        for (int jj = 0; jj < 2; ++jj) {
+          const int o = tb_sw(ab[jj] - dr, e0);
+          accj[jj] = mfma32_x3(bh, bl, ts_ld8(g2p + o), ts_ld8(g2pl + o), accj[jj]);
+        }
       }
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
@@ -1132,7 +1145,7 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
         const float keep = m < 100 ? 1.f : 0.f;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const bf16x4 mk = *(const bf16x4*)(a1 + P * 32 + 8 * g + 4 * half);
+          const bf16x4 mk = *(const bf16x4*)(a1 + tb_sw(P, 8 * g + 4 * half));
           bf16x4 vh, vl;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
