@@ -1243,17 +1243,23 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
   }
 }
 
-// dW3 += g3 . im2col(act2) and db3 (3 passes), straight from global dX3 / out3 / act2.
-__global__ __launch_bounds__(512) void torso_dw3_sp_kernel(const TBSArgs a) {
+// dW3 += g3 . im2col(act2) and db3 (3 passes), straight from global dX3 / out3 / act2.  Two
+// frames in flight per workgroup (1024 threads: half fs of the workgroup takes frames
+// 2 blockIdx + fs + 2 k gridDim): per frame the work is ~12 MFMAs per wave against a global
+// prefetch, an LDS scatter and two barriers, so a second frame's waves hide the first's waits.
+// The halves' accumulators are summed through LDS before the slab store (slab of blockIdx.x).
+__global__ __launch_bounds__(1024) void torso_dw3_sp_kernel(const TBSArgs a) {
   using namespace tbs;
   constexpr int G3C_S = 72;
-  __shared__ __attribute__((aligned(16))) bf16 g3c[2][32 * G3C_S];
-  __shared__ __attribute__((aligned(16))) bf16 a2[2][P2 * 32];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  __shared__ __attribute__((aligned(16))) bf16 g3c[2][2][32 * G3C_S];
+  __shared__ __attribute__((aligned(16))) bf16 a2s[2][2][P2 * 32];
+  const int fs = threadIdx.x >> 9, tid = threadIdx.x & 511, wave = tid >> 6, lane = tid & 63;
   const int l32 = lane & 31, half = lane >> 5;
   const int grp = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
   const int colb = 16 * (grp & 1) + 4 * pp;
-  for (int i = tid; i < 2 * 32 * G3C_S * 2 / 16; i += NT) ((u32x4*)g3c)[i] = u32x4{0, 0, 0, 0};
+  bf16 (&g3)[2][32 * G3C_S] = g3c[fs];
+  bf16 (&a2)[2][P2 * 32] = a2s[fs];
+  for (int i = threadIdx.x; i < 2 * 2 * 32 * G3C_S * 2 / 16; i += 1024) ((u32x4*)g3c)[i] = u32x4{0, 0, 0, 0};
   f32x16 acc = {}, acc8 = {};
   float db3p = 0.f;
   u32x4 pa2, pa2l, pdx, pdxl, po3;
@@ -1268,7 +1274,9 @@ __global__ __launch_bounds__(512) void torso_dw3_sp_kernel(const TBSArgs a) {
       po3 = ((const u32x4*)(a.out3 + (size_t)f * 1568))[tid];
     }
   };
-  if (blockIdx.x < a.n) prefetch(blockIdx.x);
+  const int fstride = 2 * gridDim.x;
+  int f = 2 * blockIdx.x + fs;
+  if (f < a.n) prefetch(f);
   __syncthreads();
   auto im2col_off3 = [&](int s, int r) {
     int P = 16 * s + 8 * half + 4 * r + q;
@@ -1277,44 +1285,85 @@ __global__ __launch_bounds__(512) void torso_dw3_sp_kernel(const TBSArgs a) {
   };
   const int b0 = ((wave / 3) * 9 + wave % 3) * 32;
   const int b8 = (2 * 9 + 2) * 32;
-  for (int f = blockIdx.x; f < a.n; f += gridDim.x) {
-    if (tid < P2 * 4) { ((u32x4*)a2[0])[tid] = pa2; ((u32x4*)a2[1])[tid] = pa2l; }
-    if (tid < 196) {
-      const bf16x8 dx = __builtin_bit_cast(bf16x8, pdx), dxl = __builtin_bit_cast(bf16x8, pdxl);
-      const bf16x8 o3 = __builtin_bit_cast(bf16x8, po3);
+  // both halves run the same number of iterations (barriers); a half past the end idles
+  const int iters = (a.n - 2 * (int)blockIdx.x + fstride - 1) / fstride;
+  for (int it = 0; it < iters; ++it, f += fstride) {
+    const bool have = f < a.n;
+    if (have) {
+      if (tid < P2 * 4) { ((u32x4*)a2[0])[tid] = pa2; ((u32x4*)a2[1])[tid] = pa2l; }
+      if (tid < 196) {
+        const bf16x8 dx = __builtin_bit_cast(bf16x8, pdx), dxl = __builtin_bit_cast(bf16x8, pdxl);
+        const bf16x8 o3 = __builtin_bit_cast(bf16x8, po3);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int i = tid * 8 + e, co = i / P3, p = i % P3;
-        const bool on = (float)o3[e] > 0.f;
-        g3c[0][co * G3C_S + p] = on ? dx[e] : (bf16)0.f;
-        g3c[1][co * G3C_S + p] = on ? dxl[e] : (bf16)0.f;
+        for (int e = 0; e < 8; ++e) {
+          const int i = tid * 8 + e, co = i / P3, p = i % P3;
+          const bool on = (float)o3[e] > 0.f;
+          g3[0][co * G3C_S + p] = on ? dx[e] : (bf16)0.f;
+          g3[1][co * G3C_S + p] = on ? dxl[e] : (bf16)0.f;
+        }
       }
+      if (f + fstride < a.n) prefetch(f + fstride);
     }
-    if (f + (int)gridDim.x < a.n) prefetch(f + gridDim.x);
     lds_sync();
+    if (have) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int ao = l32 * G3C_S + s * 16 + half * 8;
-      const bf16x8 ah = ts_ld8(g3c[0] + ao), al = ts_ld8(g3c[1] + ao);
-      const int o0 = im2col_off3(s, 0), o1 = im2col_off3(s, 1);
-      acc = mfma32_x3(ah, al, ts_tr8(a2[0] + b0 + o0, a2[0] + b0 + o1), ts_tr8(a2[1] + b0 + o0, a2[1] + b0 + o1), acc);
-      if (wave == 0)
-        acc8 = mfma32_x3(ah, al, ts_tr8(a2[0] + b8 + o0, a2[0] + b8 + o1), ts_tr8(a2[1] + b8 + o0, a2[1] + b8 + o1), acc8);
-    }
-    if (wave == 7) {
-      float sum = 0.f;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const bf16x8 v = ts_ld8(g3c[0] + l32 * G3C_S + half * 32 + c * 8);
-        const bf16x8 vl = ts_ld8(g3c[1] + l32 * G3C_S + half * 32 + c * 8);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) sum += (float)v[e] + (float)vl[e];
+      for (int s = 0; s < 4; ++s) {
+        const int ao = l32 * G3C_S + s * 16 + half * 8;
+        const bf16x8 ah = ts_ld8(g3[0] + ao), al = ts_ld8(g3[1] + ao);
+        const int o0 = im2col_off3(s, 0), o1 = im2col_off3(s, 1);
+        acc = mfma32_x3(ah, al, ts_tr8(a2[0] + b0 + o0, a2[0] + b0 + o1), ts_tr8(a2[1] + b0 + o0, a2[1] + b0 + o1), acc);
+        if (wave == 0)
+          acc8 = mfma32_x3(ah, al, ts_tr8(a2[0] + b8 + o0, a2[0] + b8 + o1), ts_tr8(a2[1] + b8 + o0, a2[1] + b8 + o1), acc8);
       }
-      sum += __shfl_xor(sum, 32, 64);
-      db3p += sum;
+      if (wave == 7) {
+        float sum = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const bf16x8 v = ts_ld8(g3[0] + l32 * G3C_S + half * 32 + c * 8);
+          const bf16x8 vl = ts_ld8(g3[1] + l32 * G3C_S + half * 32 + c * 8);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) sum += (float)v[e] + (float)vl[e];
+        }
+        sum += __shfl_xor(sum, 32, 64);
+        db3p += sum;
+      }
     }
     lds_sync();
   }
+  // half 1's accumulators -> LDS (the g3 images are dead: 18 KB), half 0 adds them; every
+  // thread takes every barrier
+  float* xa = (float*)g3c;
+#pragma unroll
+  for (int pass = 0; pass < 3; ++pass) {
+    // pass 0 / 1: acc rows 8 pass .. +7 of the 8 waves (16 KB); pass 2: wave 0's acc8 + db3
+    if (fs == 1) {
+      if (pass < 2) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) xa[(wave * 8 + r) * 64 + lane] = acc[pass * 8 + r];
+      } else {
+        if (wave == 0) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) xa[r * 64 + lane] = acc8[r];
+        }
+        if (wave == 7) xa[16 * 64 + lane] = db3p;
+      }
+    }
+    __syncthreads();
+    if (fs == 0) {
+      if (pass < 2) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) acc[pass * 8 + r] += xa[(wave * 8 + r) * 64 + lane];
+      } else {
+        if (wave == 0) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc8[r] += xa[r * 64 + lane];
+        }
+        if (wave == 7) db3p += xa[16 * 64 + lane];
+      }
+    }
+    __syncthreads();
+  }
+  if (fs == 1) return;
   float* sl = a.slab + (size_t)blockIdx.x * SLAB;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -1356,7 +1405,7 @@ extern "C" int r2_torso_bwd_sp(const uint8_t* frames, const int* rows, int n, co
             slab, n, g_tbs_dbg, g_tbs_trace};
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(torso_bwd_sp_kernel, dim3(grid), dim3(tbs::NT), tbs::LDS, s, a);
-  hipLaunchKernelGGL(torso_dw3_sp_kernel, dim3(grid), dim3(tbs::NT), 0, s, a);
+  hipLaunchKernelGGL(torso_dw3_sp_kernel, dim3(grid), dim3(1024), 0, s, a);
   R2_CHECK_LAUNCH();
   return r2_torso_grad_reduce(slab, grid, dst, scale, grad, stream);
 }
