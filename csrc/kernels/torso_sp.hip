@@ -21,7 +21,7 @@
 //   * outputs: torso features (PyTorch CHW flatten) as hi / lo planes (the x-projection GEMM's A
 //     operand), optional channels-last act1 / act2 hi / lo planes for the backward.
 //
-// Backward (torso_bwd_sp_kernel / torso_dw3_sp_kernel, LDS 146.6 KB): see the comment there.
+// Backward (torso_bwd_sp_kernel / torso_dw3_sp_kernel, LDS 145.7 KB): see the comment there.
 #include "../common.h"
 #include "../split.h"
 
@@ -836,13 +836,16 @@ extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs,
 }
 
 // ============================================================================================
-// Backward, fp32-accurate.  Per learning frame, in LDS (146.6 KB), the stages of torso_bwd.hip
+// Backward, fp32-accurate.  Per learning frame, in LDS (145.7 KB), the stages of torso_bwd.hip
 // with hi / lo images:
 //   S0  act1 hi / lo + act2 hi (mask) -> region R; g3 = dX3 * (out3 > 0) hi / lo (bordered HWC);
-//       the frame's uint8 bytes start loading into registers
-//   S1  g2 = convT(g3, W3) * (act2 > 0)   (waves 5-7; W3 hi / lo fragments from L2; 3 passes)
+//       W3 hi / lo -> the g1 region by LDS-DMA (g1 is not live until S2)
+//   S1  g2 = convT(g3, W3) * (act2 > 0)   (waves 0-5, one 16-pixel tile each, 16x16x32 MFMAs;
+//       transposed product: lane = pixel, 8-byte channel-quad stores; 3 passes)
 //   S2  dW2 += g2 . im2col(act1)          (3 passes; both operands by transposed reads)
-//       g1 = convT_s2(g2, W2) * (act1 > 0) (4 output phases; W2 phase slices from L2)
+//       g1 = convT_s2(g2, W2) * (act1 > 0) (4 output phases; W2 phase slices from L2; transposed
+//       product, g1 rows with an 8-byte chunk swizzle that S3's transposed reads undo)
+//   Every [rows][32] image (act1, act2, g3, g2) keeps a 16-byte chunk XOR swizzle (tb_sw).
 //   S2b the frame -> region R as exact bf16 (act1 / act2 are dead by now: R is shared)
 //   S3  dW1 += g1 . im2col(frame)         (2 passes: the frame is exact in bf16)
 // dW3 / db3: torso_dw3_sp_kernel.  Slabs and their reduction are shared with the bf16 path.
