@@ -974,9 +974,9 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
   __syncthreads();
 
   int it_dbg = 0;
-  long long* tr = (a.trace && blockIdx.x == 0 && lane == 0) ? a.trace + wave * 16 * 7 : nullptr;
+  long long* tr = (a.trace && blockIdx.x == 0 && lane == 0) ? a.trace + wave * 16 * 9 : nullptr;
 #define TBS_STAMP(k) \
-  if (tr && it_dbg < 16) tr[it_dbg * 7 + (k)] = (long long)__builtin_readcyclecounter();
+  if (tr && it_dbg < 16) tr[it_dbg * 9 + (k)] = (long long)__builtin_readcyclecounter();
   for (int f = blockIdx.x; f < a.n; f += gridDim.x) {
     TBS_STAMP(0);
     int oz;
@@ -1136,6 +1136,7 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
           accj[jj] = mfma32_x3(bh, bl, ts_ld8(g2p + o), ts_ld8(g2pl + o), accj[jj]);
         }
       }
+      TBS_STAMP(7);
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
         const int mt = (wave & 1) * 2 + jj;
@@ -1164,6 +1165,7 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
       }
     }
     if (f + (int)gridDim.x < a.n) prefetch_acts(f + gridDim.x);
+    TBS_STAMP(8);
     lds_sync();
     TBS_STAMP(3);
 
@@ -1383,8 +1385,8 @@ extern "C" int r2_torso_grad_reduce(const float* slab, int grid, const int* dst,
 static long long* g_tbs_trace = nullptr;
 static int g_tbs_dbg = 0;   // timing probes: bit 0 W2 fragments not re-fetched, bit 1 no g1 stores
 extern "C" int r2_torso_bwd_sp_debug(int bits) { g_tbs_dbg = bits; return 0; }
-// stage clock stamps of workgroup 0: [wave][frame < 16][7] (loop top, after S0, S1, S2, S2b, S3,
-// S2 dW2 part done)
+// stage clock stamps of workgroup 0: [wave][frame < 16][9] (loop top, after S0, S1, S2, S2b, S3,
+// S2 dW2 part done, S2 dact1 MFMA loop done, S2 epilogue + prefetch issued)
 extern "C" int r2_torso_bwd_sp_trace(long long* p) { g_tbs_trace = p; return 0; }
 
 // Split-precision torso backward: every activation / gradient operand as hi / lo planes (out3:

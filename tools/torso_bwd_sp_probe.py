@@ -46,12 +46,12 @@ for _ in range(10):
 e1.record()
 torch.cuda.synchronize()
 res["bwd_sp_us"] = e0.elapsed_time(e1) / 10 * 1e3
-tr = torch.zeros(8 * 16 * 7, dtype=torch.int64, device=DEV)
+tr = torch.zeros(8 * 16 * 9, dtype=torch.int64, device=DEV)
 k.r2_torso_bwd_sp_trace(ptr(tr))
 run()
 torch.cuda.synchronize()
 k.r2_torso_bwd_sp_trace(0)
-t = tr.view(8, 16, 7).cpu()
+t = tr.view(8, 16, 9).cpu()
 stages = []
 for fi in range(1, 8):
     row = [int(t[:, fi, j + 1].max() - t[:, fi, j].max()) for j in range(5)]
@@ -62,6 +62,11 @@ res["median"] = [int(np.median([r[j] for r in stages])) for j in range(6)]
 # S2 split: dW2 part per wave (from the S1 barrier to the wave's stamp 6), dact1 part
 res["S2_dW2_cycles_per_wave"] = [int(t[w, 3, 6] - t[:, 3, 2].max()) for w in range(8)]
 res["S2_dact1_cycles_per_wave"] = [int(t[w, 3, 3] - t[w, 3, 6]) for w in range(8)]
+# dact1 split per wave: K loop (stamp 6 -> 7), epilogue + next-frame prefetch issue (7 -> 8),
+# barrier wait (8 -> 3)
+res["S2_dact1_kloop_epi_barrier_per_wave"] = [[int(t[w, 3, 7] - t[w, 3, 6]), int(t[w, 3, 8] - t[w, 3, 7]),
+                                               int(t[w, 3, 3] - t[w, 3, 8])] for w in range(8)]
+# S1 per wave (barrier after S0 -> this wave's stamp... S1 ends with the barrier: whole stage)
 for bits in (1, 2, 3):
     k.r2_torso_bwd_sp_debug(bits)
     run()
