@@ -864,8 +864,11 @@ constexpr int G2P = G3PL + 121 * 32 * 2;                  // g2 hi, lo: [122][32
 constexpr int G2PL = G2P + 122 * 32 * 2;
 constexpr int G1H = G2PL + 122 * 32 * 2;                  // g1 hi, lo: [406][32] each
 constexpr int G1L = G1H + 406 * 32 * 2;
-constexpr int TBL2 = G1L + 406 * 32 * 2;                  // dW2 gather offsets int2 [12][64]
-constexpr int LDS = TBL2 + 12 * 64 * 8;                   // 145664
+// S2: all four W2 phase slices hi / lo (2 planes x 4 x 32 x 128 bf16 = 64 KB) staged by LDS-DMA
+// from G1H (g1 is not written until the dact1 epilogue); the gather table sits above them
+constexpr int W2ST = G1H, W2PL = 4 * 32 * 128 * 2;        // 32 KB per plane
+constexpr int TBL2 = W2ST + 2 * W2PL;                     // dW2 gather offsets int2 [12][64]
+constexpr int LDS = TBL2 + 12 * 64 * 8;                   // 159232
 // S0 / S1: W3 hi / lo staged in the g1 region (free until S2), rows of W3S bf16
 constexpr int W3S = 296, W3PL = 19 * 1024;                // 32 x 592 B per plane, padded to 19 KB
 constexpr int G2_TRASH = 121, G1_TRASH = 400;
@@ -874,7 +877,7 @@ constexpr int PFF = (IN_CHUNKS + NT - 1) / NT;            // frame chunks per th
 constexpr int SLAB = 32 * 256 + 32 * 512 + 32 * 288 + 96;
 constexpr int OFF_W2 = 32 * 256, OFF_W3 = OFF_W2 + 32 * 512, OFF_B = OFF_W3 + 32 * 288;
 static_assert(R_A2 + P2 * 32 * 2 <= R_BYTES, "R");
-static_assert(LDS <= 160 * 1024, "LDS");
+static_assert(LDS <= 160 * 1024 && G1L + 406 * 32 * 2 <= TBL2, "LDS");
 }  // namespace tbs
 
 struct TBSArgs {
@@ -925,7 +928,6 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
     const int arow = P < P2 ? (Pc / 9 + 1) * 11 + Pc % 9 + 1 : 0;
     ((int2*)(lds + TBL2))[i] = make_int2(tb_sw(arow, cb), (2 * (Pc / 9)) * 20 + 2 * (Pc % 9));
   }
-  const __amdgpu_buffer_rsrc_t w2rs = ts_rsrc(a.w2dg, 4 * 32 * 128 * 2), w2lrs = ts_rsrc(a.w2dgl, 4 * 32 * 128 * 2);
 
   f32x16 acc1 = {}, acc2a = {}, acc2b = {};
   float db1v[16] = {};   // db1 partials: this lane's channel quads (dact1 epilogue layout)
@@ -1080,6 +1082,17 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
     }
     lds_sync();
     TBS_STAMP(2);
+    // W2 slices -> LDS (64 wave-instructions of 1 KB, 8 per wave); landed + visible before the
+    // dact1 K loop (the dW2 products below run meanwhile).  Chunk j of a plane: phase j / 512,
+    // row (j / 16) % 32, 16-byte column (j % 16) ^ (row & 15): the K loop's 32 rows x one column
+    // per read hit 16 distinct bank groups
+    for (int i = wave; i < 64; i += 8) {
+      const int pl = i >> 5, j = (i & 31) * 64 + lane;
+      const int ph = j >> 9, r = (j >> 4) & 31, c = (j & 15) ^ (r & 15);
+      const bf16* src = (pl ? a.w2dgl : a.w2dg) + (ph * 32 + r) * 128 + c * 8;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(lds + W2ST + pl * W2PL + (i & 31) * 1024),
+                                       16, 0, 0);
+    }
 
     // ======== S2: dW2 (tiles wave, wave+8) and dact1 -> g1 (jobs 2w, 2w+1)
     {
@@ -1111,7 +1124,6 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
       // lane with the pixel-row layout: ~16k cycles per frame against 1.5k of MFMA).  g1 rows keep
       // S3's 4x4-block order; the 8-byte channel chunk c of row R sits at c ^ ((R >> 1) & 7).
       const int phase = wave >> 1, py = phase >> 1, px = phase & 1;
-      const int vb = ((phase * 32 + l32) * 128 + half * 8) * 2;
       int ab[2];
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
@@ -1119,15 +1131,15 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
         const int m = mt * 32 + l32, mc = m < 100 ? m : 99;
         ab[jj] = (mc / 10 + 1) * 11 + mc % 10 + 1;   // g2 bordered row of tap (0, 0)
       }
-      constexpr int D = 3;
-      bf16x8 rbh[D], rbl[D];
-#pragma unroll
-      for (int s = 0; s < D; ++s) { rbh[s] = ts_bl(w2rs, vb, s * 32); rbl[s] = ts_bl(w2lrs, vb, s * 32); }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's W2 DMAs landed
+      __syncthreads();                                     // ... and every other wave's
+      const bf16* w2row = (const bf16*)(lds + W2ST + oz) + (phase * 32 + l32) * 128;
+      const int wsw = l32 & 15;
       f32x16 accj[2] = {{}, {}};
 #pragma unroll
       for (int s = 0; s < 8; ++s) {
-        const bf16x8 bh = rbh[s % D], bl = rbl[s % D];
-        if (s + D < 8) { rbh[s % D] = ts_bl(w2rs, vb, (s + D) * 32); rbl[s % D] = ts_bl(w2lrs, vb, (s + D) * 32); }
+        const int wo = (((2 * s + half) ^ wsw) << 3);
+        const bf16x8 bh = ts_ld8(w2row + wo), bl = ts_ld8(w2row + W2PL / 2 + wo);
         const int tap = s >> 1;
         const int dr = (tap >> 1) * 11 + (tap & 1), e0 = (s & 1) * 16 + half * 8;
 #pragma unroll
@@ -1136,6 +1148,7 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
           accj[jj] = mfma32_x3(bh, bl, ts_ld8(g2p + o), ts_ld8(g2pl + o), accj[jj]);
         }
       }
+      lds_sync();   // every wave's W2 reads done before g1 (same region) is written
       TBS_STAMP(7);
 #pragma unroll
       for (int jj = 0; jj < 2; ++jj) {
