@@ -753,7 +753,8 @@ class LearnerEngine:
                      c_lo=self.dX_lo)
         if self.cfg.learner.sp_gemm == "fused":
             splits = [int(v) for v in self.cfg.learner.sp_group_splits.replace(":", ",").split(",")]
-            self._gemm_sp("group", [w_jobs[2], w_jobs[1], w_jobs[0], x_job], splits)
+            self._gemm_sp("group", [w_jobs[2], w_jobs[1], w_jobs[0], x_job], splits,
+                          cfg=int(self.cfg.learner.sp_group_cfg))
             self._dX = self.dX
             return
         splits = self._group_splits(w_jobs, x_job)
@@ -764,7 +765,7 @@ class LearnerEngine:
             gemm(x_job)
         self._dX = self.dX
 
-    def _gemm_sp(self, site: str, probs, splits=None):
+    def _gemm_sp(self, site: str, probs, splits=None, cfg: int = -1):
         """Split-precision GEMMs of one call site: the fused one-pass kernel (gemm_sp.hip) with a
         per-site split-K workspace sized before capture, or the multi-pass kernels
         (``learner.sp_gemm``)."""
@@ -780,7 +781,7 @@ class LearnerEngine:
             cur = (torch.zeros(max(need // 4, 1), dtype=torch.float32, device=self.device),
                    torch.zeros(4096, dtype=torch.int32, device=self.device))
             self._sp_ws[site] = cur
-        gemm_sp(probs, splits=splits, ws=cur[0], tickets=cur[1], n_cus=self.n_cus)
+        gemm_sp(probs, splits=splits, cfg=cfg, ws=cur[0], tickets=cur[1], n_cus=self.n_cus)
 
     def _backward_core(self):
         """Head backward, BPTT, LSTM/head weight gradients -> grad bucket 'core'."""
