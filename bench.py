@@ -92,6 +92,13 @@ def main(argv=None):
     if shared:
         local = local % torch.cuda.device_count()
     use_pg = world > 1 or args.force_dp
+    if use_pg and "RANK" not in os.environ:   # --force-dp without a launcher: a one-rank group
+        import socket
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        os.environ.update({"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0",
+                           "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     if use_pg:
         torch.cuda.set_device(local)
         if shared:
