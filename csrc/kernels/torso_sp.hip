@@ -910,6 +910,16 @@ __device__ __forceinline__ bf16x8 ts_bl(const __amdgpu_buffer_rsrc_t r, int v, i
 // c of row r at chunk c ^ ((r >> 2) & 3): 16 lanes on 16 consecutive rows at one chunk (the b128 /
 // b64 reads and stores of the transposed products, the pixel-row gathers) hit 16 distinct bank
 // groups instead of 4 (64-byte rows).  Element offset of (row r, channel e):
+// sum over each 16-lane row on DPP (VALU; __shfl_xor goes through ds_bpermute at LDS latency):
+// rotate by 8 and 4 within the row, then the two quad swaps -- every lane holds its row's sum
+__device__ __forceinline__ float tb_rowsum16(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4e, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xb1, 0xf, 0xf, false));
+  return v;
+}
+
 __device__ __forceinline__ int tb_sw(int r, int e) {
   return r * 32 + ((((e >> 3) ^ (r >> 2)) & 3) << 3) + (e & 7);
 }
@@ -976,9 +986,9 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
   __syncthreads();
 
   int it_dbg = 0;
-  long long* tr = (a.trace && blockIdx.x == 0 && lane == 0) ? a.trace + wave * 16 * 9 : nullptr;
+  long long* tr = (a.trace && blockIdx.x == 0 && lane == 0) ? a.trace + wave * 16 * 11 : nullptr;
 #define TBS_STAMP(k) \
-  if (tr && it_dbg < 16) tr[it_dbg * 9 + (k)] = (long long)__builtin_readcyclecounter();
+  if (tr && it_dbg < 16) tr[it_dbg * 11 + (k)] = (long long)__builtin_readcyclecounter();
   for (int f = blockIdx.x; f < a.n; f += gridDim.x) {
     TBS_STAMP(0);
     int oz;
@@ -1055,6 +1065,7 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
           acc[ch] = mfma16_x3(ts_ld8(w3h + ch * 16 * W3S + 32 * t), ts_ld8(w3l + ch * 16 * W3S + 32 * t),
                               bh, bl, acc[ch]);
       }
+      TBS_STAMP(9);
       const int row = qv < P2 ? (qc / 9 + 1) * 11 + qc % 9 + 1 : G2_TRASH;
       float db[8];
 #pragma unroll
@@ -1073,13 +1084,13 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
         *(bf16x4*)(g2pl + tb_sw(row, c0)) = vl;
       }
       // db2: sum over the tile's 16 pixel lanes; lane l16 = i < 8 keeps channel quad value i
+      // row sums with every lane active (DPP reads of EXEC-masked lanes return 0), then the select
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < 8; ++i) db[i] = tb_rowsum16(db[i]);
 #pragma unroll
-        for (int o2 = 1; o2 < 16; o2 <<= 1) db[i] += __shfl_xor(db[i], o2, 64);
-        db2p += l16 == i ? db[i] : 0.f;
-      }
+      for (int i = 0; i < 8; ++i) db2p += l16 == i ? db[i] : 0.f;
     }
+    TBS_STAMP(10);
     lds_sync();
     TBS_STAMP(2);
     // W2 slices -> LDS (64 wave-instructions of 1 KB, 8 per wave); landed + visible before the
@@ -1131,6 +1142,16 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
         const int m = mt * 32 + l32, mc = m < 100 ? m : 99;
         ab[jj] = (mc / 10 + 1) * 11 + mc % 10 + 1;   // g2 bordered row of tap (0, 0)
       }
+      // the epilogue's act1 mask rows (act1 stays put until S2b), read ahead of the K loop so
+      // their latency is not exposed one quad at a time after it
+      bf16x4 mk[2][4];
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        const int m = ((wave & 1) * 2 + jj) * 32 + l32, mc = m < 100 ? m : 99;
+        const int P = (2 * (mc / 10) + py) * 20 + 2 * (mc % 10) + px;   // act1 pixel
+#pragma unroll
+        for (int g = 0; g < 4; ++g) mk[jj][g] = *(const bf16x4*)(a1 + tb_sw(P, 8 * g + 4 * half));
+      }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's W2 DMAs landed
       __syncthreads();                                     // ... and every other wave's
       const bf16* w2row = (const bf16*)(lds + W2ST + oz) + (phase * 32 + l32) * 128;
@@ -1155,18 +1176,16 @@ __global__ __launch_bounds__(512) void torso_bwd_sp_kernel(const TBSArgs a) {
         const int mt = (wave & 1) * 2 + jj;
         const int m = mt * 32 + l32, mc = m < 100 ? m : 99;
         const int ay = mc / 10, bx = mc % 10;
-        const int P = (2 * ay + py) * 20 + 2 * bx + px;                 // act1 pixel
         const int row = m < 100 ? 16 * (5 * (ay >> 1) + (bx >> 1)) + 8 * (ay & 1) + 2 * (bx & 1) +
                                   4 * py + px : G1_TRASH;
         const int sw = (row >> 1) & 7;
         const float keep = m < 100 ? 1.f : 0.f;
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const bf16x4 mk = *(const bf16x4*)(a1 + tb_sw(P, 8 * g + 4 * half));
           bf16x4 vh, vl;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const float v = (float)mk[e] > 0.f ? accj[jj][4 * g + e] : 0.f;
+            const float v = (float)mk[jj][g][e] > 0.f ? accj[jj][4 * g + e] : 0.f;
             vh[e] = (bf16)v;
             vl[e] = sp_lo(v);
             db1v[4 * g + e] = fmaf(v, keep, db1v[4 * g + e]);
@@ -1398,8 +1417,9 @@ extern "C" int r2_torso_grad_reduce(const float* slab, int grid, const int* dst,
 static long long* g_tbs_trace = nullptr;
 static int g_tbs_dbg = 0;   // timing probes: bit 0 W2 fragments not re-fetched, bit 1 no g1 stores
 extern "C" int r2_torso_bwd_sp_debug(int bits) { g_tbs_dbg = bits; return 0; }
-// stage clock stamps of workgroup 0: [wave][frame < 16][9] (loop top, after S0, S1, S2, S2b, S3,
-// S2 dW2 part done, S2 dact1 MFMA loop done, S2 epilogue + prefetch issued)
+// stage clock stamps of workgroup 0: [wave][frame < 16][11] (loop top, after S0, S1, S2, S2b, S3,
+// S2 dW2 part done, S2 dact1 MFMA loop done, S2 epilogue + prefetch issued, S1 tap loop done,
+// S1 epilogue done)
 extern "C" int r2_torso_bwd_sp_trace(long long* p) { g_tbs_trace = p; return 0; }
 
 // Split-precision torso backward: every activation / gradient operand as hi / lo planes (out3:

@@ -46,12 +46,12 @@ for _ in range(10):
 e1.record()
 torch.cuda.synchronize()
 res["bwd_sp_us"] = e0.elapsed_time(e1) / 10 * 1e3
-tr = torch.zeros(8 * 16 * 9, dtype=torch.int64, device=DEV)
+tr = torch.zeros(8 * 16 * 11, dtype=torch.int64, device=DEV)
 k.r2_torso_bwd_sp_trace(ptr(tr))
 run()
 torch.cuda.synchronize()
 k.r2_torso_bwd_sp_trace(0)
-t = tr.view(8, 16, 9).cpu()
+t = tr.view(8, 16, 11).cpu()
 stages = []
 for fi in range(1, 8):
     row = [int(t[:, fi, j + 1].max() - t[:, fi, j].max()) for j in range(5)]
@@ -66,7 +66,9 @@ res["S2_dact1_cycles_per_wave"] = [int(t[w, 3, 3] - t[w, 3, 6]) for w in range(8
 # barrier wait (8 -> 3)
 res["S2_dact1_kloop_epi_barrier_per_wave"] = [[int(t[w, 3, 7] - t[w, 3, 6]), int(t[w, 3, 8] - t[w, 3, 7]),
                                                int(t[w, 3, 3] - t[w, 3, 8])] for w in range(8)]
-# S1 per wave (barrier after S0 -> this wave's stamp... S1 ends with the barrier: whole stage)
+# S1 per wave (waves 0-5): tap loop (stamp 1 -> 9), epilogue + db2 reduction (9 -> 10), barrier (10 -> 2)
+res["S1_loop_epi_barrier_per_wave"] = [[int(t[w, 3, 9] - t[w, 3, 1]), int(t[w, 3, 10] - t[w, 3, 9]),
+                                        int(t[w, 3, 2] - t[w, 3, 10])] for w in range(6)]
 for bits in (1, 2, 3):
     k.r2_torso_bwd_sp_debug(bits)
     run()
