@@ -126,6 +126,7 @@ class LearnerConfig:
     sp_gemm: str = "fused"
     sp_group_splits: str = "4,4,4,1"  # K splits of the fused post-BPTT group (dW_ih, dW_hh, dW_head1, dX)
     sp_group_cfg: int = -1            # its tile (ops/gemm.py G5_CFGS index); -1 = the CU-round model
+    sp_heads_cfg: int = -1            # tile of the heads' layer-1 split GEMM (same convention)
     # split GEMMs on gemm6 (gemm_sp.hip: the fragment planes refilled between the three product
     # passes, one barrier per LDS tile; the heads' layer-1 GEMMs join the one-pass kernel too):
     # x-projection 115-129 -> 102-110 us, tools/gemm6_probe.py
