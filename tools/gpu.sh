@@ -8,6 +8,7 @@
 #   tools/gpu.sh ab KEY=V[,KEY=V] ...           bench.py under override sets (same box A/B)
 #   tools/gpu.sh prof TAG [bench args...]       rocprofv3 kernel trace + step breakdown
 #   tools/gpu.sh pmc TAG [filters...]           PMC passes over the bench step (kernel trace only)
+#   tools/gpu.sh bytes TAG [bench args...]      FETCH_SIZE / WRITE_SIZE passes (roofline bytes)
 #   tools/gpu.sh learn [learn_check args...]    tools/learn_check.py
 #   tools/gpu.sh native [bench_native args...]  actor + learner loop (serial / concurrent)
 #   tools/gpu.sh cfg2 [N] [steps]               main.py --cpu-actors N with an injected actor crash
@@ -72,6 +73,21 @@ case "$cmd" in
     python tools/pmc_summary.py "gpurun_out/pmc_$tag/p*/**/*counter_collection.csv" "${filters[@]}" \
       > gpurun_out/pmc_$tag/summary.txt
     head -60 gpurun_out/pmc_$tag/summary.txt ;;
+  bytes)
+    # HBM-side byte counters per kernel (roofline input): FETCH_SIZE (3 TCC slots) and WRITE_SIZE
+    # (2) in passes of their own, MFMA busy cycles beside them
+    tag=$1; shift
+    mkdir -p gpurun_out/bytes_$tag
+    i=0
+    for grp in "FETCH_SIZE SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES" \
+               "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"; do
+      i=$((i+1))
+      timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d gpurun_out/bytes_$tag/p$i -- \
+        python bench.py --steps 3 --warmup 2 "$@" > gpurun_out/bytes_$tag/p$i.log 2>&1 || fail "bytes pass $i" gpurun_out/bytes_$tag/p$i.log
+    done
+    python tools/pmc_summary.py "gpurun_out/bytes_$tag/p*/**/*counter_collection.csv" \
+      > gpurun_out/bytes_$tag/summary.txt
+    head -40 gpurun_out/bytes_$tag/summary.txt ;;
   learn)
     timeout -k 10 300 python -u tools/learn_check.py "$@" > gpurun_out/learn.log 2>&1 || fail learn gpurun_out/learn.log
     grep -h '^{' gpurun_out/learn.log ;;
