@@ -48,7 +48,13 @@ struct IngestArgs {
   int max_dirty;
   int FB, H2, cap_e;
   int rows_per_sub;         // > 0: rows i*rps .. (i+1)*rps - 1 go to sub-ring sub + i (an actor
-                            // rank's E env windows in one record); 0: every row to sub-ring sub
+                            // rank's E env blocks in one record); 0: every row to sub-ring sub
+  int start_lag;            // rows_per_sub > 0: the start flag / sequence priority of record row j
+                            // belong to sub-ring position head + j - start_lag (a start becomes
+                            // sampleable with the last row of its window, which arrives start_lag
+                            // rows after it); 0: to the row itself
+  int n_sub;                // sub-rings of the replay (a record addressing more is rejected)
+  int pad_;
 };
 
 struct RecView {
@@ -87,6 +93,10 @@ __device__ bool parse_record(const IngestArgs& a, RecView& v) {
   if (v.code[1] != 2 || v.per_row[1] != a.H2 || v.code[2] != 2 || v.per_row[2] != a.H2) return false;
   if (v.code[4] != 2 || v.code[7] != 2 || v.code[8] != 2) return false;
   if (v.code[3] == 2 || v.code[9] == 2) return false;
+  // env-major blocks: whole blocks only, every addressed sub-ring inside the replay
+  if (a.rows_per_sub > 0 &&
+      (v.n % a.rows_per_sub != 0 || a.sub + v.n / a.rows_per_sub > a.n_sub)) return false;
+  if (a.rows_per_sub <= 0 && a.sub >= a.n_sub) return false;
   return true;
 }
 
@@ -104,14 +114,22 @@ __global__ __launch_bounds__(256) void ingest_rows_kernel(const IngestArgs a) {
     if (blockIdx.x == 0 && tid == 0) atomicOr(a.err, 1u);
     return;
   }
-  long long src, row;
-  if (a.rows_per_sub > 0) {   // env-major windows: one per sub-ring, rows_per_sub <= cap_e
+  long long src, row, srow = -1;   // srow: the row whose start flag this block writes
+  bool clear_own = true;
+  if (a.rows_per_sub > 0) {   // env-major blocks: one per sub-ring, rows_per_sub <= cap_e
     const long long i = blockIdx.x;
     if (i >= v.n) return;
     const int sub = a.sub + (int)(i / a.rows_per_sub);
     const long long j = i % a.rows_per_sub;
     src = i;
-    row = (long long)sub * a.cap_e + (a.ihead[sub] + j) % a.cap_e;
+    const long long base = (long long)sub * a.cap_e;
+    row = base + (a.ihead[sub] + j) % a.cap_e;
+    if (a.start_lag > 0) {
+      // the record's start column is lagged: it marks position head + j - lag; this row's own
+      // start comes with a later block (j + lag < rows_per_sub) or a later record (cleared now)
+      srow = base + ((a.ihead[sub] + j - a.start_lag) % a.cap_e + a.cap_e) % a.cap_e;
+      clear_own = j + a.start_lag >= a.rows_per_sub;
+    }
   } else {
     const long long keep = v.n < a.cap_e ? v.n : a.cap_e;
     const long long i = blockIdx.x;
@@ -149,15 +167,23 @@ __global__ __launch_bounds__(256) void ingest_rows_kernel(const IngestArgs a) {
   a.priority[row] = scalar_at(a.rec + v.off[7], 2, src);
   const int st = scalar_at(a.rec + v.off[9], v.code[9], src) != 0.f;
   const float leaf = st ? scalar_at(a.rec + v.off[8], 2, src) : 0.f;
-  const int was = a.is_start[row];
-  a.is_start[row] = (uint8_t)st;
-  if (was != st) atomicAdd(a.n_valid, st - was);
-  if (was || st || a.leaves[row] != 0.f) {
-    a.leaves[row] = leaf;
-    if (a.dirty) {
-      const int slot = atomicAdd(a.count, 1);
-      if (slot < a.max_dirty) a.dirty[slot] = (int)row;
+  auto set_start = [&](long long r, int s_, float lf) {
+    const int was = a.is_start[r];
+    a.is_start[r] = (uint8_t)s_;
+    if (was != s_) atomicAdd(a.n_valid, s_ - was);
+    if (was || s_ || a.leaves[r] != 0.f) {
+      a.leaves[r] = lf;
+      if (a.dirty) {
+        const int slot = atomicAdd(a.count, 1);
+        if (slot < a.max_dirty) a.dirty[slot] = (int)r;
+      }
     }
+  };
+  if (srow < 0) {
+    set_start(row, st, leaf);
+  } else {
+    set_start(srow, st, leaf);
+    if (clear_own) set_start(row, 0, 0.f);
   }
 }
 
@@ -193,9 +219,9 @@ struct PackArgs {
   uint8_t* rec;
   long long off[ING_FIELDS];   // byte offset of every field in the record
   long long h0;                // first ring position (same for every sub-ring: lockstep envs)
-  int E, K, cap_e, FB, H2;     // K rows per env window
-  int start_from, start_to;    // starts kept only for window rows j in [start_from, start_to)
-  int pad_;
+  int E, K, cap_e, FB, H2;     // K rows per env block
+  int start_from, start_to;    // starts kept only for block rows j in [start_from, start_to)
+  int lag;                     // the start column of row j describes ring position h0 + j - lag
 };
 
 __global__ __launch_bounds__(256) void pack_rows_kernel(const PackArgs a) {
@@ -222,8 +248,9 @@ __global__ __launch_bounds__(256) void pack_rows_kernel(const PackArgs a) {
   reinterpret_cast<float*>(a.rec + a.off[5])[i] = a.done[row] ? 1.f : 0.f;
   a.rec[a.off[6] + i] = 0;                                           // stack_count
   reinterpret_cast<float*>(a.rec + a.off[7])[i] = a.priority[row];
-  const bool st = a.is_start[row] && j >= a.start_from && j < a.start_to;
-  reinterpret_cast<float*>(a.rec + a.off[8])[i] = st ? a.leaves[row] : 0.f;
+  const long long srow = (long long)e * a.cap_e + ((a.h0 + j - a.lag) % a.cap_e + a.cap_e) % a.cap_e;
+  const bool st = a.is_start[srow] && j >= a.start_from && j < a.start_to;
+  reinterpret_cast<float*>(a.rec + a.off[8])[i] = st ? a.leaves[srow] : 0.f;
   a.rec[a.off[9] + i] = st ? 1 : 0;
 }
 

@@ -761,13 +761,358 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
   }
 }
 
+// ============================================================================================
+// Forward v3 (the default).  v2 runs its three convs in two serialised phases per frame (conv1 ||
+// conv3, then conv2 on three waves while five wait): 13.1k cycles per frame against 5.7k of MFMA
+// per SIMD, 35 % MFMA busy (profiles/r04_roofline_base.txt).  v3 pipelines the convs of three
+// consecutive frames through ONE phase per frame, with every SIMD running one wave of each role:
+//
+//   waves 4..7 ("C1"): conv1(f_i) on the int8 matrix cores (16x16x64, three W1 digits as in v2,
+//                      exact int32 sums) for one 16-channel half over half of the 25 4x4-pixel
+//                      tiles, then conv3(f_{i-2}) (16x16x32 bf16, 3 passes) for the same channel
+//                      half over two 4x4 tiles of the 7x7 output; W1 digits (48 VGPRs) and W3 (72)
+//                      register-resident
+//   waves 0..3 ("C2"): conv2(f_{i-1}) (16x16x32 bf16, 3 passes) for one channel half over three of
+//                      six 16-pixel tiles, W2 (128 VGPRs) register-resident; they also stage frame
+//                      f_{i+1} (dword loads during iteration i, stored at the start of i+1 while the
+//                      C1 waves run conv3, then an LDS counter releases conv1)
+//
+// so the int8 conv1's VALU-heavy epilogue issues beside the other wave's bf16 MFMAs on the same
+// SIMD.  act1 / act2 are double-buffered in LDS (W2 moved out of LDS pays for it).  Layouts
+// (conflict-free for every MFMA operand read, by a bank model of the ds_read_b128 lane groups):
+//   * frame: space-to-depth 4x4 blocks, 16 bytes each (one conv1 B fragment = one ds_read_b128),
+//     rows of 24 blocks, channel planes of 508 blocks;
+//   * act1: pixel (y, x) in slot y*20 + (x ^ ((x >> 2) & 1)), 16-byte channel chunk c at position
+//     c ^ 2((y >> 1) & 1) ^ ((x >> 1) & 1);
+//   * act2: slot y*9 + x, chunk position c ^ ((y >> 1) & 1) ^ (2(x & 1) | ((x >> 1) & 1)).
+// Products accumulate in 32-wide K steps (v2: 16), so outputs match v2 to fp32 rounding, not bit
+// for bit (tests/test_split_gpu.py).
+namespace tsp3 {
+using tsp::NT; using tsp::IN_BYTES;
+constexpr int FRP = 508 * 16;                // frame channel plane (bytes)
+constexpr int OFF_FR = 0;
+constexpr int A1P = 400 * 64;                // one act1 plane
+constexpr int OFF_A1 = 4 * FRP;              // 32512: [buffer 2][hi, lo]
+constexpr int A2P = 81 * 64;                 // one act2 plane
+constexpr int OFF_A2 = OFF_A1 + 4 * A1P;     // 134912: [buffer 2][hi, lo]
+constexpr int OFF_B = OFF_A2 + 4 * A2P;      // 155648: biases conv2, conv3, conv1
+constexpr int OFF_SC = OFF_B + 96 * 4;       // 156032: int8 conv1 row corrections [2][32]
+constexpr int OFF_FLAG = OFF_SC + 64 * 4;    // 156288: frame-ready counter
+constexpr int LDS_BYTES = OFF_FLAG + 16;     // 156304
+constexpr int NBLK = 4 * 441;                // s2d blocks per frame
+constexpr int PFQ = (NBLK + 255) / 256;      // blocks per C2 thread (7)
+static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+}  // namespace tsp3
+
+__device__ __forceinline__ int a1v3_off(int y, int x, int c) {
+  return (y * 20 + (x ^ ((x >> 2) & 1))) * 64 + ((c ^ (((y >> 1) & 1) << 1) ^ ((x >> 1) & 1)) << 4);
+}
+__device__ __forceinline__ int a2v3_off(int y, int x, int c) {
+  return (y * 9 + x) * 64 + ((c ^ ((y >> 1) & 1) ^ (((x & 1) << 1) | ((x >> 1) & 1))) << 4);
+}
+// s2d block b (channel-major, 21 x 21 per channel) -> its source dword offset in the frame and its
+// LDS offset in the frame image
+__device__ __forceinline__ void fr3_block(int b, int& src, int& dst) {
+  const int ci = b / 441, rem = b - 441 * ci, r = rem / 21, c = rem - 21 * r;
+  src = ci * 7056 + 4 * r * 84 + 4 * c;
+  dst = ci * tsp3::FRP + (r * 24 + c) * 16;
+}
+
+__global__ __launch_bounds__(512) void torso_fwd_sp3_kernel(const TSArgs args) {
+  using namespace tsp3;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  float* lb = (float*)(lds + OFF_B);
+  int* flag = (int*)(lds + OFF_FLAG);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int l16 = lane & 15, kq = lane >> 4;
+  const int wk = blockIdx.x;
+  int ji = 0;
+#pragma unroll
+  for (int i = 1; i < TS_MAX_JOBS; ++i)
+    if (i < args.njobs && wk >= args.job[i].wbegin) ji = i;
+  const TSJob& J = args.job[ji];
+  const int stride = J.wcount;
+  const int first = wk - J.wbegin;
+  if (first >= stride || first >= J.n) return;
+  const int nf = (J.n - first + stride - 1) / stride;   // frames of this workgroup
+  auto frame_row = [&](int k) -> size_t {
+    const int f = first + k * stride;
+    return J.rows ? (size_t)ld_uniform_i32(J.rows, f) : (size_t)f;
+  };
+
+  // ---- once: W1 digits (all threads; the act1 region is scratch), biases, frame 0, counter
+  const float c1_scale = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(
+      c1_digits(J.w1, J.w1l, tid, lds + OFF_A1, (int*)(lds + OFF_SC), (float*)(lds + OFF_A1 + 3 * 8192)))));
+  if (tid < 96) lb[tid] = tid < 32 ? J.b2[tid] : tid < 64 ? J.b3[tid - 32] : J.b1[tid - 64];
+  if (tid == 0) *flag = 0;
+  {
+    const __amdgpu_buffer_rsrc_t frs = ts_rsrc(args.frames + frame_row(0) * IN_BYTES, IN_BYTES);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int b = tid + 512 * q;
+      if (b < NBLK) {
+        int src, dst;
+        fr3_block(b, src, dst);
+        u32x4 v;
+#pragma unroll
+        for (int dy = 0; dy < 4; ++dy) v[dy] = __builtin_amdgcn_raw_buffer_load_b32(frs, src * 1 + dy * 84, 0, 0) ^ 0x80808080u;
+        *(u32x4*)(lds + OFF_FR + dst) = v;
+      }
+    }
+  }
+  __syncthreads();   // digits + frame 0 + biases in LDS
+  // optional clock stamps of workgroup 0 (r2_torso_sp_trace): [wave][iteration < 16][4] = loop
+  // top, conv3 / frame staging done, conv1 / conv2 done, after the barrier
+  long long* tr = (args.trace && blockIdx.x == 0 && lane == 0) ? args.trace + wave * 16 * 4 : nullptr;
+#define TS3_STAMP(it, k) \
+  if (tr && (it) < 16) tr[(it) * 4 + (k)] = (long long)__builtin_readcyclecounter();
+
+  if (wave >= 4) {
+    // ================================ C1: conv1(f_i) then (next iteration first) conv3(f_{i-2})
+    const int c1 = wave - 4, hc = c1 & 1, grp = c1 >> 1;
+    const int ch0 = 16 * hc + 4 * kq;
+    i32x4_t wd[12];   // W1 digit fragments (kb, d) of channel half hc
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int d = 0; d < 3; ++d)
+        wd[3 * kb + d] = *(const i32x4_t*)(lds + OFF_A1 + d * 8192 + (16 * hc + l16) * 256 + (4 * kb + kq) * 16);
+    bf16x8 w3h[9], w3l[9];
+#pragma unroll
+    for (int s = 0; s < 9; ++s) {
+      w3h[s] = *(const bf16x8*)(J.w3 + (16 * hc + l16) * 288 + s * 32 + 8 * kq);
+      w3l[s] = *(const bf16x8*)(J.w3l + (16 * hc + l16) * 288 + s * 32 + 8 * kq);
+    }
+    const i32x4_t sc0 = *(const i32x4_t*)(lds + OFF_SC + ch0 * 4);
+    const i32x4_t sc2 = *(const i32x4_t*)(lds + OFF_SC + (32 + ch0) * 4);
+    float b1v[4], b3v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { b1v[e] = lb[64 + ch0 + e]; b3v[e] = lb[32 + ch0 + e]; }
+    __syncthreads();   // every C1 wave holds its digits before conv1(f_0) overwrites the scratch
+    const int t_beg = grp ? 13 : 0, t_end = grp ? 25 : 13;
+    // lane-constant parts of the conv1 fragment / epilogue offsets
+    const int fr_lane = OFF_FR + kq * FRP + ((l16 >> 2) * 24 + (l16 & 3)) * 16;
+    for (int i = 0; i < nf + 2; ++i) {
+      TS3_STAMP(i, 0);
+      if (i >= 2) {
+        // conv3(f_{i-2}): act2 buffer (i-2)&1, two 4x4 tiles of the 7x7 output
+        const int k = i - 2;
+        const uint8_t* a2h = lds + OFF_A2 + (k & 1) * 2 * A2P;
+        const uint8_t* a2l = a2h + A2P;
+        const size_t fo = (size_t)(first + k * stride) * 1568;
+#pragma unroll 1
+        for (int tt = 0; tt < 2; ++tt) {
+          const int t = 2 * grp + tt;
+          const int y3 = (t >> 1) * 4 + (l16 >> 2), x3 = (t & 1) * 4 + (l16 & 3);
+          const int yc = min(y3, 6), xc = min(x3, 6);
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+          bf16x8 rh[2], rl[2];
+          auto ld = [&](int s, bf16x8& h, bf16x8& l) {
+            const int o = a2v3_off(yc + s / 3, xc + s % 3, kq);
+            h = *(const bf16x8*)(a2h + o);
+            l = *(const bf16x8*)(a2l + o);
+          };
+          ld(0, rh[0], rl[0]);
+          ld(1, rh[1], rl[1]);
+#pragma unroll
+          for (int s = 0; s < 9; ++s) {
+            const bf16x8 h = rh[s & 1], l = rl[s & 1];
+            if (s + 2 < 9) ld(s + 2, rh[s & 1], rl[s & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+            acc = mfma16_x3(w3h[s], w3l[s], h, l, acc);
+          }
+          if (y3 < 7 && x3 < 7) {
+            bf16* oh = J.out + fo + y3 * 7 + x3;
+            bf16* ol = J.out_l + fo + y3 * 7 + x3;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float v = fmaxf(acc[e] + b3v[e], 0.f);
+              oh[(ch0 + e) * 49] = (bf16)v;
+              ol[(ch0 + e) * 49] = sp_lo(v);
+            }
+          }
+        }
+      }
+      TS3_STAMP(i, 1);
+      if (i < nf) {
+        if (i >= 1) {   // frame f_i staged by the C2 waves
+          while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 4 * i)
+            __builtin_amdgcn_s_sleep(1);
+        }
+        uint8_t* a1h = lds + OFF_A1 + (i & 1) * 2 * A1P;
+        uint8_t* a1l = a1h + A1P;
+        const int fidx = first + i * stride;
+        bf16* s1 = J.s1 ? J.s1 + (size_t)fidx * 400 * 32 : nullptr;
+        bf16* s1l = J.s1 ? J.s1l + (size_t)fidx * 400 * 32 : nullptr;
+        auto ldb = [&](int t, i32x4_t (&x)[4]) {
+          const int ty = t / 5, tx = t - 5 * ty;
+          const uint8_t* p = lds + fr_lane + (ty * 4 * 24 + tx * 4) * 16;
+          x[0] = *(const i32x4_t*)(p);
+          x[1] = *(const i32x4_t*)(p + 16);
+          x[2] = *(const i32x4_t*)(p + 24 * 16);
+          x[3] = *(const i32x4_t*)(p + 25 * 16);
+        };
+        // one 4x4-pixel tile: 12 int8 MFMAs (3 digits x 4 K blocks) + the epilogue; the next
+        // tile's fragments are loaded (into `nx`) before the MFMAs
+        auto tile = [&](int t, const i32x4_t (&cur)[4], i32x4_t (&nx)[4]) {
+          if (t + 1 < t_end) ldb(t + 1, nx);
+          __builtin_amdgcn_sched_barrier(0);
+          i32x4_t acc[3];
+          acc[0] = sc0;
+          acc[1] = i32x4_t{0, 0, 0, 0};
+          acc[2] = sc2;
+#pragma unroll
+          for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+            for (int d = 0; d < 3; ++d)
+              acc[d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wd[3 * kb + d], cur[kb], acc[d], 0, 0, 0);
+          const int ty = t / 5, tx = t - 5 * ty;
+          const int y = 4 * ty + (l16 >> 2), x = 4 * tx + (l16 & 3);
+          bf16x4 vh, vl;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int i0 = acc[0][e];
+            const int i12 = acc[1][e] * 128 + acc[2][e];
+            const float tq = fmaf((float)i12, 1.f / 16384.f, (float)i0);
+            const float v = fmaxf(fmaf(tq, c1_scale, b1v[e]), 0.f);
+            vh[e] = (bf16)v;
+            vl[e] = sp_lo(v);
+          }
+          const int o = a1v3_off(y, x, ch0 >> 3) + 8 * (kq & 1);
+          *(bf16x4*)(a1h + o) = vh;
+          *(bf16x4*)(a1l + o) = vl;
+          if (s1) {
+            const size_t g = (size_t)(y * 20 + x) * 32 + ch0;
+            *(bf16x4*)(s1 + g) = vh;
+            *(bf16x4*)(s1l + g) = vl;
+          }
+        };
+        i32x4_t bA[4], bB[4];
+        ldb(t_beg, bA);
+#pragma unroll 1
+        for (int t = t_beg; t < t_end; t += 2) {
+          tile(t, bA, bB);
+          if (t + 1 < t_end) tile(t + 1, bB, bA);
+        }
+      }
+      TS3_STAMP(i, 2);
+      lds_sync();
+      TS3_STAMP(i, 3);
+    }
+  } else {
+    // ================================ C2: stage frame f_i, load f_{i+1}, conv2(f_{i-1})
+    const int c2 = wave, h = c2 & 1, grp = c2 >> 1;
+    const int chc = 16 * h + 4 * kq;
+    bf16x8 w2h[16], w2l[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      w2h[s] = *(const bf16x8*)(J.w2 + (16 * h + l16) * 512 + s * 32 + 8 * kq);
+      w2l[s] = *(const bf16x8*)(J.w2l + (16 * h + l16) * 512 + s * 32 + 8 * kq);
+    }
+    float b2v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) b2v[e] = lb[chc + e];
+    int fsrc[PFQ], fdst[PFQ];
+#pragma unroll
+    for (int q = 0; q < PFQ; ++q) {
+      const int b = tid + 256 * q;
+      fr3_block(b < NBLK ? b : NBLK - 1, fsrc[q], fdst[q]);
+    }
+    __syncthreads();   // pairs the C1 waves' digit barrier
+    u32x4 pf[PFQ];
+    for (int i = 0; i < nf + 2; ++i) {
+      TS3_STAMP(i, 0);
+      if (i >= 1 && i < nf) {
+        // frame f_i -> LDS (conv1(f_{i-1}) finished reading the image at the last barrier)
+#pragma unroll
+        for (int q = 0; q < PFQ; ++q)
+          if (tid + 256 * q < NBLK) *(u32x4*)(lds + OFF_FR + fdst[q]) = pf[q] ^ 0x80808080u;
+        if (lane == 0) __hip_atomic_fetch_add(flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      if (i + 1 < nf) {
+        const __amdgpu_buffer_rsrc_t frs = ts_rsrc(args.frames + frame_row(i + 1) * IN_BYTES, IN_BYTES);
+#pragma unroll
+        for (int q = 0; q < PFQ; ++q)
+#pragma unroll
+          for (int dy = 0; dy < 4; ++dy)
+            pf[q][dy] = __builtin_amdgcn_raw_buffer_load_b32(frs, fsrc[q], dy * 84, 0);
+      }
+      TS3_STAMP(i, 1);
+      if (i >= 1 && i <= nf) {
+        const int k = i - 1;
+        const uint8_t* a1h = lds + OFF_A1 + (k & 1) * 2 * A1P;
+        const uint8_t* a1l = a1h + A1P;
+        uint8_t* a2h = lds + OFF_A2 + (k & 1) * 2 * A2P;
+        uint8_t* a2l = a2h + A2P;
+        const int fidx = first + k * stride;
+        bf16* s2 = J.s2 ? J.s2 + (size_t)fidx * 81 * 32 : nullptr;
+        bf16* s2l = J.s2 ? J.s2l + (size_t)fidx * 81 * 32 : nullptr;
+#pragma unroll 1
+        for (int tt = 0; tt < 3; ++tt) {
+          const int t = 3 * grp + tt;
+          int y2, x2;
+          bool ok = true;
+          if (t < 4) { y2 = (t >> 1) * 4 + (l16 >> 2); x2 = (t & 1) * 4 + (l16 & 3); }
+          else if (t == 4) { y2 = l16 < 8 ? l16 : 8; x2 = l16 < 8 ? 8 : l16 - 8; }
+          else { y2 = 8; x2 = 8; ok = l16 == 0; }
+          int yo[4], xo[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int y = 2 * y2 + j, x = 2 * x2 + j;
+            yo[j] = y * 1280 + ((((kq >> 1) ^ (y >> 1)) & 1) << 5);
+            xo[j] = ((x ^ ((x >> 2) & 1)) << 6) + ((((kq & 1) ^ (x >> 1)) & 1) << 4);
+          }
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+          bf16x8 rh[2], rl[2];
+          auto ld = [&](int s, bf16x8& hh, bf16x8& ll) {
+            const int o = yo[s >> 2] + xo[s & 3];
+            hh = *(const bf16x8*)(a1h + o);
+            ll = *(const bf16x8*)(a1l + o);
+          };
+          ld(0, rh[0], rl[0]);
+          ld(1, rh[1], rl[1]);
+#pragma unroll
+          for (int s = 0; s < 16; ++s) {
+            const bf16x8 hh = rh[s & 1], ll = rl[s & 1];
+            if (s + 2 < 16) ld(s + 2, rh[s & 1], rl[s & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+            acc = mfma16_x3(w2h[s], w2l[s], hh, ll, acc);
+          }
+          if (ok) {
+            bf16x4 vh, vl;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float v = fmaxf(acc[e] + b2v[e], 0.f);
+              vh[e] = (bf16)v;
+              vl[e] = sp_lo(v);
+            }
+            const int o = a2v3_off(y2, x2, chc >> 3) + 8 * (kq & 1);
+            *(bf16x4*)(a2h + o) = vh;
+            *(bf16x4*)(a2l + o) = vl;
+            if (s2) {
+              const size_t g = (size_t)(y2 * 9 + x2) * 32 + chc;
+              *(bf16x4*)(s2 + g) = vh;
+              *(bf16x4*)(s2l + g) = vl;
+            }
+          }
+        }
+      }
+      TS3_STAMP(i, 2);
+      lds_sync();
+      TS3_STAMP(i, 3);
+    }
+  }
+#undef TS3_STAMP
+}
+
 static int g_tsp_dbg = 0;
 static long long* g_tsp_trace = nullptr;
 // v2 phase clock stamps of workgroup 0: [wave][frame < 16][5] (loop top, phase A done, barrier,
 // phase B done, barrier), s_memrealtime-free cycle counter
 extern "C" int r2_torso_sp_trace(long long* p) { g_tsp_trace = p; return 0; }
 // timing probes only (tools/sp_micro.py): bit 0 skips conv1, bit 1 conv2, bit 2 conv3;
-// bit 3 runs the v1 kernel; bit 7 runs v2 with the bf16 split conv1 (else int8 digits)
+// bit 3 runs the v1 kernel; bit 7 runs v2 with the bf16 split conv1; bit 8 runs v3 (else v2 with
+// the int8 conv1)
 extern "C" int r2_torso_sp_debug(int bits) { g_tsp_dbg = bits; return 0; }
 
 extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs, int njobs,
@@ -827,9 +1172,19 @@ extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs,
     if (a.dbg & 128)   // bf16 split conv1 (the previous v2 path)
       hipLaunchKernelGGL(torso_fwd_sp2_kernel<false>, dim3(grid), dim3(tsp::NT), tsp2::LDS_BYTES,
                          (hipStream_t)stream, a);
-    else
+    else if (!(a.dbg & 256))   // v2 (int8 conv1, two phases per frame)
       hipLaunchKernelGGL(torso_fwd_sp2_kernel<true>, dim3(grid), dim3(tsp::NT), tsp2::LDS_BYTES_I8,
                          (hipStream_t)stream, a);
+    else {   // v3
+      static bool attr3 = false;
+      if (!attr3) {
+        hipFuncSetAttribute((const void*)torso_fwd_sp3_kernel,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, tsp3::LDS_BYTES);
+        attr3 = true;
+      }
+      hipLaunchKernelGGL(torso_fwd_sp3_kernel, dim3(grid), dim3(tsp::NT), tsp3::LDS_BYTES,
+                         (hipStream_t)stream, a);
+    }
   }
   R2_CHECK_LAUNCH();
   return 0;

@@ -185,11 +185,14 @@ class DistConfig:
     # (parallel/sharded_replay.py: one 12-byte all-gather per step, shard-ratio loss weights)
     global_sampling: bool = True
     # split topology (parallel/actor_ranks.py, runner.run_split): the last ``actor_ranks`` ranks
-    # run actor groups only and feed the learner ranks over RCCL; per round every actor rank takes
-    # ``push_rows`` env steps and ships one record, every learner rank trains
-    # ``learner_steps_per_round`` steps; weights are broadcast every ``publish_rounds`` rounds
+    # run actor groups only and feed the learner ranks over asynchronous RCCL links; every
+    # ``push_rows`` env steps an actor rank ships one record of its newest final rows (each row
+    # once), blocking only when ``push_slots`` records are untaken; learner rank 0 sends weights
+    # every ``publish_steps`` learner steps to the actor ranks that took the previous snapshot
     actor_ranks: int = 0
     push_rows: int = 32
+    push_slots: int = 4
+    publish_steps: int = 100
     # rehearsal: run the data-parallel step machinery (segmented graphs, bucketed RCCL
     # all-reduces on the comm stream, CU reservation, the shard-stats all-gather) at world 1
     # (bench.py --force-dp under torchrun): the collectives are one-rank no-ops, the code path is
@@ -200,8 +203,11 @@ class DistConfig:
     # machinery's overhead at one forced rank 1.180 -> 1.122 ms against 1.102 for the plain step
     # (tools/dp_overhead_ab.sh, profiles/r03_force_dp_ab.txt)
     graph_collectives: bool = True
-    learner_steps_per_round: int = 1
-    publish_rounds: int = 8
+    # ... also at world > 1.  Off until a run with two or more RCCL ranks has shown matching
+    # weights across ranks and a zero error word (the multi-rank DP path runs the segment graphs
+    # with the collectives issued between them, the form the multi-rank tests pin)
+    graph_collectives_multi: bool = False
+    learner_steps_per_round: int = 1    # run_split default run length: rounds x this
 
 
 @dataclass

@@ -45,16 +45,21 @@ class IngestArgs(ctypes.Structure):
         (n, _VP) for n in ("ihead", "rows_total", "err", "frames", "hs_cs", "ths_cs", "action",
                            "reward", "done", "priority", "is_start", "leaves", "n_valid", "dirty",
                            "count")] + [
-        (n, ctypes.c_int) for n in ("max_dirty", "FB", "H2", "cap_e", "rows_per_sub")]
+        (n, ctypes.c_int) for n in ("max_dirty", "FB", "H2", "cap_e", "rows_per_sub", "start_lag",
+                                    "n_sub", "pad_")]
 
 
 def ingest_args(replay, rec: int, rec_bytes: int, sub: int, use_dirty: bool,
-                rows_per_sub: int = 0) -> IngestArgs:
+                rows_per_sub: int = 0, start_lag: int = 0) -> IngestArgs:
+    """``rows_per_sub`` > 0: the record is env-major blocks of that many rows, block i to sub-ring
+    ``sub + i``; ``start_lag``: its start column marks the position ``start_lag`` rows before each
+    row (an actor rank's blocks, parallel/actor_ranks.py).  The device rejects (error word) a
+    record that is not whole blocks or addresses sub-rings past the replay's."""
     if ctypes.sizeof(IngestArgs) != kernels().r2_ingest_args_bytes():
         raise RuntimeError("IngestArgs layout differs from csrc/kernels/ingest.hip")
     rp = replay
     a = IngestArgs()
-    a.rec, a.rec_bytes, a.sub = rec, int(rec_bytes), int(sub) % rp.n_sub
+    a.rec, a.rec_bytes, a.sub = rec, int(rec_bytes), int(sub)
     a.max_rows = int(min(rp.cap_e, rec_bytes // max(rp.frame_bytes, 1) + 1))
     for name, t in (("ihead", rp.ihead), ("rows_total", rp.rows_total_d), ("err", rp.ingest_err),
                     ("frames", rp.frames), ("hs_cs", rp.hs_cs), ("ths_cs", rp.target_hs_cs),
@@ -64,7 +69,7 @@ def ingest_args(replay, rec: int, rec_bytes: int, sub: int, use_dirty: bool,
         setattr(a, name, ptr(t))
     a.dirty = ptr(rp.dirty) if use_dirty else 0
     a.max_dirty, a.FB, a.H2, a.cap_e = rp.max_dirty, rp.frame_bytes, 2 * rp.H, rp.cap_e
-    a.rows_per_sub = int(rows_per_sub)
+    a.rows_per_sub, a.start_lag, a.n_sub = int(rows_per_sub), int(start_lag), rp.n_sub
     if rows_per_sub > 0:   # env-major windows: every row of the record is kept
         a.max_rows = int(rec_bytes // max(rp.frame_bytes, 1) + 1)
     return a

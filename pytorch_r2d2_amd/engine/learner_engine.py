@@ -1150,7 +1150,8 @@ class LearnerEngine:
         torch.cuda.synchronize(self.device)
         self.graphs = []
         self._one_dp_graph = False
-        if self.dp and self.cfg.dist.graph_collectives and self._pg_backend() == "nccl":
+        one = self.cfg.dist.graph_collectives and (self.world == 1 or self.cfg.dist.graph_collectives_multi)
+        if self.dp and one and self._pg_backend() == "nccl":
             # the whole DP step in ONE graph: the bucket all-reduces and the shard-stats
             # all-gather are captured on their side streams (fork / join as graph edges), so the
             # ~15 us gap of every segment boundary disappears

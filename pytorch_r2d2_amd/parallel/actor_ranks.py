@@ -1,30 +1,33 @@
 """Actor ranks: GPU actor groups on ranks that own no learner (the split topology).
 
 Reference: N actor processes push experience to ONE learner through pickled files and pull
-weights from a Manager dict (``/root/reference/main.py:20-27``, ``replay_memory.py:125-173``,
-``learner.py:122-124``, ``actor.py:137-142``).  With ``dist.actor_ranks = A`` of the W ranks (one
-process per GPU, torchrun):
+weights from a Manager dict, never waiting for each other (``/root/reference/main.py:20-27``,
+``actor.py:64-66``, ``learner.py:53-66``, ``replay_memory.py:125-173``, ``learner.py:122-124``,
+``actor.py:137-142``).  With ``dist.actor_ranks = A`` of the W ranks (one process per GPU,
+torchrun):
 
-* ranks 0 .. L-1 (L = W - A) are data-parallel learner ranks (their replay shards + a
+* ranks 0 .. L-1 (L = W - A <= A) are data-parallel learner ranks (their replay shards + a
   ``LearnerEngine`` over the learner group); ranks L .. W-1 run ``BatchedActor`` groups only (E
   envs each, the whole GPU for inference and env steps);
-* actor rank a feeds learner rank (a - L) % L.  Every round (K env steps) it packs, per env, the
-  window of its last K + W - 1 replay rows (W = T + n: the previous window's last W - 1 rows travel
-  again, so each sequence's whole window is in exactly ONE record and only the starts whose
-  window lies inside the record are kept) with the device pack kernel
-  (``csrc/kernels/ingest.hip`` pack_rows_kernel) and sends the fixed-size record with one RCCL
-  send; the learner receives it into device memory and scatters it into that actor's E sub-rings
-  (env-major ingest);
-* weights: every ``publish_rounds`` rounds learner rank 0 broadcasts master + target over the
-  {learner 0} + actor-ranks group (``WeightPublisher``: one 2 x 8 MB RCCL broadcast); the actors
-  re-pack them between env steps.
-Every rank issues the same sequence of point-to-point and collective calls per round, so the
-protocol needs no handshake.  Over gloo (CPU tests, ranks sharing a GPU) the device buffers are
-staged through host tensors.
+* actor rank a feeds learner rank (a - L) % L through an asynchronous link
+  (``parallel/channel.py``): every K env steps it packs, per env, the K newest FINAL rows (the
+  rows K + n .. n + 1 steps old: a row's n-step return, done flag and priority are final n steps
+  after it is written) with the device pack kernel (``csrc/kernels/ingest.hip``) and sends them;
+  each row travels exactly once.  A sequence start travels with the last row of its window
+  (start column lagged by W - 1 = T + n - 1 rows), so the learner's sub-ring -- one contiguous
+  stream per env -- only ever holds starts whose whole window it has received;
+* the learner polls its links between steps and ingests whatever has arrived (env-major
+  device ingest); it never waits for a particular actor, and an actor blocks only when all of
+  its ``dist.push_slots`` records are still untaken;
+* weights: every ``dist.publish_steps`` learner steps learner rank 0 sends master + target to
+  each actor rank whose previous snapshot has been taken (one 2 x 8 MB message, RCCL); actor
+  ranks take snapshots between rounds.
+Over gloo (CPU tests, ranks sharing a GPU) the device buffers are staged through host tensors.
 """
 from __future__ import annotations
 
 import ctypes
+import time
 from typing import List, Optional
 
 import numpy as np
@@ -42,14 +45,19 @@ class PackArgs(ctypes.Structure):
     _fields_ = [(n, _VP) for n in ("frames", "hs_cs", "ths_cs", "action", "reward", "done",
                                    "priority", "is_start", "leaves", "rec")] + [
         ("off", ctypes.c_longlong * len(ORDER)), ("h0", ctypes.c_longlong)] + [
-        (n, ctypes.c_int) for n in ("E", "K", "cap_e", "FB", "H2", "start_from", "start_to", "pad_")]
+        (n, ctypes.c_int) for n in ("E", "K", "cap_e", "FB", "H2", "start_from", "start_to", "lag")]
 
 
 def split_roles(world: int, actor_ranks: int):
-    """(learner ranks, actor ranks, {actor rank: learner rank it feeds})."""
+    """(learner ranks, actor ranks, {actor rank: learner rank it feeds}).  Every learner needs at
+    least one feeding actor rank (a learner without one never fills its replay, and the data-
+    parallel learners start only when every shard holds a batch)."""
     L = world - int(actor_ranks)
     if actor_ranks < 1 or L < 1:
         raise ValueError(f"actor_ranks={actor_ranks} needs 1 <= actor_ranks < world={world}")
+    if actor_ranks < L:
+        raise ValueError(f"actor_ranks={actor_ranks} < learner ranks {L}: every learner rank needs "
+                         f"an actor rank feeding it")
     learners, actors = list(range(L)), list(range(L, world))
     return learners, actors, {a: (a - L) % L for a in actors}
 
@@ -58,116 +66,174 @@ def _is_gloo(group=None) -> bool:
     return dist.is_initialized() and dist.get_backend(group) == "gloo"
 
 
-def _aligned(nbytes: int, device) -> torch.Tensor:
-    buf = torch.zeros(nbytes + 64, dtype=torch.uint8, device=device)
-    off = (-buf.data_ptr()) % 64
-    return buf[off: off + nbytes]
+def record_link(actor_rank: int) -> str:
+    return f"r2d2/rec/{actor_rank}"
+
+
+def weight_link(actor_rank: int) -> str:
+    return f"r2d2/w/{actor_rank}"
 
 
 class TrajectoryPusher:
-    """Actor-rank side: pack the E env windows of one round and send them to ``dst``."""
+    """Actor-rank side: every K env steps pack the E env blocks of K final rows and send them to
+    learner rank ``dst`` over an asynchronous link with ``slots`` record buffers."""
 
-    def __init__(self, replay, K: int, dst: int, group=None):
+    def __init__(self, replay, K: int, dst: int, slots: int = 4, group=None, link=True):
         rp = replay
         self.rp, self.K, self.dst, self.group = rp, int(K), int(dst), group
-        self.W = rp.cfg.replay.seq_len + rp.cfg.replay.n_step
-        self.R = self.K + self.W - 1                   # rows per env window
-        if self.R + self.K > rp.cap_e:
-            raise ValueError(f"actor-rank sub-ring of {rp.cap_e} rows < window {self.R} + round {self.K}")
+        self.n = rp.cfg.replay.n_step
+        self.W = rp.cfg.replay.seq_len + self.n
+        self.lag = self.W - 1
+        if self.K + self.n + self.W > rp.cap_e:
+            raise ValueError(f"actor-rank sub-ring of {rp.cap_e} rows < round {self.K} + n {self.n} "
+                             f"+ window {self.W}")
         self.E = rp.n_sub
-        hdr, offs, total = record_spec(self.E * self.R, rp.frame_bytes, 2 * rp.H)
+        hdr, offs, total = record_spec(self.E * self.K, rp.frame_bytes, 2 * rp.H)
         self.nbytes = total
-        self.rec = _aligned(total, rp.device)
-        self.rec[: hdr.size].copy_(torch.from_numpy(hdr))
-        self.host = torch.empty(total, dtype=torch.uint8, pin_memory=rp.device.type == "cuda") \
-            if _is_gloo(group) else None
+        self.hdr = torch.from_numpy(hdr)
         if ctypes.sizeof(PackArgs) != kernels().r2_pack_args_bytes():
             raise RuntimeError("PackArgs layout differs from csrc/kernels/ingest.hip")
         a = PackArgs()
         for name, t in (("frames", rp.frames), ("hs_cs", rp.hs_cs), ("ths_cs", rp.target_hs_cs),
                         ("action", rp.action), ("reward", rp.reward), ("done", rp.done),
-                        ("priority", rp.priority), ("is_start", rp.is_start), ("leaves", rp.tree),
-                        ("rec", self.rec)):
+                        ("priority", rp.priority), ("is_start", rp.is_start), ("leaves", rp.tree)):
             setattr(a, name, ptr(t))
         for i, o in enumerate(offs):
             a.off[i] = o
-        a.E, a.K, a.cap_e, a.FB, a.H2 = self.E, self.R, rp.cap_e, rp.frame_bytes, 2 * rp.H
-        a.start_to = self.K
+        a.E, a.K, a.cap_e, a.FB, a.H2 = self.E, self.K, rp.cap_e, rp.frame_bytes, 2 * rp.H
+        a.start_to, a.lag = self.K, self.lag
         self.args = a
+        self.link = None
+        if link:
+            from .channel import LinkSender
+            self.link = LinkSender(record_link(dist.get_rank()), self.dst, total, slots, rp.device,
+                                   data_group=group, host_stage=_is_gloo(group))
+            for b in self.link.bufs:
+                b[: hdr.size].copy_(self.hdr)
         self.windows = 0
 
-    def pack(self, window: int) -> torch.Tensor:
-        """Window c = ring rows [cK - (W-1), (c+1)K) of every env (the first W-1 rows of window 0
-        are before the first step: never starts).  Call after the round's K env steps."""
+    def pack(self, window: int, rec: torch.Tensor) -> torch.Tensor:
+        """Block c = stream rows [cK - n, (c+1)K - n) of every env (all final after the round's K
+        env steps), start column of stream rows [cK - n - (W-1), ...) -- stream rows < 0 carry no
+        starts.  Call after the round's K env steps."""
         a = self.args
-        a.h0 = (window * self.K - (self.W - 1)) % self.rp.cap_e
-        a.start_from = self.W - 1 if window == 0 else 0
+        a.rec = ptr(rec)
+        a.h0 = (window * self.K - self.n) % self.rp.cap_e
+        a.start_from = max(0, self.lag + self.n - window * self.K)
         check(kernels().r2_pack_rows(ctypes.byref(a), _VP(stream_handle())), "pack_rows")
-        return self.rec
+        return rec
 
     def push(self, window: int) -> None:
-        rec = self.pack(window)
-        if self.host is not None:
-            self.host.copy_(rec)
-            torch.cuda.current_stream(self.rp.device).synchronize() if self.rp.device.type == "cuda" else None
-            dist.send(self.host, self.dst, group=self.group)
-        else:
-            dist.send(rec, self.dst, group=self.group)
+        rec = self.link.acquire()
+        self.pack(window, rec)
+        self.link.send()
         self.windows += 1
+
+    def finish(self) -> None:
+        self.link.flush()
+        self.link.close()
 
 
 class TrajectoryReceiver:
-    """Learner side: one fixed-size record per feeding actor rank per round, scattered env-major
-    into sub-rings [i E, (i + 1) E) for the i-th source."""
+    """Learner side: the links of the actor ranks ``srcs``; ``poll()`` ingests every record that
+    has arrived, env-major into sub-rings [i E, (i + 1) E) for the i-th source."""
 
     def __init__(self, replay, srcs: List[int], E: int, K: int, group=None):
+        from .channel import LinkReceiver
         rp = replay
         self.rp, self.srcs, self.E, self.K, self.group = rp, list(srcs), int(E), int(K), group
-        self.W = rp.cfg.replay.seq_len + rp.cfg.replay.n_step
-        self.R = self.K + self.W - 1
+        self.n = rp.cfg.replay.n_step
+        self.lag = rp.cfg.replay.seq_len + self.n - 1
         if rp.n_sub < self.E * len(self.srcs):
             raise ValueError("the learner replay needs E sub-rings per feeding actor rank")
-        _, _, total = record_spec(self.E * self.R, rp.frame_bytes, 2 * rp.H)
+        _, _, total = record_spec(self.E * self.K, rp.frame_bytes, 2 * rp.H)
         self.nbytes = total
-        self.recs = [_aligned(total, rp.device) for _ in self.srcs]
-        gloo = _is_gloo(group)
-        self.host = [torch.empty(total, dtype=torch.uint8) for _ in self.srcs] if gloo else None
         self.rows = 0
         self.records = 0
+        self._budget = 0
+        self._big = False
+        self.link = LinkReceiver([record_link(a) for a in self.srcs], self.srcs, total, rp.device,
+                                 self._ingest, data_group=group, host_stage=_is_gloo(group))
 
-    def recv_all(self) -> int:
+    def _ingest(self, i: int, rec: torch.Tensor) -> None:
         from ..engine.ingest import ingest_args
         rp = self.rp
-        rows_rec = self.E * self.R
-        # the dirty list takes every record's rows; past half of it, rebuild
-        budget, used, big = rp.max_dirty // 2, 0, False
-        for i, src in enumerate(self.srcs):
-            if self.host is not None:
-                dist.recv(self.host[i], src, group=self.group)
-                self.recs[i].copy_(self.host[i], non_blocking=True)
-            else:
-                dist.recv(self.recs[i], src, group=self.group)
-            need = rows_rec
-            use_dirty = not big and used + need <= budget
-            big |= not use_dirty
-            used += need if use_dirty else 0
-            a = ingest_args(rp, ptr(self.recs[i]), self.nbytes, i * self.E, use_dirty,
-                            rows_per_sub=self.R)
-            check(kernels().r2_ingest_record(ctypes.byref(a), _VP(stream_handle())), "ingest")
-            self.rows += rows_rec
-            self.records += 1
-        rp.repair_after_ingest(full=big)
-        rp.total_written += rows_rec * len(self.srcs)
-        return rows_rec * len(self.srcs)
+        need = 2 * self.E * self.K          # a data row and a start row per record row
+        use_dirty = not self._big and self._budget + need <= rp.max_dirty // 2
+        self._big |= not use_dirty
+        self._budget += need if use_dirty else 0
+        a = ingest_args(rp, ptr(rec), self.nbytes, i * self.E, use_dirty, rows_per_sub=self.K,
+                        start_lag=self.lag)
+        check(kernels().r2_ingest_record(ctypes.byref(a), _VP(stream_handle())), "ingest")
+        self.rows += self.E * self.K
+        self.records += 1
+        rp.total_written += self.E * self.K
+
+    def poll(self, **kw) -> int:
+        self._budget, self._big = 0, False
+        got = self.link.poll(**kw)
+        if got:
+            self.rp.repair_after_ingest(full=self._big)
+        return got
+
+    def drain(self, rounds: int) -> None:
+        """Block until every source has delivered ``rounds`` records (end of a run)."""
+        while any(r < rounds for r in self.link.received):
+            if self.poll() == 0:
+                time.sleep(0.0005)
 
 
-def broadcast_weights(pub, engine, version: int, actor_weights=None) -> None:
-    """One publication round of ``WeightPublisher`` over the {learner 0} + actor-ranks group:
-    learner rank 0 passes its engine, actor ranks their (online, target) ``PackedWeights``."""
-    if engine is not None:
-        pub.publish(engine.master, engine.target, version)
-    else:
-        pub.publish(None, None, version)
-        on, tg, _ = pub.current()
-        actor_weights[0].load_flat(on, version)
-        actor_weights[1].load_flat(tg, version)
+class WeightLinks:
+    """Learner rank 0 -> actor ranks: master + target snapshots ([online | target] fp32) over one
+    single-slot link per actor rank, published only to actors that took the previous one."""
+
+    def __init__(self, numel: int, device, actors: List[int], src: int, role: str, group=None):
+        from .channel import LinkReceiver, LinkSender
+        self.numel = int(numel)
+        nbytes = 2 * self.numel * 4
+        stage = _is_gloo(group)
+        self.published = 0
+        self.senders, self.receiver = [], None
+        if role == "learner":
+            self.senders = [LinkSender(weight_link(a), a, nbytes, 1, device, data_group=group,
+                                       tag=1, host_stage=stage) for a in actors]
+        else:
+            self.taken = 0
+            self.receiver = LinkReceiver([weight_link(dist.get_rank())], [src], nbytes, device,
+                                         self._load, data_group=group, tag=1, host_stage=stage)
+            self.targets = None
+
+    def publish(self, master: torch.Tensor, target: torch.Tensor) -> int:
+        """Learner 0: send to every actor rank whose previous snapshot was taken (non-blocking
+        apart from one store round trip per actor rank).  Returns how many were sent."""
+        sent = 0
+        for tx in self.senders:
+            if tx.in_flight() == 0:
+                buf = tx.acquire().view(torch.float32)
+                buf[: self.numel].copy_(master.reshape(-1)[: self.numel])
+                buf[self.numel:].copy_(target.reshape(-1)[: self.numel])
+                tx.send()
+                sent += 1
+        self.published += 1 if sent else 0
+        return sent
+
+    def close(self) -> None:
+        for tx in self.senders:
+            tx.flush()
+            tx.close()
+
+    # actor side
+    def attach(self, online, target) -> None:
+        self.targets = (online, target)
+
+    def _load(self, i: int, buf: torch.Tensor) -> None:
+        f = buf.view(torch.float32)
+        self.taken += 1
+        self.targets[0].load_flat(f[: self.numel], self.taken)
+        self.targets[1].load_flat(f[self.numel:], self.taken)
+
+    def poll(self) -> int:
+        return self.receiver.poll()
+
+    def wait_closed(self) -> None:
+        self.receiver.wait_closed()

@@ -7,11 +7,10 @@ file (replay_memory.py:125-173) -- 233 MB per 5k rows, 1.5 s save / 1.2 s load (
 Two MI355X-native transports, both moving *packed rows* (uint8 frames + fp32 [h|c] x2 +
 scalars, the §2.5 schema) in fixed-size chunks:
 
-* ``RcclTrajectoryChannel`` -- GPU actor groups on one rank, learner replay shard on another:
-  a chunk is one ``dist.send`` of a size tensor + one of a packed byte tensor (device memory,
-  RCCL over xGMI), received with ``dist.recv`` into device memory and scattered into the HBM
-  replay by the ingest kernel (``HBMReplay.ingest_device_record``) -- the bytes never visit the
-  host.
+* ``parallel/channel.py`` + ``parallel/actor_ranks.py`` -- GPU actor groups on one rank, learner
+  replay shard on another: records packed on the device, sent over asynchronous RCCL links,
+  received into device memory and scattered into the HBM replay by the ingest kernel -- the
+  bytes never visit the host.
 * ``ShmTrajectoryWriter/Reader`` -- CPU actor processes on the same host: records go through
   the native shared-memory SPSC ring (``runtime.ShmRing``) -- no files, no pickles, no locks --
   and the learner DMAs them into HBM (``engine/ingest.py``).
@@ -182,41 +181,3 @@ class ShmTrajectoryReader:
 
     def close(self):
         self.ring.close(unlink=True)
-
-
-class RcclTrajectoryChannel:
-    """Point-to-point chunk transport between ranks (device tensors on RCCL, CPU on gloo)."""
-
-    def __init__(self, device, group=None):
-        self.device = torch.device(device)
-        self.group = group
-
-    def send(self, rec, dst: int) -> None:
-        """``rec``: a packed record already in device memory (actor ranks: the pack kernel, see
-        ``parallel.actor_ranks``), or a row dict (tools / tests: packed on the host)."""
-        buf = rec if isinstance(rec, torch.Tensor) else torch.from_numpy(pack_rows(rec)).to(self.device)
-        size = torch.tensor([buf.numel()], dtype=torch.int64, device=self.device)
-        dist.send(size, dst, group=self.group)
-        dist.send(buf, dst, group=self.group)
-
-    def recv(self, src: int, state_shape=None) -> Dict[str, np.ndarray]:
-        """Host copy of a record (tests / tools); the learner path is ``recv_into``."""
-        buf = self._recv_buf(src)
-        return unpack_rows(buf.cpu().numpy(), state_shape)
-
-    def _recv_buf(self, src: int) -> torch.Tensor:
-        size = torch.zeros(1, dtype=torch.int64, device=self.device)
-        dist.recv(size, src, group=self.group)
-        # the record length is the only value read on the host (it sizes the receive buffer)
-        buf = torch.empty(int(size.item()), dtype=torch.uint8, device=self.device)
-        dist.recv(buf, src, group=self.group)
-        return buf
-
-    def recv_into(self, replay, src: int, subring: int) -> int:
-        """Receive one record straight into the HBM replay's sub-ring ``subring``: the payload
-        stays in device memory and the ingest kernel scatters it (no D2H).  Returns rows."""
-        buf = self._recv_buf(src)
-        head = buf[: header_bytes()].cpu().numpy()       # header only (<= 320 bytes)
-        if buf.device != replay.device:                   # gloo (CPU) transport: one H2D copy
-            buf = buf.to(replay.device)
-        return replay.ingest_device_record(buf, head, subring)

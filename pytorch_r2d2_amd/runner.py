@@ -166,13 +166,21 @@ def run_native(cfg: R2D2Config, steps: int = 1000, actor_steps_per_update: int =
 
 def run_split(cfg: R2D2Config, rounds: int = 200, actor_ranks: Optional[int] = None,
               capacity: Optional[int] = None, log_every: int = 50, use_graph: bool = True,
-              backend: str = "auto") -> Dict:
+              backend: str = "auto", learner_steps: Optional[int] = None,
+              actor_delay_s: float = 0.0) -> Dict:
     """Split topology (parallel/actor_ranks.py): learner ranks 0 .. L-1 (data parallel), actor
-    ranks L .. W-1 (``BatchedActor`` groups only).  Per round: every actor rank takes
-    ``dist.push_rows`` env steps and sends one device-packed record to its learner; every learner
-    receives, ingests, then (once every learner shard holds a batch of sequences) trains
-    ``dist.learner_steps_per_round`` steps; every ``dist.publish_rounds`` rounds learner 0
-    broadcasts its weights to the actor ranks.  Returns per-role throughput."""
+    ranks L .. W-1 (``BatchedActor`` groups only), decoupled like the reference's processes:
+
+    * every actor rank runs ``rounds`` rounds of ``dist.push_rows`` env steps and pushes one
+      record per round over its asynchronous link (blocking only when all ``dist.push_slots``
+      records are untaken), taking weight snapshots between rounds;
+    * every learner rank polls its links between steps and ingests what has arrived; once every
+      learner shard holds a batch of sequences the learners train ``learner_steps`` steps
+      (default ``rounds * dist.learner_steps_per_round``) without waiting on any actor, learner
+      0 publishing weights every ``dist.publish_steps`` steps; then they drain the remaining
+      records and close the weight links.
+
+    ``actor_delay_s``: extra host time per round on actor rank W-1 (a slow actor, tests)."""
     import torch.distributed as dist
 
     from .actor_batched import BatchedActor, PackedWeights
@@ -180,10 +188,8 @@ def run_split(cfg: R2D2Config, rounds: int = 200, actor_ranks: Optional[int] = N
     from .engine.learner_engine import LearnerEngine
     from .engine.replay_hbm import HBMReplay
     from .envs.synthetic import VecSyntheticAtari
-    from .parallel.actor_ranks import (TrajectoryPusher, TrajectoryReceiver, broadcast_weights,
-                                       split_roles)
+    from .parallel.actor_ranks import TrajectoryPusher, TrajectoryReceiver, WeightLinks, split_roles
     from .parallel.dist import init_distributed
-    from .parallel.weights import WeightPublisher
     from .utils.faults import Liveness
 
     info = init_distributed(backend=backend)
@@ -195,14 +201,14 @@ def run_split(cfg: R2D2Config, rounds: int = 200, actor_ranks: Optional[int] = N
     W = rc.seq_len + rc.n_step
     # every rank creates the same groups in the same order
     g_learn = dist.new_group(learners) if len(learners) > 1 else None
-    g_bcast = dist.new_group([learners[0]] + actors)
     torch.manual_seed(cfg.seed)
     L = ParamLayout(cfg.model, cfg.env)
     live = Liveness("learner" if info.rank in learners else "actor", info.rank, None)
     out = {"rank": info.rank, "role": "learner" if info.rank in learners else "actor",
            "rounds": rounds, "world": info.world, "actor_ranks": A}
-    P = max(1, int(dc.publish_rounds))
-    version = 0
+    P = max(1, int(dc.publish_steps))
+    if learner_steps is None:
+        learner_steps = rounds * int(dc.learner_steps_per_round)
     if info.rank in learners:
         mine = [a for a in actors if feeds[a] == info.rank]
         n_sub = max(1, E * len(mine))
@@ -211,15 +217,16 @@ def run_split(cfg: R2D2Config, rounds: int = 200, actor_ranks: Optional[int] = N
         eng = LearnerEngine(cfg, replay, dev, rank=learners.index(info.rank), world=len(learners),
                             process_group=g_learn)
         recv = TrajectoryReceiver(replay, mine, E, K)
-        pub = WeightPublisher(L.padded, dev, src_rank=learners[0], group=g_bcast) \
-            if info.rank == learners[0] else None
-        if pub is not None:
-            broadcast_weights(pub, eng, version)
-        steps, t_train, captured = 0, None, False
+        wl = WeightLinks(L.padded, dev, actors, learners[0], "learner") if info.rank == learners[0] else None
+        if wl is not None:
+            wl.publish(eng.master, eng.target)
+        steps, polls, t_train, captured = 0, 0, None, False
         warm = torch.zeros(1, dtype=torch.float32, device=dev)
-        for r in range(rounds):
-            live.tick(r)
-            recv.recv_all()
+        t0 = time.perf_counter()
+        while steps < learner_steps:
+            live.tick(steps)
+            polls += 1
+            got = recv.poll()
             if not captured:
                 # every learner shard must hold a batch of sequences before any of them steps
                 # (the DP step's collectives need all learner ranks in it)
@@ -232,29 +239,39 @@ def run_split(cfg: R2D2Config, rounds: int = 200, actor_ranks: Optional[int] = N
                     captured = True
                     torch.cuda.synchronize(dev)
                     t_train = time.perf_counter()
-            if captured:
-                for _ in range(int(dc.learner_steps_per_round)):
-                    eng.step()
-                    steps += 1
-            if pub is not None and (r + 1) % P == 0:
-                version += 1
-                broadcast_weights(pub, eng, version)
-            if info.rank == learners[0] and log_every and (r + 1) % log_every == 0 and captured:
-                print(f"[split] round {r + 1} learner steps {steps} loss {eng.loss_value():.4f} "
-                      f"rows {recv.rows}", flush=True)
+                elif not got:
+                    time.sleep(0.0005)
+                continue
+            eng.step()
+            steps += 1
+            if wl is not None and steps % P == 0:
+                wl.publish(eng.master, eng.target)
+            if info.rank == learners[0] and log_every and steps % log_every == 0:
+                print(f"[split] learner steps {steps} loss {eng.loss_value():.4f} rows {recv.rows}",
+                      flush=True)
+        torch.cuda.synchronize(dev)
+        t_end = time.perf_counter()
+        recv.drain(rounds)
+        if wl is not None:
+            wl.close()
         torch.cuda.synchronize(dev)
         eng.check_errors()
-        el = time.perf_counter() - t_train if t_train else 0.0
+        el = t_end - t_train if t_train else 0.0
         out.update(learner_steps=steps, learner_steps_per_s=steps / el if el > 0 else 0.0,
-                   rows_ingested=recv.rows, records=recv.records, weights_version=version,
+                   rows_ingested=recv.rows, records=recv.records,
+                   weights_version=wl.published if wl is not None else None,
                    n_valid=int(replay.n_valid.item()), final_loss=eng.loss_value() if steps else None,
+                   ingest_err=int(replay.ingest_err.item()), warm_s=(t_train or t_end) - t0,
                    engine=eng, replay=replay)
     else:
-        cap_e = max(2 * (K + W), 512)
+        cap_e = max(2 * (K + W + rc.n_step), 512)
         replay = HBMReplay(cfg, dev, capacity=cap_e * E, n_subrings=E)
         w_on, w_tg = PackedWeights(L, dev), PackedWeights(L, dev)
-        pub = WeightPublisher(L.padded, dev, src_rank=learners[0], group=g_bcast)
-        broadcast_weights(pub, None, version, (w_on, w_tg))
+        wl = WeightLinks(L.padded, dev, actors, learners[0], "actor")
+        wl.attach(w_on, w_tg)
+        while wl.taken == 0:          # the initial snapshot
+            if wl.poll() == 0:
+                time.sleep(0.0005)
         env = VecSyntheticAtari(E, dev, seed=cfg.seed + 101 * info.rank, episode_len=cfg.env.episode_len,
                                 n_actions=cfg.model.n_actions,
                                 n_stacks=cfg.env.channels_per_frame * cfg.env.n_stacks,
@@ -263,24 +280,31 @@ def run_split(cfg: R2D2Config, rounds: int = 200, actor_ranks: Optional[int] = N
         idx = actors.index(info.rank)
         actor = BatchedActor(cfg, replay, env, w_on, w_tg, global_env_offset=idx * E,
                              total_envs=A * E, seed=cfg.seed + info.rank)
+        # an RCCL send may sit on this chip while the actor keeps stepping: the actor group's
+        # kernels must never need co-residency of the whole grid
+        actor.lstm_step = True
         if use_graph and cfg.actor.use_graph and actor.can_capture:
             actor.capture(warmup=0)
-        push = TrajectoryPusher(replay, K, feeds[info.rank])
+        push = TrajectoryPusher(replay, K, feeds[info.rank], slots=int(dc.push_slots))
+        slow = actor_delay_s if info.rank == actors[-1] else 0.0
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for r in range(rounds):
             live.tick(r)
             for _ in range(K):
                 actor.step()
+            if slow:
+                torch.cuda.synchronize(dev)
+                time.sleep(slow)
             push.push(r)
-            if (r + 1) % P == 0:
-                version += 1
-                broadcast_weights(pub, None, version, (w_on, w_tg))
+            wl.poll()
+        push.finish()
         torch.cuda.synchronize(dev)
         el = time.perf_counter() - t0
+        wl.wait_closed()
         out.update(env_steps=actor.env_steps, env_steps_per_s=actor.env_steps / el,
-                   windows=push.windows, weights_version=w_on.version,
-                   returns=list(actor.finished_returns))
+                   windows=push.windows, weights_version=wl.taken, push_stalls=push.link.stalls,
+                   push_stall_s=push.link.stall_s, returns=list(actor.finished_returns))
     return out
 
 

@@ -72,19 +72,27 @@ def _worker(rank, world, port, outdir):
     wp.publish(on if rank == 0 else None, tg if rank == 0 else None, version=5)
     o, t, v = wp.current()
     res["bcast_ok"] = bool(torch.equal(o, torch.arange(16.0) * 7) and torch.equal(t, -torch.arange(16.0) * 7) and v == 5)
-    # --- trajectory push rank 0 -> rank 1 (packed rows, p2p)
-    from pytorch_r2d2_amd.parallel.trajectory import RcclTrajectoryChannel
+    # --- trajectory push rank 0 -> rank 1 (packed rows over an asynchronous link)
+    from pytorch_r2d2_amd.parallel.channel import LinkReceiver, LinkSender
+    from pytorch_r2d2_amd.parallel.trajectory import pack_rows, unpack_rows
     from pytorch_r2d2_amd.replay import ReplayMemory
-    ch = RcclTrajectoryChannel("cpu")
     m = ReplayMemory(8, 2, 3)
     m.memory["reward"][:, 0] = np.arange(8)
     m.memory["state"][:] = 3
     m.memory["is_seq_start"][[1, 5]] = 1
+    rec = torch.from_numpy(pack_rows(m.memory))
     if rank == 0:
-        ch.send(m.memory, dst=1)
+        tx = LinkSender("traj/0", 1, rec.numel(), 2, "cpu")
+        tx.acquire().copy_(rec)
+        tx.send()
+        tx.flush()
+        tx.close()
     else:
-        got = ch.recv(0, state_shape=(4, 84, 84))
-        res["push_ok"] = all(np.array_equal(got[k], m.memory[k]) for k in m.memory)
+        got = []
+        rx = LinkReceiver(["traj/0"], [0], rec.numel(), "cpu",
+                          lambda i, buf: got.append(unpack_rows(buf.numpy().copy(), (4, 84, 84))))
+        rx.wait_closed()
+        res["push_ok"] = len(got) == 1 and all(np.array_equal(got[0][k], m.memory[k]) for k in m.memory)
     # --- shard totals for two-level sampling
     from pytorch_r2d2_amd.parallel.sharded_replay import gather_stats, local_stats
     st = gather_stats(local_stats(torch.tensor([1.0 + rank]), torch.tensor([10 * (rank + 1)]),
@@ -148,6 +156,8 @@ def test_split_roles_and_record_spec_match_pack_rows():
     assert split_roles(8, 6) == ([0, 1], [2, 3, 4, 5, 6, 7], {2: 0, 3: 1, 4: 0, 5: 1, 6: 0, 7: 1})
     with pytest.raises(ValueError):
         split_roles(2, 2)
+    with pytest.raises(ValueError):     # 7 learner ranks, 1 actor rank: six learners never fed
+        split_roles(8, 1)
     rm = ReplayMemory(13, 8, 3, (84, 84), 256, 4, 4, obs_shape=(4, 84, 84))
     buf = pack_rows(rm.memory)
     hdr, offs, total = record_spec(13, 4 * 84 * 84, 512)
@@ -188,3 +198,87 @@ def test_weight_broadcast_over_actor_rank_group(tmp_path):
     for k in (2, 3):
         for v, (on, tg, ver) in enumerate(r[k]):
             assert ver == v and torch.equal(on, torch.full((10,), float(v + 1))) and torch.equal(tg, -on)
+
+
+
+def _link_worker(rank, world, port, outdir, slow_rank, rounds, steps):
+    """Rank 0: a learner stand-in (2 ms of work per step, polling its record links between steps);
+    ranks 1..: actor stand-ins (2 ms of work per record, ``slow_rank`` 10 ms) that push `rounds`
+    records through a 4-slot LinkSender and take weight snapshots from rank 0 when they arrive."""
+    import time
+    _init(rank, world, port)
+    from pytorch_r2d2_amd.parallel.channel import LinkReceiver, LinkSender
+    nb = 4096
+    res = {}
+    if rank == 0:
+        seen = {i: [] for i in range(world - 1)}
+
+        def on_rec(i, buf):
+            seq = int(buf[:4].view(torch.int32)[0])
+            ok = bool((buf[4:12] == (i * 97 + seq) % 251).all()) and int(buf[-1]) == seq % 256
+            seen[i].append((seq, ok))
+
+        rx = LinkReceiver([f"rec/{a}" for a in range(1, world)], list(range(1, world)), nb, "cpu", on_rec)
+        wtx = [LinkSender(f"w/{a}", a, 64, 1, "cpu", tag=1) for a in range(1, world)]
+        t0 = time.perf_counter()
+        for it in range(steps):
+            end = time.perf_counter() + 0.002          # the learner step
+            while time.perf_counter() < end:
+                pass
+            rx.poll()
+            if it % 25 == 0:                           # weight publication, never waited for
+                for tx in wtx:
+                    if tx.in_flight() == 0:
+                        tx.acquire().fill_(it % 256)
+                        tx.send()
+        res["steps_per_s"] = steps / (time.perf_counter() - t0)
+        rx.wait_for({i: rounds for i in range(world - 1)})
+        for tx in wtx:
+            tx.flush()
+            tx.close()
+        res["seen"] = seen
+    else:
+        got = []
+        tx = LinkSender(f"rec/{rank}", 0, nb, 4, "cpu")
+        wrx = LinkReceiver([f"w/{rank}"], [0], 64, "cpu", lambda i, buf: got.append(int(buf[0])), tag=1)
+        dt = 0.010 if rank == slow_rank else 0.002
+        for r in range(rounds):
+            end = time.perf_counter() + dt             # K env steps
+            while time.perf_counter() < end:
+                pass
+            wrx.poll()
+            b = tx.acquire()
+            b.fill_(0)
+            b[:4] = torch.tensor([r], dtype=torch.int32).view(torch.uint8)
+            b[4:12] = ((rank - 1) * 97 + r) % 251
+            b[-1] = r % 256
+            tx.send()
+        tx.flush()
+        tx.close()
+        wrx.wait_closed()
+        res["weights"] = got
+        res["stalls"] = tx.stalls
+    torch.save(res, os.path.join(outdir, f"link{rank}_{slow_rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_async_links_decouple_learner_from_slow_actor(tmp_path):
+    """Split-topology transport (parallel/channel.py) over gloo, world 3 (1 learner + 2 actor
+    ranks): with one actor rank 5x slower the learner's step rate stays within 10 % of the run
+    with two fast actors (it never waits on a record), and every record of every actor arrives
+    exactly once, in order, intact; weight snapshots reach both actors in publication order."""
+    rounds, steps = 60, 250
+    rates = {}
+    for slow in (0, 2):
+        tmp.spawn(_link_worker, args=(3, _free_port(), str(tmp_path), slow, rounds, steps),
+                  nprocs=3, join=True)
+        r0 = torch.load(os.path.join(tmp_path, f"link0_{slow}.pt"), weights_only=True)
+        rates[slow] = r0["steps_per_s"]
+        for i in (0, 1):
+            assert [s for s, _ in r0["seen"][i]] == list(range(rounds))
+            assert all(ok for _, ok in r0["seen"][i])
+        for a in (1, 2):
+            ra = torch.load(os.path.join(tmp_path, f"link{a}_{slow}.pt"), weights_only=True)
+            assert ra["weights"] and ra["weights"] == sorted(ra["weights"])
+    assert rates[2] >= 0.9 * rates[0], rates

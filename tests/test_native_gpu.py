@@ -333,15 +333,30 @@ def _traj_worker(rank, world, port, outdir):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK="0")
-    from pytorch_r2d2_amd.parallel.trajectory import RcclTrajectoryChannel
+    from pytorch_r2d2_amd.parallel.channel import LinkReceiver, LinkSender
+    from pytorch_r2d2_amd.parallel.trajectory import header_bytes, pack_rows
     dist.init_process_group("gloo")
-    ch = RcclTrajectoryChannel("cpu")
+    recs = [torch.from_numpy(pack_rows(_record(90 + j, 40 + j))) for j in range(2)]
+    nb = max(r.numel() for r in recs)
     if rank == 0:
-        for j in range(2):
-            ch.send(_record(90 + j, 40 + j), 1)
+        tx = LinkSender("traj/0", 1, nb, 2, "cpu")
+        for r in recs:
+            b = tx.acquire()
+            b.zero_()
+            b[: r.numel()].copy_(r)
+            tx.send()
+        tx.flush()
+        tx.close()
     else:
         rp = HBMReplay(_small_cfg(), DEV, capacity=2 * 256, n_subrings=2)
-        got = [ch.recv_into(rp, 0, subring=1) for _ in range(2)]
+        got = []
+
+        def ingest(i, buf):
+            d = buf.to(DEV)
+            got.append(rp.ingest_device_record(d, buf[: header_bytes()].numpy(), subring=1))
+
+        rx = LinkReceiver(["traj/0"], [0], nb, "cpu", ingest)
+        rx.wait_closed()
         torch.cuda.synchronize()
         _check_replay_rows(rp, _record(90, 40), 1, 0)
         _check_replay_rows(rp, _record(91, 41), 1, 90)
@@ -351,7 +366,10 @@ def _traj_worker(rank, world, port, outdir):
     dist.destroy_process_group()
 
 
-def test_trajectory_channel_recv_into_hbm_replay(tmp_path):
+def test_trajectory_link_ingests_into_hbm_replay(tmp_path):
+    """Host-packed records over an asynchronous link (parallel/channel.py, gloo) into a device
+    record buffer and the HBM replay's sub-ring 1 (the ingest kernel): rows bit-identical, the
+    sum tree consistent."""
     import os
     import socket
     import torch.multiprocessing as tmp
@@ -411,12 +429,13 @@ def test_td_row_priorities_last_write_wins(fused):
     assert torch.equal(outs[0], outs[1])
 
 
-def test_actor_rank_window_pack_and_env_major_ingest():
-    """Split topology data path without the network: an actor group's replay windows packed on the
-    device (pack_rows_kernel: K + W - 1 rows per env, only starts whose window lies inside the
-    record) and scattered env-major into a learner replay: every row bit-identical, every learner
-    start a start of the actor with its whole window received, each actor sequence shipped
-    exactly once, the tree consistent."""
+def test_actor_rank_block_pack_and_lagged_ingest():
+    """Split topology data path without the network: an actor group's newest FINAL rows (K per env
+    per round, n steps behind the write head, each row shipped once) packed on the device
+    (pack_rows_kernel) with the start column lagged by W - 1 rows, and scattered env-major into a
+    learner replay (ingest_rows_kernel, start_lag): every row bit-identical to the actor's stream
+    row n earlier, every start set exactly when the last row of its window arrives, a row's own
+    start cleared until then, the tree consistent."""
     import ctypes as C
     from pytorch_r2d2_amd.actor_batched import BatchedActor, PackedWeights
     from pytorch_r2d2_amd.engine.ingest import ingest_args
@@ -427,7 +446,9 @@ def test_actor_rank_window_pack_and_env_major_ingest():
     from pytorch_r2d2_amd.parallel.actor_ranks import TrajectoryPusher
     cfg = _small_cfg()
     E, K = 4, 16
-    W = cfg.replay.seq_len + cfg.replay.n_step
+    n = cfg.replay.n_step
+    W = cfg.replay.seq_len + n
+    lag = W - 1
     act_rp = HBMReplay(cfg, DEV, capacity=E * 128, n_subrings=E)
     L = ParamLayout(cfg.model, cfg.env)
     w = PackedWeights(L, DEV)
@@ -435,36 +456,47 @@ def test_actor_rank_window_pack_and_env_major_ingest():
     w.load(QNet("cpu", cfg.model, cfg.env).state_dict())
     env = VecSyntheticAtari(E, DEV, seed=9, episode_len=23)
     actor = BatchedActor(cfg, act_rp, env, w, w, seed=2)
-    push = TrajectoryPusher(act_rp, K, dst=0)
-    R = push.R
+    push = TrajectoryPusher(act_rp, K, dst=0, link=False)
+    raw = torch.zeros(push.nbytes + 64, dtype=torch.uint8, device=DEV)
+    off = (-raw.data_ptr()) % 64
+    rec = raw[off: off + push.nbytes]
+    rec[: push.hdr.numel()].copy_(push.hdr)
     lrn = HBMReplay(cfg, DEV, capacity=E * 300, n_subrings=E)
+    ca, cl = act_rp.cap_e, lrn.cap_e
+    er = torch.arange(E, device=DEV)[:, None]
+    jr = torch.arange(K, device=DEV)[None, :]
     shipped_starts = 0
     for c in range(12):
         for _ in range(K):
             actor.step()
-        rec = push.pack(c)
-        torch.cuda.synchronize()
-        h_act = (c * K - (W - 1)) % act_rp.cap_e
-        a_rows = (torch.arange(E, device=DEV)[:, None] * act_rp.cap_e
-                  + (h_act + torch.arange(R, device=DEV)[None, :]) % act_rp.cap_e).reshape(-1)
-        h_lrn = lrn.ihead.clone()
-        a = ingest_args(lrn, ptr(rec), push.nbytes, 0, True, rows_per_sub=R)
+        push.pack(c, rec)
+        a = ingest_args(lrn, ptr(rec), push.nbytes, 0, True, rows_per_sub=K, start_lag=lag)
         assert kernels().r2_ingest_record(C.byref(a), C.c_void_p(stream_handle())) == 0
         lrn.repair_after_ingest()
         torch.cuda.synchronize()
-        l_rows = (torch.arange(E, device=DEV)[:, None] * lrn.cap_e
-                  + (h_lrn[:, None] + torch.arange(R, device=DEV)[None, :]) % lrn.cap_e).reshape(-1)
+        a_rows = (er * ca + (c * K + jr - n) % ca).reshape(-1)
+        l_rows = (er * cl + (c * K + jr) % cl).reshape(-1)
         for name in ("frames", "hs_cs", "target_hs_cs", "action", "reward", "done", "priority"):
             assert torch.equal(getattr(lrn, name)[l_rows], getattr(act_rp, name)[a_rows]), (c, name)
-        j = torch.arange(R, device=DEV).repeat(E)
-        keep = (j < K) & (j >= (W - 1 if c == 0 else 0))
-        exp = act_rp.is_start[a_rows].bool() & keep
-        assert torch.equal(lrn.is_start[l_rows].bool(), exp), c
-        assert torch.equal(lrn.tree[l_rows], torch.where(exp, act_rp.tree[a_rows], 0.0)), c
+        # starts: this record marks learner positions cK + j - lag (actor stream rows n earlier);
+        # stream rows < 0 never start; the record's own rows stay non-starts (K < lag)
+        s_l = (er * cl + (c * K + jr - lag) % cl).reshape(-1)
+        s_a = (er * ca + (c * K + jr - lag - n) % ca).reshape(-1)
+        keep = ((c * K + jr - lag - n) >= 0).expand(E, K).reshape(-1)
+        exp = act_rp.is_start[s_a].bool() & keep
+        assert torch.equal(lrn.is_start[s_l].bool(), exp), c
+        assert torch.equal(lrn.tree[s_l], torch.where(exp, act_rp.tree[s_a], 0.0)), c
+        assert not lrn.is_start[l_rows].bool().any(), c
         shipped_starts += int(exp.sum())
-        assert int(lrn.ihead[0]) == (c + 1) * R % lrn.cap_e
+        assert int(lrn.ihead[0]) == (c + 1) * K % cl
     _tree_consistent(lrn)
     assert shipped_starts > 20 and int(lrn.ingest_err.item()) == 0
+    # a record that addresses sub-rings past the replay's is rejected (error word), not written
+    a = ingest_args(lrn, ptr(rec), push.nbytes, 1, True, rows_per_sub=K, start_lag=lag)
+    head = lrn.ihead.clone()
+    assert kernels().r2_ingest_record(C.byref(a), C.c_void_p(stream_handle())) == 0
+    torch.cuda.synchronize()
+    assert int(lrn.ingest_err.item()) != 0 and torch.equal(lrn.ihead, head)
 
 
 def _split_worker(rank, world, port, outdir):
@@ -472,10 +504,10 @@ def _split_worker(rank, world, port, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK="0")
     from pytorch_r2d2_amd.runner import run_split
-    cfg = _small_cfg(**{"actor.envs_per_actor": 8, "dist.push_rows": 16, "dist.publish_rounds": 4,
-                        "learner.publish_interval": 4, "env.episode_len": 30})
+    cfg = _small_cfg(**{"actor.envs_per_actor": 8, "dist.push_rows": 16, "dist.publish_steps": 4,
+                        "env.episode_len": 30})
     out = run_split(cfg, rounds=16, actor_ranks=world - 1, capacity=8 * 600, backend="gloo",
-                    log_every=0)
+                    log_every=0, learner_steps=12)
     keep = {k: v for k, v in out.items() if isinstance(v, (int, float, str)) or v is None}
     if out["role"] == "learner":
         keep["master"] = out["engine"].master.detach().cpu()
@@ -487,7 +519,8 @@ def _split_worker(rank, world, port, outdir):
 
 def test_split_topology_actor_rank_feeds_learner_rank(tmp_path):
     """run_split with 1 learner rank + 1 actor rank sharing this GPU (gloo staging): 16 rounds of
-    device-packed windows -> learner ingest -> training, weights broadcast every 4 rounds."""
+    device-packed blocks over the asynchronous link -> learner ingest -> 12 training steps,
+    weights published every 4 learner steps; every record arrives, nothing is lost."""
     import socket
     import torch.multiprocessing as tmp
     s = socket.socket()
@@ -499,7 +532,7 @@ def test_split_topology_actor_rank_feeds_learner_rank(tmp_path):
     ac = torch.load(tmp_path / "split1.pt", weights_only=True)
     assert lr["role"] == "learner" and ac["role"] == "actor"
     assert ac["windows"] == 16 and lr["records"] == 16
-    assert lr["rows_ingested"] == 16 * 8 * (16 + 12)     # rounds x E x (K + W - 1)
-    assert lr["learner_steps"] > 0 and lr["n_valid"] > 0
-    assert ac["weights_version"] == lr["weights_version"] == 4
+    assert lr["rows_ingested"] == 16 * 8 * 16            # rounds x E x K: each row once
+    assert lr["learner_steps"] == 12 and lr["n_valid"] > 0 and lr["ingest_err"] == 0
+    assert ac["weights_version"] == lr["weights_version"] >= 2
     assert torch.isfinite(lr["master"]).all()

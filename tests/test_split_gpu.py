@@ -275,7 +275,7 @@ def test_engine_fp32_graph_step_and_seaquest_actions():
     assert eng3.error_word() == 0
 
 
-def test_torso_fwd_sp_v2_bit_identical_to_v1():
+def test_torso_fwd_sp_versions_agree():
     """torso_fwd_sp2_kernel (frame in LDS, swizzled act1, conv3 on one wave) with its bf16-split
     conv1 (debug bit 7) keeps v1's accumulation order: every output and saved activation plane
     must match bit for bit, over 4 jobs with uneven frame counts (partial last rounds) and
@@ -323,15 +323,20 @@ def test_torso_fwd_sp_v2_bit_identical_to_v1():
             k.r2_torso_sp_debug(0)
         return outs
 
-    v1, v2, v2i = run(8), run(128), run(0)
-    for (a, sa1, sa2), (b, sb1, sb2), (c, sc1, sc2) in zip(v1, v2, v2i):
+    v1, v2, v2i, v3 = run(8), run(128), run(0), run(256)
+    both = lambda x: x[0].double() + x[1].double()   # noqa: E731
+    for (a, sa1, sa2), (b, sb1, sb2), (c, sc1, sc2), (d, sd1, sd2) in zip(v1, v2, v2i, v3):
         assert torch.equal(a, b)
-        assert not (a == 7.0).any() and not (c == 7.0).any()
-        both = lambda x: x[0].double() + x[1].double()   # noqa: E731
+        assert not (a == 7.0).any() and not (c == 7.0).any() and not (d == 7.0).any()
         assert _rel(both(c), both(a)) < 5e-6
+        # v3 (pipelined roles, 32-wide K steps): conv1 bit-identical to v2's int8 path (same
+        # digits, same epilogue), conv2 / conv3 to fp32 rounding
+        assert _rel(both(d), both(c)) < 5e-6
         if sa1 is not None:
             assert torch.equal(sa1, sb1) and torch.equal(sa2, sb2)
             assert _rel(both(sc1), both(sa1)) < 5e-6 and _rel(both(sc2), both(sa2)) < 5e-6
+            assert torch.equal(sd1, sc1)
+            assert _rel(both(sd2), both(sc2)) < 5e-6
 
 
 def test_td_fused_dh_matches_fp64_split():

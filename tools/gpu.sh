@@ -73,6 +73,22 @@ case "$cmd" in
     python tools/pmc_summary.py "gpurun_out/pmc_$tag/p*/**/*counter_collection.csv" "${filters[@]}" \
       > gpurun_out/pmc_$tag/summary.txt
     head -60 gpurun_out/pmc_$tag/summary.txt ;;
+  pmcmicro)
+    # the pmc passes over a micro-benchmark instead of the bench step: pmcmicro TAG script args...
+    tag=$1; shift
+    mkdir -p gpurun_out/pmc_$tag
+    i=0
+    for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
+               "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_ACTIVE_INST_LDS" \
+               "SQ_INSTS_VALU SQ_INSTS_VALU_MFMA_BF16 SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_SALU" \
+               "SQ_INSTS_VMEM_RD SQ_INSTS_LDS_STORE SQ_INSTS_LDS_LOAD SQ_WAIT_INST_ANY"; do
+      i=$((i+1))
+      timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d gpurun_out/pmc_$tag/p$i -- \
+        python "$@" > gpurun_out/pmc_$tag/p$i.log 2>&1 || fail "pmcmicro pass $i" gpurun_out/pmc_$tag/p$i.log
+    done
+    python tools/pmc_summary.py "gpurun_out/pmc_$tag/p*/**/*counter_collection.csv" \
+      > gpurun_out/pmc_$tag/summary.txt
+    cat gpurun_out/pmc_$tag/summary.txt ;;
   bytes)
     # HBM-side byte counters per kernel (roofline input): FETCH_SIZE (3 TCC slots) and WRITE_SIZE
     # (2) in passes of their own, MFMA busy cycles beside them

@@ -77,6 +77,31 @@ if which in ("torso", "both"):
     n_cus = torch.cuda.get_device_properties(0).multi_processor_count
     res["torso_fwd_sp_us_10560"] = timeit(lambda: k.r2_torso_fwd_sp_multi(
         ptr(frames), jobs.ctypes.data, 4, n_cus, stream_handle()))
+    if "ab" in sys.argv:
+        # v3 (debug bit 8) vs v2 (int8 conv1), interleaved, min of the per-round means
+        best = {}
+        for _ in range(5):
+            for bits, name in ((256, "v3"), (0, "v2")):
+                k.r2_torso_sp_debug(bits)
+                t = timeit(lambda: k.r2_torso_fwd_sp_multi(ptr(frames), jobs.ctypes.data, 4, n_cus,
+                                                           stream_handle()))
+                best[name] = min(best.get(name, 1e30), t)
+        k.r2_torso_sp_debug(0)
+        res.update({f"torso_{k_}_us": round(v, 1) for k_, v in best.items()})
+    if "probe3" in sys.argv:
+        # v3 per-wave clock stamps of workgroup 0: [wave][iteration][loop top, conv3 / staging done,
+        # conv1 / conv2 done, after the barrier]; mean cycles per segment over iterations 3..12
+        tr = torch.zeros(8 * 16 * 4, dtype=torch.int64, device=DEV)
+        k.r2_torso_sp_trace(ptr(tr))
+        k.r2_torso_sp_debug(256)
+        k.r2_torso_fwd_sp_multi(ptr(frames), jobs.ctypes.data, 4, n_cus, stream_handle())
+        torch.cuda.synchronize()
+        k.r2_torso_sp_debug(0)
+        k.r2_torso_sp_trace(0)
+        t = tr.view(8, 16, 4).cpu().double()
+        seg = {"a": t[:, 3:13, 1] - t[:, 3:13, 0], "b": t[:, 3:13, 2] - t[:, 3:13, 1],
+               "wait": t[:, 3:13, 3] - t[:, 3:13, 2], "iter": t[:, 4:14, 0] - t[:, 3:13, 0]}
+        res["v3_segments_cycles_per_wave"] = {n: [round(v, 0) for v in x.mean(1).tolist()] for n, x in seg.items()}
     if "probe" in sys.argv:
         # phase costs: skip conv1 / conv2 / conv3 (timing only) etc.; variants interleaved over 7
         # rounds, min of the per-round means (single back-to-back timings drift by +-15 %)
