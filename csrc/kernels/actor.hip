@@ -72,6 +72,7 @@ struct ActArgs {
   const float* env_finished;  // (E)
   float* ret_ring;            // (R)
   int64_t* ret_cnt;           // (1)
+  int* ret_env;               // (R) env of each ring return (per-epsilon return statistics)
   int* marks;                 // (E * (n + 2)) start rows to mark, -1 = none
   int* pend;                  // deferred mode: pending start edits (mark row | clear -2-row)
   int* pend_cnt;              // (1) entries appended (reset by the learner's apply)
@@ -213,7 +214,11 @@ __global__ __launch_bounds__(256) void actor_post_kernel(const ActArgs a) {
     int before = 0;
     for (int j = tid; j < e; j += blockDim.x) before += a.env_done[j] != 0;
     before = (int)wave_sum((float)before);   // blockDim == 64
-    if (tid == 0) a.ret_ring[pymod(*a.ret_cnt + before, a.R)] = a.env_finished[e];
+    if (tid == 0) {
+      const long long slot = pymod(*a.ret_cnt + before, a.R);
+      a.ret_ring[slot] = a.env_finished[e];
+      a.ret_env[slot] = e;
+    }
   }
   if (tid != 0) return;
   // this step enters the n-step history

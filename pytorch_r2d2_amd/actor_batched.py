@@ -47,8 +47,8 @@ class ActArgs(ctypes.Structure):
         (name, _VP * 2) for name in ("st_h", "st_c", "h_new", "c_new", "h32", "c", "h_bf")] + [
         (name, _VP) for name in (
             "h_row", "h_q", "h_a", "h_r", "h_step", "h_valid", "ep_start", "t", "head", "eps", "act",
-            "env_reward", "env_done", "env_finished", "ret_ring", "ret_cnt", "marks", "pend",
-            "pend_cnt")] + [
+            "env_reward", "env_done", "env_finished", "ret_ring", "ret_cnt", "ret_env", "marks",
+            "pend", "pend_cnt")] + [
         ("FB", ctypes.c_longlong), ("seed", ctypes.c_ulonglong)] + [
         (name, ctypes.c_int) for name in ("E", "A", "H", "n", "T", "stride", "cap_e", "W", "wrap",
                                           "max_dirty", "R", "value_rescale", "pend_cap",
@@ -157,8 +157,12 @@ class BatchedActor:
         self.marks = z(E * (n + 2), dt=torch.int32)
         self.ret_ring = z(self.R + 1)
         self.ret_cnt = z(1, dt=torch.int64)
+        self.ret_env = z(self.R + 1, dt=torch.int32)
         self._ret_read = 0
         self._returns = []
+        self._return_envs = []
+        self.global_env_offset = int(global_env_offset)
+        self.eps_host = [float(x) for x in eps]
         self.env_steps = 0
         self.graphs = None
         # concurrent topology (engine/concurrent.py): start edits go to one of two pending lists
@@ -192,9 +196,25 @@ class BatchedActor:
         lo = max(self._ret_read, cnt - self.R)
         if cnt > lo:
             ring = self.ret_ring[: self.R].cpu()
+            envs = self.ret_env[: self.R].cpu()
             self._returns.extend(float(ring[i % self.R]) for i in range(lo, cnt))
+            self._return_envs.extend(int(envs[i % self.R]) for i in range(lo, cnt))
         self._ret_read = cnt
         return self._returns
+
+    def returns_by_epsilon(self, last: int = 256, buckets: int = 4) -> Dict[str, float]:
+        """Mean return of the last ``last`` finished episodes per epsilon bucket (the Ape-X ladder
+        split into ``buckets`` contiguous env ranges, keyed by the bucket's mean epsilon): the
+        reference prints every actor's return next to its fixed epsilon (actor.py:109-110)."""
+        rets = self.finished_returns[-last:]
+        envs = self._return_envs[-len(rets):] if rets else []
+        out: Dict[str, list] = {}
+        for r, e in zip(rets, envs):
+            b = min(buckets - 1, e * buckets // max(self.E, 1))
+            lo_, hi_ = b * self.E // buckets, max(b * self.E // buckets + 1, (b + 1) * self.E // buckets)
+            key = f"{sum(self.eps_host[lo_:hi_]) / (hi_ - lo_):.3g}"
+            out.setdefault(key, []).append(r)
+        return {k: float(np.mean(v)) for k, v in sorted(out.items(), key=lambda kv: -float(kv[0]))}
 
     # ------------------------------------------------------------------ inference
     def _infer(self):
@@ -299,7 +319,8 @@ class BatchedActor:
                         ("h_row", self.h_row), ("h_q", self.h_q), ("h_a", self.h_a), ("h_r", self.h_r),
                         ("h_step", self.h_step), ("h_valid", self.h_valid), ("ep_start", self.ep_start),
                         ("t", self.t_d), ("head", self.head_d), ("eps", self.eps), ("act", self.act),
-                        ("ret_ring", self.ret_ring), ("ret_cnt", self.ret_cnt), ("marks", self.marks)):
+                        ("ret_ring", self.ret_ring), ("ret_cnt", self.ret_cnt), ("ret_env", self.ret_env),
+                        ("marks", self.marks)):
             setattr(a, name, ptr(t))
         for i, key in enumerate(("on", "tg")):
             a.st_h[i] = ptr(self.h32[key] if pre else self.h32_new[key])

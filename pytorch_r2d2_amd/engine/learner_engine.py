@@ -1258,6 +1258,27 @@ class LearnerEngine:
     def loss_value(self) -> float:
         return float(self.loss.item())
 
+    @torch.no_grad()
+    def stats(self) -> Dict[str, float]:
+        """Learner diagnostics of the last step (the reference prints only a step
+        count, ``/root/reference/learner.py:57-59``): loss, Q(s, .) of the online net over the
+        learning rows (mean, mean of max_a, max), |TD error| (mean, max: the priority input),
+        IS weights (mean, min), the replay's sampleable sequences, fill and priority total (the
+        sum tree's root).  One D2H copy; call at log cadence, not per step."""
+        rp = self.replay
+        N = self.Ll * self.B
+        q = self.q_on[:N]
+        td = self.td_abs[:N]
+        root = rp.tree[int(rp.tree_offs[-1]): int(rp.tree_offs[-1]) + 1]
+        v = torch.stack([self.loss.reshape(()), q.mean(), q.max(1).values.mean(), q.max(),
+                         td.mean(), td.max(), self.is_w.mean(), self.is_w.min(),
+                         root.reshape(()).float(), rp.n_valid.reshape(()).float()]).tolist()
+        keys = ("loss", "q_mean", "q_max_a_mean", "q_max", "td_abs_mean", "td_abs_max",
+                "is_w_mean", "is_w_min", "priority_sum", "n_valid")
+        out = dict(zip(keys, v))
+        out["replay_fill"] = rp.size / rp.capacity
+        return out
+
     def error_word(self) -> int:
         """The persistent kernels' error word (non-zero: a bounded hand-off spin timed out, so the
         step's recurrent state is garbage).  One D2H read."""

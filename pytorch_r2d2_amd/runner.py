@@ -122,15 +122,16 @@ def run_native(cfg: R2D2Config, steps: int = 1000, actor_steps_per_update: int =
         if (it + 1) % log_every == 0 or it == steps - 1:
             if drv is not None:
                 torch.cuda.current_stream(dev).wait_stream(drv.s_learn)
-            loss = eng.loss_value()
+            st = eng.stats()
+            loss = st["loss"]
             losses.append(loss)
             rets = actor.finished_returns[-64:]
             el = time.perf_counter() - t1
-            rec = dict(step=it + 1, loss=loss, replay_rows=replay.size,
-                       n_valid=int(replay.n_valid.item()), env_steps=actor.env_steps,
+            rec = dict(step=it + 1, replay_rows=replay.size, env_steps=actor.env_steps,
                        mean_return=float(np.mean(rets)) if rets else None,
+                       return_by_eps=actor.returns_by_epsilon(),
                        learner_steps_per_s=(it + 1) / el, dp_imbalance=eng.dp_imbalance(),
-                       env_steps_per_s=(actor.env_steps - env0) / el)
+                       env_steps_per_s=(actor.env_steps - env0) / el, **st)
             if mlog:
                 mlog.log("native", **rec)
             if info.is_main:
@@ -393,9 +394,8 @@ def run_native_cpu_actors(cfg: R2D2Config, n_actors: int, steps: int = 1000,
                 ingest.check_errors()
             weights.poll()
             if it % log_every == 0 or it == steps:
-                loss = eng.loss_value()
-                rec = dict(step=it, loss=loss, rows=ingest.rows, records=ingest.records,
-                           learner_steps_per_s=it / (time.perf_counter() - t_train0))
+                rec = dict(step=it, rows=ingest.rows, records=ingest.records,
+                           learner_steps_per_s=it / (time.perf_counter() - t_train0), **eng.stats())
                 if mlog:
                     mlog.log("native_cpu", **rec)
                 print("[native-cpu]", rec, flush=True)
