@@ -290,7 +290,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp_kernel(const TSArgs args) {
 // jobs: njobs x TS_JOB_WORDS int64 {rows, n, w1, w1l, b1, w2, w2l, b2, w3, w3l, b3, out, out_l,
 // s1, s1l, s2, s2l, 0, 0, 0}.  grid <= 0: one workgroup per CU (the caller passes the CU count).
 // ============================================================================================
-// Forward v2 (the default): the v1 profile (tools/sp_micro.py probe, profiles/r02_torso_sp_*)
+// Forward v2 (the default): the v1 profile (tools/sp_micro.py probe, profiles/archive/r02_torso_sp_*)
 // showed conv1's B fragments (two 4-byte buffer loads per K step from L1 / L2) and conv3's W3
 // fragments (L2, re-read by two waves per frame: 72 KB / frame) latency-bound, the next-frame
 // warm-up waited on inside phase B, and 2-3-way bank conflicts on the padded act1 image.  v2:
@@ -955,7 +955,9 @@ __global__ __launch_bounds__(512) void torso_fwd_sp3_kernel(const TSArgs args) {
         // one 4x4-pixel tile: 12 int8 MFMAs (3 digits x 4 K blocks) + the epilogue; the next
         // tile's fragments are loaded (into `nx`) before the MFMAs
         auto tile = [&](int t, const i32x4_t (&cur)[4], i32x4_t (&nx)[4]) {
-          if (t + 1 < t_end) ldb(t + 1, nx);
+          // unconditional (the last tile re-reads itself): a prefetch under a branch made the
+          // compiler's lgkmcnt bookkeeping wait for it before the current tile's MFMAs
+          ldb(min(t + 1, t_end - 1), nx);
           __builtin_amdgcn_sched_barrier(0);
           i32x4_t acc[3];
           acc[0] = sc0;

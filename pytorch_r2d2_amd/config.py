@@ -122,11 +122,9 @@ class LearnerConfig:
     lstm_xcd_pairs: bool = True
     # split precision (compute_dtype fp32) GEMMs: "fused" = gemm_sp.hip (hi / lo planes staged
     # once, 3 MFMAs per fragment pair: x-projection 164 -> 125 us, post-BPTT group 142 -> 106 us
-    # at K splits 4,4,4,1, dh 26 -> 18 us; profiles/r02_gemm_sp_micro_v1.txt) | "multipass"
+    # at K splits 4,4,4,1, dh 26 -> 18 us; profiles/archive/r02_gemm_sp_micro_v1.txt) | "multipass"
     sp_gemm: str = "fused"
     sp_group_splits: str = "4,4,4,1"  # K splits of the fused post-BPTT group (dW_ih, dW_hh, dW_head1, dX)
-    sp_group_cfg: int = -1            # its tile (ops/gemm.py G5_CFGS index); -1 = the CU-round model
-    sp_heads_cfg: int = -1            # tile of the heads' layer-1 split GEMM (same convention)
     # split GEMMs on gemm6 (gemm_sp.hip: the fragment planes refilled between the three product
     # passes, one barrier per LDS tile; the heads' layer-1 GEMMs join the one-pass kernel too):
     # x-projection 115-129 -> 102-110 us, tools/gemm6_probe.py
@@ -134,12 +132,6 @@ class LearnerConfig:
     # split precision: the dueling head's gradient reduction on the BPTT launch's idle workgroups
     # (r2_lstm_bwd_tag_sp_hg) instead of its own 28 us launch
     sp_head_grads_in_bptt: bool = True
-    # single-GPU step: the priority refresh + tree repair (they need only the TD's priorities) run
-    # on a side stream beside the BPTT, whose persistent launch leaves most CUs idle; the step
-    # counter follows the optimizer update on the main stream.  Off: the 16 us tail does leave the
-    # critical path, but the two-queue graph pays it back at the graph boundary (same-box A/B
-    # 0.9987 / 0.9984 / 1.0017 vs 0.9995 / 1.0001 / 1.0017 ms, profiles/r03_prio_side_stream_ab.txt)
-    prio_side_stream: bool = False
     torso_bwd: str = "fused"         # fused (HIP kernel) | library (MIOpen convolution_backward)
     # library conv path (frame geometries without the fused HIP torso, e.g. DMLab): MIOpen find
     # mode (torch.backends.cudnn.benchmark) instead of its immediate-mode heuristics

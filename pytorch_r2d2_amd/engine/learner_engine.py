@@ -446,7 +446,7 @@ class LearnerEngine:
             probs = [Gemm(h, pk["head1"].t(), zb, a_lo=hl, b_lo=pkl["head1"].t())
                      for (pk, h, zb, _, _), (pkl, hl) in zip(jobs, lo)]
             if self.cfg.learner.sp_gemm6 and self.cfg.learner.sp_gemm == "fused":
-                self._gemm_sp("heads", probs, cfg=int(self.cfg.learner.sp_heads_cfg))   # gemm6
+                self._gemm_sp("heads", probs, cfg=-1)   # gemm6
             else:
                 gemm(*probs)
             zs = [zb for _, _, zb, _, _ in jobs]
@@ -754,7 +754,7 @@ class LearnerEngine:
         if self.cfg.learner.sp_gemm == "fused":
             splits = [int(v) for v in self.cfg.learner.sp_group_splits.replace(":", ",").split(",")]
             self._gemm_sp("group", [w_jobs[2], w_jobs[1], w_jobs[0], x_job], splits,
-                          cfg=int(self.cfg.learner.sp_group_cfg))
+                          cfg=-1)
             self._dX = self.dX
             return
         splits = self._group_splits(w_jobs, x_job)
@@ -1059,45 +1059,21 @@ class LearnerEngine:
         self._priorities()
 
     def _single_body(self, timer=None):
-        """The world == 1 step as stream operations (eager or captured).  With
-        ``learner.prio_side_stream`` the priority refresh + tree repair (they read only the TD's
-        priorities and the sampled starts) run on a side stream beside the BPTT, whose persistent
-        launch occupies 64 of the chip's CUs: the main stream records an event after the TD and
-        issues its own launches first (so the graph keeps the critical path on the launch's queue),
-        the side stream waits on that event, its tree tail resets the dirty list, and the step
-        counter is advanced on the main stream after the optimizer / target-sync launches read it.
-        The side stream is joined at the very end (no launch waits on it inside the step)."""
+        """The world == 1 step as stream operations (eager or captured).  (Running the priority
+        refresh + tree repair on a side stream beside the BPTT was measured neutral and removed:
+        profiles/r03_prio_side_stream_ab.txt.)"""
         import contextlib
         ph = timer.phase if timer is not None else (lambda name: contextlib.nullcontext())
-        side = self.cfg.learner.prio_side_stream and self.device.type == "cuda"
         with ph("forward+td"):
             self._forward_loss()
-        if side:
-            main = torch.cuda.current_stream(self.device)
-            if getattr(self, "_prio_stream", None) is None:
-                self._prio_stream = torch.cuda.Stream(device=self.device)
-                self._prio_event = torch.cuda.Event()
-            ps = self._prio_stream
-            self._prio_event.record(main)
         with ph("backward_core"):
             self._backward_core()
         with ph("backward_torso"):
             self._seg_torso()
         with ph("update"):
             self._update()
-        if side:
-            self.replay.step_inc()
-            ps.wait_event(self._prio_event)
-            with torch.cuda.stream(ps):
-                rp = self.replay
-                rp.refresh_sequences(self.starts, self.B, self.Lb, self.T)
-                if not (self.cfg.replay.fused_tree_tail and rp.update_tree_and_reset_dirty()):
-                    rp.update_tree()
-                    rp.reset_dirty()
-            main.wait_stream(ps)
-        else:
-            with ph("priorities"):
-                self._priorities()
+        with ph("priorities"):
+            self._priorities()
 
     # DP (world > 1): the priority refresh + tree repair need only the forward's TD errors, so
     # they run while the torso bucket is all-reduced; the update and the step counter follow

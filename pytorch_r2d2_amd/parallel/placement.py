@@ -2,7 +2,7 @@
 
 An MI355X exposes 256 CUs in 8 XCDs.  A HIP stream can be restricted to a CU subset
 (``hipExtStreamCreateWithCUMask``); measured on the device (``tools/cumask_probe.py``,
-``profiles/r02_cumask_probe.txt``): mask bit ``i`` selects a CU of XCD ``i % 8``, so the first
+``profiles/archive/r02_cumask_probe.txt``): mask bit ``i`` selects a CU of XCD ``i % 8``, so the first
 ``8 k`` bits give every XCD ``k`` CUs and their complement gives every XCD ``32 - k``.  Both roles
 therefore keep all 8 L2 slices and every XCD-aware tiling stays balanced.
 

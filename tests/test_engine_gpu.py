@@ -110,28 +110,6 @@ def test_engine_graph_replay_matches_eager():
     assert _rel(rp2.tree, rp.tree) < 1e-5
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
-def test_priority_side_stream_matches_serial_tail(dtype):
-    """learner.prio_side_stream: the priority refresh + tree repair on a side stream beside the
-    BPTT (graph-captured fork / join) give the same weights, tree, priorities and step counter as
-    the serial tail, step for step, including the target-sync step of a short interval."""
-    over = {"learner.compute_dtype": dtype, "learner.target_update_interval": 2}
-    _, rp, eng, _, _ = _make("fixed", B=8, **{**over, "learner.prio_side_stream": True})
-    _, rp2, eng2, _, _ = _make("fixed", B=8, **{**over, "learner.prio_side_stream": False})
-    eng.capture(warmup=0)
-    eng2.capture(warmup=0)
-    for _ in range(4):
-        eng.step()
-        eng2.step()
-    torch.cuda.synchronize()
-    assert torch.equal(rp.step, rp2.step) and int(rp.step.item()) == 4
-    assert torch.equal(rp.dirty_count, rp2.dirty_count)
-    for a, b in ((eng.master, eng2.master), (eng.target, eng2.target),
-                 (rp.priority, rp2.priority), (rp.tree, rp2.tree)):
-        assert _rel(a, b) < 1e-6
-    assert eng.error_word() == 0
-
-
 def test_engine_resume_from_full_checkpoint(tmp_path):
     from pytorch_r2d2_amd.utils.checkpoint import load_full_checkpoint, save_full_checkpoint
     cfg, rp, eng, net, tgt = _make("shifted", B=8)
