@@ -797,8 +797,9 @@ constexpr int A2P = 81 * 64;                 // one act2 plane
 constexpr int OFF_A2 = OFF_A1 + 4 * A1P;     // 134912: [buffer 2][hi, lo]
 constexpr int OFF_B = OFF_A2 + 4 * A2P;      // 155648: biases conv2, conv3, conv1
 constexpr int OFF_SC = OFF_B + 96 * 4;       // 156032: int8 conv1 row corrections [2][32]
-constexpr int OFF_FLAG = OFF_SC + 64 * 4;    // 156288: frame-ready counter
-constexpr int LDS_BYTES = OFF_FLAG + 16;     // 156304
+constexpr int OFF_FLAG = OFF_SC + 64 * 4;    // 156288: frame-ready counter, staging-drained counter
+constexpr int OFF_ST = OFF_FLAG + 16;        // 156304: conv3 output staging [hi, lo][1568] bf16 (CHW)
+constexpr int LDS_BYTES = OFF_ST + 2 * 1568 * 2;   // 162576
 constexpr int NBLK = 4 * 441;                // s2d blocks per frame
 constexpr int PFQ = (NBLK + 255) / 256;      // blocks per C2 thread (7)
 static_assert(LDS_BYTES <= 160 * 1024, "LDS");
@@ -818,12 +819,18 @@ __device__ __forceinline__ void fr3_block(int b, int& src, int& dst) {
   dst = ci * tsp3::FRP + (r * 24 + c) * 16;
 }
 
+// D2 / D3: depth of the conv2 / conv3 LDS operand rings (K steps in flight)
+template <int D2, int D3>
 __global__ __launch_bounds__(512) void torso_fwd_sp3_kernel(const TSArgs args) {
   using namespace tsp3;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   float* lb = (float*)(lds + OFF_B);
   int* flag = (int*)(lds + OFF_FLAG);
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  int* drained = flag + 1;   // staging copies done (C2 waves, one add per wave per frame)
+  bf16* st = (bf16*)(lds + OFF_ST);
+  // the wave index through readfirstlane: every role / tile decision and its index math is
+  // then scalar (SALU), not repeated per lane on the VALU the conv1 epilogue needs
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int l16 = lane & 15, kq = lane >> 4;
   const int wk = blockIdx.x;
   int ji = 0;
@@ -844,7 +851,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp3_kernel(const TSArgs args) {
   const float c1_scale = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(
       c1_digits(J.w1, J.w1l, tid, lds + OFF_A1, (int*)(lds + OFF_SC), (float*)(lds + OFF_A1 + 3 * 8192)))));
   if (tid < 96) lb[tid] = tid < 32 ? J.b2[tid] : tid < 64 ? J.b3[tid - 32] : J.b1[tid - 64];
-  if (tid == 0) *flag = 0;
+  if (tid == 0) { *flag = 0; *drained = 0; }
   {
     const __amdgpu_buffer_rsrc_t frs = ts_rsrc(args.frames + frame_row(0) * IN_BYTES, IN_BYTES);
 #pragma unroll
@@ -892,49 +899,49 @@ __global__ __launch_bounds__(512) void torso_fwd_sp3_kernel(const TSArgs args) {
     const int t_beg = grp ? 13 : 0, t_end = grp ? 25 : 13;
     // lane-constant parts of the conv1 fragment / epilogue offsets
     const int fr_lane = OFF_FR + kq * FRP + ((l16 >> 2) * 24 + (l16 & 3)) * 16;
+    // conv3: the act2 operand offsets of both tiles (frame-invariant) and the output pixels
+    int o3[2][9], p3[2];
+    bool ok3[2];
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int t = 2 * grp + tt;
+      const int y3 = (t >> 1) * 4 + (l16 >> 2), x3 = (t & 1) * 4 + (l16 & 3);
+      const int yc = min(y3, 6), xc = min(x3, 6);
+#pragma unroll
+      for (int s_ = 0; s_ < 9; ++s_) o3[tt][s_] = a2v3_off(yc + s_ / 3, xc + s_ % 3, kq);
+      p3[tt] = y3 * 7 + x3;
+      ok3[tt] = y3 < 7 && x3 < 7;
+    }
     for (int i = 0; i < nf + 2; ++i) {
       TS3_STAMP(i, 0);
-      if (i >= 2) {
-        // conv3(f_{i-2}): act2 buffer (i-2)&1, two 4x4 tiles of the 7x7 output
+      f32x4 acc3[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      if (i >= 2 && !(args.dbg & 16384)) {   // (bit 14: timing probe without conv3)
+        // conv3(f_{i-2}): act2 buffer (i-2)&1, two 4x4 tiles of the 7x7 output (accumulators
+        // held until the staging write after conv1)
         const int k = i - 2;
         const uint8_t* a2h = lds + OFF_A2 + (k & 1) * 2 * A2P;
         const uint8_t* a2l = a2h + A2P;
-        const size_t fo = (size_t)(first + k * stride) * 1568;
-#pragma unroll 1
+#pragma unroll
         for (int tt = 0; tt < 2; ++tt) {
-          const int t = 2 * grp + tt;
-          const int y3 = (t >> 1) * 4 + (l16 >> 2), x3 = (t & 1) * 4 + (l16 & 3);
-          const int yc = min(y3, 6), xc = min(x3, 6);
-          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-          bf16x8 rh[2], rl[2];
+          f32x4& acc = acc3[tt];
+          bf16x8 rh[D3], rl[D3];
           auto ld = [&](int s, bf16x8& h, bf16x8& l) {
-            const int o = a2v3_off(yc + s / 3, xc + s % 3, kq);
-            h = *(const bf16x8*)(a2h + o);
-            l = *(const bf16x8*)(a2l + o);
+            h = *(const bf16x8*)(a2h + o3[tt][s]);
+            l = *(const bf16x8*)(a2l + o3[tt][s]);
           };
-          ld(0, rh[0], rl[0]);
-          ld(1, rh[1], rl[1]);
+#pragma unroll
+          for (int s = 0; s < D3; ++s) ld(s, rh[s], rl[s]);
 #pragma unroll
           for (int s = 0; s < 9; ++s) {
-            const bf16x8 h = rh[s & 1], l = rl[s & 1];
-            if (s + 2 < 9) ld(s + 2, rh[s & 1], rl[s & 1]);
+            const bf16x8 h = rh[s % D3], l = rl[s % D3];
+            if (s + D3 < 9) ld(s + D3, rh[s % D3], rl[s % D3]);
             __builtin_amdgcn_sched_barrier(0);
             acc = mfma16_x3(w3h[s], w3l[s], h, l, acc);
-          }
-          if (y3 < 7 && x3 < 7) {
-            bf16* oh = J.out + fo + y3 * 7 + x3;
-            bf16* ol = J.out_l + fo + y3 * 7 + x3;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float v = fmaxf(acc[e] + b3v[e], 0.f);
-              oh[(ch0 + e) * 49] = (bf16)v;
-              ol[(ch0 + e) * 49] = sp_lo(v);
-            }
           }
         }
       }
       TS3_STAMP(i, 1);
-      if (i < nf) {
+      if (i < nf && !(args.dbg & 4096)) {   // (bit 12: timing probe without conv1)
         if (i >= 1) {   // frame f_i staged by the C2 waves
           while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 4 * i)
             __builtin_amdgcn_s_sleep(1);
@@ -997,6 +1004,25 @@ __global__ __launch_bounds__(512) void torso_fwd_sp3_kernel(const TSArgs args) {
           if (t + 1 < t_end) tile(t + 1, bB, bA);
         }
       }
+      if (i >= 2) {
+        // conv3(f_{i-2}) -> the CHW staging image, once the C2 waves have copied f_{i-3}'s out
+        // (they do so at the start of iteration i: this wait is normally already satisfied)
+        if (i >= 3) {
+          while (__hip_atomic_load(drained, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 4 * (i - 2))
+            __builtin_amdgcn_s_sleep(1);
+        }
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+          if (ok3[tt]) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float v = fmaxf(acc3[tt][e] + b3v[e], 0.f);
+              st[(ch0 + e) * 49 + p3[tt]] = (bf16)v;
+              st[1568 + (ch0 + e) * 49 + p3[tt]] = sp_lo(v);
+            }
+          }
+        }
+      }
       TS3_STAMP(i, 2);
       lds_sync();
       TS3_STAMP(i, 3);
@@ -1022,8 +1048,23 @@ __global__ __launch_bounds__(512) void torso_fwd_sp3_kernel(const TSArgs args) {
     }
     __syncthreads();   // pairs the C1 waves' digit barrier
     u32x4 pf[PFQ];
+    // the staged conv3 outputs of frame k (CHW hi / lo, 2 x 196 16-byte chunks) -> global
+    auto drain = [&](int k) {
+      const size_t fo = (size_t)(first + k * stride) * 1568;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int c = tid + 256 * q;          // chunk: plane c / 196, 8 bf16 each
+        if (c < 392) {
+          const int pl = c >= 196, cc = c - 196 * pl;
+          const u32x4 v = *(const u32x4*)(st + pl * 1568 + cc * 8);
+          if (!(args.dbg & 1024)) *(u32x4*)((pl ? J.out_l : J.out) + fo + cc * 8) = v;
+        }
+      }
+      if (lane == 0) __hip_atomic_fetch_add(drained, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
     for (int i = 0; i < nf + 2; ++i) {
       TS3_STAMP(i, 0);
+      if (i >= 3) drain(i - 3);
       if (i >= 1 && i < nf) {
         // frame f_i -> LDS (conv1(f_{i-1}) finished reading the image at the last barrier)
 #pragma unroll
@@ -1031,7 +1072,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp3_kernel(const TSArgs args) {
           if (tid + 256 * q < NBLK) *(u32x4*)(lds + OFF_FR + fdst[q]) = pf[q] ^ 0x80808080u;
         if (lane == 0) __hip_atomic_fetch_add(flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
-      if (i + 1 < nf) {
+      if (i + 1 < nf && !(args.dbg & 2048)) {   // (bit 11: timing probe without the staging loads)
         const __amdgpu_buffer_rsrc_t frs = ts_rsrc(args.frames + frame_row(i + 1) * IN_BYTES, IN_BYTES);
 #pragma unroll
         for (int q = 0; q < PFQ; ++q)
@@ -1040,7 +1081,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp3_kernel(const TSArgs args) {
             pf[q][dy] = __builtin_amdgcn_raw_buffer_load_b32(frs, fsrc[q], dy * 84, 0);
       }
       TS3_STAMP(i, 1);
-      if (i >= 1 && i <= nf) {
+      if (i >= 1 && i <= nf && !(args.dbg & 8192)) {   // (bit 13: without conv2)
         const int k = i - 1;
         const uint8_t* a1h = lds + OFF_A1 + (k & 1) * 2 * A1P;
         const uint8_t* a1l = a1h + A1P;
@@ -1057,6 +1098,8 @@ __global__ __launch_bounds__(512) void torso_fwd_sp3_kernel(const TSArgs args) {
           if (t < 4) { y2 = (t >> 1) * 4 + (l16 >> 2); x2 = (t & 1) * 4 + (l16 & 3); }
           else if (t == 4) { y2 = l16 < 8 ? l16 : 8; x2 = l16 < 8 ? 8 : l16 - 8; }
           else { y2 = 8; x2 = 8; ok = l16 == 0; }
+          // tap (kh, kw) offset = yo[kh] + xo[kw]: the act1 swizzle splits into a row bit and a
+          // column bit
           int yo[4], xo[4];
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -1065,18 +1108,18 @@ __global__ __launch_bounds__(512) void torso_fwd_sp3_kernel(const TSArgs args) {
             xo[j] = ((x ^ ((x >> 2) & 1)) << 6) + ((((kq & 1) ^ (x >> 1)) & 1) << 4);
           }
           f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-          bf16x8 rh[2], rl[2];
+          bf16x8 rh[D2], rl[D2];
           auto ld = [&](int s, bf16x8& hh, bf16x8& ll) {
             const int o = yo[s >> 2] + xo[s & 3];
             hh = *(const bf16x8*)(a1h + o);
             ll = *(const bf16x8*)(a1l + o);
           };
-          ld(0, rh[0], rl[0]);
-          ld(1, rh[1], rl[1]);
+#pragma unroll
+          for (int s = 0; s < D2; ++s) ld(s, rh[s], rl[s]);
 #pragma unroll
           for (int s = 0; s < 16; ++s) {
-            const bf16x8 hh = rh[s & 1], ll = rl[s & 1];
-            if (s + 2 < 16) ld(s + 2, rh[s & 1], rl[s & 1]);
+            const bf16x8 hh = rh[s % D2], ll = rl[s % D2];
+            if (s + D2 < 16) ld(s + D2, rh[s % D2], rl[s % D2]);
             __builtin_amdgcn_sched_barrier(0);
             acc = mfma16_x3(w2h[s], w2l[s], hh, ll, acc);
           }
@@ -1103,6 +1146,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp3_kernel(const TSArgs args) {
       lds_sync();
       TS3_STAMP(i, 3);
     }
+    drain(nf - 1);   // the last frame's outputs (staged in iteration nf + 1)
   }
 #undef TS3_STAMP
 }
@@ -1177,15 +1221,21 @@ extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs,
     else if (!(a.dbg & 256))   // v2 (int8 conv1, two phases per frame)
       hipLaunchKernelGGL(torso_fwd_sp2_kernel<true>, dim3(grid), dim3(tsp::NT), tsp2::LDS_BYTES_I8,
                          (hipStream_t)stream, a);
-    else {   // v3
+    else {   // v3 (bit 9: 4-deep operand rings)
       static bool attr3 = false;
       if (!attr3) {
-        hipFuncSetAttribute((const void*)torso_fwd_sp3_kernel,
+        hipFuncSetAttribute((const void*)torso_fwd_sp3_kernel<2, 2>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, tsp3::LDS_BYTES);
+        hipFuncSetAttribute((const void*)torso_fwd_sp3_kernel<4, 3>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, tsp3::LDS_BYTES);
         attr3 = true;
       }
-      hipLaunchKernelGGL(torso_fwd_sp3_kernel, dim3(grid), dim3(tsp::NT), tsp3::LDS_BYTES,
-                         (hipStream_t)stream, a);
+      if (a.dbg & 512)
+        hipLaunchKernelGGL((torso_fwd_sp3_kernel<4, 3>), dim3(grid), dim3(tsp::NT), tsp3::LDS_BYTES,
+                           (hipStream_t)stream, a);
+      else
+        hipLaunchKernelGGL((torso_fwd_sp3_kernel<2, 2>), dim3(grid), dim3(tsp::NT), tsp3::LDS_BYTES,
+                           (hipStream_t)stream, a);
     }
   }
   R2_CHECK_LAUNCH();

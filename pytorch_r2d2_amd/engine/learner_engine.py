@@ -1235,7 +1235,7 @@ class LearnerEngine:
         return float(self.loss.item())
 
     @torch.no_grad()
-    def stats(self) -> Dict[str, float]:
+    def diagnostics(self) -> Dict[str, float]:
         """Learner diagnostics of the last step (the reference prints only a step
         count, ``/root/reference/learner.py:57-59``): loss, Q(s, .) of the online net over the
         learning rows (mean, mean of max_a, max), |TD error| (mean, max: the priority input),

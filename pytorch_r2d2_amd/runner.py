@@ -122,7 +122,7 @@ def run_native(cfg: R2D2Config, steps: int = 1000, actor_steps_per_update: int =
         if (it + 1) % log_every == 0 or it == steps - 1:
             if drv is not None:
                 torch.cuda.current_stream(dev).wait_stream(drv.s_learn)
-            st = eng.stats()
+            st = eng.diagnostics()
             loss = st["loss"]
             losses.append(loss)
             rets = actor.finished_returns[-64:]
@@ -395,7 +395,7 @@ def run_native_cpu_actors(cfg: R2D2Config, n_actors: int, steps: int = 1000,
             weights.poll()
             if it % log_every == 0 or it == steps:
                 rec = dict(step=it, rows=ingest.rows, records=ingest.records,
-                           learner_steps_per_s=it / (time.perf_counter() - t_train0), **eng.stats())
+                           learner_steps_per_s=it / (time.perf_counter() - t_train0), **eng.diagnostics())
                 if mlog:
                     mlog.log("native_cpu", **rec)
                 print("[native-cpu]", rec, flush=True)

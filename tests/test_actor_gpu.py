@@ -240,12 +240,12 @@ def test_native_loop_learns_synthetic_cue_task():
     assert rets[-200:].mean() > 3 * random_return, (rets[:200].mean(), rets[-200:].mean())
 
 
-def _memory_task(ablation: str, steps: int):
+def _memory_task(ablation: str, steps: int, extra=()):
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tools"))
     from learn_check import make_cfg, memoryless_ceiling, parse
     from pytorch_r2d2_amd.runner import run_native
-    args = parse(["--memory", "--ablation", ablation, "--steps", str(steps)])
+    args = parse(["--memory", "--ablation", ablation, "--steps", str(steps), *extra])
     cfg = make_cfg(args, "fp32")
     out = run_native(cfg, steps=steps, log_every=steps, capacity=args.envs * 1000)
     rets = np.asarray(out["returns"])
@@ -261,6 +261,21 @@ def test_recurrent_learner_solves_memory_task():
     rets, ceil = _memory_task("none", 4000)
     assert len(rets) > 1000
     assert rets[-300:].mean() >= 2.0 * ceil, (rets[:300].mean(), rets[-300:].mean(), ceil)
+
+
+def test_stored_state_beats_zero_state_on_long_memory():
+    """What stored recurrent state + burn-in buy (/root/reference/learner.py:71-79,
+    replay_memory.py:238-241): the cue is shown once per 64-step target phase, the training
+    window is 4 burn-in + 8 learned steps, so a learner that starts every sequence from a zero
+    state (no burn-in, 12 learned steps) never sees the cue in most windows and cannot learn to
+    hold it for 63 steps; the full learner starts from the actors' stored states.  Full must beat
+    zero-state by >= 1.3x (profiles/r04_learn_stored_state.txt: 115.6 vs 64.5 after 8000 steps)."""
+    extra = ("--switch", "64", "--episode-len", "128", "--burn-in", "4", "--learn", "8")
+    full, ceil = _memory_task("none", 6000, extra)
+    zero, _ = _memory_task("zero_state", 6000, extra)
+    assert len(full) > 1000 and len(zero) > 1000
+    f, z = full[-300:].mean(), zero[-300:].mean()
+    assert f >= 1.3 * z and f >= 2.0 * ceil, (f, z, ceil)
 
 
 def test_memoryless_ablation_stays_at_ceiling():

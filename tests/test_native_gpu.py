@@ -479,14 +479,16 @@ def test_actor_rank_block_pack_and_lagged_ingest():
         for name in ("frames", "hs_cs", "target_hs_cs", "action", "reward", "done", "priority"):
             assert torch.equal(getattr(lrn, name)[l_rows], getattr(act_rp, name)[a_rows]), (c, name)
         # starts: this record marks learner positions cK + j - lag (actor stream rows n earlier);
-        # stream rows < 0 never start; the record's own rows stay non-starts (K < lag)
+        # stream rows < 0 never start; the record's own rows j >= K - lag (windows not complete
+        # yet) stay non-starts
         s_l = (er * cl + (c * K + jr - lag) % cl).reshape(-1)
         s_a = (er * ca + (c * K + jr - lag - n) % ca).reshape(-1)
         keep = ((c * K + jr - lag - n) >= 0).expand(E, K).reshape(-1)
         exp = act_rp.is_start[s_a].bool() & keep
         assert torch.equal(lrn.is_start[s_l].bool(), exp), c
         assert torch.equal(lrn.tree[s_l], torch.where(exp, act_rp.tree[s_a], 0.0)), c
-        assert not lrn.is_start[l_rows].bool().any(), c
+        own = (er * cl + (c * K + torch.arange(max(0, K - lag), K, device=DEV)[None, :]) % cl).reshape(-1)
+        assert not lrn.is_start[own].bool().any(), c
         shipped_starts += int(exp.sum())
         assert int(lrn.ihead[0]) == (c + 1) * K % cl
     _tree_consistent(lrn)

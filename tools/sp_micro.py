@@ -81,7 +81,9 @@ if which in ("torso", "both"):
         # v3 (debug bit 8) vs v2 (int8 conv1), interleaved, min of the per-round means
         best = {}
         for _ in range(5):
-            for bits, name in ((256, "v3"), (0, "v2")):
+            for bits, name in ((256, "v3"), (256 | 1024, "v3_no_out3"), (256 | 2048, "v3_no_frame_loads"),
+                               (256 | 4096, "v3_no_conv1"), (256 | 8192, "v3_no_conv2"),
+                               (256 | 16384, "v3_no_conv3"), (256 | 4096 | 8192, "v3_no_conv12"), (0, "v2")):
                 k.r2_torso_sp_debug(bits)
                 t = timeit(lambda: k.r2_torso_fwd_sp_multi(ptr(frames), jobs.ctypes.data, 4, n_cus,
                                                            stream_handle()))
