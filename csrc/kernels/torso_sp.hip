@@ -870,9 +870,9 @@ __global__ __launch_bounds__(512) void torso_fwd_sp3_kernel(const TSArgs args) {
   __syncthreads();   // digits + frame 0 + biases in LDS
   // optional clock stamps of workgroup 0 (r2_torso_sp_trace): [wave][iteration < 16][4] = loop
   // top, conv3 / frame staging done, conv1 / conv2 done, after the barrier
-  long long* tr = (args.trace && blockIdx.x == 0 && lane == 0) ? args.trace + wave * 16 * 4 : nullptr;
+  long long* tr = (args.trace && blockIdx.x == 0 && lane == 0) ? args.trace + wave * 16 * 24 : nullptr;
 #define TS3_STAMP(it, k) \
-  if (tr && (it) < 16) tr[(it) * 4 + (k)] = (long long)__builtin_readcyclecounter();
+  if (tr && (it) < 16) tr[(it) * 24 + (k)] = (long long)__builtin_readcyclecounter();
 
   if (wave >= 4) {
     // ================================ C1: conv1(f_i) then (next iteration first) conv3(f_{i-2})
@@ -940,73 +940,10 @@ __global__ __launch_bounds__(512) void torso_fwd_sp3_kernel(const TSArgs args) {
           }
         }
       }
-      TS3_STAMP(i, 1);
-      if (i < nf && !(args.dbg & 4096)) {   // (bit 12: timing probe without conv1)
-        if (i >= 1) {   // frame f_i staged by the C2 waves
-          while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 4 * i)
-            __builtin_amdgcn_s_sleep(1);
-        }
-        uint8_t* a1h = lds + OFF_A1 + (i & 1) * 2 * A1P;
-        uint8_t* a1l = a1h + A1P;
-        const int fidx = first + i * stride;
-        bf16* s1 = J.s1 ? J.s1 + (size_t)fidx * 400 * 32 : nullptr;
-        bf16* s1l = J.s1 ? J.s1l + (size_t)fidx * 400 * 32 : nullptr;
-        auto ldb = [&](int t, i32x4_t (&x)[4]) {
-          const int ty = t / 5, tx = t - 5 * ty;
-          const uint8_t* p = lds + fr_lane + (ty * 4 * 24 + tx * 4) * 16;
-          x[0] = *(const i32x4_t*)(p);
-          x[1] = *(const i32x4_t*)(p + 16);
-          x[2] = *(const i32x4_t*)(p + 24 * 16);
-          x[3] = *(const i32x4_t*)(p + 25 * 16);
-        };
-        // one 4x4-pixel tile: 12 int8 MFMAs (3 digits x 4 K blocks) + the epilogue; the next
-        // tile's fragments are loaded (into `nx`) before the MFMAs
-        auto tile = [&](int t, const i32x4_t (&cur)[4], i32x4_t (&nx)[4]) {
-          // unconditional (the last tile re-reads itself): a prefetch under a branch made the
-          // compiler's lgkmcnt bookkeeping wait for it before the current tile's MFMAs
-          ldb(min(t + 1, t_end - 1), nx);
-          __builtin_amdgcn_sched_barrier(0);
-          i32x4_t acc[3];
-          acc[0] = sc0;
-          acc[1] = i32x4_t{0, 0, 0, 0};
-          acc[2] = sc2;
-#pragma unroll
-          for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-            for (int d = 0; d < 3; ++d)
-              acc[d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wd[3 * kb + d], cur[kb], acc[d], 0, 0, 0);
-          const int ty = t / 5, tx = t - 5 * ty;
-          const int y = 4 * ty + (l16 >> 2), x = 4 * tx + (l16 & 3);
-          bf16x4 vh, vl;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int i0 = acc[0][e];
-            const int i12 = acc[1][e] * 128 + acc[2][e];
-            const float tq = fmaf((float)i12, 1.f / 16384.f, (float)i0);
-            const float v = fmaxf(fmaf(tq, c1_scale, b1v[e]), 0.f);
-            vh[e] = (bf16)v;
-            vl[e] = sp_lo(v);
-          }
-          const int o = a1v3_off(y, x, ch0 >> 3) + 8 * (kq & 1);
-          *(bf16x4*)(a1h + o) = vh;
-          *(bf16x4*)(a1l + o) = vl;
-          if (s1) {
-            const size_t g = (size_t)(y * 20 + x) * 32 + ch0;
-            *(bf16x4*)(s1 + g) = vh;
-            *(bf16x4*)(s1l + g) = vl;
-          }
-        };
-        i32x4_t bA[4], bB[4];
-        ldb(t_beg, bA);
-#pragma unroll 1
-        for (int t = t_beg; t < t_end; t += 2) {
-          tile(t, bA, bB);
-          if (t + 1 < t_end) tile(t + 1, bB, bA);
-        }
-      }
       if (i >= 2) {
         // conv3(f_{i-2}) -> the CHW staging image, once the C2 waves have copied f_{i-3}'s out
-        // (they do so at the start of iteration i: this wait is normally already satisfied)
+        // (they do so at the start of iteration i, right after staging the frame: by the end of
+        // conv3 this wait is normally satisfied; the accumulators then die before conv1)
         if (i >= 3) {
           while (__hip_atomic_load(drained, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 4 * (i - 2))
             __builtin_amdgcn_s_sleep(1);
@@ -1021,6 +958,115 @@ __global__ __launch_bounds__(512) void torso_fwd_sp3_kernel(const TSArgs args) {
               st[1568 + (ch0 + e) * 49 + p3[tt]] = sp_lo(v);
             }
           }
+        }
+      }
+      TS3_STAMP(i, 1);
+      if (i < nf && !(args.dbg & 4096)) {   // (bit 12: timing probe without conv1)
+        if (i >= 1) {   // frame f_i staged by the C2 waves
+          while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 4 * i)
+            __builtin_amdgcn_s_sleep(1);
+        }
+        uint8_t* a1h = lds + OFF_A1 + (i & 1) * 2 * A1P;
+        uint8_t* a1l = a1h + A1P;
+        const int fidx = first + i * stride;
+        const bool keep_s1 = J.s1 && !(args.dbg & 131072);   // (bit 17: probe without s1 stores)
+        bf16* s1 = keep_s1 ? J.s1 + (size_t)fidx * 400 * 32 : nullptr;
+        bf16* s1l = keep_s1 ? J.s1l + (size_t)fidx * 400 * 32 : nullptr;
+        auto ldb = [&](int t, i32x4_t (&x)[4]) {
+          if (args.dbg & 262144) {   // (bit 18: probe without the fragment loads)
+            x[0] = x[1] = x[2] = x[3] = i32x4_t{t, 1, 2, 3};
+            return;
+          }
+          const int ty = t / 5, tx = t - 5 * ty;
+          const uint8_t* p = lds + fr_lane + (ty * 4 * 24 + tx * 4) * 16;
+          x[0] = *(const i32x4_t*)(p);
+          x[1] = *(const i32x4_t*)(p + 16);
+          x[2] = *(const i32x4_t*)(p + 24 * 16);
+          x[3] = *(const i32x4_t*)(p + 25 * 16);
+        };
+        // Software-pipelined over tiles: the 12 int8 MFMAs of tile t+1 (3 digits x 4 K blocks)
+        // are issued before the epilogue of tile t, and the scheduler interleaves that epilogue's
+        // VALU into the MFMA gaps (sched_group_barrier: 1 MFMA : 2 VALU), so the epilogue -- the
+        // conv1 wave's bottleneck when it followed its own MFMAs -- runs under the matrix pipe.
+        auto mfma12 = [&](const i32x4_t (&b)[4], i32x4_t (&acc)[3]) {
+          acc[0] = sc0;
+          acc[1] = i32x4_t{0, 0, 0, 0};
+          acc[2] = sc2;
+          if (args.dbg & 65536) {   // (bit 16: timing probe, no conv1 MFMAs)
+            acc[1] = b[0] ^ b[1] ^ b[2] ^ b[3];
+            return;
+          }
+#pragma unroll
+          for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+            for (int d = 0; d < 3; ++d)
+              acc[d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wd[3 * kb + d], b[kb], acc[d], 0, 0, 0);
+        };
+        auto epi = [&](int t, const i32x4_t (&acc)[3]) {
+          const int ty = t / 5, tx = t - 5 * ty;
+          const int y = 4 * ty + (l16 >> 2), x = 4 * tx + (l16 & 3);
+          bf16x4 vh, vl;
+          if (args.dbg & 32768) {   // (bit 15: timing probe, no epilogue math)
+            vh = __builtin_bit_cast(bf16x4, u32x2{(uint32_t)acc[0][0], (uint32_t)acc[1][1]});
+            vl = __builtin_bit_cast(bf16x4, u32x2{(uint32_t)acc[2][2], (uint32_t)acc[0][3]});
+          } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int i0 = acc[0][e];
+            const int i12 = acc[1][e] * 128 + acc[2][e];
+            const float tq = fmaf((float)i12, 1.f / 16384.f, (float)i0);
+            const float v = fmaxf(fmaf(tq, c1_scale, b1v[e]), 0.f);
+            vh[e] = (bf16)v;
+            vl[e] = sp_lo(v);
+          }
+          }
+          const int o = a1v3_off(y, x, ch0 >> 3) + 8 * (kq & 1);
+          *(bf16x4*)(a1h + o) = vh;
+          *(bf16x4*)(a1l + o) = vl;
+          if (s1) {
+            const size_t g = (size_t)(y * 20 + x) * 32 + ch0;
+            *(bf16x4*)(s1 + g) = vh;
+            *(bf16x4*)(s1l + g) = vl;
+          }
+        };
+        auto interleave = [&]() {
+#pragma unroll
+          for (int q = 0; q < 12; ++q) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // 2 VALU
+          }
+        };
+        i32x4_t F0[4], F1[4], A0[3], A1[3];
+        ldb(t_beg, F0);
+        ldb(t_beg + 1, F1);   // t_end - t_beg >= 12: always a valid tile
+        mfma12(F0, A0);
+#pragma unroll 1
+        for (int t = t_beg; t < t_end; t += 2) {
+          // unconditional loads (the last tiles re-read the final one): a prefetch under a branch
+          // made the compiler's lgkmcnt bookkeeping wait for it before the MFMAs
+          TS3_STAMP(i, 4 + (t - t_beg));
+          ldb(min(t + 2, t_end - 1), F0);
+          __builtin_amdgcn_sched_barrier(0);
+          if (t + 1 < t_end) {
+            mfma12(F1, A1);
+            epi(t, A0);
+            interleave();
+          } else {
+            epi(t, A0);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if (t + 1 >= t_end) break;
+          TS3_STAMP(i, 5 + (t - t_beg));
+          ldb(min(t + 3, t_end - 1), F1);
+          __builtin_amdgcn_sched_barrier(0);
+          if (t + 2 < t_end) {
+            mfma12(F0, A0);
+            epi(t + 1, A1);
+            interleave();
+          } else {
+            epi(t + 1, A1);
+          }
+          __builtin_amdgcn_sched_barrier(0);
         }
       }
       TS3_STAMP(i, 2);
@@ -1040,14 +1086,22 @@ __global__ __launch_bounds__(512) void torso_fwd_sp3_kernel(const TSArgs args) {
     float b2v[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) b2v[e] = lb[chc + e];
-    int fsrc[PFQ], fdst[PFQ];
+    // frame staging: a (row y, 3-block column group k) pair of all 4 channels per load set --
+    // 12-byte loads (21 dwords a row = 7 x 3: never across a row), each dword to its s2d block
+    // (y >> 2, 3k + m) at row y & 3; channel offsets are immediates.  Pairs t, t + 256, t + 512
+    // (< 588) of thread t: 8-12 loads a frame instead of 28 dword loads
+    constexpr int NPAIR = 84 * 7;
+    int fsrc[3], fdst[3];
 #pragma unroll
-    for (int q = 0; q < PFQ; ++q) {
-      const int b = tid + 256 * q;
-      fr3_block(b < NBLK ? b : NBLK - 1, fsrc[q], fdst[q]);
+    for (int j = 0; j < 3; ++j) {
+      const int pr = min(tid + 256 * j, NPAIR - 1), y = pr / 7, k = pr - 7 * y;
+      fsrc[j] = y * 84 + 12 * k;
+      fdst[j] = OFF_FR + ((y >> 2) * 24 + 3 * k) * 16 + (y & 3) * 4;
     }
+    const bool third = tid + 512 < NPAIR;
     __syncthreads();   // pairs the C1 waves' digit barrier
-    u32x4 pf[PFQ];
+    typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+    u32x3 pf[3][4];
     // the staged conv3 outputs of frame k (CHW hi / lo, 2 x 196 16-byte chunks) -> global
     auto drain = [&](int k) {
       const size_t fo = (size_t)(first + k * stride) * 1568;
@@ -1064,24 +1118,39 @@ __global__ __launch_bounds__(512) void torso_fwd_sp3_kernel(const TSArgs args) {
     };
     for (int i = 0; i < nf + 2; ++i) {
       TS3_STAMP(i, 0);
-      if (i >= 3) drain(i - 3);
       if (i >= 1 && i < nf) {
         // frame f_i -> LDS (conv1(f_{i-1}) finished reading the image at the last barrier)
 #pragma unroll
-        for (int q = 0; q < PFQ; ++q)
-          if (tid + 256 * q < NBLK) *(u32x4*)(lds + OFF_FR + fdst[q]) = pf[q] ^ 0x80808080u;
+        for (int j = 0; j < 3; ++j) {
+          if (j < 2 || third) {
+#pragma unroll
+            for (int ci = 0; ci < 4; ++ci) {
+              uint32_t* d = (uint32_t*)(lds + fdst[j] + ci * FRP);
+              d[0] = pf[j][ci][0] ^ 0x80808080u;
+              d[4] = pf[j][ci][1] ^ 0x80808080u;
+              d[8] = pf[j][ci][2] ^ 0x80808080u;
+            }
+          }
+        }
         if (lane == 0) __hip_atomic_fetch_add(flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
-      if (i + 1 < nf && !(args.dbg & 2048)) {   // (bit 11: timing probe without the staging loads)
-        const __amdgpu_buffer_rsrc_t frs = ts_rsrc(args.frames + frame_row(i + 1) * IN_BYTES, IN_BYTES);
+      if (i >= 3) drain(i - 3);
+      // frame f_{i+1} -> registers, issued in three groups between the conv2 tiles (28 dword
+      // loads at once backed the vector-memory queue up into the staging phase the conv1 waves
+      // wait on)
+      const bool ld_next = i + 1 < nf && !(args.dbg & 2048);   // (bit 11: probe without them)
+      const __amdgpu_buffer_rsrc_t frs =
+          ts_rsrc(args.frames + (ld_next ? frame_row(i + 1) : 0) * IN_BYTES, IN_BYTES);
+      auto issue = [&](int j) {
+        if (!ld_next || (j == 2 && !third)) return;
 #pragma unroll
-        for (int q = 0; q < PFQ; ++q)
-#pragma unroll
-          for (int dy = 0; dy < 4; ++dy)
-            pf[q][dy] = __builtin_amdgcn_raw_buffer_load_b32(frs, fsrc[q], dy * 84, 0);
-      }
+        for (int ci = 0; ci < 4; ++ci)
+          pf[j][ci] = __builtin_bit_cast(u32x3, __builtin_amdgcn_raw_buffer_load_b96(frs, fsrc[j], ci * 7056, 0));
+      };
       TS3_STAMP(i, 1);
-      if (i >= 1 && i <= nf && !(args.dbg & 8192)) {   // (bit 13: without conv2)
+      const bool c2_on = i >= 1 && i <= nf && !(args.dbg & 8192);   // (bit 13: without conv2)
+      if (!c2_on) { issue(0); issue(1); issue(2); }
+      if (c2_on) {
         const int k = i - 1;
         const uint8_t* a1h = lds + OFF_A1 + (k & 1) * 2 * A1P;
         const uint8_t* a1l = a1h + A1P;
@@ -1140,6 +1209,9 @@ __global__ __launch_bounds__(512) void torso_fwd_sp3_kernel(const TSArgs args) {
               *(bf16x4*)(s2l + g) = vl;
             }
           }
+          if (tt == 0) issue(0);
+          else if (tt == 1) issue(1);
+          else issue(2);
         }
       }
       TS3_STAMP(i, 2);
@@ -1221,21 +1293,15 @@ extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs,
     else if (!(a.dbg & 256))   // v2 (int8 conv1, two phases per frame)
       hipLaunchKernelGGL(torso_fwd_sp2_kernel<true>, dim3(grid), dim3(tsp::NT), tsp2::LDS_BYTES_I8,
                          (hipStream_t)stream, a);
-    else {   // v3 (bit 9: 4-deep operand rings)
+    else {   // v3 (2-deep operand rings: 3- / 4-deep measured no faster)
       static bool attr3 = false;
       if (!attr3) {
         hipFuncSetAttribute((const void*)torso_fwd_sp3_kernel<2, 2>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, tsp3::LDS_BYTES);
-        hipFuncSetAttribute((const void*)torso_fwd_sp3_kernel<4, 3>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, tsp3::LDS_BYTES);
         attr3 = true;
       }
-      if (a.dbg & 512)
-        hipLaunchKernelGGL((torso_fwd_sp3_kernel<4, 3>), dim3(grid), dim3(tsp::NT), tsp3::LDS_BYTES,
-                           (hipStream_t)stream, a);
-      else
-        hipLaunchKernelGGL((torso_fwd_sp3_kernel<2, 2>), dim3(grid), dim3(tsp::NT), tsp3::LDS_BYTES,
-                           (hipStream_t)stream, a);
+      hipLaunchKernelGGL((torso_fwd_sp3_kernel<2, 2>), dim3(grid), dim3(tsp::NT), tsp3::LDS_BYTES,
+                         (hipStream_t)stream, a);
     }
   }
   R2_CHECK_LAUNCH();

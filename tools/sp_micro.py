@@ -93,14 +93,15 @@ if which in ("torso", "both"):
     if "probe3" in sys.argv:
         # v3 per-wave clock stamps of workgroup 0: [wave][iteration][loop top, conv3 / staging done,
         # conv1 / conv2 done, after the barrier]; mean cycles per segment over iterations 3..12
-        tr = torch.zeros(8 * 16 * 4, dtype=torch.int64, device=DEV)
+        tr = torch.zeros(8 * 16 * 24, dtype=torch.int64, device=DEV)
         k.r2_torso_sp_trace(ptr(tr))
-        k.r2_torso_sp_debug(256)
+        k.r2_torso_sp_debug(256 | int(os.environ.get("SP3_DBG", "0")))
         k.r2_torso_fwd_sp_multi(ptr(frames), jobs.ctypes.data, 4, n_cus, stream_handle())
         torch.cuda.synchronize()
         k.r2_torso_sp_debug(0)
         k.r2_torso_sp_trace(0)
-        t = tr.view(8, 16, 4).cpu().double()
+        t = tr.view(8, 16, 24).cpu().double()
+        res["v3_conv1_tile_stamps_wave4_it5"] = (t[4, 5, 4:18] - t[4, 5, 1]).tolist()
         seg = {"a": t[:, 3:13, 1] - t[:, 3:13, 0], "b": t[:, 3:13, 2] - t[:, 3:13, 1],
                "wait": t[:, 3:13, 3] - t[:, 3:13, 2], "iter": t[:, 4:14, 0] - t[:, 3:13, 0]}
         res["v3_segments_cycles_per_wave"] = {n: [round(v, 0) for v in x.mean(1).tolist()] for n, x in seg.items()}
