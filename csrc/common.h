@@ -46,6 +46,38 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// All-lane wave sum on the VALU: DPP exchanges inside each 16-lane row (xor 1, xor 2, the other
+// quad of the 8, the other half of the row: every lane of a row then holds the same row sum,
+// adds are commutative) and v_readlane of the four row sums, added as (r0 + r1) + (r2 + r3).
+// ~10 dependent VALU ops instead of wave_sum's six ds_bpermute round trips through the LDS unit;
+// a different (fixed) association than wave_sum, so kernels that must agree bit for bit (the
+// dueling forward in head.hip and td.hip) both use this one.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float wave_sum_x(float v) {
+  v += dpp_mov<0xB1>(v);    // quad_perm [1,0,3,2]: xor 1
+  v += dpp_mov<0x4E>(v);    // quad_perm [2,3,0,1]: xor 2
+  v += dpp_mov<0x141>(v);   // row_half_mirror: the other quad of the 8
+  v += dpp_mov<0x140>(v);   // row_mirror: the other half of the row
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return (r0 + r1) + (r2 + r3);
+}
+__device__ __forceinline__ float wave_max_x(float v) {
+  v = fmaxf(v, dpp_mov<0xB1>(v));
+  v = fmaxf(v, dpp_mov<0x4E>(v));
+  v = fmaxf(v, dpp_mov<0x141>(v));
+  v = fmaxf(v, dpp_mov<0x140>(v));
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
+}
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

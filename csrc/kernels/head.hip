@@ -67,13 +67,13 @@ __global__ __launch_bounds__(256) void dueling_fwd_kernel(const DuelArgs args) {
   float v = 0.f;
 #pragma unroll
   for (int e = 0; e < PER; ++e) v += hv[e] * w2[lane * PER + e];
-  v = wave_sum(v) + b2[0];
+  v = wave_sum_x(v) + b2[0];
   float amean = 0.f, mine = 0.f;
   for (int a = 0; a < A; ++a) {
     float s = 0.f;
 #pragma unroll
     for (int e = 0; e < PER; ++e) s += ha[e] * w2[(size_t)(1 + a) * HD + lane * PER + e];
-    s = wave_sum(s) + b2[1 + a];
+    s = wave_sum_x(s) + b2[1 + a];
     mine = (a == lane) ? s : mine;
     amean += s;
   }

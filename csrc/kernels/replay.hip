@@ -33,12 +33,18 @@ __device__ __forceinline__ int ring_row_s(int start, int t, int cap_e) {
   return base + r;
 }
 
+// inclusive wave scan on the VALU (DPP): Hillis-Steele inside each 16-lane row (row_shr 1, 2, 4,
+// 8; lanes shifted in from outside the row read 0), then the row totals carried across rows
+// with row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) -- instead of six ds_bpermute round
+// trips on the tree descent's per-level critical path
 __device__ __forceinline__ float wave_incl_scan(float v, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const float n = __shfl_up(v, o, 64);
-    if (lane >= o) v += n;
-  }
+  (void)lane;
+  v += dpp_mov<0x111>(v);   // row_shr:1
+  v += dpp_mov<0x112>(v);   // row_shr:2
+  v += dpp_mov<0x114>(v);   // row_shr:4
+  v += dpp_mov<0x118>(v);   // row_shr:8
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xA, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x143, 0xC, 0xF, false));
   return v;
 }
 
@@ -143,7 +149,7 @@ __global__ void tree_rebuild_level_kernel(float* __restrict__ tree, TreeGeom g, 
        p += nwaves) {
     const int64_t c = p * 64 + lane;
     float v = c < g.size[lvl] ? child[c] : 0.f;
-    v = wave_sum(v);
+    v = wave_sum_x(v);
     if (lane == 0) parent[p] = v;
   }
 }
@@ -162,7 +168,7 @@ __global__ void tree_update_level_kernel(float* __restrict__ tree, TreeGeom g, i
     const int64_t p = node >> 6;
     const int64_t c = p * 64 + lane;
     float v = c < g.size[lvl] ? child[c] : 0.f;
-    v = wave_sum(v);
+    v = wave_sum_x(v);
     if (lane == 0) parent[p] = v;
   }
 }
@@ -170,7 +176,7 @@ __global__ void tree_update_level_kernel(float* __restrict__ tree, TreeGeom g, i
 // ---- the same repair at level 1 (-> level 2) with the small upper levels folded into the
 // launch: every workgroup publishes its level-2 sums write-through (sc1 stores, drained), one
 // lane per workgroup adds to an arrival ticket, and the workgroup whose add comes last
-// recomputes every node of levels 3.. from the level below (sc1 loads; the same wave_sum order,
+// recomputes every node of levels 3.. from the level below (sc1 loads; the same wave_sum_x order,
 // so the values are bit-identical to the per-level launches) and, with end_step, also does
 // step_end_kernel's work.  Replaces levels - 2 launches (+ step_end) of ~4.5 us each in a graph
 // (MI355X_MICROARCH.md hand-off table: last-arriver row).  Needs every level >= 3 to have
@@ -190,7 +196,7 @@ __global__ void tree_update_tail_kernel(float* __restrict__ tree, TreeGeom g,
       const int64_t p = (((int64_t)dirty[e]) >> 6) >> 6;
       const int64_t c = p * 64 + lane;
       float v = c < g.size[1] ? child[c] : 0.f;
-      v = wave_sum(v);
+      v = wave_sum_x(v);
       if (lane == 0) __hip_atomic_store(parent + p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -207,7 +213,7 @@ __global__ void tree_update_tail_kernel(float* __restrict__ tree, TreeGeom g,
     for (int64_t p = wave; p < g.size[l + 1]; p += nw) {
       const int64_t c = p * 64 + lane;
       float v = c < g.size[l] ? __hip_atomic_load(child + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
-      v = wave_sum(v);
+      v = wave_sum_x(v);
       if (lane == 0) __hip_atomic_store(parent + p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -220,21 +226,22 @@ __global__ void tree_update_tail_kernel(float* __restrict__ tree, TreeGeom g,
   }
 }
 
-// ---- eta-mixed sequence priority of every marked start overlapping the updated window
-// For sampled start s_b the learner rewrote rows [s_b + upd_lo, s_b + upd_hi).  Sequence s
-// (rows [s, s+T)) overlaps iff s in (s_b + upd_lo - T, s_b + upd_hi).
-__global__ void seqprio_refresh_kernel(const int* __restrict__ starts, int B,
-                                       const uint8_t* __restrict__ is_start,
-                                       const float* __restrict__ priority,
-                                       float* __restrict__ leaves, int T, int upd_lo,
-                                       int upd_hi, int cap_e, float eta,
-                                       int* __restrict__ dirty, int* __restrict__ count,
-                                       int max_dirty) {
-  // one workgroup per sampled start: the waves scan 64-offset chunks of the candidate range into
-  // an LDS list, then take the listed starts round-robin (a wave per start, not a start loop)
+// one workgroup per sampled start: the waves scan 64-offset chunks of the candidate range into
+// an LDS list, then take the listed starts round-robin (a wave per start, not a start loop).
+// SC1: leaves / dirty entries stored write-through at agent scope (prio_tail_kernel reads them
+// from other CUs after its grid barrier).
+template <bool SC1>
+__device__ __forceinline__ void seqprio_refresh_wg(const int* __restrict__ starts,
+                                                   const uint8_t* __restrict__ is_start,
+                                                   const float* __restrict__ priority,
+                                                   float* __restrict__ leaves, int T, int upd_lo,
+                                                   int upd_hi, int cap_e, float eta,
+                                                   int* __restrict__ dirty, int* __restrict__ count,
+                                                   int max_dirty) {
   constexpr int MAXC = 2048;     // host checks the candidate range fits
   __shared__ int list[MAXC];
   __shared__ int n_list;
+  __shared__ int dbase;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int b = blockIdx.x;
   if (threadIdx.x == 0) n_list = 0;
@@ -255,26 +262,126 @@ __global__ void seqprio_refresh_kernel(const int* __restrict__ starts, int B,
   const int nl = min(n_list, MAXC);
   // one dirty-list reservation per workgroup (a per-start atomicAdd on the shared counter
   // serialised ~4 x B agent-scope atomics on one address)
-  __shared__ int dbase;
   if (threadIdx.x == 0) dbase = nl > 0 ? atomicAdd(count, nl) : 0;
   __syncthreads();
   for (int i = wave; i < nl; i += nw) {
-    {
-      const int s = list[i];
-      float mx = 0.f, sm = 0.f;
-      for (int t = lane; t < T; t += 64) {
-        const float p = priority[ring_row_s(s, t, cap_e)];
-        mx = fmaxf(mx, p);
-        sm += p;
-      }
-      mx = wave_max(mx);
-      sm = wave_sum(sm);
-      if (lane == 0) {
-        leaves[s] = eta * mx + (1.f - eta) * (sm / (float)T);
-        const int slot = dbase + i;
+    const int s = list[i];
+    float mx = 0.f, sm = 0.f;
+    for (int t = lane; t < T; t += 64) {
+      const float p = priority[ring_row_s(s, t, cap_e)];
+      mx = fmaxf(mx, p);
+      sm += p;
+    }
+    mx = wave_max_x(mx);
+    sm = wave_sum_x(sm);
+    if (lane == 0) {
+      const float leaf = eta * mx + (1.f - eta) * (sm / (float)T);
+      const int slot = dbase + i;
+      if constexpr (SC1) {
+        __hip_atomic_store(leaves + s, leaf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (slot < max_dirty) __hip_atomic_store(dirty + slot, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        leaves[s] = leaf;
         if (slot < max_dirty) dirty[slot] = s;
       }
     }
+  }
+}
+
+// ---- eta-mixed sequence priority of every marked start overlapping the updated window
+// For sampled start s_b the learner rewrote rows [s_b + upd_lo, s_b + upd_hi).  Sequence s
+// (rows [s, s+T)) overlaps iff s in (s_b + upd_lo - T, s_b + upd_hi).
+__global__ void seqprio_refresh_kernel(const int* __restrict__ starts, int B,
+                                       const uint8_t* __restrict__ is_start,
+                                       const float* __restrict__ priority,
+                                       float* __restrict__ leaves, int T, int upd_lo,
+                                       int upd_hi, int cap_e, float eta,
+                                       int* __restrict__ dirty, int* __restrict__ count,
+                                       int max_dirty) {
+  (void)B;
+  seqprio_refresh_wg<false>(starts, is_start, priority, leaves, T, upd_lo, upd_hi, cap_e, eta,
+                            dirty, count, max_dirty);
+}
+
+// grid barrier of a launch whose workgroups are all resident (B <= 256 small workgroups): every
+// thread drains its stores, one arrival add per workgroup, thread 0 polls the counter
+// (agent-scope loads).  Bounded: after ~0.2 s of polling it sets *err and goes on (a wrong tree
+// rather than a hung GPU; the host reads err).
+__device__ __forceinline__ void prio_grid_barrier(unsigned* ctr, unsigned target, unsigned* err) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned it = 0;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++it > (1u << 22)) {
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// ---- the learner's whole priority tail in ONE launch (seqprio_refresh + tree_update_level(0)
+// + tree_update_tail): refresh of the sampled windows' sequence priorities (leaves), grid
+// barrier, level-0 repair of the dirty list, grid barrier, level-1 repair, arrival ticket, and
+// the last arriver recomputes levels 3.. and (with step) ends the learner step.  Same leaves, the
+// same wave_sum_x sums over the same children: bit-identical to the three launches.
+// sync[0..2]: barrier counters + ticket (zero between launches, reset by the last arriver);
+// sync[3]: error word (barrier timeout).
+__global__ __launch_bounds__(256) void prio_tail_kernel(
+    const int* __restrict__ starts, const uint8_t* __restrict__ is_start,
+    const float* __restrict__ priority, float* __restrict__ tree, TreeGeom g, int T, int upd_lo,
+    int upd_hi, int cap_e, float eta, int* __restrict__ dirty, int* __restrict__ count,
+    int max_dirty, unsigned* __restrict__ sync, int64_t* __restrict__ step, int reset_count) {
+  __shared__ int last;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int nwaves = gridDim.x * nw;
+  seqprio_refresh_wg<true>(starts, is_start, priority, tree, T, upd_lo, upd_hi, cap_e, eta, dirty,
+                           count, max_dirty);
+  prio_grid_barrier(sync + 0, gridDim.x, sync + 3);
+  const int n = min(__hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), max_dirty);
+  for (int lvl = 0; lvl < 2; ++lvl) {
+    const float* child = tree + g.off[lvl];
+    float* parent = tree + g.off[lvl + 1];
+    for (int e = blockIdx.x * nw + wave; e < n; e += nwaves) {
+      const int64_t p = ((int64_t)__hip_atomic_load(dirty + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                        >> (6 * (lvl + 1));
+      const int64_t c = p * 64 + lane;
+      float v = c < g.size[lvl]
+                    ? __hip_atomic_load(child + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+      v = wave_sum_x(v);
+      if (lane == 0) __hip_atomic_store(parent + p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lvl == 0) prio_grid_barrier(sync + 1, gridDim.x, sync + 3);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(sync + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  for (int l = 2; l + 1 < g.levels; ++l) {
+    const float* child = tree + g.off[l];
+    float* parent = tree + g.off[l + 1];
+    for (int64_t p = wave; p < g.size[l + 1]; p += nw) {
+      const int64_t c = p * 64 + lane;
+      float v = c < g.size[l] ? __hip_atomic_load(child + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+      v = wave_sum_x(v);
+      if (lane == 0) __hip_atomic_store(parent + p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    sync[0] = 0u;
+    sync[1] = 0u;
+    sync[2] = 0u;
+    if (step) *step += 1;
+    if (reset_count) *count = 0;
   }
 }
 
@@ -297,8 +404,8 @@ __global__ void mark_starts_kernel(const int* __restrict__ rows, const int* __re
     mx = fmaxf(mx, p);
     sm += p;
   }
-  mx = wave_max(mx);
-  sm = wave_sum(sm);
+  mx = wave_max_x(mx);
+  sm = wave_sum_x(sm);
   if (lane == 0) {
     if (!is_start[s]) atomicAdd(n_valid, 1);
     is_start[s] = 1;
@@ -340,8 +447,8 @@ __global__ void apply_pending_kernel(const int* __restrict__ pend, const int* __
         mx = fmaxf(mx, p);
         sm += p;
       }
-      mx = wave_max(mx);
-      sm = wave_sum(sm);
+      mx = wave_max_x(mx);
+      sm = wave_sum_x(sm);
       if (lane == 0) {
         if (!flag_exchange(is_start, v, 1)) atomicAdd(n_valid, 1);
         leaves[v] = eta * mx + (1.f - eta) * (sm / (float)T);
@@ -534,6 +641,26 @@ extern "C" int r2_seqprio_refresh(const int* starts, int B, const uint8_t* is_st
   hipLaunchKernelGGL(seqprio_refresh_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream,
                      starts, B, is_start, priority, leaves, T, upd_lo, upd_hi, cap_e, eta, dirty,
                      count, max_dirty);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
+// the fused priority tail (prio_tail_kernel); sync: 4 zeroed uints.  -3: the tree shape does not
+// allow the fold (tree_update_fused's conditions) or B > 256 (all workgroups must be resident)
+extern "C" int r2_prio_tail(const int* starts, int B, const uint8_t* is_start, const float* priority,
+                            float* tree, const int64_t* offs, const int64_t* sizes, int levels,
+                            int T, int upd_lo, int upd_hi, int cap_e, float eta, int* dirty,
+                            int* count, int max_dirty, unsigned* sync, int64_t* step,
+                            int reset_count, void* stream) {
+  if (upd_hi - upd_lo + T - 1 > 2048) return -2;
+  if (B <= 0 || B > 256) return -3;
+  if (levels < 4 || levels > TREE_MAX_LEVELS) return -3;
+  for (int l = 3; l < levels; ++l)
+    if (sizes[l - 1] > 64 * 64) return -3;
+  TreeGeom g = make_geom(offs, sizes, levels);
+  hipLaunchKernelGGL(prio_tail_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, starts, is_start,
+                     priority, tree, g, T, upd_lo, upd_hi, cap_e, eta, dirty, count, max_dirty, sync,
+                     step, reset_count);
   R2_CHECK_LAUNCH();
   return 0;
 }

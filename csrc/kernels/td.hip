@@ -214,98 +214,186 @@ struct TdDuelArgs {
   const float* b2[2];   // online, target
   float* qo[3];
   int fuse_fwd;
+  // optional stage stamps (r2_td_duel_set_trace): [workgroup][wave][8] s_memrealtime (100 MHz)
+  long long* trace;
 };
 
-// head.hip dueling_fwd_kernel for one row on one wave (same order of operations): returns the
-// lane's Q (lane < A); hv / ha = relu(z + b1) of the lane's features.  REGS: the advantage rows
-// below MAXA come from the caller's register copy (static indices only: no scratch)
-template <int HD, typename ZT, int MAXA, bool REGS>
-__device__ __forceinline__ float td_duel_row(const ZT* zrow, const float* b1, const float* w2,
-                                             const float* b2, int A, int lane, float (&hv)[HD / 64],
-                                             float (&ha)[HD / 64], const float (&w2a)[MAXA][HD / 64]) {
+// head.hip dueling_fwd_kernel for one row on one wave (same order of operations, same
+// wave_sum_x, so the Q rows agree bit for bit): returns the lane's Q (lane < A); hv / ha =
+// relu(z + b1) of the lane's features.  z: the row's pre-bias layer-1 outputs (already in
+// registers), b1 / w2 / b2: the net's head parameters staged in LDS -- second-layer rows up to
+// MAXA there, further rows (many-action heads) from w2g in memory.  The 1 + A lane partials are
+// formed first (their LDS / memory reads issued together), then reduced; amean accumulates in
+// action order as in dueling_fwd_kernel.
+template <int HD, typename ZT, int MAXA>
+__device__ __forceinline__ float td_duel_row(const ZT (&z)[2 * (HD / 64)], const float* b1,
+                                             const float* w2, const float* w2g, const float* b2,
+                                             int A, int lane, float (&hv)[HD / 64],
+                                             float (&ha)[HD / 64]) {
   constexpr int PER = HD / 64;
 #pragma unroll
   for (int e = 0; e < PER; ++e) {
     const int c = lane * PER + e;
-    hv[e] = fmaxf((float)zrow[c] + b1[c], 0.f);
-    ha[e] = fmaxf((float)zrow[HD + c] + b1[HD + c], 0.f);
+    hv[e] = fmaxf((float)z[e] + b1[c], 0.f);
+    ha[e] = fmaxf((float)z[PER + e] + b1[HD + c], 0.f);
   }
-  float v = 0.f;
+  float part[1 + MAXA];
+  part[0] = 0.f;
 #pragma unroll
-  for (int e = 0; e < PER; ++e) v += hv[e] * w2[lane * PER + e];
-  v = wave_sum(v) + b2[0];
+  for (int e = 0; e < PER; ++e) part[0] += hv[e] * w2[lane * PER + e];
+#pragma unroll
+  for (int a = 0; a < MAXA; ++a) {
+    float s = 0.f;
+    if (a < A) {
+#pragma unroll
+      for (int e = 0; e < PER; ++e) s += ha[e] * w2[(1 + a) * HD + lane * PER + e];
+    }
+    part[1 + a] = s;
+  }
+  float red[1 + MAXA];
+#pragma unroll
+  for (int a = 0; a <= MAXA; ++a) red[a] = (a <= A) ? wave_sum_x(part[a]) : 0.f;
+  const float v = red[0] + b2[0];
   float amean = 0.f, mine = 0.f;
-  auto act = [&](int a, float s) {
-    s = wave_sum(s) + b2[1 + a];
-    mine = (a == lane) ? s : mine;
-    amean += s;
-  };
-  if constexpr (REGS) {
 #pragma unroll
-    for (int a = 0; a < MAXA; ++a)
-      if (a < A) {
-        float s = 0.f;
-#pragma unroll
-        for (int e = 0; e < PER; ++e) s += ha[e] * w2a[a][e];
-        act(a, s);
-      }
+  for (int a = 0; a < MAXA; ++a) {
+    if (a < A) {
+      const float s = red[1 + a] + b2[1 + a];
+      mine = (a == lane) ? s : mine;
+      amean += s;
+    }
   }
-  for (int a = REGS ? MAXA : 0; a < A; ++a) {
+  for (int a = MAXA; a < A; ++a) {
     float s = 0.f;
 #pragma unroll
-    for (int e = 0; e < PER; ++e) s += ha[e] * w2[(size_t)(1 + a) * HD + lane * PER + e];
-    act(a, s);
+    for (int e = 0; e < PER; ++e) s += ha[e] * w2g[(size_t)(1 + a) * HD + lane * PER + e];
+    s = wave_sum_x(s) + b2[1 + a];
+    mine = (a == lane) ? s : mine;
+    amean += s;
   }
   amean /= (float)A;
   return v + mine - amean;
 }
 
-// SP: zr fp32, dz written as hi / lo planes (split.h).  Actions beyond the MAXA register-resident
-// second-layer rows are read from memory inside the same loop (same order, same bits).
+// SP: zr fp32, dz written as hi / lo planes (split.h).  Actions beyond the MAXA LDS-staged
+// second-layer rows are read from memory inside the same loops (same order, same bits).
+//
+// Latency layout (one wave per transition, 16 per workgroup; the kernel is a chain of dependent
+// round trips, not bandwidth): every independent load is issued at the top -- the wave's z rows of
+// all three heads, the start -> row -> action / reward / done chain, the workgroup's cooperative
+// staging of both nets' head parameters into LDS, the IS-weight maximum -- before ONE barrier;
+// the wave re-derives its own sample's IS weight instead of a second barrier; the loss ticket is
+// taken before the dh product so its round trip hides under the MFMAs; dh reads W1^T two K steps
+// per 128-byte line (a K permutation shared by both operands), not half a line per load.
 template <int HD, bool SP>
 __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
-  // 16 waves per workgroup: one arrival-ticket atomic per 16 transitions (a single counter's
-  // agent-scope atomics serialise: 640 four-wave workgroups cost as much as the fusion saved)
   constexpr int PER = HD / 64, MAXA = 8, NW = 16;
+  constexpr int WROWS = (1 + MAXA) * HD;     // staged second-layer rows of one net
   const TdArgs& a = args.td;
-  __shared__ float wsh[256];
   __shared__ int sst[256];
   __shared__ float red[NW];
+  __shared__ float lred[NW];
   __shared__ float tot_sh[NW];
   __shared__ int last;
+  __shared__ __attribute__((aligned(16))) float w2s[2][WROWS];
+  __shared__ __attribute__((aligned(16))) float b1s[2][2 * HD];
+  __shared__ float b2s[2][1 + HEAD_FWD_MAXA];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid < a.B) sst[tid] = a.starts[tid];
+  long long* tr = (args.trace && lane == 0) ? args.trace + ((size_t)blockIdx.x * NW + wave) * 8 : nullptr;
+#define TD_STAMP(k) if (tr) tr[k] = (long long)__builtin_amdgcn_s_memrealtime();
+  TD_STAMP(0);
   const int n = a.Tl * a.B;
   const int i = blockIdx.x * NW + wave;      // this wave's transition
   const bool valid = i < n;
   const int b = valid ? i % a.B : 0, tl = valid ? i / a.B : 0;
-  // ---- everything that does not depend on the TD error is loaded first, so the dependent
-  // chain below (start -> row -> action / reward / done) is the only serial part
   const int start = valid ? a.starts[b] : 0;
   const float NEG = -3.0e38f;
   typedef typename std::conditional<SP, float, bf16>::type ZT;
+  const bool fwd = args.fuse_fwd != 0;
+  // ---- the wave's rows: z of the three heads (fused forward) or the online relu'd row
+  ZT zq[3][2 * PER];
+#pragma unroll
+  for (int h = 0; h < 3; ++h)
+#pragma unroll
+    for (int e = 0; e < 2 * PER; ++e) zq[h][e] = (ZT)0.f;
+  float qa = NEG, qt = 0.f, qs = 0.f;
+  if (valid) {
+    if (fwd) {
+#pragma unroll
+      for (int h = 0; h < 3; ++h) {
+        const ZT* zrow = (const ZT*)args.zh[h] + (size_t)i * 2 * HD;
+#pragma unroll
+        for (int e = 0; e < PER; ++e) {
+          zq[h][e] = zrow[lane * PER + e];
+          zq[h][PER + e] = zrow[HD + lane * PER + e];
+        }
+      }
+    } else {
+      const ZT* zrow = (const ZT*)args.zr + (size_t)i * 2 * HD;
+#pragma unroll
+      for (int e = 0; e < PER; ++e) {
+        zq[0][e] = zrow[lane * PER + e];
+        zq[0][PER + e] = zrow[HD + lane * PER + e];
+      }
+      if (lane < a.A) {
+        qa = a.q_arg[(size_t)i * a.A + lane];
+        qt = a.q_tgt[(size_t)i * a.A + lane];
+        qs = a.q_sa[(size_t)i * a.A + lane];
+      }
+    }
+  }
+  const int row = valid ? ring_row(start, a.burn_in + tl, a.cap_e) : 0;
+  const int act = valid ? (int)a.action[row] : 0;
+  const float rew = valid ? a.reward[row] : 0.f;
+  const bool dn = valid ? a.done[row] != 0 : true;
+  // ---- workgroup staging: second-layer rows 0..min(A, MAXA) of the online (and target) head,
+  // b1 / b2 of both nets (forward fusion), the B starts; IS-weight maxima per wave
+  {
+    const int rows = 1 + min(a.A, MAXA);
+    const int nets = fwd ? 2 : 1;
+    for (int q = tid; q < nets * rows * (HD / 4); q += NW * 64) {
+      const int net = q / (rows * (HD / 4)), r = q - net * rows * (HD / 4);
+      const float* src = net ? args.w2t : args.w2;
+      *(f32x4*)&w2s[net][4 * r] = *(const f32x4*)(src + 4 * r);
+    }
+    if (fwd) {
+      for (int q = tid; q < 2 * (2 * HD / 4); q += NW * 64) {
+        const int net = q / (2 * HD / 4), r = q - net * (2 * HD / 4);
+        *(f32x4*)&b1s[net][4 * r] = *(const f32x4*)(args.b1[net] + 4 * r);
+      }
+      if (tid < 2 * (1 + a.A)) {
+        const int net = tid / (1 + a.A), r = tid - net * (1 + a.A);
+        b2s[net][r] = args.b2[net][r];
+      }
+    }
+  }
+  if (tid < a.B) sst[tid] = a.starts[tid];
+  bool gn = false;
+  const float w_t = tid < a.B ? is_weight(a, tid, &gn) : 1.f;
+  const float m = wave_max(tid < a.B ? w_t : 0.f);
+  if (lane == 0) red[wave] = m;
+  TD_STAMP(1);
+  __syncthreads();
+  float wmax = red[0];
+#pragma unroll
+  for (int q = 1; q < NW; ++q) wmax = fmaxf(wmax, red[q]);
+  if (gn) wmax = 1.f;
+  if (tid < a.B && a.is_w && blockIdx.x == 0) a.is_w[tid] = w_t / wmax;
+  TD_STAMP(2);
+
+  // ---- the three heads' dueling forward for row i (online, online-on-next, target)
   ZT zv[PER], za[PER];
-  float w2v[PER], w2a[MAXA][PER];
 #pragma unroll
-  for (int e = 0; e < PER; ++e) w2v[e] = args.w2[lane * PER + e];
-#pragma unroll
-  for (int k = 0; k < MAXA; ++k)
-#pragma unroll
-    for (int e = 0; e < PER; ++e)
-      w2a[k][e] = k < a.A ? args.w2[(size_t)(1 + k) * HD + lane * PER + e] : 0.f;
-  float qa, qt, qs;
-  if (args.fuse_fwd) {
-    // the three heads' dueling forward for row i (online, online-on-next, target)
+  for (int e = 0; e < PER; ++e) { zv[e] = zq[0][e]; za[e] = zq[0][PER + e]; }
+  if (fwd) {
     float hv[PER], ha[PER];
     qs = qa = qt = 0.f;
     if (valid) {
 #pragma unroll
       for (int h = 0; h < 3; ++h) {
-        const ZT* zrow = (const ZT*)args.zh[h] + (size_t)i * 2 * HD;
-        const float q = h < 2 ? td_duel_row<HD, ZT, MAXA, true>(zrow, args.b1[0], args.w2, args.b2[0],
-                                                                a.A, lane, hv, ha, w2a)
-                              : td_duel_row<HD, ZT, MAXA, false>(zrow, args.b1[1], args.w2t, args.b2[1],
-                                                                 a.A, lane, hv, ha, w2a);
+        const int net = h == 2;
+        const float q = td_duel_row<HD, ZT, MAXA>(zq[h], b1s[net], w2s[net], net ? args.w2t : args.w2,
+                                                  b2s[net], a.A, lane, hv, ha);
         if (args.qo[h] && lane < a.A) args.qo[h][(size_t)i * a.A + lane] = q;
         if (h == 0) {
           qs = q;
@@ -325,35 +413,7 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
       }
     }
     if (!(valid && lane < a.A)) { qa = NEG; qt = 0.f; qs = 0.f; }
-  } else {
-    qa = (valid && lane < a.A) ? a.q_arg[(size_t)i * a.A + lane] : NEG;
-    qt = (valid && lane < a.A) ? a.q_tgt[(size_t)i * a.A + lane] : 0.f;
-    qs = (valid && lane < a.A) ? a.q_sa[(size_t)i * a.A + lane] : 0.f;
-    if (valid) {
-      const ZT* zrow = (const ZT*)args.zr + (size_t)i * 2 * HD;
-#pragma unroll
-      for (int e = 0; e < PER; ++e) { zv[e] = zrow[lane * PER + e]; za[e] = zrow[HD + lane * PER + e]; }
-    }
   }
-  const int row = valid ? ring_row(start, a.burn_in + tl, a.cap_e) : 0;
-  const int act = valid ? (int)a.action[row] : 0;
-  const float rew = valid ? a.reward[row] : 0.f;
-  const bool dn = valid ? a.done[row] != 0 : true;
-  // ---- IS weights (B <= 256), as td_kernel
-  bool gn = false;
-  const float w = tid < a.B ? is_weight(a, tid, &gn) : 1.f;
-  const float m = wave_max(tid < a.B ? w : 0.f);
-  if (lane == 0) red[wave] = m;
-  __syncthreads();
-  float wmax = red[0];
-#pragma unroll
-  for (int q = 1; q < NW; ++q) wmax = fmaxf(wmax, red[q]);
-  if (gn) wmax = 1.f;
-  if (tid < a.B) {
-    wsh[tid] = w / wmax;
-    if (a.is_w && blockIdx.x == 0) a.is_w[tid] = w / wmax;
-  }
-  __syncthreads();
 
   const float inv_n = 1.f / (float)n;
   float lsum = 0.f;
@@ -375,7 +435,8 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
     float y = rew + (dn ? 0.f : a.gamma_n * boot);
     if (a.value_rescale) y = vr_h(y, a.vr_eps);
     const float delta = __shfl(qs, act, 64) - y;
-    const float wb = wsh[b];
+    bool gdummy;
+    const float wb = is_weight(a, b, &gdummy) / wmax;   // == the staged w / wmax of sample b
     const float g = wb * delta * inv_n;      // dL/dQ[act]; every other action 0
     // the wave checks the B starts 64 at a time for a later duplicate of this row
     const bool own = a.priority ? __all(prio_owner(sst, a.B, a.Tl, a.burn_in, a.cap_e, tl, b, lane, 64))
@@ -398,11 +459,11 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
     float ov[PER], oa[PER];
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
-      const float gv = dv * w2v[e];
+      const float gv = dv * w2s[0][lane * PER + e];
       float ga = 0.f;
 #pragma unroll
       for (int k = 0; k < MAXA; ++k)
-        if (k < a.A) ga += (((k == act) ? g : 0.f) - dmean) * w2a[k][e];
+        if (k < a.A) ga += (((k == act) ? g : 0.f) - dmean) * w2s[0][(1 + k) * HD + lane * PER + e];
       for (int k = MAXA; k < a.A; ++k)     // many-action heads (Seaquest 18, DMLab 15)
         ga += (((k == act) ? g : 0.f) - dmean) * args.w2[(size_t)(1 + k) * HD + lane * PER + e];
       ov[e] = ((float)zv[e] > 0.f) ? gv : 0.f;
@@ -421,11 +482,27 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
       }
     }
   }
+  TD_STAMP(3);
   // ---- fused dh = dz @ W1 of the 16 rows (dz staged in LDS; wave w owns dh columns 16w..16w+15,
-  // K = 2HD on v_mfma_f32_16x16x32_bf16, W1^T fragments from L2; 3 passes in split precision)
+  // K = 2HD on v_mfma_f32_16x16x32_bf16, W1^T fragments from L2; 3 passes in split precision).
+  // K order: MFMA step s covers k = 64 (s >> 1) + 16 kq + 8 (s & 1) + [0, 8) for lane group kq, so
+  // the two steps of a pair read one 32-byte run per lane (a full 128-byte line per row).
   constexpr int KD = 2 * HD, DZS = KD + 8;             // padded LDS rows
+  constexpr int KS = KD / 32, D = 4;
   __shared__ __attribute__((aligned(16))) bf16 dzs[SP ? 2 : 1][NW * DZS];
+  const int r16 = lane & 15, kq = lane >> 4;
+  auto koff = [&](int s) { return 64 * (s >> 1) + 16 * kq + 8 * (s & 1); };
+  bf16x8 rb[D], rbl[D];
+  const bf16* bt = args.w1t ? args.w1t + (size_t)(wave * 16 + r16) * KD : nullptr;
+  const bf16* btl = (SP && args.w1t) ? args.w1t_lo + (size_t)(wave * 16 + r16) * KD : nullptr;
   if (args.w1t) {
+    // the first W1^T fragments are independent of this launch's results: in flight across the
+    // staging barrier
+#pragma unroll
+    for (int s = 0; s < D; ++s) {
+      rb[s] = *(const bf16x8*)(bt + koff(s));
+      if constexpr (SP) rbl[s] = *(const bf16x8*)(btl + koff(s));
+    }
 #pragma unroll
     for (int e = 0; e < PER; ++e) {
       const float v0 = valid ? ((float)zv[e] > 0.f ? dz_v[e] : 0.f) : 0.f;
@@ -438,20 +515,21 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
       }
     }
   }
-  // ---- loss: wave partial (lane 0) -> workgroup partial -> last arriver, fixed order
-  if (lane == 0) red[wave] = lsum;
+  // ---- loss: wave partial (lane 0) -> workgroup partial -> arrival ticket (before dh: the
+  // atomic's round trip overlaps the product) -> the last arriver sums in workgroup order
+  if (lane == 0) lred[wave] = lsum;
   __syncthreads();
-  if (args.w1t) {
-    const int r16 = lane & 15, kq = 8 * (lane >> 4);
-    const bf16* bt = args.w1t + (size_t)(wave * 16 + r16) * KD + kq;
-    const bf16* btl = SP ? args.w1t_lo + (size_t)(wave * 16 + r16) * KD + kq : nullptr;
-    constexpr int KS = KD / 32, D = 4;
-    bf16x8 rb[D], rbl[D];
+  TD_STAMP(4);
+  unsigned tk = 0;
+  if (tid == 0) {
+    float v = 0.f;
 #pragma unroll
-    for (int s = 0; s < D; ++s) {
-      rb[s] = *(const bf16x8*)(bt + 32 * s);
-      if constexpr (SP) rbl[s] = *(const bf16x8*)(btl + 32 * s);
-    }
+    for (int q = 0; q < NW; ++q) v += lred[q];
+    __hip_atomic_store(a.part + blockIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tk = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (args.w1t) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
@@ -459,34 +537,28 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
       bf16x8 b1;
       if constexpr (SP) b1 = rbl[s % D];
       if (s + D < KS) {
-        rb[s % D] = *(const bf16x8*)(bt + 32 * (s + D));
-        if constexpr (SP) rbl[s % D] = *(const bf16x8*)(btl + 32 * (s + D));
+        rb[s % D] = *(const bf16x8*)(bt + koff(s + D));
+        if constexpr (SP) rbl[s % D] = *(const bf16x8*)(btl + koff(s + D));
       }
-      const bf16x8 a0 = *(const bf16x8*)(&dzs[0][r16 * DZS + 32 * s + kq]);
+      const bf16x8 a0 = *(const bf16x8*)(&dzs[0][r16 * DZS + koff(s)]);
       if constexpr (SP) {
-        const bf16x8 a1 = *(const bf16x8*)(&dzs[SP ? 1 : 0][r16 * DZS + 32 * s + kq]);
+        const bf16x8 a1 = *(const bf16x8*)(&dzs[SP ? 1 : 0][r16 * DZS + koff(s)]);
         acc = mfma16_x3(a0, a1, b0, b1, acc);
       } else {
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc, 0, 0, 0);
       }
     }
-    // acc[e] = dh[row 4(lane>>4)+e of the workgroup][column 16 wave + (lane & 15)]
+    // acc[e] = dh[row 4 kq + e of the workgroup][column 16 wave + r16]
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int ri = blockIdx.x * NW + 4 * (lane >> 4) + e;
+      const int ri = blockIdx.x * NW + 4 * kq + e;
       if (ri < n) args.dh[(size_t)ri * 256 + wave * 16 + r16] = acc[e];
     }
   }
-  if (tid == 0) {
-    float v = 0.f;
-#pragma unroll
-    for (int q = 0; q < NW; ++q) v += red[q];
-    __hip_atomic_store(a.part + blockIdx.x, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = t == gridDim.x - 1;
-  }
+  TD_STAMP(5);
+  if (tid == 0) last = tk == gridDim.x - 1;
   __syncthreads();
+  TD_STAMP(6);
   if (!last) return;
   float s = 0.f;
   for (unsigned g = tid; g < gridDim.x; g += NW * 64)
@@ -501,6 +573,8 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
     *a.loss = t * inv_n;
     __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  TD_STAMP(7);
+#undef TD_STAMP
 }
 
 template <bool SP>
@@ -528,6 +602,11 @@ extern "C" int r2_td_duel_dh(const float*, const float*, const float*, const int
 // b2_on, b2_tg, q_on, q_nx, q_tg (q outs may be 0)} -- zr of r2_td_duel_dh becomes an output.
 static thread_local int64_t g_td_fwd[12];
 static thread_local bool g_td_fwd_on = false;
+static long long* g_td_trace = nullptr;
+extern "C" int r2_td_duel_set_trace(long long* tr) {
+  g_td_trace = tr;
+  return 0;
+}
 extern "C" int r2_td_duel_fwd_set(const int64_t* fwd) {
   g_td_fwd_on = fwd != nullptr;
   if (fwd)
@@ -573,6 +652,7 @@ extern "C" int r2_td_duel_dh(const float* q_sa, const float* q_arg, const float*
                 prio_eps, beta, value_rescale, dp},
                zr, w2, dz, dva, dz_lo, w1t, w1t_lo, dh};
   d.fuse_fwd = 0;
+  d.trace = g_td_trace;
   if (g_td_fwd_on) {
     g_td_fwd_on = false;   // one launch per set
     if (A > HEAD_FWD_MAXA) return -6;

@@ -66,6 +66,9 @@ class ReplayConfig:
     # learner tail: sum-tree levels >= 2 and the step counter folded into the level-1 repair
     # launch (last-arriving workgroup), 2 launches instead of levels - 1 + 1
     fused_tree_tail: bool = True
+    # ... and the sequence-priority refresh + level-0 repair in the same launch (grid barriers
+    # between the levels, replay.hip prio_tail_kernel): the whole priority tail is one launch
+    fused_prio_tail: bool = True
 
     @property
     def seq_len(self) -> int:
@@ -199,6 +202,9 @@ class DistConfig:
     # weights across ranks and a zero error word (the multi-rank DP path runs the segment graphs
     # with the collectives issued between them, the form the multi-rank tests pin)
     graph_collectives_multi: bool = False
+    # rmsprop writes the LSTM / head row packs itself (optim.hip rmsprop_pack_kernel) instead of
+    # a gather over the updated master in the pack launch
+    fuse_opt_pack: bool = True
     learner_steps_per_round: int = 1    # run_split default run length: rounds x this
 
 

@@ -196,19 +196,25 @@ class ParamLayout:
                    (4, c1, 4 * c2))
         else:
             add_bf("mlp", off("vis_layers.0.weight") + np.arange(self.D * self.cin), (self.D, self.cin))
-        add_bf("w_ih", off("lstm.weight_ih") + perm[:, None] * D + np.arange(D)[None, :], (G, D))
-        add_bf("w_hh", off("lstm.weight_hh") + perm[:, None] * H + np.arange(H)[None, :],
-               (nwg, 64, H))
         permr = perm.reshape(nwg, 64)
         whhT = off("lstm.weight_hh") + permr[:, None, :] * H + np.arange(H)[None, :, None]
         add_bf("w_hhT", whhT, (nwg, H, 64))
-        add_bf("head1", off("val.0.weight") + np.arange(2 * HD * H), (2 * HD, H))
         # W1^T (H, 2HD), k contiguous: B operand of the dh = dz @ W1 product fused into the TD
         # launch (td.hip r2_td_duel_dh)
         hh, kk = np.meshgrid(np.arange(H), np.arange(2 * HD), indexing="ij")
         add_bf("head1T", off("val.0.weight") + kk * H + hh, (H, 2 * HD))
+        # the packs from here on are whole master rows in another row order (w_ih / w_hh: gate
+        # permutation; head1: identity) -- the optimizer writes them itself (optim.hip
+        # rmsprop_pack_kernel, one destination per master float4, rows are multiples of 4), the
+        # pack launch only gathers the prefix above
+        self.bf_rows_begin = cur
+        add_bf("w_ih", off("lstm.weight_ih") + perm[:, None] * D + np.arange(D)[None, :], (G, D))
+        add_bf("w_hh", off("lstm.weight_hh") + perm[:, None] * H + np.arange(H)[None, :],
+               (nwg, 64, H))
+        add_bf("head1", off("val.0.weight") + np.arange(2 * HD * H), (2 * HD, H))
         self.bf_numel = cur
         self.bf_index = torch.from_numpy(np.concatenate(bf).astype(np.int32))
+        self.row_dst4 = self._row_dst4(np.concatenate(bf), self.bf_rows_begin)
 
         f: List[np.ndarray] = []
         self.f_offsets: Dict[str, Tuple[int, Tuple[int, ...]]] = OrderedDict()
@@ -244,6 +250,23 @@ class ParamLayout:
         inv[perm] = np.arange(perm.size)
         self.gate_perm = torch.from_numpy(perm)
         self.gate_inv = torch.from_numpy(inv)
+
+    def _row_dst4(self, idx: np.ndarray, begin: int):
+        """(padded / 4) int32: the packed position of master float4 q when the packs at and after
+        ``begin`` hold it as 4 consecutive elements at a 4-aligned position, else -1.  Every
+        packed element from ``begin`` on (padding aside) must be covered exactly once, or None
+        (the optimizer then does not write packs)."""
+        dst = np.full(self.padded // 4, -1, dtype=np.int64)
+        tail = idx[begin:].reshape(-1, 4)           # the packs are padded to 8 elements
+        pad_v = self.segs["lstm.bias_ih"].offset
+        run = (tail[:, 0] % 4 == 0) & np.all(np.diff(tail, axis=1) == 1, axis=1)
+        q = tail[run, 0] // 4
+        if np.unique(q).size != q.size:
+            return None
+        dst[q] = begin + 4 * np.nonzero(run)[0]
+        if not np.all(run | np.all(tail == pad_v, axis=1)):
+            return None
+        return torch.from_numpy(dst.astype(np.int32))
 
     def torso_grad_map(self):
         """(dst index into the flat grad buffer, scale) for every element of the fused torso

@@ -131,6 +131,8 @@ class LearnerEngine:
         self.opt_a = torch.zeros_like(self.master)
         self.opt_b = torch.zeros_like(self.master)
         self.bf_index = L.bf_index.to(d)
+        self.row_dst4 = (L.row_dst4.to(d) if L.row_dst4 is not None and lc.fuse_opt_pack
+                         else None)
         self.f_index = L.f_index.to(d)
         # split precision (compute_dtype "fp32", csrc/split.h): every bf16 kernel layout is packed as
         # a hi plane and a lo plane, (2, bf_numel); pk / pk_t view the hi planes, pk_lo / pk_t_lo
@@ -349,10 +351,13 @@ class LearnerEngine:
             check(k.r2_gather_f32(ptr(self.target), ptr(self.f_index), ptr(self.f32_t), L.f_numel, s), "gather_t")
             torch.add(self.pk_t["b_ih"], self.pk_t["b_hh"], out=self.lstm_b_t)
 
-    def _pack_step(self, interval: int, s):
+    def _pack_step(self, interval: int, s, rows_done: bool = False):
+        """rows_done: the optimizer already wrote the row packs and the target master
+        (optim.hip rmsprop_pack_kernel): gather only the packs before layout.bf_rows_begin."""
         L = self.layout
-        check(kernels().r2_pack_step(ptr(self.master), ptr(self.target), L.padded, ptr(self.bf_index),
-                                     ptr(self.bf), ptr(self.bf_t), L.bf_numel, ptr(self.f_index),
+        n_master, n_bf = (0, L.bf_rows_begin) if rows_done else (L.padded, L.bf_numel)
+        check(kernels().r2_pack_step(ptr(self.master), ptr(self.target), n_master, ptr(self.bf_index),
+                                     ptr(self.bf), ptr(self.bf_t), n_bf, ptr(self.f_index),
                                      ptr(self.f32), ptr(self.f32_t), L.f_numel,
                                      L.f_offsets["b_ih"][0], L.f_offsets["b_hh"][0],
                                      ptr(self.lstm_b), ptr(self.lstm_b_t), L.G, ptr(self.replay.step),
@@ -1005,6 +1010,18 @@ class LearnerEngine:
                             float(lc.lr), float(lc.adam_betas[0]), float(lc.adam_betas[1]),
                             float(lc.eps), gscale, ptr(self.replay.step), clip,
                             float(lc.grad_clip), s), "adam")
+        elif self.row_dst4 is not None:
+            # the update writes the row packs (w_ih / w_hh / head1) and, when due, the target
+            # master itself; the pack launch below gathers the rest
+            check(k.r2_rmsprop_pack(ptr(self.master), ptr(self.grad), ptr(self.opt_a),
+                                    ptr(self.opt_b), n, float(lc.lr), float(lc.rms_alpha),
+                                    float(lc.eps), gscale, clip, float(lc.grad_clip),
+                                    ptr(self.row_dst4), ptr(self.bf), ptr(self.bf_t),
+                                    L.bf_numel if self.sp else 0, ptr(self.target),
+                                    ptr(self.replay.step), int(lc.target_update_interval), s),
+                  "rmsprop_pack")
+            self._pack_step(int(lc.target_update_interval), s, rows_done=True)
+            return
         else:
             check(k.r2_rmsprop_centered(ptr(self.master), ptr(self.grad), ptr(self.opt_a),
                                         ptr(self.opt_b), n, float(lc.lr), float(lc.rms_alpha),
@@ -1016,6 +1033,8 @@ class LearnerEngine:
 
     def _priorities(self, end: bool = True):
         rp = self.replay
+        if self.cfg.replay.fused_prio_tail and rp.prio_tail(self.starts, self.B, self.Lb, self.T, end):
+            return
         rp.refresh_sequences(self.starts, self.B, self.Lb, self.T)
         if self.cfg.replay.fused_tree_tail and rp.update_tree_and_end_step(end):
             return

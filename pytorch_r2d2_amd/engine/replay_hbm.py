@@ -189,6 +189,29 @@ class HBMReplay:
         check(rc, "tree_update_fused_reset")
         return True
 
+    def prio_tail(self, starts: torch.Tensor, B: int, upd_lo: int, upd_hi: int,
+                  end_step: bool = True, stream=None) -> bool:
+        """The learner's priority tail in ONE launch (replay.hip prio_tail_kernel): sequence
+        priorities of the sampled windows, tree repair of every dirty leaf (grid barriers between
+        the levels, the upper levels by the last-arriving workgroup) and, with ``end_step``, the
+        step counter + dirty-list reset -- bit-identical to refresh_sequences +
+        update_tree_and_end_step.  False (nothing launched) when the shape does not allow it."""
+        if self.tree.device.type != "cuda":
+            return False
+        if getattr(self, "prio_sync", None) is None:
+            self.prio_sync = torch.zeros(4, dtype=torch.int32, device=self.tree.device)
+        rc = self.cfg.replay
+        r = kernels().r2_prio_tail(
+            ptr(starts), B, ptr(self.is_start), ptr(self.priority), ptr(self.tree),
+            self.tree_offs.ctypes.data, self.tree_sizes.ctypes.data, self.tree_levels, rc.seq_len,
+            upd_lo, upd_hi, self.cap_e, float(rc.eta), ptr(self.dirty), ptr(self.dirty_count),
+            self.max_dirty, ptr(self.prio_sync), ptr(self.step) if end_step else 0,
+            1 if end_step else 0, self._ts(stream))
+        if r == -3:
+            return False
+        check(r, "prio_tail")
+        return True
+
     def reset_dirty(self, stream=None) -> None:
         check(kernels().r2_step_end(0, ptr(self.dirty_count), self._ts(stream)), "reset_dirty")
 

@@ -75,6 +75,7 @@ _SIGS = {
     "r2_gather_state": [P, P, I, I, I, I, P, P, P, P],
     "r2_step_end": [P, P, P],
     "r2_rmsprop_centered": [P, P, P, P, I64, F, F, F, F, P, F, P],
+    "r2_rmsprop_pack": [P, P, P, P, I64, F, F, F, F, P, F, P, P, P, I64, P, P, I64, P],
     "r2_adam": [P, P, P, P, I64, F, F, F, F, F, P, P, F, P],
     "r2_sumsq": [P, I64, P, P],
     "r2_pack_bf16": [P, P, P, I64, P],
@@ -101,6 +102,8 @@ _SIGS = {
     "r2_lstm_sp_handoff8": [I],
     "r2_lstm_bwd_handoff8": [I],
     "r2_td_duel_fwd_set": [P],
+    "r2_prio_tail": [P, I, P, P, P, P, P, I, I, I, I, I, F, P, P, I, P, P, I, P],
+    "r2_td_duel_set_trace": [P],
     "r2_lstm_persist_force_slow": [I],
     "r2_xcc_probe": [P, I, I, I, P],
     "r2_gradsum_ws_floats": [],

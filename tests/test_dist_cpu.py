@@ -222,10 +222,8 @@ def _link_worker(rank, world, port, outdir, slow_rank, rounds, steps):
         wtx = [LinkSender(f"w/{a}", a, 64, 1, "cpu", tag=1) for a in range(1, world)]
         t0 = time.perf_counter()
         for it in range(steps):
-            end = time.perf_counter() + 0.002          # the learner step
-            while time.perf_counter() < end:
-                pass
-            rx.poll()
+            time.sleep(0.002)                          # the learner step (sleeps: a spinning
+            rx.poll()                                  # stand-in measures the CPU load instead)
             if it % 25 == 0:                           # weight publication, never waited for
                 for tx in wtx:
                     if tx.in_flight() == 0:
@@ -243,9 +241,7 @@ def _link_worker(rank, world, port, outdir, slow_rank, rounds, steps):
         wrx = LinkReceiver([f"w/{rank}"], [0], 64, "cpu", lambda i, buf: got.append(int(buf[0])), tag=1)
         dt = 0.010 if rank == slow_rank else 0.002
         for r in range(rounds):
-            end = time.perf_counter() + dt             # K env steps
-            while time.perf_counter() < end:
-                pass
+            time.sleep(dt)                             # K env steps
             wrx.poll()
             b = tx.acquire()
             b.fill_(0)
@@ -270,9 +266,18 @@ def test_async_links_decouple_learner_from_slow_actor(tmp_path):
     exactly once, in order, intact; weight snapshots reach both actors in publication order."""
     rounds, steps = 60, 250
     rates = {}
+    # both jobs run at the same time (two worlds of 3), so they see the same background CPU load
+    ports = [_free_port()]
+    while len(ports) < 2:
+        p = _free_port()
+        if p not in ports:
+            ports.append(p)
+    ctxs = [tmp.spawn(_link_worker, args=(3, port, str(tmp_path), slow, rounds, steps),
+                      nprocs=3, join=False) for slow, port in zip((0, 2), ports)]
+    for c in ctxs:
+        while not c.join():
+            pass
     for slow in (0, 2):
-        tmp.spawn(_link_worker, args=(3, _free_port(), str(tmp_path), slow, rounds, steps),
-                  nprocs=3, join=True)
         r0 = torch.load(os.path.join(tmp_path, f"link0_{slow}.pt"), weights_only=True)
         rates[slow] = r0["steps_per_s"]
         for i in (0, 1):

@@ -424,6 +424,66 @@ def test_rmsprop_centered_matches_torch():
     assert torch.allclose(p, ref.detach(), atol=1e-6, rtol=1e-5)
 
 
+@pytest.mark.parametrize("sp,due", [(True, False), (True, True), (False, True)])
+def test_rmsprop_pack_matches_update_then_gather(sp, due):
+    """optim.hip rmsprop_pack_kernel (the update writes the LSTM / head row packs and, when due,
+    the target master) + the prefix pack launch == rmsprop_centered + the full pack launch, bit
+    for bit: master, optimizer state, online and target packs (hi and lo planes)."""
+    cfg = get_config("atari57")
+    L = ParamLayout(cfg.model, cfg.env)
+    assert L.row_dst4 is not None
+    n = L.padded
+    torch.manual_seed(0)
+    p0 = torch.randn(n, device=DEV) * 0.05
+    g = torch.randn(n, device=DEV) * 1e-3
+    sq0 = torch.rand(n, device=DEV) * 1e-6 + 1e-6
+    ga0 = torch.randn(n, device=DEV) * 1e-5
+    idx, fidx, dst4 = L.bf_index.to(DEV), L.f_index.to(DEV), L.row_dst4.to(DEV)
+    nb = 2 * L.bf_numel if sp else L.bf_numel
+    lo = L.bf_numel if sp else 0
+    step = torch.tensor([1 if due else 0], dtype=torch.int64, device=DEV)   # interval 2
+    k, s = kernels(), stream_handle()
+    outs = []
+    for fused in (False, True):
+        p, sq, ga = p0.clone(), sq0.clone(), ga0.clone()
+        tgt = torch.zeros(n, device=DEV)
+        bf = torch.zeros(nb, dtype=torch.bfloat16, device=DEV)
+        bft = torch.zeros(nb, dtype=torch.bfloat16, device=DEV)
+        f32 = torch.zeros(L.f_numel, device=DEV)
+        f32t = torch.zeros(L.f_numel, device=DEV)
+        lb = torch.zeros(L.G, device=DEV)
+        lbt = torch.zeros(L.G, device=DEV)
+        if fused:
+            assert k.r2_rmsprop_pack(ptr(p), ptr(g), ptr(sq), ptr(ga), n, 6.25e-5, 0.95, 1.5e-7, 1.0,
+                                     0, 0.0, ptr(dst4), ptr(bf), ptr(bft), lo, ptr(tgt), ptr(step), 2,
+                                     s) == 0
+            n_master, n_bf = 0, L.bf_rows_begin
+        else:
+            assert k.r2_rmsprop_centered(ptr(p), ptr(g), ptr(sq), ptr(ga), n, 6.25e-5, 0.95, 1.5e-7,
+                                         1.0, 0, 0.0, s) == 0
+            n_master, n_bf = n, L.bf_numel
+        assert k.r2_pack_step(ptr(p), ptr(tgt), n_master, ptr(idx), ptr(bf), ptr(bft), n_bf,
+                              ptr(fidx), ptr(f32), ptr(f32t), L.f_numel, L.f_offsets["b_ih"][0],
+                              L.f_offsets["b_hh"][0], ptr(lb), ptr(lbt), L.G, ptr(step), 2, lo,
+                              s) == 0
+        torch.cuda.synchronize()
+        outs.append((p, sq, ga, tgt, bf, bft, f32, f32t, lb, lbt))
+    # padding slots of the packs (no master element) are not written by the fused path
+    real = torch.ones(L.bf_numel, dtype=torch.bool, device=DEV)
+    real[L.bf_rows_begin:] = L.bf_index[L.bf_rows_begin:].to(DEV) != L.segs["lstm.bias_ih"].offset
+    if sp:
+        real = torch.cat([real, real])
+    for name, a, b in zip(("p", "sq", "ga", "target", "bf", "bf_t", "f32", "f32_t", "lb", "lb_t"),
+                          outs[0], outs[1]):
+        if name in ("bf", "bf_t"):
+            a, b = a[real], b[real]
+        assert torch.equal(a.view(torch.int16) if a.dtype == torch.bfloat16 else a,
+                           b.view(torch.int16) if b.dtype == torch.bfloat16 else b), name
+    if due:
+        assert torch.equal(outs[1][3], outs[1][0])
+        assert outs[1][5].abs().sum() > 0
+
+
 def test_adam_matches_torch():
     n = 4099
     p = torch.randn(n, device=DEV)
@@ -511,6 +571,43 @@ def test_fused_tree_tail_matches_per_level_repair(cap):
     assert a.update_tree_and_end_step(False)
     torch.cuda.synchronize()
     assert int(a.step.item()) == 3 and int(a.dirty_count.item()) == n
+
+
+@pytest.mark.parametrize("cap", [1_000_000, 70_000])
+def test_fused_prio_tail_matches_refresh_and_tree_repair(cap):
+    """replay.hip prio_tail_kernel (sequence-priority refresh, grid barrier, level-0 repair, grid
+    barrier, level-1 repair, last-arriver upper levels + step end, one launch) == refresh +
+    the two-launch tree repair, bit for bit, rounds in a row (its counters reset themselves);
+    windows of neighbouring samples overlap (shared leaves and parents across workgroups)."""
+    from pytorch_r2d2_amd.engine.replay_hbm import HBMReplay
+    cfg = get_config("reference", **{"replay.capacity": cap, "replay.n_subrings": 8})
+    a = HBMReplay(cfg, DEV)
+    a.fill_synthetic(episode_len=120, seed=7)
+    b = HBMReplay(cfg, DEV)
+    b.fill_synthetic(episode_len=120, seed=7)
+    g = torch.Generator(device=DEV).manual_seed(cap + 1)
+    for rnd in range(4):
+        B = 64
+        idx = torch.zeros(B, dtype=torch.int32, device=DEV)
+        prob = torch.zeros(B, device=DEV)
+        a.sample(B, idx, prob)
+        if rnd == 3:
+            idx[32:] = idx[:32]          # duplicate samples: identical windows in two workgroups
+        pr = torch.rand(cap, generator=g, device=DEV) * 3
+        for r in (a, b):
+            r.priority.copy_(pr)
+        assert a.prio_tail(idx, B, 0, cfg.replay.seq_len, end_step=True)
+        b.refresh_sequences(idx, B, 0, cfg.replay.seq_len)
+        assert b.update_tree_and_end_step(True)
+        torch.cuda.synchronize()
+        assert torch.equal(a.tree, b.tree), rnd
+        assert int(a.step.item()) == int(b.step.item()) == rnd + 1
+        assert int(a.dirty_count.item()) == 0
+        assert a.prio_sync.tolist() == [0, 0, 0, 0], a.prio_sync.tolist()
+    # without end_step the counter and the dirty list are left alone
+    a.prio_tail(idx, 64, 0, cfg.replay.seq_len, end_step=False)
+    torch.cuda.synchronize()
+    assert int(a.step.item()) == 4 and int(a.dirty_count.item()) > 0
 
 
 @pytest.mark.parametrize("N", [2560, 333])
