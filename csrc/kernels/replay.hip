@@ -275,7 +275,8 @@ __device__ __forceinline__ void seqprio_refresh_wg(const int* __restrict__ start
     mx = wave_max_x(mx);
     sm = wave_sum_x(sm);
     if (lane == 0) {
-      const float leaf = eta * mx + (1.f - eta) * (sm / (float)T);
+      // one explicit fma: the two kernels that inline this must round identically
+      const float leaf = __builtin_fmaf(eta, mx, (1.f - eta) * (sm / (float)T));
       const int slot = dbase + i;
       if constexpr (SC1) {
         __hip_atomic_store(leaves + s, leaf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -214,7 +214,7 @@ struct TdDuelArgs {
   const float* b2[2];   // online, target
   float* qo[3];
   int fuse_fwd;
-  // optional stage stamps (r2_td_duel_set_trace): [workgroup][wave][8] s_memrealtime (100 MHz)
+  // optional stage stamps (r2_td_duel_set_trace): [workgroup][wave][12] s_memrealtime (100 MHz)
   long long* trace;
 };
 
@@ -283,14 +283,14 @@ __device__ __forceinline__ float td_duel_row(const ZT (&z)[2 * (HD / 64)], const
 // all three heads, the start -> row -> action / reward / done chain, the workgroup's cooperative
 // staging of both nets' head parameters into LDS, the IS-weight maximum -- before ONE barrier;
 // the wave re-derives its own sample's IS weight instead of a second barrier; the loss ticket is
-// taken before the dh product so its round trip hides under the MFMAs; dh reads W1^T two K steps
-// per 128-byte line (a K permutation shared by both operands), not half a line per load.
+// taken before the dh product so its round trip hides under the MFMAs; 8 W1^T fragments in flight.
 template <int HD, bool SP>
 __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
   constexpr int PER = HD / 64, MAXA = 8, NW = 16;
   constexpr int WROWS = (1 + MAXA) * HD;     // staged second-layer rows of one net
   const TdArgs& a = args.td;
   __shared__ int sst[256];
+  __shared__ float wst[256];    // un-normalised IS weight of every sample (this launch's staging)
   __shared__ float red[NW];
   __shared__ float lred[NW];
   __shared__ float tot_sh[NW];
@@ -299,7 +299,7 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
   __shared__ __attribute__((aligned(16))) float b1s[2][2 * HD];
   __shared__ float b2s[2][1 + HEAD_FWD_MAXA];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  long long* tr = (args.trace && lane == 0) ? args.trace + ((size_t)blockIdx.x * NW + wave) * 8 : nullptr;
+  long long* tr = (args.trace && lane == 0) ? args.trace + ((size_t)blockIdx.x * NW + wave) * 12 : nullptr;
 #define TD_STAMP(k) if (tr) tr[k] = (long long)__builtin_amdgcn_s_memrealtime();
   TD_STAMP(0);
   const int n = a.Tl * a.B;
@@ -370,6 +370,7 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
   if (tid < a.B) sst[tid] = a.starts[tid];
   bool gn = false;
   const float w_t = tid < a.B ? is_weight(a, tid, &gn) : 1.f;
+  if (tid < a.B) wst[tid] = w_t;
   const float m = wave_max(tid < a.B ? w_t : 0.f);
   if (lane == 0) red[wave] = m;
   TD_STAMP(1);
@@ -414,6 +415,7 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
     }
     if (!(valid && lane < a.A)) { qa = NEG; qt = 0.f; qs = 0.f; }
   }
+  TD_STAMP(8);
 
   const float inv_n = 1.f / (float)n;
   float lsum = 0.f;
@@ -421,22 +423,18 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
 #pragma unroll
   for (int e = 0; e < PER; ++e) { dz_v[e] = 0.f; dz_a[e] = 0.f; }
   if (valid) {
-    // argmax_a Q_online(s_{t+n}): first maximum, as td_kernel's sequential scan
-    float bv = qa;
-    int best = lane < a.A ? lane : 1 << 20;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(bv, o, 64);
-      const int oi = __shfl_xor(best, o, 64);
-      if (ov > bv || (ov == bv && oi < best)) { bv = ov; best = oi; }
-    }
-    float boot = __shfl(qt, best, 64);
+    // argmax_a Q_online(s_{t+n}): first maximum, as td_kernel's sequential scan -- the wave max
+    // (DPP), then the lowest lane holding it (ballot); best / act are wave-uniform, so the lane
+    // reads are v_readlane, not LDS permutes
+    const float bv = wave_max_x(qa);
+    const unsigned long long hit = __ballot(lane < a.A && qa == bv);
+    const int best = hit ? __ffsll((long long)hit) - 1 : 0;
+    float boot = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qt), best));
     if (a.value_rescale) boot = vr_hinv(boot, a.vr_eps);
     float y = rew + (dn ? 0.f : a.gamma_n * boot);
     if (a.value_rescale) y = vr_h(y, a.vr_eps);
-    const float delta = __shfl(qs, act, 64) - y;
-    bool gdummy;
-    const float wb = is_weight(a, b, &gdummy) / wmax;   // == the staged w / wmax of sample b
+    const float delta = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(qs), act)) - y;
+    const float wb = wst[b] / wmax;          // == td_kernel's staged w / wmax of sample b
     const float g = wb * delta * inv_n;      // dL/dQ[act]; every other action 0
     // the wave checks the B starts 64 at a time for a later duplicate of this row
     const bool own = a.priority ? __all(prio_owner(sst, a.B, a.Tl, a.burn_in, a.cap_e, tl, b, lane, 64))
@@ -448,6 +446,7 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
       if (own) a.priority[row] = powf(ad + a.prio_eps, a.alpha);
     }
     if (lane < a.A) a.dq[(size_t)i * a.A + lane] = lane == act ? g : 0.f;
+    TD_STAMP(9);
     // dueling backward of row i (dueling_bwd_kernel's arithmetic on dq = g e_act)
     float dv = 0.f;
     for (int k = 0; k < a.A; ++k) dv += (k == act) ? g : 0.f;
@@ -485,13 +484,13 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
   TD_STAMP(3);
   // ---- fused dh = dz @ W1 of the 16 rows (dz staged in LDS; wave w owns dh columns 16w..16w+15,
   // K = 2HD on v_mfma_f32_16x16x32_bf16, W1^T fragments from L2; 3 passes in split precision).
-  // K order: MFMA step s covers k = 64 (s >> 1) + 16 kq + 8 (s & 1) + [0, 8) for lane group kq, so
-  // the two steps of a pair read one 32-byte run per lane (a full 128-byte line per row).
+  // K order: step s covers k = 32 s + 8 kq + [0, 8) for lane group kq -- the dh GEMM's own order,
+  // so dh is bit-identical to the separate launch (tests/test_engine_gpu.py)
   constexpr int KD = 2 * HD, DZS = KD + 8;             // padded LDS rows
-  constexpr int KS = KD / 32, D = 4;
+  constexpr int KS = KD / 32, D = SP ? 8 : 4;         // W1^T fragments in flight
   __shared__ __attribute__((aligned(16))) bf16 dzs[SP ? 2 : 1][NW * DZS];
   const int r16 = lane & 15, kq = lane >> 4;
-  auto koff = [&](int s) { return 64 * (s >> 1) + 16 * kq + 8 * (s & 1); };
+  auto koff = [&](int s) { return 32 * s + 8 * kq; };
   bf16x8 rb[D], rbl[D];
   const bf16* bt = args.w1t ? args.w1t + (size_t)(wave * 16 + r16) * KD : nullptr;
   const bf16* btl = (SP && args.w1t) ? args.w1t_lo + (size_t)(wave * 16 + r16) * KD : nullptr;

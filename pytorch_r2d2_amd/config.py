@@ -112,6 +112,9 @@ class LearnerConfig:
     # post-BPTT GEMMs: "group" = weight gradients + dX in one grid (58 us vs 85 separate),
     # "group:a,b,c,d" = with K splits, "separate"
     bwd_gemm: str = "group"
+    # rmsprop writes the LSTM / head row packs itself (optim.hip rmsprop_pack_kernel) instead of
+    # a gather over the updated master in the pack launch
+    fuse_opt_pack: bool = True
     td_fuse_head_bwd: bool = True     # dueling-head backward inside the TD launch (td_duel_kernel)
     # ... and the heads' dueling FORWARD too (fixed / reference target modes: the TD launch forms
     # relu(z + b1) and the Q rows of all three heads itself; no separate dueling_fwd launch)
@@ -202,9 +205,6 @@ class DistConfig:
     # weights across ranks and a zero error word (the multi-rank DP path runs the segment graphs
     # with the collectives issued between them, the form the multi-rank tests pin)
     graph_collectives_multi: bool = False
-    # rmsprop writes the LSTM / head row packs itself (optim.hip rmsprop_pack_kernel) instead of
-    # a gather over the updated master in the pack launch
-    fuse_opt_pack: bool = True
     learner_steps_per_round: int = 1    # run_split default run length: rounds x this
 
 

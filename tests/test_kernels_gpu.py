@@ -585,6 +585,7 @@ def test_fused_prio_tail_matches_refresh_and_tree_repair(cap):
     a.fill_synthetic(episode_len=120, seed=7)
     b = HBMReplay(cfg, DEV)
     b.fill_synthetic(episode_len=120, seed=7)
+    assert torch.equal(a.tree, b.tree) and int(a.dirty_count.item()) == int(b.dirty_count.item())
     g = torch.Generator(device=DEV).manual_seed(cap + 1)
     for rnd in range(4):
         B = 64
@@ -600,7 +601,13 @@ def test_fused_prio_tail_matches_refresh_and_tree_repair(cap):
         b.refresh_sequences(idx, B, 0, cfg.replay.seq_len)
         assert b.update_tree_and_end_step(True)
         torch.cuda.synchronize()
-        assert torch.equal(a.tree, b.tree), rnd
+        if not torch.equal(a.tree, b.tree):
+            d = torch.nonzero(a.tree != b.tree).flatten().cpu()
+            offs = [int(o) for o in a.tree_offs]
+            lv = [sum(int(i) >= o for o in offs[1:]) for i in d[:8]]
+            raise AssertionError(f"round {rnd}: {d.numel()} differ, first {d[:8].tolist()} levels {lv} "
+                                 f"a {a.tree[d[:8]].tolist()} b {b.tree[d[:8]].tolist()} "
+                                 f"offs {offs} sync {a.prio_sync.tolist()}")
         assert int(a.step.item()) == int(b.step.item()) == rnd + 1
         assert int(a.dirty_count.item()) == 0
         assert a.prio_sync.tolist() == [0, 0, 0, 0], a.prio_sync.tolist()

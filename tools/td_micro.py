@@ -93,7 +93,7 @@ res = {name: timeit(launch(d, f_)) for name, d, f_ in
        (("plain", False, False), ("dh", True, False), ("fwd_dh", True, True))}
 # stage stamps of the engine's launch: per-stage median / max over waves (us), and the spread
 # of workgroup start times
-tr = torch.zeros((n + 15) // 16, 16, 8, dtype=torch.int64, device=DEV)
+tr = torch.zeros((n + 15) // 16, 16, 12, dtype=torch.int64, device=DEV)
 k.r2_td_duel_set_trace(ptr(tr))
 launch(True, True)()
 torch.cuda.synchronize()
@@ -101,9 +101,12 @@ k.r2_td_duel_set_trace(None)
 t = tr.cpu().numpy().astype(np.float64) / 100.0      # s_memrealtime: 100 MHz -> us
 t0 = t[:, :, 0].min()
 stages = {}
-names = ["issue", "barrier1", "fwd_td_dz", "barrier2", "dh", "last_flag"]
-for j, nm in enumerate(names):
-    d = t[:, :, j + 1] - t[:, :, j]
+# stamp order in the kernel: 0 top, 1 staging issued, 2 after barrier 1, 8 heads forward done,
+# 9 TD done, 3 dz stored, 4 after barrier 2, 5 dh done, 6 last flag, 7 loss (last workgroup)
+seq = [(0, 1, "issue"), (1, 2, "barrier1"), (2, 8, "heads_fwd"), (8, 9, "td"), (9, 3, "dz"),
+       (3, 4, "barrier2"), (4, 5, "dh"), (5, 6, "last_flag")]
+for a_, b_, nm in seq:
+    d = t[:, :, b_] - t[:, :, a_]
     stages[nm] = [round(float(np.median(d)), 2), round(float(d.max()), 2)]
 stages["wg_start_spread"] = round(float(t[:, 0, 0].max() - t0), 2)
 stages["wave_end_max"] = round(float(t[:, :, 6].max() - t0), 2)
