@@ -87,6 +87,8 @@ class HBMReplay:
         self.step = torch.zeros(1, dtype=torch.int64, device=d)
         # arrival ticket of the fused tree repair (allocated before any graph capture)
         self.tree_ticket = torch.zeros(1, dtype=torch.int32, device=d) if d.type == "cuda" else None
+        # prio_tail_kernel: two grid-barrier counters, the arrival ticket, an error word
+        self.prio_sync = torch.zeros(4, dtype=torch.int32, device=d) if d.type == "cuda" else None
         self.seed = int(cfg.seed) * 0x9E3779B1 + 12345
         self.heads = np.zeros(n_sub, dtype=np.int64)   # per-sub-ring write heads (host mirror)
         self.total_written = 0
@@ -198,8 +200,6 @@ class HBMReplay:
         update_tree_and_end_step.  False (nothing launched) when the shape does not allow it."""
         if self.tree.device.type != "cuda":
             return False
-        if getattr(self, "prio_sync", None) is None:
-            self.prio_sync = torch.zeros(4, dtype=torch.int32, device=self.tree.device)
         rc = self.cfg.replay
         r = kernels().r2_prio_tail(
             ptr(starts), B, ptr(self.is_start), ptr(self.priority), ptr(self.tree),

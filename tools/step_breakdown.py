@@ -5,7 +5,7 @@ import glob
 import sys
 
 
-def main(path_glob, out=None, last=1, marker=('step_end', 'tree_update_tail')):
+def main(path_glob, out=None, last=1, marker=('step_end', 'prio_tail', 'tree_update_tail')):
     import os
     paths = sorted(glob.glob(path_glob), key=os.path.getmtime, reverse=True)
     rows = list(csv.DictReader(open(paths[0])))
@@ -37,4 +37,4 @@ def main(path_glob, out=None, last=1, marker=('step_end', 'tree_update_tail')):
 if __name__ == "__main__":
     main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None,
          int(sys.argv[3]) if len(sys.argv) > 3 else 1,
-         sys.argv[4] if len(sys.argv) > 4 else ('step_end', 'tree_update_tail'))
+         sys.argv[4] if len(sys.argv) > 4 else ('step_end', 'prio_tail', 'tree_update_tail'))
