@@ -618,6 +618,48 @@ static int g5_tiles(const GemmProb& p, int bm, int bn) {
   return ((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn);
 }
 
+// Automatic K splits (split[i] == 0) once the tile is fixed: the problem's split grows while its
+// per-item K steps exceed both the longest fixed-split problem's and 2, and the launch's items
+// still fit one round on nc CUs.  Small-M launches (the reference config's 80-row dX, 184-row
+// x-projection: 7-64 items of 25-32 K steps on 256 CUs) then spread their K over the idle CUs;
+// launches that already fill the chip keep split 1.  Splits >= 1 pass through.
+static void g5_auto_split(const GemmProb* p, const int* split_in, int np, int cfg, int nc,
+                          int* out) {
+  const int bm = g5_cfgs[cfg][0], bn = g5_cfgs[cfg][1], bk = g5_cfgs[cfg][2];
+  long long items = 0;
+  int target = 2;
+  for (int i = 0; i < np; ++i) {
+    out[i] = split_in && split_in[i] > 0 ? split_in[i] : 1;
+    items += (long long)g5_tiles(p[i], bm, bn) * out[i];
+    if (split_in && split_in[i] > 0) {
+      const int ks = (p[i].K + bk - 1) / bk;
+      target = max(target, (ks + out[i] - 1) / out[i]);
+    }
+  }
+  if (!split_in) return;
+  // a split pays only when it shortens the launch's longest item: every auto problem at the
+  // current maximum grows together (one of them alone leaves the critical path where it was)
+  auto per = [&](int i) {
+    const int ks = (p[i].K + bk - 1) / bk;
+    return (ks + out[i] - 1) / out[i];
+  };
+  for (;;) {
+    int mx = 0;
+    for (int i = 0; i < np; ++i) mx = max(mx, per(i));
+    if (mx <= target) return;
+    long long extra = 0;
+    for (int i = 0; i < np; ++i) {
+      if (per(i) != mx) continue;
+      if (split_in[i] != 0) return;                  // a fixed-split problem sets the pace
+      extra += g5_tiles(p[i], bm, bn);
+    }
+    if (items + extra > nc) return;
+    for (int i = 0; i < np; ++i)
+      if (per(i) == mx) out[i] += 1;
+    items += extra;
+  }
+}
+
 // descs: np x GEMM_DESC (gemm.hip r2_gemm layout), every operand split (A_lo and B_lo set), one B
 // layout per launch.  split: np K splits (null = 1).  cfg: index into g5_cfgs, or -1 = pick by a
 // CU-utilisation model for n_cus resident workgroups (one per CU).  Returns the cfg used (>= 0)
@@ -636,7 +678,7 @@ extern "C" int r2_gemm5(const int64_t* descs, const int* split, int np, int cfg,
     if (bkm < 0) bkm = a.p[i].b_kmajor;
     if (bkm != a.p[i].b_kmajor) return -5;
     all_k = all_k && a.p[i].a_kmajor;
-    a.split[i] = split && split[i] > 1 ? split[i] : 1;
+    a.split[i] = split && split[i] > 1 ? split[i] : 1;   // auto (0) counts as 1 for the tile choice
   }
   auto ok = [&](int c) {
     const int bm = g5_cfgs[c][0], bn = g5_cfgs[c][1];
@@ -664,6 +706,11 @@ extern "C" int r2_gemm5(const int64_t* descs, const int* split, int np, int cfg,
     }
   }
   if (cfg < 0 || cfg >= g5_ncfg || !ok(cfg)) return -8;
+  {
+    int sp[gm::MAXP];
+    g5_auto_split(a.p, split, np, cfg, n_cus > 0 ? n_cus : 256, sp);
+    for (int i = 0; i < np; ++i) a.split[i] = sp[i];
+  }
   const int bm = g5_cfgs[cfg][0], bn = g5_cfgs[cfg][1];
   int items = 0, tks = 0;
   long long slabs = 0;
@@ -731,15 +778,22 @@ extern "C" int r2_gemm5(const int64_t* descs, const int* split, int np, int cfg,
 }
 
 // bytes of split-K workspace for configuration cfg
-extern "C" long long r2_gemm5_ws_bytes(const int64_t* descs, const int* split, int np, int cfg) {
-  if (cfg < 0 || cfg >= g5_ncfg) return -1;
+extern "C" long long r2_gemm5_ws_bytes_nc(const int64_t* descs, const int* split, int np, int cfg,
+                                          int n_cus) {
+  if (cfg < 0 || cfg >= g5_ncfg || np < 1 || np > gm::MAXP) return -1;
+  GemmProb p[gm::MAXP];
+  for (int i = 0; i < np; ++i)
+    if (gemm_parse_desc(descs + GEMM_DESC * i, p[i])) return -1;
+  int sp[gm::MAXP];
+  g5_auto_split(p, split, np, cfg, n_cus > 0 ? n_cus : 256, sp);
   long long b = 0;
-  for (int i = 0; i < np; ++i) {
-    GemmProb p;
-    if (gemm_parse_desc(descs + GEMM_DESC * i, p)) return -1;
-    if (split && split[i] > 1)
-      b += (long long)g5_tiles(p, g5_cfgs[cfg][0], g5_cfgs[cfg][1]) * split[i] * g5_cfgs[cfg][0] *
+  for (int i = 0; i < np; ++i)
+    if (sp[i] > 1)
+      b += (long long)g5_tiles(p[i], g5_cfgs[cfg][0], g5_cfgs[cfg][1]) * sp[i] * g5_cfgs[cfg][0] *
            g5_cfgs[cfg][1] * 4;
-  }
   return b;
+}
+
+extern "C" long long r2_gemm5_ws_bytes(const int64_t* descs, const int* split, int np, int cfg) {
+  return r2_gemm5_ws_bytes_nc(descs, split, np, cfg, 256);
 }

@@ -130,7 +130,9 @@ class LearnerConfig:
     # once, 3 MFMAs per fragment pair: x-projection 164 -> 125 us, post-BPTT group 142 -> 106 us
     # at K splits 4,4,4,1, dh 26 -> 18 us; profiles/archive/r02_gemm_sp_micro_v1.txt) | "multipass"
     sp_gemm: str = "fused"
-    sp_group_splits: str = "4,4,4,1"  # K splits of the fused post-BPTT group (dW_ih, dW_hh, dW_head1, dX)
+    # K splits of the fused post-BPTT group (dW_ih, dW_hh, dW_head1, dX), or "auto"
+    # (learner_engine._auto_group_splits: paper config 4,4,4,1, reference config 1,1,1,4)
+    sp_group_splits: str = "auto"
     # split GEMMs on gemm6 (gemm_sp.hip: the fragment planes refilled between the three product
     # passes, one barrier per LDS tile; the heads' layer-1 GEMMs join the one-pass kernel too):
     # x-projection 115-129 -> 102-110 us, tools/gemm6_probe.py

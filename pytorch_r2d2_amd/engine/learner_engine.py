@@ -451,7 +451,7 @@ class LearnerEngine:
             probs = [Gemm(h, pk["head1"].t(), zb, a_lo=hl, b_lo=pkl["head1"].t())
                      for (pk, h, zb, _, _), (pkl, hl) in zip(jobs, lo)]
             if self.cfg.learner.sp_gemm6 and self.cfg.learner.sp_gemm == "fused":
-                self._gemm_sp("heads", probs, cfg=-1)   # gemm6
+                self._gemm_sp("heads", probs, splits=[0] * len(probs), cfg=-1)   # gemm6
             else:
                 gemm(*probs)
             zs = [zb for _, _, zb, _, _ in jobs]
@@ -584,7 +584,7 @@ class LearnerEngine:
                 Gemm(self.X_on, pk["w_ih"].t(), xp_on, bias=self.lstm_b, a_lo=self.X_on_lo,
                      b_lo=self.pk_lo["w_ih"].t()),
                 Gemm(self.X_tg, pt["w_ih"].t(), xp_tg, bias=self.lstm_b_t, a_lo=self.X_tg_lo,
-                     b_lo=self.pk_t_lo["w_ih"].t())])
+                     b_lo=self.pk_t_lo["w_ih"].t())], splits=[0, 0])   # automatic K splits
         else:
             xp_on, xp_tg = self.xp_on, self.xp_tg
             gemm(Gemm(self.X_on, pk["w_ih"].t(), xp_on, bias=self.lstm_b),
@@ -721,7 +721,8 @@ class LearnerEngine:
             check(k.r2_head_grads_sp(*hg, s), "head_grads_sp")
         dh = self.dh
         if not self._dh_done:   # else produced by the TD launch
-            self._gemm_sp("dh", [Gemm(self.dz, pk["head1"], dh, a_lo=self.dz_lo, b_lo=pkl["head1"])])
+            self._gemm_sp("dh", [Gemm(self.dz, pk["head1"], dh, a_lo=self.dz_lo, b_lo=pkl["head1"])],
+                          splits=[0])
         bptt = [ptr(dh), ptr(self.gates), ptr(self.cseq["on"]), ptr(self.c0["on"]), ptr(pk["w_hhT"]),
                 ptr(pkl["w_hhT"]), ptr(self.dgates), ptr(self.dgates_lo), B, T, Lb, H, ptr(self.ctr),
                 ptr(self.err), ptr(self.ring_b), ptr(self.bias_ws), ptr(self.gate_perm_i32),
@@ -757,7 +758,9 @@ class LearnerEngine:
         x_job = Gemm(self.dgates, pk["w_ih"], self.dX, a_lo=self.dgates_lo, b_lo=pkl["w_ih"],
                      c_lo=self.dX_lo)
         if self.cfg.learner.sp_gemm == "fused":
-            splits = [int(v) for v in self.cfg.learner.sp_group_splits.replace(":", ",").split(",")]
+            sg = self.cfg.learner.sp_group_splits
+            splits = (self._auto_group_splits([w_jobs[2], w_jobs[1], w_jobs[0], x_job]) if sg == "auto"
+                      else [int(v) for v in sg.replace(":", ",").split(",")])
             self._gemm_sp("group", [w_jobs[2], w_jobs[1], w_jobs[0], x_job], splits,
                           cfg=-1)
             self._dX = self.dX
@@ -769,6 +772,20 @@ class LearnerEngine:
             gemm(w_jobs[2], w_jobs[1], w_jobs[0])
             gemm(x_job)
         self._dX = self.dX
+
+    def _auto_group_splits(self, probs):
+        """K splits of the post-BPTT group [dW_head1, dW_hh, dW_ih, dX] on 256 x 256 tiles: the
+        weight gradients (K = learn x batch) split 4 ways when they have >= 32 K steps (paper
+        config: 80), else 1 (a split's partial-tile write + reduction outweighs 1-3 K steps);
+        dX (K = 4H) takes the largest of 4 / 2 ways whose items still fit one round on the CUs.
+        Measured: paper 4,4,4,1 (profiles/r04_group_splits_ab.txt: 3,4,4,2 / 3,5,5,2 slower);
+        reference config 1,1,1,4 = 0.2455 ms vs 0.3038 at 4,4,4,1."""
+        t = lambda g: -(-g.a.shape[0] // 256) * -(-g.b.shape[1] // 256)   # noqa: E731
+        ks_w = -(-probs[0].a.shape[1] // 32)
+        sw = 4 if ks_w >= 32 else 1
+        items = sw * sum(t(g) for g in probs[:3])
+        sx = next((c for c in (4, 2) if items + c * t(probs[3]) <= self.n_cus), 1)
+        return [sw, sw, sw, sx]
 
     def _gemm_sp(self, site: str, probs, splits=None, cfg: int = -1):
         """Split-precision GEMMs of one call site: the fused one-pass kernel (gemm_sp.hip) with a
@@ -782,7 +799,7 @@ class LearnerEngine:
             self._sp_ws = {}
         cur = self._sp_ws.get(site)
         if cur is None:   # (inside a capture: from the graph's pool, kept alive here)
-            need = max(gemm_sp_ws_bytes(probs, splits, c) for c in range(len(G5_CFGS)))
+            need = max(gemm_sp_ws_bytes(probs, splits, c, self.n_cus) for c in range(len(G5_CFGS)))
             cur = (torch.zeros(max(need // 4, 1), dtype=torch.float32, device=self.device),
                    torch.zeros(4096, dtype=torch.int32, device=self.device))
             self._sp_ws[site] = cur

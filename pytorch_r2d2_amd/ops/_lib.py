@@ -121,6 +121,7 @@ _SIGS = {
     "r2_apply_pending": [P, P, I, P, P, P, I, I, F, P, P, P, I, P, P],
     "r2_gemm5": [P, P, I, I, P, I64, P, I, I, P],
     "r2_gemm5_ws_bytes": [P, P, I, I],
+    "r2_gemm5_ws_bytes_nc": [P, P, I, I, I],
     "r2_gemm5_set_mode": [I],
     "r2_ingest_record": [P, P],
     "r2_ingest_args_bytes": [],
@@ -166,7 +167,7 @@ def kernels():
             if fn is None:
                 continue
             fn.argtypes = argtypes
-            fn.restype = ctypes.c_longlong if name.endswith("_ws_bytes") else ctypes.c_int
+            fn.restype = ctypes.c_longlong if ("_ws_bytes" in name) else ctypes.c_int
         _lib = lib
         return lib
 

@@ -106,8 +106,10 @@ def gemm_sp(problems: List[Gemm], splits: Optional[List[int]] = None, cfg: int =
             n_cus: int = 0, stream=None) -> int:
     """Fused split-precision GEMM (csrc/kernels/gemm_sp.hip): up to 4 problems (every operand
     split, shared B layout, any A layout) in one launch, each with a K split; all three hi / lo
-    products from ONE pass over K.  ``cfg``: index into ``G5_CFGS`` or -1 = the launcher picks the
-    tile for ``n_cus`` CUs.  ``ws`` / ``tickets``: split-K workspace (fp32) and zeroed int32
+    products from ONE pass over K.  ``splits``: K split per problem, 0 = automatic (spread a
+    small-M problem's K over CUs the launch leaves idle, gemm_sp.hip g5_auto_split).  ``cfg``:
+    index into ``G5_CFGS`` or -1 = the launcher picks the tile for ``n_cus`` CUs.  ``ws`` /
+    ``tickets``: split-K workspace (fp32) and zeroed int32
     tickets; allocated (and cached per device) when omitted -- pass them explicitly inside a graph
     capture.  Returns the configuration used."""
     arr = np.asarray([v for p in problems for v in p.desc()], dtype=np.int64)
@@ -116,10 +118,10 @@ def gemm_sp(problems: List[Gemm], splits: Optional[List[int]] = None, cfg: int =
     if ws is None or tickets is None:
         dev = problems[0].c.device
         need = 0
-        if (sp > 1).any():
+        if (sp != 1).any():
             for c in ([cfg] if cfg >= 0 else range(len(G5_CFGS))):
-                need = max(need, int(k.r2_gemm5_ws_bytes(arr.ctypes.data, sp.ctypes.data,
-                                                         len(problems), c)))
+                need = max(need, int(k.r2_gemm5_ws_bytes_nc(arr.ctypes.data, sp.ctypes.data,
+                                                            len(problems), c, int(n_cus))))
         key = str(dev)
         cur = _G5_WS.get(key)
         if cur is None or cur[0].numel() * 4 < need:
@@ -137,7 +139,8 @@ def gemm_sp(problems: List[Gemm], splits: Optional[List[int]] = None, cfg: int =
     return rc
 
 
-def gemm_sp_ws_bytes(problems: List[Gemm], splits: List[int], cfg: int) -> int:
+def gemm_sp_ws_bytes(problems: List[Gemm], splits: List[int], cfg: int, n_cus: int = 0) -> int:
     arr = np.asarray([v for p in problems for v in p.desc()], dtype=np.int64)
     sp = np.asarray(splits, dtype=np.int32)
-    return int(kernels().r2_gemm5_ws_bytes(arr.ctypes.data, sp.ctypes.data, len(problems), cfg))
+    return int(kernels().r2_gemm5_ws_bytes_nc(arr.ctypes.data, sp.ctypes.data, len(problems), cfg,
+                                              int(n_cus)))
