@@ -365,18 +365,31 @@ __global__ __launch_bounds__(256) void prio_tail_kernel(
            gridDim.x - 1;
   __syncthreads();
   if (!last) return;
+  // levels 3.. recomputed by this workgroup alone: level 2 comes from memory (the other
+  // workgroups' sc1 stores), every level above from the LDS copy of the one below it -- one
+  // memory round trip for the whole top of the tree instead of one per level (the stores still
+  // go out write-through for the next step's sampling)
+  __shared__ float lvl_buf[2][64];       // levels >= 3 hold <= 64 nodes (r2_prio_tail checks)
+  int cur = 0;
   for (int l = 2; l + 1 < g.levels; ++l) {
     const float* child = tree + g.off[l];
     float* parent = tree + g.off[l + 1];
     for (int64_t p = wave; p < g.size[l + 1]; p += nw) {
       const int64_t c = p * 64 + lane;
-      float v = c < g.size[l] ? __hip_atomic_load(child + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+      float v = 0.f;
+      if (c < g.size[l])
+        v = l == 2 ? __hip_atomic_load(child + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                   : lvl_buf[cur ^ 1][c];
       v = wave_sum_x(v);
-      if (lane == 0) __hip_atomic_store(parent + p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) {
+        __hip_atomic_store(parent + p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lvl_buf[cur][p] = v;
+      }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    cur ^= 1;
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (threadIdx.x == 0) {
     sync[0] = 0u;
     sync[1] = 0u;
