@@ -1293,10 +1293,18 @@ class LearnerEngine:
 
     def error_word(self) -> int:
         """The persistent kernels' error word (non-zero: a bounded hand-off spin timed out, so the
-        step's recurrent state is garbage).  One D2H read."""
-        return int(self.err.item())
+        step's recurrent state is garbage; bit 30: the priority tail's grid barrier timed out, so
+        the sum tree missed a repair).  One or two D2H reads."""
+        w = int(self.err.item())
+        ps = getattr(self.replay, "prio_sync", None)
+        if ps is not None and int(ps[3].item()) != 0:
+            w |= 1 << 30
+        return w
 
     def check_errors(self) -> None:
         """Raise if a persistent kernel's bounded spin timed out (hand-off failure)."""
-        if self.error_word() != 0:
+        w = self.error_word()
+        if w & (1 << 30):
+            raise RuntimeError("priority tail kernel reported a grid-barrier timeout")
+        if w != 0:
             raise RuntimeError("persistent LSTM kernel reported a hand-off timeout")
