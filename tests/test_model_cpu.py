@@ -95,6 +95,33 @@ def test_layout_roundtrip_and_packing():
     assert L.torso_offset >= L.core_numel and L.torso_offset % 4 == 0
 
 
+@pytest.mark.parametrize("preset", ["atari57", "seaquest8", "dmlab30"])
+def test_row_pack_map_reproduces_the_gather(preset):
+    """layout.row_dst4 (the packs the RMSprop update writes itself, optim.hip rmsprop_pack_kernel):
+    scattering every master float4 to its destination reproduces the gather pack of everything
+    from bf_rows_begin on (padding slots aside), each destination written once, and the prefix
+    the pack launch still gathers holds the other packs."""
+    cfg = get_config(preset)
+    L = ParamLayout(cfg.model, cfg.env)
+    dst = L.row_dst4
+    assert dst is not None
+    master = torch.randn(L.padded)
+    ref = master[L.bf_index.long()]
+    out = torch.full((L.bf_numel,), float("nan"))
+    q = torch.nonzero(dst >= 0).flatten()
+    d = dst[q].long()
+    for e in range(4):
+        out[d + e] = master[4 * q + e]
+    assert torch.unique(d).numel() == d.numel()
+    tail = slice(L.bf_rows_begin, L.bf_numel)
+    pad = L.bf_index[tail] == L.segs["lstm.bias_ih"].offset
+    assert torch.equal(out[tail][~pad], ref[tail][~pad])
+    for name in ("w_ih", "w_hh", "head1"):
+        assert L.bf_offsets[name][0] >= L.bf_rows_begin
+    for name in ("w_hhT", "head1T"):
+        assert L.bf_offsets[name][0] < L.bf_rows_begin
+
+
 def _toy_batch(cfg, B=3, seed=0):
     g = torch.Generator().manual_seed(seed)
     rc = cfg.replay
