@@ -304,10 +304,11 @@ __global__ void seqprio_refresh_kernel(const int* __restrict__ starts, int B,
                             dirty, count, max_dirty);
 }
 
-// grid barrier of a launch whose workgroups are all resident (B <= 256 small workgroups): every
-// thread drains its stores, one arrival add per workgroup, thread 0 polls the counter
-// (agent-scope loads).  Bounded: after ~0.2 s of polling it sets *err and goes on (a wrong tree
-// rather than a hung GPU; the host reads err).
+// grid barrier of a launch whose workgroups are all resident (r2_prio_tail checks B against the
+// occupancy-derived resident capacity): every thread drains its stores, one arrival add per
+// workgroup, thread 0 polls the counter (agent-scope loads).  Bounded: 2^22 polls with
+// s_sleep 2 (~128 cycles each) plus the load round trip, i.e. a few seconds, then it sets *err
+// and goes on (a wrong tree rather than a hung GPU; LearnerEngine.check_errors reads the word).
 __device__ __forceinline__ void prio_grid_barrier(unsigned* ctr, unsigned target, unsigned* err) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -661,6 +662,8 @@ extern "C" int r2_seqprio_refresh(const int* starts, int B, const uint8_t* is_st
 
 // the fused priority tail (prio_tail_kernel); sync: 4 zeroed uints.  -3: the tree shape does not
 // allow the fold (tree_update_fused's conditions) or B > 256 (all workgroups must be resident)
+extern "C" int r2_get_num_cus();   // lstm_persist.hip: CUs of the learner's stream
+
 extern "C" int r2_prio_tail(const int* starts, int B, const uint8_t* is_start, const float* priority,
                             float* tree, const int64_t* offs, const int64_t* sizes, int levels,
                             int T, int upd_lo, int upd_hi, int cap_e, float eta, int* dirty,
@@ -668,6 +671,13 @@ extern "C" int r2_prio_tail(const int* starts, int B, const uint8_t* is_start, c
                             int reset_count, void* stream) {
   if (upd_hi - upd_lo + T - 1 > 2048) return -2;
   if (B <= 0 || B > 256) return -3;
+  {   // every workgroup must be resident at once (grid barriers): B <= CUs x blocks per CU
+    static int per_cu = 0;
+    if (!per_cu && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)prio_tail_kernel,
+                                                                256, 0) != hipSuccess)
+      per_cu = 1;
+    if (B > r2_get_num_cus() * (per_cu > 0 ? per_cu : 1)) return -4;   // caller: 3-launch path
+  }
   if (levels < 4 || levels > TREE_MAX_LEVELS) return -3;
   for (int l = 3; l < levels; ++l)
     if (sizes[l - 1] > 64 * 64) return -3;

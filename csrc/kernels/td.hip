@@ -601,7 +601,10 @@ extern "C" int r2_td_duel_dh(const float*, const float*, const float*, const int
 // b2_on, b2_tg, q_on, q_nx, q_tg (q outs may be 0)} -- zr of r2_td_duel_dh becomes an output.
 static thread_local int64_t g_td_fwd[12];
 static thread_local bool g_td_fwd_on = false;
-static long long* g_td_trace = nullptr;
+// Stage-stamp buffer of the next eager launches on this host thread (tools/td_micro.py).  A
+// launch being captured into a graph never takes it (r2_td_duel_dh): the graph would keep
+// writing stamps into the buffer after it is cleared or freed.
+static thread_local long long* g_td_trace = nullptr;
 extern "C" int r2_td_duel_set_trace(long long* tr) {
   g_td_trace = tr;
   return 0;
@@ -651,7 +654,12 @@ extern "C" int r2_td_duel_dh(const float* q_sa, const float* q_arg, const float*
                 prio_eps, beta, value_rescale, dp},
                zr, w2, dz, dva, dz_lo, w1t, w1t_lo, dh};
   d.fuse_fwd = 0;
-  d.trace = g_td_trace;
+  {   // never bake a stamp buffer into a captured launch
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    const bool cap = hipStreamIsCapturing((hipStream_t)stream, &st) == hipSuccess &&
+                     st != hipStreamCaptureStatusNone;
+    d.trace = cap ? nullptr : g_td_trace;
+  }
   if (g_td_fwd_on) {
     g_td_fwd_on = false;   // one launch per set
     if (A > HEAD_FWD_MAXA) return -6;

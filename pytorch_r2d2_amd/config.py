@@ -193,6 +193,11 @@ class DistConfig:
     push_rows: int = 32
     push_slots: int = 4
     publish_steps: int = 100
+    # the learner reads its links' ``sent`` counters (one c10d store round trip per feeding actor
+    # rank, served by rank 0) at most every ``poll_steps`` learner steps once it is training; an
+    # actor rank ships a record every push_rows env steps, so polling every step only adds host
+    # latency to the step loop (before training starts every iteration polls)
+    poll_steps: int = 8
     # rehearsal: run the data-parallel step machinery (segmented graphs, bucketed RCCL
     # all-reduces on the comm stream, CU reservation, the shard-stats all-gather) at world 1
     # (bench.py --force-dp under torchrun): the collectives are one-rank no-ops, the code path is

@@ -207,7 +207,7 @@ class HBMReplay:
             upd_lo, upd_hi, self.cap_e, float(rc.eta), ptr(self.dirty), ptr(self.dirty_count),
             self.max_dirty, ptr(self.prio_sync), ptr(self.step) if end_step else 0,
             1 if end_step else 0, self._ts(stream))
-        if r == -3:
+        if r in (-3, -4):    # shape, or more workgroups than can be resident at once
             return False
         check(r, "prio_tail")
         return True

@@ -112,10 +112,14 @@ class Learner:
             return ReplayMemory(self.memory_size, self.batch_size, rc.n_step, (e.frame_h, e.frame_w),
                                 m.hidden, e.action_repeat, e.n_stacks, burn_in=rc.burn_in,
                                 learning=rc.learn, eta=rc.eta,
-                                obs_shape=(e.channels_per_frame * e.n_stacks, e.frame_h, e.frame_w))
+                                obs_shape=(e.channels_per_frame * e.n_stacks, e.frame_h, e.frame_w),
+                                seed=self.cfg.seed)
+        # the sampler's generator is seeded from the config: an unseeded one (OS entropy) made the
+        # in-process CartPole run differ from run to run
         return ReplayMemory(self.memory_size, self.batch_size, rc.n_step, cell_size=m.hidden,
                             action_repeat=1, n_stacks=1, burn_in=rc.burn_in, learning=rc.learn,
-                            eta=rc.eta, obs_shape=(e.obs_dim * e.n_stacks,), obs_dtype=np.float32)
+                            eta=rc.eta, obs_shape=(e.obs_dim * e.n_stacks,), obs_dtype=np.float32,
+                            seed=self.cfg.seed)
 
     # ------------------------------------------------------------------ loop (learner.py:53-66)
     def replay_size(self) -> int:

@@ -202,6 +202,12 @@ def run_split(cfg: R2D2Config, rounds: int = 200, actor_ranks: Optional[int] = N
     W = rc.seq_len + rc.n_step
     # every rank creates the same groups in the same order
     g_learn = dist.new_group(learners) if len(learners) > 1 else None
+    # weight snapshots (learner 0 -> actor ranks) on a group of their own: over RCCL a group's
+    # point-to-point traffic between two ranks shares one communicator and stream, so with the
+    # records (actor -> learner) on the same group a weight send queued on learner 0 ahead of a
+    # record recv, and a record send queued on the actor ahead of the weight recv, could each
+    # wait (payloads larger than the per-peer buffer) for the recv stuck behind the other
+    g_w = dist.new_group(sorted(set([learners[0]] + actors)))
     torch.manual_seed(cfg.seed)
     L = ParamLayout(cfg.model, cfg.env)
     live = Liveness("learner" if info.rank in learners else "actor", info.rank, None)
@@ -218,7 +224,9 @@ def run_split(cfg: R2D2Config, rounds: int = 200, actor_ranks: Optional[int] = N
         eng = LearnerEngine(cfg, replay, dev, rank=learners.index(info.rank), world=len(learners),
                             process_group=g_learn)
         recv = TrajectoryReceiver(replay, mine, E, K)
-        wl = WeightLinks(L.padded, dev, actors, learners[0], "learner") if info.rank == learners[0] else None
+        wl = (WeightLinks(L.padded, dev, actors, learners[0], "learner", group=g_w)
+              if info.rank == learners[0] else None)
+        PS = max(1, int(dc.poll_steps))
         if wl is not None:
             wl.publish(eng.master, eng.target)
         steps, polls, t_train, captured = 0, 0, None, False
@@ -226,8 +234,11 @@ def run_split(cfg: R2D2Config, rounds: int = 200, actor_ranks: Optional[int] = N
         t0 = time.perf_counter()
         while steps < learner_steps:
             live.tick(steps)
-            polls += 1
-            got = recv.poll()
+            if captured and steps % PS:       # rate-limited store round trips while training
+                got = 0
+            else:
+                polls += 1
+                got = recv.poll()
             if not captured:
                 # every learner shard must hold a batch of sequences before any of them steps
                 # (the DP step's collectives need all learner ranks in it)
@@ -268,7 +279,7 @@ def run_split(cfg: R2D2Config, rounds: int = 200, actor_ranks: Optional[int] = N
         cap_e = max(2 * (K + W + rc.n_step), 512)
         replay = HBMReplay(cfg, dev, capacity=cap_e * E, n_subrings=E)
         w_on, w_tg = PackedWeights(L, dev), PackedWeights(L, dev)
-        wl = WeightLinks(L.padded, dev, actors, learners[0], "actor")
+        wl = WeightLinks(L.padded, dev, actors, learners[0], "actor", group=g_w)
         wl.attach(w_on, w_tg)
         while wl.taken == 0:          # the initial snapshot
             if wl.poll() == 0:
