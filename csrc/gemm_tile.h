@@ -278,6 +278,99 @@ __device__ __forceinline__ void g2_tile(const GemmProb& P, int tm, int tn, uint8
   g2_epilogue(P, tm * g2::BM, tn * g2::BN, (wave >> 1) * 64, (wave & 1) * 64, lane, acc);
 }
 
+// ---- split precision (split.h) helper tile: one 128 x 128 output tile with A and B both given
+// as hi / lo planes, all THREE products (lo.hi, hi.lo, hi.hi) taken per 32-deep K tile from ONE
+// staging of the four planes (the multi-pass g2_tile re-stages K per product, so a helper that
+// waits on a producer per K tile would run two thirds of its work after the producer ended).
+// 4 waves (threads 0..255), wave tile 64 x 64 as 2 x 2 32x32x16 accumulators; NS-stage ring of
+// 32-KB stages {A hi, A lo, B hi, B lo} (8 KB planes) at `lds`.  k-major planes are [128][32 k]
+// (64-B rows; chunk c of row r at slot c ^ ((r >> 2) & 3), conflict-free fragment reads),
+// mn-major planes [32 k][128] (g2_stage / g2_frag's layout).  AUXA / AUXB: DMA cache policy of
+// the A / B loads (16 = sc1: operands another CU of the same launch wrote write-through).
+namespace g2s {
+constexpr int BM = 128, BN = 128, BK = 32, PL = 8192, ST = 4 * PL;
+}  // namespace g2s
+
+template <bool KMAJ, int AUX>
+__device__ __forceinline__ void g2s_stage(const bf16* X, int ld, int i0, int imax, int k0,
+                                          uint8_t* plane, int wave, int lane) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int blk = wave * 2 + j;                  // 8 x 1 KB blocks per plane
+    const bf16* src;
+    if (KMAJ) {
+      const int row = blk * 16 + (lane >> 2), c = (lane & 3) ^ ((row >> 2) & 3);
+      src = X + (size_t)min(i0 + row, imax - 1) * ld + k0 + c * 8;
+    } else {
+      const int kr = blk * 4 + (lane >> 4), c = (lane & 15) ^ (4 * (kr & 3));
+      const int col = i0 + c * 8;
+      src = X + (size_t)(k0 + kr) * ld + (col < imax ? col : imax - 8);
+    }
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(plane + blk * 1024),
+                                     16, 0, AUX);
+  }
+}
+
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8 g2s_frag(const uint8_t* plane, int i0, int ks, int lane) {
+  if (KMAJ) {
+    const int r = i0 + (lane & 31), c = 2 * ks + (lane >> 5);
+    return *(const bf16x8*)(plane + r * 64 + ((c ^ ((r >> 2) & 3)) * 16));
+  }
+  return g2_frag<false>(plane, i0, ks, lane);      // [32 k][128]: 256-B rows as g2's mn-major
+}
+
+// acc += the tile's product over K tiles [kt0, kt1) of 32 (ascending, or descending if desc);
+// ready(kt) is called by every wave before it issues K tile kt's DMAs.  K % 32 == 0.
+template <bool AK, bool BK_, int AUXA, int AUXB, int NS, class Ready>
+__device__ __forceinline__ void g2s_tile_acc(const GemmProb& P, int tm, int tn, uint8_t* lds,
+                                             int kt0, int kt1, bool desc, Ready ready,
+                                             f32x16 (&acc)[2][2]) {
+  using namespace g2s;
+  static_assert(NS >= 2 && NS <= 3, "ring depth");
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int nk = kt1 - kt0;
+  auto stage = [&](int i) {
+    const int kt = desc ? kt1 - 1 - i : kt0 + i;
+    ready(kt);
+    uint8_t* st = lds + (i % NS) * ST;
+    g2s_stage<AK, AUXA>(P.A, P.lda, m0, P.M, kt * BK, st, wave, lane);
+    g2s_stage<AK, AUXA>(P.A_lo, P.lda, m0, P.M, kt * BK, st + PL, wave, lane);
+    g2s_stage<BK_, AUXB>(P.B, P.ldb, n0, P.N, kt * BK, st + 2 * PL, wave, lane);
+    g2s_stage<BK_, AUXB>(P.B_lo, P.ldb, n0, P.N, kt * BK, st + 3 * PL, wave, lane);
+  };
+  if (nk <= 0) return;
+  for (int i = 0; i < NS - 1 && i < nk; ++i) stage(i);
+  for (int i = 0; i < nk; ++i) {
+    // 8 DMAs per wave per stage: stage i landed once only the stages after it remain
+    const int ahead = min(NS - 2, nk - 1 - i);
+    if (ahead >= 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();          // stage i visible; every wave done reading stage i-1
+    if (i + NS - 1 < nk) stage(i + NS - 1);
+    const uint8_t* st = lds + (i % NS) * ST;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        ah[q] = g2s_frag<AK>(st, wm + 32 * q, ks, lane);
+        al[q] = g2s_frag<AK>(st + PL, wm + 32 * q, ks, lane);
+        bh[q] = g2s_frag<BK_>(st + 2 * PL, wn + 32 * q, ks, lane);
+        bl[q] = g2s_frag<BK_>(st + 3 * PL, wn + 32 * q, ks, lane);
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int r = 0; r < 2; ++r) acc[q][r] = mfma32_x3(ah[q], al[q], bh[r], bl[r], acc[q][r]);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();            // every wave done reading the ring (epilogue reuses it)
+}
+
 // Host: parse one 16 x int64 problem descriptor (ops/gemm.py Gemm.desc layout) and check the
 // shape rules of the 128x128 paths.  0 = ok.
 static inline int gemm_parse_desc(const int64_t* d, GemmProb& p) {

@@ -59,6 +59,8 @@
 // BPTT progress for helper workgroups: word k counts the recurrence workgroups whose dgates of
 // iteration k are stored (exact per-iteration counts: a sum over iterations would let a fast
 // group hide a slow one); reset by the last workgroup
+// dX tile queue of the BPTT's split-precision helpers (atomic dequeue; reset by the last workgroup)
+#define PT_DXQ_OFF (PL_CTR_WORDS + 96)
 #define PT_ITER_OFF (PL_CTR_WORDS + 128)
 #define PT_ITER_MAX 512
 #define PT_CTR_WORDS (PL_CTR_WORDS + 128 + PT_ITER_MAX)
@@ -648,6 +650,7 @@ __device__ __forceinline__ bool pt_finish(unsigned* ctr, int groups, int total_w
     __hip_atomic_store(ctr + PL_OFF_ARRIVE + g * PL_CTR_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __hip_atomic_store(ctr + PT_DONE_OFF, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(ctr + PT_DXQ_OFF, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   for (int k = 0; k < n_iter; ++k)
     __hip_atomic_store(ctr + PT_ITER_OFF + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_fetch_add(ctr + epoch_off, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1168,7 +1171,22 @@ struct PTBArgs {
   // split precision (the _sp launcher): W_hh^T lo plane; dgates lo plane out
   const bf16* whhT_lo;
   bf16* dgates_lo;
+  // split precision, optional (r2_lstm_bwd_set_dz): the dueling head's input gradient dh_ext =
+  // dz . W1 computed HERE instead of read from dh_ext (the TD launch then skips its fused dh, which
+  // streamed all of W1^T through every one of its 160 workgroups: 11 us, tools/td_micro.py).  dz
+  // (Tl*B, 512) hi / lo planes (time-major learning rows), w1t = W1^T (H, 512) hi / lo planes.
+  // Each compute wave keeps the W1^T fragments of its K quarter for the workgroup's 16 units in
+  // VGPRs; the I/O wave stages the 16 dz rows of an iteration (32 KB) two iterations ahead into a
+  // 3-slot LDS ring (the dynamic LDS); iteration k+1's product (12 MFMAs per wave) runs right
+  // after iteration k's partial-dh publish, inside the hand-off wait it would otherwise idle in.
+  const bf16* dz;
+  const bf16* dz_lo;
+  const bf16* w1t;
+  const bf16* w1t_lo;
 };
+#define PT_DZ_K 512                                   // dz row length (2 x head hidden 256)
+#define PT_DZ_SLOT (2 * PT_ROWS * PT_DZ_K * 2)        // one ring slot: 16 rows x 512 x hi/lo = 32 KB
+#define PT_DZ_LDS (3 * PT_DZ_SLOT)                    // the ring (dynamic LDS of the launch)
 
 // SP (split precision, split.h): W_hh^T hi / lo fragments, dgates tile kept as hi / lo images for
 // the partial-dh MFMAs (3 passes) and written as hi / lo planes for the weight-gradient GEMMs.
@@ -1220,7 +1238,54 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
         }
       }
     };
-    if (h < a.n_wtiles) {
+    if (SP) {
+      // split precision (PTBArgs::gw / gx with hi / lo planes): helpers 0 .. n_wtiles-1 own one
+      // weight-gradient tile each for the whole BPTT, all three products per 32-row K tile in
+      // BPTT order (g2s_tile_acc: each K tile as soon as its dgates rows are stored); every helper
+      // then dequeues dX tiles, latest rows (first produced) first
+      const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+      if (h < a.n_wtiles) {
+        int item = h, pi = 0;
+        while (pi + 1 < a.n_gw) {
+          const int nt = a.gw[pi].tiles_n * ((a.gw[pi].M + 127) / 128);
+          if (item < nt) break;
+          item -= nt;
+          ++pi;
+        }
+        const GemmProb& P = a.gw[pi];
+        const bool wt = (a.gw_wait >> pi) & 1;
+        const int tm = item / P.tiles_n, tn = item % P.tiles_n;
+        f32x16 acc[2][2] = {};
+        g2s_tile_acc<false, false, 16, 0, 3>(P, tm, tn, pt_dyn, 0, P.K / 32, true,
+                                             [&](int kt) { if (wt) wait_rows(32 * kt, 32 * kt + 32); }, acc);
+        g2_epilogue_lds(P, tm * 128, tn * 128, wm, wn, lane, acc, pt_dyn);
+      } else if (a.hg_on) {   // the head-gradient reduction first (independent of the BPTT)
+        const int hx = h - a.n_wtiles, nx = nh - a.n_wtiles;
+        const int cbn = (2 * a.hg.HD + 63) / 64;
+        for (int it = hx; it < cbn * a.hg.RS * a.hg.NP; it += nx)
+          head_grads_body(a.hg, it % cbn, (it / cbn) % a.hg.RS, it / (cbn * a.hg.RS));
+      }
+      if (a.gx_on) {
+        const GemmProb& P = a.gx;
+        const int tmn = (P.M + 127) / 128, total = tmn * P.tiles_n;
+        __shared__ int dxq;
+        for (;;) {
+          if (tid == 0)
+            dxq = (int)__hip_atomic_fetch_add(a.ctr + PT_DXQ_OFF, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_s_barrier();
+          const int it = dxq;
+          __builtin_amdgcn_s_barrier();
+          if (it >= total) break;
+          const int tm = tmn - 1 - it / P.tiles_n, tn = it % P.tiles_n;
+          f32x16 acc[2][2] = {};
+          bool waited = false;
+          g2s_tile_acc<true, false, 16, 0, 3>(P, tm, tn, pt_dyn, 0, P.K / 32, false, [&](int) {
+            if (!waited) { wait_rows(128 * tm, 128 * tm + 128); waited = true; }
+          }, acc);
+          g2_epilogue_lds(P, tm * 128, tn * 128, wm, wn, lane, acc, pt_dyn);
+        }
+      }
+    } else if (h < a.n_wtiles) {
       // one weight-gradient tile, K tiles in BPTT order (latest time step first)
       int item = h, pi = 0;
       while (pi + 1 < a.n_gw) {
@@ -1294,10 +1359,26 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
       __builtin_amdgcn_global_load_lds(a.c_seq + (size_t)t * B * H + hidx, (lds_t*)cl[s], 16, 0, 0);
       __builtin_amdgcn_global_load_lds((t == 0 ? a.c0 : a.c_seq + (size_t)(t - 1) * B * H) + hidx,
                                        (lds_t*)cpl[s], 16, 0, 0);
-      if (a.dh_ext)
+      if (a.dh_ext && !a.dz)
         __builtin_amdgcn_global_load_lds(a.dh_ext + (size_t)tl * B * H + hidx, (lds_t*)dhl[s], 16, 0, 0);
     };
-    const int nload = a.dh_ext ? 7 : 6;     // DMA instructions per io_load
+    const bool dzon = a.dz != nullptr;
+    auto io_load_dz = [&](int k) {    // dz rows of iteration k -> ring slot k % 3 (32 DMAs)
+      typedef __attribute__((address_space(3))) void lds_t;
+      const int tl = T - 1 - k - t0;
+      uint8_t* slot = pt_dyn + (k % 3) * PT_DZ_SLOT;
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+        for (int r = 0; r < PT_ROWS; ++r) {
+          // row r: 64 chunks of 16 B; LDS chunk i holds global chunk i ^ r (conflict-free
+          // fragment reads of 16 rows at one k)
+          const int b = min(mb * PT_ROWS + r, B - 1);
+          const bf16* src = (pl ? a.dz_lo : a.dz) + ((size_t)tl * B + b) * PT_DZ_K + 8 * ((lane ^ r) & 63);
+          __builtin_amdgcn_global_load_lds(src, (lds_t*)(slot + (pl * PT_ROWS + r) * 1024), 16, 0, 0);
+        }
+    };
+    const int nload = (a.dh_ext && !dzon ? 7 : 6) + (dzon ? 32 : 0);   // DMA instructions per iteration
     const __amdgpu_buffer_rsrc_t drs = pl_rsrc(a.dgates, (uint32_t)((size_t)K * B * G * 2));
     const __amdgpu_buffer_rsrc_t drsl = pl_rsrc(SP ? a.dgates_lo : a.dgates, (uint32_t)((size_t)K * B * G * 2));
     auto io_store = [&](int k) {      // dgates tile of iteration k (write-through: helpers read it)
@@ -1318,17 +1399,32 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
         __hip_atomic_fetch_add(a.ctr + PT_ITER_OFF + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     io_load(0);
-    if (K > 1) io_load(1);
+    if (dzon) io_load_dz(0);
+    if (K > 1) {
+      io_load(1);
+      if (dzon) io_load_dz(1);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (dzon) lds_sync();                 // barrier P: dz of iteration 0 landed (compute: dh_ext(0))
     for (int k = 0; k < K; ++k) {
       lds_sync();                         // barrier A_k: operands of k landed
       if (k >= 1) io_store(k - 1);
       const bool more = k + 2 < K;
-      if (more) io_load(k + 2);
+      if (more) {
+        io_load(k + 2);
+        if (dzon) io_load_dz(k + 2);
+      }
+      if (dzon) {
+        // dz of iteration k+1 (issued in iteration k-1) must land before barrier B_k: the compute
+        // waves multiply it after B_k.  Everything older than this iteration's loads is waited
+        if (more) asm volatile("s_waitcnt vmcnt(38)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       lds_sync();                         // barrier B_k
       // operands of k+1 (issued in iteration k-1) must land before barrier A_{k+1}
       if (more) {
-        if (nload == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+        if (nload == 38) asm volatile("s_waitcnt vmcnt(38)" ::: "memory");
+        else if (nload == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1367,7 +1463,42 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   constexpr int SRC4 = NWG / 4;
   const int cr4 = lane >> 2, cq4 = 4 * (lane & 3), sq = wave;
   const bool crow4_ok = mb * PT_ROWS + cr4 < B;
+  // dh_ext = dz . W1 (a.dz): this wave's K quarter [128 wave, +128) of the 16 units' W1^T rows
+  const bool dzon = SP && a.dz != nullptr;
+  bf16x8 w1f[4], w1fl[4];
+  if (dzon) {
+    const bf16* r1 = a.w1t + (size_t)(j * PL_UNITS + (lane & 15)) * PT_DZ_K + 128 * wave + 8 * (lane >> 4);
+    const bf16* r1l = a.w1t_lo + (size_t)(j * PL_UNITS + (lane & 15)) * PT_DZ_K + 128 * wave + 8 * (lane >> 4);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      w1f[s] = *(const bf16x8*)(r1 + 32 * s);
+      w1fl[s] = *(const bf16x8*)(r1l + 32 * s);
+    }
+  }
+  // partial dh_ext of iteration kk (this wave's K quarter) -> dxp[kk & 1][wave] (read at kk's
+  // pointwise, after barrier A_kk)
+  float* dxp = (float*)(pt_dyn + PT_DZ_LDS);   // [2][4 waves][16 rows][16 units]
+  auto dz_product = [&](int kk) {
+    const uint8_t* slot = pt_dyn + (kk % 3) * PT_DZ_SLOT;
+    const int r = lane & 15;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int c = 16 * wave + 4 * s + (lane >> 4);     // 16-B chunk of the 1-KB row
+      const int o = r * 1024 + ((c ^ r) & 63) * 16;
+      const bf16x8 ah = *(const bf16x8*)(slot + o);
+      const bf16x8 al = *(const bf16x8*)(slot + PT_ROWS * 1024 + o);
+      acc = mfma16_x3(ah, al, w1f[s], w1fl[s], acc);
+    }
+    float* d = dxp + ((kk & 1) * 4 + wave) * (PT_ROWS * PL_UNITS);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) d[(4 * (lane >> 4) + e) * PL_UNITS + r] = acc[e];
+  };
   __builtin_amdgcn_s_waitcnt(0);          // drain the one-time loads (see the forward kernel)
+  if (dzon) {
+    lds_sync();                           // barrier P: dz of iteration 0 staged
+    dz_product(0);
+  }
 
   for (int k = 0; k < K; ++k) {
     const int t = T - 1 - k;
@@ -1443,7 +1574,13 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
     // ---- pointwise (row prow, unit ul)
     const int s3 = k % 3;
     const int o16 = pt_swz16(prow, ul);
-    float dh = a.dh_ext ? dhl[s3][o16] : 0.f;
+    float dh;
+    if (dzon) {
+      const float* d = dxp + (k & 1) * 4 * (PT_ROWS * PL_UNITS) + prow * PL_UNITS + ul;
+      dh = ((d[0] + d[PT_ROWS * PL_UNITS]) + d[2 * PT_ROWS * PL_UNITS]) + d[3 * PT_ROWS * PL_UNITS];
+    } else {
+      dh = a.dh_ext ? dhl[s3][o16] : 0.f;
+    }
     if (k > 0) {
       if constexpr (T4)
         dh += ((red[0][o16] + red[1][o16]) + red[T4 ? 2 : 0][o16]) + red[T4 ? 3 : 0][o16];
@@ -1521,6 +1658,8 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
           }
         }
       }
+      // next iteration's dh_ext, inside the hand-off wait (dz of k+1 landed before barrier B_k)
+      if (dzon) dz_product(k + 1);
     }
   }
     if (a.bias_ws) {
@@ -1568,6 +1707,28 @@ static const bf16* g_bwd_whhT_lo = nullptr;
 static const float* g_bwd_hg_zr32 = nullptr;
 static const bf16* g_bwd_hg_dz_lo = nullptr;
 static bf16* g_bwd_dgates_lo = nullptr;
+
+// split-precision helper GEMMs (PTBArgs::gw / gx): problems for the next r2_lstm_bwd_tag_sp*
+// call on this host thread (consumed by it): n_gw weight-gradient descriptors then (gx_on) dX
+static thread_local const int64_t* g_bwd_gemms = nullptr;
+static thread_local int g_bwd_n_gw = 0, g_bwd_gw_wait = 0, g_bwd_gx_on = 0;
+extern "C" int r2_lstm_bwd_set_gemms(const int64_t* descs, int n_gw, int gw_wait, int gx_on) {
+  g_bwd_gemms = descs;
+  g_bwd_n_gw = descs ? n_gw : 0;
+  g_bwd_gw_wait = gw_wait;
+  g_bwd_gx_on = descs ? gx_on : 0;
+  return 0;
+}
+
+// in-BPTT dh_ext (PTBArgs::dz): operands for the next r2_lstm_bwd_tag_sp* call on this host
+// thread (consumed by it); dz / w1t hi / lo planes, row length PT_DZ_K
+static thread_local const bf16* g_bwd_dz[4] = {nullptr, nullptr, nullptr, nullptr};
+extern "C" int r2_lstm_bwd_set_dz(const bf16* dz, const bf16* dz_lo, const bf16* w1t,
+                                  const bf16* w1t_lo, int kd) {
+  if (dz && (!dz_lo || !w1t || !w1t_lo || kd != PT_DZ_K)) return -1;
+  g_bwd_dz[0] = dz; g_bwd_dz[1] = dz_lo; g_bwd_dz[2] = w1t; g_bwd_dz[3] = w1t_lo;
+  return 0;
+}
 
 // A/B probe switch: 1 = the BPTT on 8-byte {partial, tag} granules (the previous hand-off)
 static int g_pl_bwd8 = 0;
@@ -1625,8 +1786,12 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
       GemmProb& p = i < n_gw ? args.gw[i] : args.gx;
       const int rc = gemm_parse_desc(gemm_descs + GEMM_DESC * i, p);
       if (rc) return -20 + rc;
-      if (p.npass > 1 || p.C_lo) return -11;   // helpers: bf16 operands only
-      if (p.K % 64) return -8;
+      if (g_bwd_whhT_lo) {        // split precision: both operands split (g2s_tile_acc)
+        if (p.npass != 3 || p.K % 32) return -11;
+      } else {
+        if (p.npass > 1 || p.C_lo) return -11;   // helpers: bf16 operands only
+        if (p.K % 64) return -8;
+      }
       const bool is_x = i == n_gw;
       if (is_x ? (!p.a_kmajor || p.b_kmajor) : (p.a_kmajor || p.b_kmajor)) return -9;
       const int tiles = p.tiles_n * ((p.M + 127) / 128);
@@ -1647,16 +1812,20 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
   args.whhT_lo = g_bwd_whhT_lo;
   args.dgates_lo = g_bwd_dgates_lo;
   const bool sp = g_bwd_whhT_lo != nullptr;
-  // split precision: the head-gradient side job (fp32 zr, hi / lo dz) only, no helper GEMMs
-  if (sp && (!args.dgates_lo || H > 256 || (taken & ~1))) return -11;
+  args.dz = g_bwd_dz[0]; args.dz_lo = g_bwd_dz[1]; args.w1t = g_bwd_dz[2]; args.w1t_lo = g_bwd_dz[3];
+  for (int i = 0; i < 4; ++i) g_bwd_dz[i] = nullptr;   // one launch per set
+  if (args.dz && (!sp || H != 256 || g_pl_bwd8)) return -13;   // split-precision T4 BPTT, H 256 only
+  int dyn_lds = args.dz ? PT_DZ_LDS + 2 * 4 * PT_ROWS * PL_UNITS * 4 : PL_LDS_RESERVE;
+  if (sp && (args.n_gw || args.gx_on)) dyn_lds = max(dyn_lds, 3 * g2s::ST);   // helper ring
+  if (sp && (!args.dgates_lo || H > 256)) return -11;
   if (sp && args.hg_on && (!args.hg.zr32 || !args.hg.dz_lo)) return -12;
   hipStream_t s = (hipStream_t)stream;   // counters are left zeroed by the previous launch
   dim3 grid(nh ? 256 : (xmap ? 8 * nwg : MB * nwg)), block(320);
 #define R2_BWD_LAUNCH1(HH, SPP, T4)                                                            \
   do {                                                                                         \
     hipFuncSetAttribute((const void*)lstm_bwd_tag_kernel<HH, SPP, T4>,                         \
-                        hipFuncAttributeMaxDynamicSharedMemorySize, PL_LDS_RESERVE);           \
-    hipLaunchKernelGGL((lstm_bwd_tag_kernel<HH, SPP, T4>), grid, block, PL_LDS_RESERVE, s, args); \
+                        hipFuncAttributeMaxDynamicSharedMemorySize, dyn_lds);                  \
+    hipLaunchKernelGGL((lstm_bwd_tag_kernel<HH, SPP, T4>), grid, block, dyn_lds, s, args);     \
   } while (0)
 #define R2_BWD_LAUNCH(HH, SPP)                                                                 \
   do {                                                                                         \
@@ -1693,9 +1862,12 @@ extern "C" int r2_lstm_bwd_tag_sp(const float* dh_ext, const float* gates, const
   if (!whhT_lo || !dgates_lo) return -5;
   g_bwd_whhT_lo = whhT_lo;
   g_bwd_dgates_lo = dgates_lo;
+  const int64_t* gd = g_bwd_gemms;
+  const int ngw = g_bwd_n_gw, gww = g_bwd_gw_wait, gx = g_bwd_gx_on;
+  g_bwd_gemms = nullptr; g_bwd_n_gw = g_bwd_gw_wait = g_bwd_gx_on = 0;
   const int rc = r2_lstm_bwd_tag(dh_ext, gates, c_seq, c0, whhT, dgates, B, T, t0, H, ctr, err, ring,
                                  bias_ws, perm, db1, db2, nullptr, nullptr, nullptr, nullptr, nullptr,
-                                 nullptr, 0, 0, 0, nullptr, nullptr, nullptr, 0, 0, 0, stream);
+                                 nullptr, 0, 0, 0, nullptr, nullptr, gd, ngw, gww, gx, stream);
   g_bwd_whhT_lo = nullptr;
   g_bwd_dgates_lo = nullptr;
   return rc;
@@ -1717,9 +1889,12 @@ extern "C" int r2_lstm_bwd_tag_sp_hg(const float* dh_ext, const float* gates, co
   g_bwd_dgates_lo = dgates_lo;
   g_bwd_hg_zr32 = hg_zr32;
   g_bwd_hg_dz_lo = hg_dz_lo;
+  const int64_t* gd = g_bwd_gemms;
+  const int ngw = g_bwd_n_gw, gww = g_bwd_gw_wait, gx = g_bwd_gx_on;
+  g_bwd_gemms = nullptr; g_bwd_n_gw = g_bwd_gw_wait = g_bwd_gx_on = 0;
   const int rc = r2_lstm_bwd_tag(dh_ext, gates, c_seq, c0, whhT, dgates, B, T, t0, H, ctr, err, ring,
                                  bias_ws, perm, db1, db2, hg_dva, nullptr, hg_dz, hg_gw2, hg_gb2,
-                                 hg_gb1, hg_N, hg_A, hg_HD, hg_ws, hg_ticket, nullptr, 0, 0, 0, stream);
+                                 hg_gb1, hg_N, hg_A, hg_HD, hg_ws, hg_ticket, gd, ngw, gww, gx, stream);
   g_bwd_whhT_lo = nullptr;
   g_bwd_dgates_lo = nullptr;
   g_bwd_hg_zr32 = nullptr;

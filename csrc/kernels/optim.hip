@@ -9,6 +9,7 @@
 // the step count read from device memory so HIP-graph replays advance it.
 // Gradient scale (1/world for DP averaging) and optional global-norm clipping are fused.
 #include "../common.h"
+#include "../pack_step.h"
 
 __global__ void rmsprop_centered_kernel(float* __restrict__ p, const float* __restrict__ g,
                                         float* __restrict__ sq, float* __restrict__ ga, int64_t n,
@@ -254,76 +255,11 @@ extern "C" int r2_copy_if_due(float* dst, const float* src, int64_t n, const int
 }
 
 // One launch for everything between the optimizer and the next step's kernels (replaces
-// copy_if_due + 2 x {bf16 pack, fp32 gather, LSTM bias add}):
-//   * online: bf16 kernel-layout pack, fp32 small-vector gather, packed b_ih + b_hh
-//   * target, only when (step + 1) % interval == 0 (learner.py:107-108 target sync): target = master,
-//     and its packs are the online packs of the same master values (no read of the copy)
-__global__ void pack_step_kernel(const float* __restrict__ master, float* __restrict__ target,
-                                 int64_t n_master, const int* __restrict__ bf_idx,
-                                 bf16* __restrict__ bf, bf16* __restrict__ bf_t, int64_t n_bf,
-                                 const int* __restrict__ f_idx, float* __restrict__ f32,
-                                 float* __restrict__ f32_t, int64_t n_f, int64_t o_bih, int64_t o_bhh,
-                                 float* __restrict__ lstm_b, float* __restrict__ lstm_b_t, int64_t G,
-                                 const int64_t* __restrict__ step, int64_t interval, int64_t lo_off) {
-  const bool due = interval <= 1 || ((*step) + 1) % interval == 0;
-  // work items: [target copy, 4 floats each (due only)] [bf pack, 4 elements each: one 16-B
-  // index load, 4 gathers, one 8-B store] [bf tail] [f32 gather] [lstm bias]
-  const int64_t nm4 = due ? n_master >> 2 : 0, nb4 = n_bf >> 2, nbt = n_bf & 3;
-  const int64_t total = nm4 + nb4 + nbt + n_f + G;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += stride) {
-    int64_t j = i;
-    if (j < nm4) {
-      ((f32x4*)target)[j] = ((const f32x4*)master)[j];
-      continue;
-    }
-    j -= nm4;
-    if (j < nb4) {
-      const int4 ix = ((const int4*)bf_idx)[j];
-      bf16x4 v;
-      v[0] = (bf16)master[ix.x];
-      v[1] = (bf16)master[ix.y];
-      v[2] = (bf16)master[ix.z];
-      v[3] = (bf16)master[ix.w];
-      ((bf16x4*)bf)[j] = v;
-      if (due) ((bf16x4*)bf_t)[j] = v;
-      if (lo_off) {   // split precision: lo plane (split.h)
-        bf16x4 l;
-        l[0] = (bf16)(master[ix.x] - (float)v[0]);
-        l[1] = (bf16)(master[ix.y] - (float)v[1]);
-        l[2] = (bf16)(master[ix.z] - (float)v[2]);
-        l[3] = (bf16)(master[ix.w] - (float)v[3]);
-        ((bf16x4*)(bf + lo_off))[j] = l;
-        if (due) ((bf16x4*)(bf_t + lo_off))[j] = l;
-      }
-      continue;
-    }
-    j -= nb4;
-    if (j < nbt) {
-      j += nb4 << 2;
-      const float x = master[bf_idx[j]];
-      const bf16 v = (bf16)x;
-      bf[j] = v;
-      if (due) bf_t[j] = v;
-      if (lo_off) {
-        const bf16 l = (bf16)(x - (float)v);
-        bf[j + lo_off] = l;
-        if (due) bf_t[j + lo_off] = l;
-      }
-      continue;
-    }
-    j -= nbt;
-    if (j < n_f) {
-      const float v = master[f_idx[j]];
-      f32[j] = v;
-      if (due) f32_t[j] = v;
-      continue;
-    }
-    j -= n_f;
-    const float b = master[f_idx[o_bih + j]] + master[f_idx[o_bhh + j]];
-    lstm_b[j] = b;
-    if (due) lstm_b_t[j] = b;
-  }
+// copy_if_due + 2 x {bf16 pack, fp32 gather, LSTM bias add}): pack_step.h pack_step_items.  The
+// learner's single-rank step runs the same items on extra workgroups of the priority-tail launch
+// instead (replay.hip r2_prio_tail_pack).
+__global__ void pack_step_kernel(const PackStepArgs a) {
+  pack_step_items(a, blockIdx.x * (int64_t)blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
 }
 
 extern "C" int r2_pack_step(const float* master, float* target, int64_t n_master, const int* bf_idx,
@@ -331,12 +267,10 @@ extern "C" int r2_pack_step(const float* master, float* target, int64_t n_master
                             float* f32_t, int64_t n_f, int64_t o_bih, int64_t o_bhh, float* lstm_b,
                             float* lstm_b_t, int64_t G, const int64_t* step, int64_t interval,
                             int64_t lo_off, void* stream) {
-  if ((n_master & 3) || (((uintptr_t)master | (uintptr_t)target | (uintptr_t)bf_idx) & 15) ||
-      (((uintptr_t)bf | (uintptr_t)bf_t) & 7) || (lo_off & 3))
-    return -1;   // vector paths: 16-B master / target / index rows, 8-B packs
-  hipLaunchKernelGGL(pack_step_kernel, dim3(1024), dim3(256), 0, (hipStream_t)stream, master, target,
-                     n_master, bf_idx, bf, bf_t, n_bf, f_idx, f32, f32_t, n_f, o_bih, o_bhh, lstm_b,
-                     lstm_b_t, G, step, interval, lo_off);
+  const PackStepArgs a{master, target, n_master, bf_idx, bf, bf_t, n_bf, f_idx, f32, f32_t, n_f,
+                       o_bih, o_bhh, lstm_b, lstm_b_t, G, step, interval, lo_off};
+  if (!pack_step_args_ok(a)) return -1;
+  hipLaunchKernelGGL(pack_step_kernel, dim3(1024), dim3(256), 0, (hipStream_t)stream, a);
   R2_CHECK_LAUNCH();
   return 0;
 }

@@ -17,6 +17,7 @@
 //    a dirty list, and the tree is repaired bottom-up one level per launch (parents are
 //    recomputed from children -- deterministic, no float drift, duplicates are benign).
 #include "../common.h"
+#include "../pack_step.h"
 
 #define TREE_MAX_LEVELS 8
 
@@ -304,6 +305,9 @@ __global__ void seqprio_refresh_kernel(const int* __restrict__ starts, int B,
                             dirty, count, max_dirty);
 }
 
+// pack workgroups of r2_prio_tail_pack (grid-stride over ~115k items of the fp32 paper config)
+#define PRIO_PACK_BLOCKS 192
+
 // grid barrier of a launch whose workgroups are all resident (r2_prio_tail checks B against the
 // occupancy-derived resident capacity): every thread drains its stores, one arrival add per
 // workgroup, thread 0 polls the counter (agent-scope loads).  Bounded: 2^22 polls with
@@ -333,31 +337,43 @@ __device__ __forceinline__ void prio_grid_barrier(unsigned* ctr, unsigned target
 // same wave_sum_x sums over the same children: bit-identical to the three launches.
 // sync[0..2]: barrier counters + ticket (zero between launches, reset by the last arriver);
 // sync[3]: error word (barrier timeout).
+//
+// Optional pack workgroups (r2_prio_tail_pack, the single-rank step): blocks nprio.. of the grid
+// run the weight repack of the step that just updated the master (pack_step.h, the former
+// pack_step_kernel launch) beside the tail; they take no part in the two grid barriers (target
+// nprio) and arrive on the final ticket like the tail's workgroups, so the step counter -- which
+// their target-sync test reads -- advances only after every one of them has read it.
 __global__ __launch_bounds__(256) void prio_tail_kernel(
     const int* __restrict__ starts, const uint8_t* __restrict__ is_start,
     const float* __restrict__ priority, float* __restrict__ tree, TreeGeom g, int T, int upd_lo,
     int upd_hi, int cap_e, float eta, int* __restrict__ dirty, int* __restrict__ count,
-    int max_dirty, unsigned* __restrict__ sync, int64_t* __restrict__ step, int reset_count) {
+    int max_dirty, unsigned* __restrict__ sync, int64_t* __restrict__ step, int reset_count,
+    int nprio, const PackStepArgs pk) {
   __shared__ int last;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int nwaves = gridDim.x * nw;
-  seqprio_refresh_wg<true>(starts, is_start, priority, tree, T, upd_lo, upd_hi, cap_e, eta, dirty,
-                           count, max_dirty);
-  prio_grid_barrier(sync + 0, gridDim.x, sync + 3);
-  const int n = min(__hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), max_dirty);
-  for (int lvl = 0; lvl < 2; ++lvl) {
-    const float* child = tree + g.off[lvl];
-    float* parent = tree + g.off[lvl + 1];
-    for (int e = blockIdx.x * nw + wave; e < n; e += nwaves) {
-      const int64_t p = ((int64_t)__hip_atomic_load(dirty + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                        >> (6 * (lvl + 1));
-      const int64_t c = p * 64 + lane;
-      float v = c < g.size[lvl]
-                    ? __hip_atomic_load(child + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
-      v = wave_sum_x(v);
-      if (lane == 0) __hip_atomic_store(parent + p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if ((int)blockIdx.x >= nprio) {
+    const int64_t pb = blockIdx.x - nprio, npb = gridDim.x - nprio;
+    pack_step_items(pk, pb * blockDim.x + threadIdx.x, npb * blockDim.x);
+  } else {
+    const int nwaves = nprio * nw;
+    seqprio_refresh_wg<true>(starts, is_start, priority, tree, T, upd_lo, upd_hi, cap_e, eta, dirty,
+                             count, max_dirty);
+    prio_grid_barrier(sync + 0, nprio, sync + 3);
+    const int n = min(__hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), max_dirty);
+    for (int lvl = 0; lvl < 2; ++lvl) {
+      const float* child = tree + g.off[lvl];
+      float* parent = tree + g.off[lvl + 1];
+      for (int e = blockIdx.x * nw + wave; e < n; e += nwaves) {
+        const int64_t p = ((int64_t)__hip_atomic_load(dirty + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                          >> (6 * (lvl + 1));
+        const int64_t c = p * 64 + lane;
+        float v = c < g.size[lvl]
+                      ? __hip_atomic_load(child + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+        v = wave_sum_x(v);
+        if (lane == 0) __hip_atomic_store(parent + p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (lvl == 0) prio_grid_barrier(sync + 1, nprio, sync + 3);
     }
-    if (lvl == 0) prio_grid_barrier(sync + 1, gridDim.x, sync + 3);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -664,11 +680,11 @@ extern "C" int r2_seqprio_refresh(const int* starts, int B, const uint8_t* is_st
 // allow the fold (tree_update_fused's conditions) or B > 256 (all workgroups must be resident)
 extern "C" int r2_get_num_cus();   // lstm_persist.hip: CUs of the learner's stream
 
-extern "C" int r2_prio_tail(const int* starts, int B, const uint8_t* is_start, const float* priority,
+static int prio_tail_launch(const int* starts, int B, const uint8_t* is_start, const float* priority,
                             float* tree, const int64_t* offs, const int64_t* sizes, int levels,
                             int T, int upd_lo, int upd_hi, int cap_e, float eta, int* dirty,
                             int* count, int max_dirty, unsigned* sync, int64_t* step,
-                            int reset_count, void* stream) {
+                            int reset_count, const PackStepArgs* pk, void* stream) {
   if (upd_hi - upd_lo + T - 1 > 2048) return -2;
   if (B <= 0 || B > 256) return -3;
   {   // every workgroup must be resident at once (grid barriers): B <= CUs x blocks per CU
@@ -682,11 +698,45 @@ extern "C" int r2_prio_tail(const int* starts, int B, const uint8_t* is_start, c
   for (int l = 3; l < levels; ++l)
     if (sizes[l - 1] > 64 * 64) return -3;
   TreeGeom g = make_geom(offs, sizes, levels);
-  hipLaunchKernelGGL(prio_tail_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, starts, is_start,
+  PackStepArgs none{};
+  int grid = B;
+  if (pk) {
+    if (!pack_step_args_ok(*pk) || !step) return -5;
+    grid += PRIO_PACK_BLOCKS;
+  }
+  hipLaunchKernelGGL(prio_tail_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, starts, is_start,
                      priority, tree, g, T, upd_lo, upd_hi, cap_e, eta, dirty, count, max_dirty, sync,
-                     step, reset_count);
+                     step, reset_count, B, pk ? *pk : none);
   R2_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int r2_prio_tail(const int* starts, int B, const uint8_t* is_start, const float* priority,
+                            float* tree, const int64_t* offs, const int64_t* sizes, int levels,
+                            int T, int upd_lo, int upd_hi, int cap_e, float eta, int* dirty,
+                            int* count, int max_dirty, unsigned* sync, int64_t* step,
+                            int reset_count, void* stream) {
+  return prio_tail_launch(starts, B, is_start, priority, tree, offs, sizes, levels, T, upd_lo, upd_hi,
+                          cap_e, eta, dirty, count, max_dirty, sync, step, reset_count, nullptr, stream);
+}
+
+// r2_prio_tail + the step's weight repack (the r2_pack_step arguments) on PRIO_PACK_BLOCKS extra
+// workgroups of the same launch: one launch fewer between the optimizer and the next step.  The
+// tail must end the step (step != null): the counter advances after the pack workgroups read it.
+extern "C" int r2_prio_tail_pack(const int* starts, int B, const uint8_t* is_start,
+                                 const float* priority, float* tree, const int64_t* offs,
+                                 const int64_t* sizes, int levels, int T, int upd_lo, int upd_hi,
+                                 int cap_e, float eta, int* dirty, int* count, int max_dirty,
+                                 unsigned* sync, int64_t* step, int reset_count,
+                                 const float* master, float* target, int64_t n_master,
+                                 const int* bf_idx, bf16* bf, bf16* bf_t, int64_t n_bf,
+                                 const int* f_idx, float* f32, float* f32_t, int64_t n_f,
+                                 int64_t o_bih, int64_t o_bhh, float* lstm_b, float* lstm_b_t,
+                                 int64_t G, int64_t interval, int64_t lo_off, void* stream) {
+  const PackStepArgs pk{master, target, n_master, bf_idx, bf, bf_t, n_bf, f_idx, f32, f32_t, n_f,
+                        o_bih, o_bhh, lstm_b, lstm_b_t, G, step, interval, lo_off};
+  return prio_tail_launch(starts, B, is_start, priority, tree, offs, sizes, levels, T, upd_lo, upd_hi,
+                          cap_e, eta, dirty, count, max_dirty, sync, step, reset_count, &pk, stream);
 }
 
 extern "C" int r2_mark_starts(const int* rows, const int* n_rows, int max_rows, uint8_t* is_start,

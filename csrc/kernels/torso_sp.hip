@@ -6,20 +6,18 @@
 // resident in LDS, one 512-thread workgroup per CU, grid-stride over frames), re-laid out for hi /
 // lo operand pairs, which double every image that feeds an MFMA:
 //
-// Forward, per frame (LDS 143.8 KB):
-//   * conv1: the uint8 frame is exact in bf16, so conv1 is 2 passes (x.W1_lo + x.W1_hi) with the
-//     W1 hi / lo fragments resident in VGPRs; the frame is NOT staged in LDS (it would not fit
-//     beside the hi / lo images): each lane's B fragment is two 4-byte buffer loads straight from
-//     the replay row (L1 / L2; the frame's lines are warmed one frame ahead), the space-to-depth
-//     order making each fragment 2 x 4 contiguous bytes; the u8 -> bf16 conversion is VALU work
-//     beside the MFMAs.
-//   * conv2: W2 hi / lo and act1 hi / lo images in LDS, 3 passes.
-//   * conv3: act2 hi / lo in LDS, W3 hi / lo fragments from L2 (buffer loads), 3 passes.
-//   * pipeline as torso.hip: phase A = conv1(f) on all waves || conv3(f-1) on waves 2 and 6
-//     (both on SIMD 2, which gets one conv1 tile fewer: ~130 MFMAs per SIMD); phase B = conv2(f)
-//     on waves 0..2 || act1 save + next-frame warm-up on waves 3..7.
+// Forward (torso_fwd_sp2_kernel, LDS 159.8 KB), per frame in two phases:
+//   * phase A: conv1(f) on the int8 matrix cores (the uint8 frame, staged in LDS, is exact as
+//     int8 after a -128 shift; W1 = s (d0 + d1/128 + d2/16384) as three int8 digit fragments in
+//     VGPRs; exact int32 sums, one fp32 combine) on 7 waves || conv3(f-1) (3 bf16 passes over
+//     act2 hi / lo, W3 in VGPRs) on wave 2; the next frame is loaded into registers meanwhile;
+//   * phase B: conv2(f) (W2 hi / lo and act1 hi / lo images in LDS, 3 passes, 32x32x16 tiles) on
+//     waves 0..2 || next frame -> LDS and the act1 save on the others.
 //   * outputs: torso features (PyTorch CHW flatten) as hi / lo planes (the x-projection GEMM's A
 //     operand), optional channels-last act1 / act2 hi / lo planes for the backward.
+//   Rejected rebalancings and their numbers: profiles/r04_torso_fwd_v3_probe.txt (v3: pipelined
+//   roles, W2 in registers) and profiles/r05_torso_fwd_v4_rejected.txt (v4: conv2 on all waves as
+//   16x16x32 blocks -- conv2 is LDS-bound); their code is gone.
 //
 // Backward (torso_bwd_sp_kernel / torso_dw3_sp_kernel, LDS 145.7 KB): see the comment there.
 #include "../common.h"
@@ -29,22 +27,7 @@ namespace tsp {
 constexpr int IN_BYTES = 4 * 84 * 84;    // 28224
 constexpr int NT = 512;
 constexpr int P1 = 400, P2 = 81, P3 = 49;
-constexpr int ACTS = 40;                  // bf16 per pixel row (32 + 8 pad) = 80 B
-constexpr int W2S = 512 + 8;              // bf16 per conv2 weight row (1040 B)
-constexpr int OFF_A1H = 0;
-constexpr int OFF_A1L = OFF_A1H + P1 * ACTS * 2;   // 32000
-constexpr int OFF_A2H = OFF_A1L + P1 * ACTS * 2;   // 64000
-constexpr int OFF_A2L = OFF_A2H + P2 * ACTS * 2;   // 70480
-constexpr int OFF_W2H = OFF_A2L + P2 * ACTS * 2;   // 76960
-constexpr int OFF_W2L = OFF_W2H + 32 * W2S * 2;    // 110240
-constexpr int OFF_B23 = OFF_W2L + 32 * W2S * 2;    // 143520
-constexpr int LDS_BYTES = OFF_B23 + 96 * 4;        // 143904 (biases: conv2, conv3, conv1)
-static_assert(OFF_A2H % 16 == 0 && OFF_A2L % 16 == 0 && OFF_W2H % 16 == 0 && OFF_W2L % 16 == 0, "align");
 }  // namespace tsp
-
-// conv1 pixel tiles per wave (13 tiles); conv3 runs on waves 2 and 6 (SIMD 2)
-__constant__ int c_s1_begin[8] = {0, 2, 4, 4, 6, 8, 10, 11};
-__constant__ int c_s1_count[8] = {2, 2, 0, 2, 2, 2, 1, 2};
 
 #define TS_MAX_JOBS 4
 #define TS_JOB_WORDS 20
@@ -69,228 +52,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t ts_rsrc(const void* p, uint32_
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, bytes, 0x00020000);
 }
 
-__global__ __launch_bounds__(512) void torso_fwd_sp_kernel(const TSArgs args) {
-  using namespace tsp;
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  bf16* a1h = (bf16*)(lds + OFF_A1H);
-  bf16* a1l = (bf16*)(lds + OFF_A1L);
-  bf16* a2h = (bf16*)(lds + OFF_A2H);
-  bf16* a2l = (bf16*)(lds + OFF_A2L);
-  bf16* w2h = (bf16*)(lds + OFF_W2H);
-  bf16* w2l = (bf16*)(lds + OFF_W2L);
-  float* lb23 = (float*)(lds + OFF_B23);
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int half = lane >> 5, l32 = lane & 31;
-  const int wk = blockIdx.x;
-  int ji = 0;
-#pragma unroll
-  for (int i = 1; i < TS_MAX_JOBS; ++i)
-    if (i < args.njobs && wk >= args.job[i].wbegin) ji = i;
-  const TSJob& J = args.job[ji];
-  const int stride = J.wcount;
-  if (wk - J.wbegin >= stride) return;
-  const int n_frames = J.n;
-  int f = wk - J.wbegin;
-  if (f >= n_frames) return;
-
-  // ---- weights: W2 hi / lo -> LDS (padded rows); W1 hi / lo fragments -> VGPRs; biases
-  for (int i = tid; i < 32 * 64; i += NT) {
-    const int r = i >> 6, c = i & 63;
-    *(bf16x8*)(w2h + r * W2S + c * 8) = *(const bf16x8*)(J.w2 + r * 512 + c * 8);
-    *(bf16x8*)(w2l + r * W2S + c * 8) = *(const bf16x8*)(J.w2l + r * 512 + c * 8);
-  }
-  bf16x8 wf1h[16], wf1l[16];
-#pragma unroll
-  for (int s = 0; s < 16; ++s) {
-    wf1h[s] = *(const bf16x8*)(J.w1 + l32 * 256 + s * 16 + half * 8);
-    wf1l[s] = *(const bf16x8*)(J.w1l + l32 * 256 + s * 16 + half * 8);
-  }
-  // biases in LDS (broadcast reads in the epilogues; registers go to the W1 fragments)
-  if (tid < 96) lb23[tid] = tid < 32 ? J.b2[tid] : tid < 64 ? J.b3[tid - 32] : J.b1[tid - 64];
-  const int t1b = c_s1_begin[wave], t1n = c_s1_count[wave];
-  const bool conv3_wave = wave == 2 || wave == 6, conv2_wave = wave < 3;
-  const __amdgpu_buffer_rsrc_t w3rs = ts_rsrc(J.w3, 32 * 288 * 2);
-  const __amdgpu_buffer_rsrc_t w3lrs = ts_rsrc(J.w3l, 32 * 288 * 2);
-  __syncthreads();
-
-  uint32_t sink = 0;
-  int fprev = -1;
-  for (;;) {
-    const bool have = f < n_frames;
-    const int fn = f + stride;
-    // =================== phase A: conv1(f) || conv3(f-1)
-    if (have && !(args.dbg & 1)) {
-      const size_t row = J.rows ? (size_t)ld_uniform_i32(J.rows, f) : (size_t)f;
-      const __amdgpu_buffer_rsrc_t frs = ts_rsrc(args.frames + row * IN_BYTES, IN_BYTES);
-      for (int i = 0; i < t1n; ++i) {
-        const int p = (t1b + i) * 32 + l32;
-        const int pc = p < P1 ? p : P1 - 1;
-        const int oy = pc / 20, ox = pc % 20;
-        // K step s: s2d block (by, bx) = (s>>3, (s>>2)&1), channel ci = s&3, rows dy = 2h, 2h+1,
-        // columns dx 0..3: bytes frame[ci][4(oy+by) + dy][4(ox+bx) .. +3]
-        const int vb = (4 * oy + 2 * half) * 84 + 4 * ox;
-        constexpr int D = 5;
-        uint32_t r0[D], r1[D];
-        auto ld = [&](int s, uint32_t& x0, uint32_t& x1) {
-          const int so = (s & 3) * 7056 + (s >> 3) * 336 + ((s >> 2) & 1) * 4;
-          x0 = __builtin_amdgcn_raw_buffer_load_b32(frs, vb, so, 0);
-          x1 = __builtin_amdgcn_raw_buffer_load_b32(frs, vb, so + 84, 0);
-        };
-#pragma unroll
-        for (int s = 0; s < D; ++s) ld(s, r0[s], r1[s]);
-        f32x16 acc = {};
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-          const uint32_t x0 = r0[s % D], x1 = r1[s % D];
-          if (s + D < 16) ld(s + D, r0[s % D], r1[s % D]);
-          const bf16x8 x = u8x8_to_bf16(x0, x1);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf1l[s], x, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf1h[s], x, acc, 0, 0, 0);
-        }
-        if (p < P1) {
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            bf16x4 vh, vl;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float v = fmaxf(acc[4 * g + e] * (1.f / 255.f) + lb23[64 + 8 * g + 4 * half + e], 0.f);
-              vh[e] = (bf16)v;
-              vl[e] = sp_lo(v);
-            }
-            *(bf16x4*)(a1h + p * ACTS + 8 * g + 4 * half) = vh;
-            *(bf16x4*)(a1l + p * ACTS + 8 * g + 4 * half) = vl;
-          }
-        }
-      }
-    }
-    if (fprev >= 0 && conv3_wave && !(args.dbg & 4)) {
-      // conv3(f-1): pixel tile (wave == 6), K = 288 = (kh 3, kw 3, ci 32); A = W3 from L2
-      const int p = (wave == 6 ? 32 : 0) + l32;
-      const int pc = p < P3 ? p : P3 - 1;
-      const int oy = pc / 7, ox = pc % 7;
-      const int va = (l32 * 288 + half * 8) * 2;
-      const bf16* bh = a2h + (oy * 9 + ox) * ACTS + half * 8;
-      const bf16* bl = a2l + (oy * 9 + ox) * ACTS + half * 8;
-      constexpr int D = 3;
-      bf16x8 rah[D], ral[D];
-      auto lda = [&](int s, bf16x8& h, bf16x8& l) {
-        h = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w3rs, va, s * 32, 0));
-        l = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(w3lrs, va, s * 32, 0));
-      };
-#pragma unroll
-      for (int s = 0; s < D; ++s) lda(s, rah[s], ral[s]);
-      f32x16 acc = {};
-#pragma unroll
-      for (int s = 0; s < 18; ++s) {
-        const bf16x8 ah = rah[s % D], al = ral[s % D];
-        if (s + D < 18) lda(s + D, rah[s % D], ral[s % D]);
-        const int khkw = s >> 1, kh = khkw / 3, kw = khkw % 3;
-        const int o = (kh * 9 + kw) * ACTS + (s & 1) * 16;
-        acc = mfma32_x3(ah, al, *(const bf16x8*)(bh + o), *(const bf16x8*)(bl + o), acc);
-      }
-      if (p < P3) {
-        const size_t o = (size_t)fprev * 1568 + p;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int co = (r & 3) + 8 * (r >> 2) + 4 * half;
-          const float v = fmaxf(acc[r] + lb23[32 + co], 0.f);
-          J.out[o + co * 49] = (bf16)v;
-          J.out_l[o + co * 49] = sp_lo(v);
-        }
-      }
-    }
-    lds_sync();
-    if (!have) break;
-
-    // =================== phase B: conv2(f) on waves 0..2; act1 save + next-frame warm-up
-    if (conv2_wave) {
-      if (args.dbg & 2) goto conv2_done;
-      {
-      const int p = wave * 32 + l32;
-      const int pc = p < P2 ? p : P2 - 1;
-      const int oy = pc / 9, ox = pc % 9;
-      const bf16* ah = w2h + l32 * W2S + half * 8;
-      const bf16* al = w2l + l32 * W2S + half * 8;
-      const bf16* bh = a1h + ((2 * oy) * 20 + 2 * ox) * ACTS + half * 8;
-      const bf16* bl = a1l + ((2 * oy) * 20 + 2 * ox) * ACTS + half * 8;
-      constexpr int D = 2;
-      bf16x8 rah[D], ral[D], rbh[D], rbl[D];
-      auto ld = [&](int s, bf16x8& xah, bf16x8& xal, bf16x8& xbh, bf16x8& xbl) {
-        const int khkw = s >> 1, kh = khkw >> 2, kw = khkw & 3;
-        const int ob = (kh * 20 + kw) * ACTS + (s & 1) * 16;
-        xah = *(const bf16x8*)(ah + s * 16);
-        xal = *(const bf16x8*)(al + s * 16);
-        xbh = *(const bf16x8*)(bh + ob);
-        xbl = *(const bf16x8*)(bl + ob);
-      };
-#pragma unroll
-      for (int s = 0; s < D; ++s) ld(s, rah[s], ral[s], rbh[s], rbl[s]);
-      f32x16 acc = {};
-#pragma unroll
-      for (int s = 0; s < 32; ++s) {
-        const bf16x8 xah = rah[s % D], xal = ral[s % D], xbh = rbh[s % D], xbl = rbl[s % D];
-        if (s + D < 32) ld(s + D, rah[s % D], ral[s % D], rbh[s % D], rbl[s % D]);
-        __builtin_amdgcn_sched_barrier(0);
-        acc = mfma32_x3(xah, xal, xbh, xbl, acc);
-      }
-      if (p < P2) {
-        bf16* d2 = J.s2 ? J.s2 + ((size_t)f * P2 + p) * 32 : nullptr;
-        bf16* d2l = J.s2 ? J.s2l + ((size_t)f * P2 + p) * 32 : nullptr;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          bf16x4 vh, vl;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int co = 4 * half + 8 * g + e;
-            const float v = fmaxf(acc[4 * g + e] + lb23[co], 0.f);
-            vh[e] = (bf16)v;
-            vl[e] = sp_lo(v);
-          }
-          *(bf16x4*)(a2h + p * ACTS + 8 * g + 4 * half) = vh;
-          *(bf16x4*)(a2l + p * ACTS + 8 * g + 4 * half) = vl;
-          if (d2) {
-            *(bf16x4*)(d2 + 8 * g + 4 * half) = vh;
-            *(bf16x4*)(d2l + 8 * g + 4 * half) = vl;
-          }
-        }
-      }
-      }
-    conv2_done:;
-    } else {
-      const int t5 = tid - 192;   // 0..319
-      // warm the next frame's lines into L2 / L1 (consumed below, after the act1 copy-out)
-      uint32_t wv[2] = {0, 0};
-      if (fn < n_frames) {
-        const size_t rn = J.rows ? (size_t)ld_uniform_i32(J.rows, fn) : (size_t)fn;
-        const uint8_t* fr = args.frames + rn * IN_BYTES;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const int c = t5 + 320 * q;
-          if (c < IN_BYTES / 64) wv[q] = *(const uint32_t*)(fr + c * 64);
-        }
-      }
-      if (J.s1 != nullptr) {
-        bf16* d1 = J.s1 + (size_t)f * P1 * 32;
-        bf16* d1l = J.s1l + (size_t)f * P1 * 32;
-        for (int c = t5; c < P1 * 4; c += 320) {   // 4 chunks of 8 channels per pixel
-          const int px = c >> 2, q = c & 3;
-          *(bf16x8*)(d1 + px * 32 + q * 8) = *(const bf16x8*)(a1h + px * ACTS + q * 8);
-          *(bf16x8*)(d1l + px * 32 + q * 8) = *(const bf16x8*)(a1l + px * ACTS + q * 8);
-        }
-      }
-      sink += wv[0] ^ wv[1];
-    }
-    lds_sync();
-    fprev = f;
-    f = fn;
-  }
-  if (J.keep && sink == 0x9E3779B9u) J.out[0] = (bf16)0.f;   // keeps the warm-up loads alive
-}
-
-// jobs: njobs x TS_JOB_WORDS int64 {rows, n, w1, w1l, b1, w2, w2l, b2, w3, w3l, b3, out, out_l,
-// s1, s1l, s2, s2l, 0, 0, 0}.  grid <= 0: one workgroup per CU (the caller passes the CU count).
 // ============================================================================================
-// Forward v2 (the default): the v1 profile (tools/sp_micro.py probe, profiles/archive/r02_torso_sp_*)
+// Forward v2 (the only forward): the v1 profile (tools/sp_micro.py probe, profiles/archive/r02_torso_sp_*)
 // showed conv1's B fragments (two 4-byte buffer loads per K step from L1 / L2) and conv3's W3
 // fragments (L2, re-read by two waves per frame: 72 KB / frame) latency-bound, the next-frame
 // warm-up waited on inside phase B, and 2-3-way bank conflicts on the padded act1 image.  v2:
@@ -415,7 +178,6 @@ __device__ __forceinline__ void c1_frags(const uint8_t* dig, int lane, bf16x8 (&
 __constant__ int c_s2_begin[8] = {0, 2, 4, 4, 6, 8, 10, 11};
 __constant__ int c_s2_count[8] = {2, 2, 0, 2, 2, 2, 1, 2};
 
-template <bool I8>
 __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
   using namespace tsp2;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -454,13 +216,13 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
   }
   bf16x8 wfh[16], wfl[16];
   float c1_scale = 0.f;
-  if (I8) {   // int8 digits of W1 -> LDS (act1 region) -> conv1 lanes' fragments
+  {   // int8 digits of W1 -> LDS (act1 region) -> conv1 lanes' fragments
     c1_scale = c1_digits(J.w1, J.w1l, tid, a1h, (int*)(lds + OFF_SC), (float*)(a1h + 3 * 8192));
     c1_scale = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(c1_scale)));   // SGPR
     __syncthreads();
     if (!conv3_wave) c1_frags(a1h, lane, wfh, wfl);
   }
-  if (!I8 || conv3_wave) {
+  if (conv3_wave) {
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
       const bf16* ph = conv3_wave ? J.w3 + l32 * 288 + s * 16 + half * 8 : J.w1 + l32 * 256 + s * 16 + half * 8;
@@ -479,7 +241,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
     const u32x4* src = (const u32x4*)(args.frames + row * IN_BYTES);
     // int8 conv1 reads the frame as (byte - 128): the shift is applied once here / at the
     // phase-B store, not per conv1 lane per K step (16 XORs per 16-pixel half tile)
-    const uint32_t sh = I8 ? 0x80808080u : 0u;
+    const uint32_t sh = 0x80808080u;
     for (int c = tid; c < IN_CHUNKS2; c += NT) ((u32x4*)fr)[c] = src[c] ^ sh;
   }
   const int t1b = c_s2_begin[wave], t1n = c_s2_count[wave];
@@ -487,7 +249,6 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
   __syncthreads();
 
   int fprev = -1;
-  u32x4 pf[4];
   int it_dbg = 0;
   long long* tr = (args.trace && blockIdx.x == 0 && lane == 0) ? args.trace + wave * 16 * 5 : nullptr;
 #define TS2_STAMP(k) \
@@ -508,17 +269,16 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
       const u32x4* src = (const u32x4*)(args.frames + (size_t)row_nx * IN_BYTES);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int c = I8 ? t7 + 448 * q : tid + NT * q;
-        if (c < IN_CHUNKS2 && (!I8 || !conv3_wave)) {
+        const int c = t7 + 448 * q;
+        if (c < IN_CHUNKS2 && !conv3_wave) {
           // int8 path: the 7 conv1 waves prefetch (4 chunks per thread) and park the chunks in
           // wfl[8..11], which only the conv3 wave uses (W3 K steps 8..11 lo); the conv1 digits
           // fill slots 0..23
-          if (I8) wfl[8 + q] = __builtin_bit_cast(bf16x8, src[c]);
-          else pf[q] = src[c];
+          wfl[8 + q] = __builtin_bit_cast(bf16x8, src[c]);
         }
       }
     }
-    if (I8 && have && !(args.dbg & 1)) {
+    if (have && !(args.dbg & 1)) {
       // conv1(f) on the int8 matrix cores (c1_digits): per 16-pixel half tile, the 4 K blocks'
       // frame bytes (4 rows x 4 bytes per lane, -128 by XOR), 3 digits x 2 channel halves of
       // v_mfma_i32_16x16x64_i8, exact int32 sums
@@ -575,50 +335,6 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
               *(bf16x4*)(a1h + o) = vh;
               *(bf16x4*)(a1l + o) = vl;
             }
-          }
-        }
-      }
-    }
-    if (!I8 && have && !(args.dbg & 1)) {
-      for (int i = 0; i < t1n; ++i) {
-        const int p = (t1b + i) * 32 + l32;
-        const int pc = p < P1 ? p : P1 - 1;
-        const int oy = pc / 20, ox = pc % 20;
-        // K step s: s2d block (by, bx) = (s>>3, (s>>2)&1), channel ci = s&3, rows dy = 2h, 2h+1,
-        // columns 0..3: bytes frame[ci][4(oy+by) + dy][4(ox+bx) .. +3]
-        const uint8_t* fb = fr + (4 * oy + 2 * half) * 84 + 4 * ox + oz;
-        constexpr int D = 6;
-        uint32_t r0[D], r1[D];
-        auto ld = [&](int s, uint32_t& x0, uint32_t& x1) {
-          const int so = (s & 3) * 7056 + (s >> 3) * 336 + ((s >> 2) & 1) * 4;
-          x0 = *(const uint32_t*)(fb + so);
-          x1 = *(const uint32_t*)(fb + so + 84);
-        };
-#pragma unroll
-        for (int s = 0; s < D; ++s) ld(s, r0[s], r1[s]);
-        f32x16 acc = {};
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-          const uint32_t x0 = r0[s % D], x1 = r1[s % D];
-          if (s + D < 16) ld(s + D, r0[s % D], r1[s % D]);
-          __builtin_amdgcn_sched_barrier(0);
-          const bf16x8 x = u8x8_to_bf16(x0, x1);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wfl[s], x, acc, 0, 0, 0);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wfh[s], x, acc, 0, 0, 0);
-        }
-        if (p < P1) {
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            bf16x4 vh, vl;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float v = fmaxf(acc[4 * g + e] * (1.f / 255.f) + lb[64 + 8 * g + 4 * half + e], 0.f);
-              vh[e] = (bf16)v;
-              vl[e] = sp_lo(v);
-            }
-            const int o = a1_off(p, g) + 8 * half;
-            *(bf16x4*)(a1h + o) = vh;
-            *(bf16x4*)(a1l + o) = vl;
           }
         }
       }
@@ -681,9 +397,9 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
     if (fn < n_frames && !(args.dbg & 16)) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int c = I8 ? t7 + 448 * q : tid + NT * q;
-        if (c < IN_CHUNKS2 && (!I8 || !conv3_wave))
-          ((u32x4*)fr)[c] = I8 ? (__builtin_bit_cast(u32x4, wfl[8 + q]) ^ 0x80808080u) : pf[q];
+        const int c = t7 + 448 * q;
+        if (c < IN_CHUNKS2 && !conv3_wave)
+          ((u32x4*)fr)[c] = __builtin_bit_cast(u32x4, wfl[8 + q]) ^ 0x80808080u;
       }
     }
     if (conv2_wave) {
@@ -761,468 +477,6 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
   }
 }
 
-// ============================================================================================
-// Forward v3 (the default).  v2 runs its three convs in two serialised phases per frame (conv1 ||
-// conv3, then conv2 on three waves while five wait): 13.1k cycles per frame against 5.7k of MFMA
-// per SIMD, 35 % MFMA busy (profiles/r04_roofline_base.txt).  v3 pipelines the convs of three
-// consecutive frames through ONE phase per frame, with every SIMD running one wave of each role:
-//
-//   waves 4..7 ("C1"): conv1(f_i) on the int8 matrix cores (16x16x64, three W1 digits as in v2,
-//                      exact int32 sums) for one 16-channel half over half of the 25 4x4-pixel
-//                      tiles, then conv3(f_{i-2}) (16x16x32 bf16, 3 passes) for the same channel
-//                      half over two 4x4 tiles of the 7x7 output; W1 digits (48 VGPRs) and W3 (72)
-//                      register-resident
-//   waves 0..3 ("C2"): conv2(f_{i-1}) (16x16x32 bf16, 3 passes) for one channel half over three of
-//                      six 16-pixel tiles, W2 (128 VGPRs) register-resident; they also stage frame
-//                      f_{i+1} (dword loads during iteration i, stored at the start of i+1 while the
-//                      C1 waves run conv3, then an LDS counter releases conv1)
-//
-// so the int8 conv1's VALU-heavy epilogue issues beside the other wave's bf16 MFMAs on the same
-// SIMD.  act1 / act2 are double-buffered in LDS (W2 moved out of LDS pays for it).  Layouts
-// (conflict-free for every MFMA operand read, by a bank model of the ds_read_b128 lane groups):
-//   * frame: space-to-depth 4x4 blocks, 16 bytes each (one conv1 B fragment = one ds_read_b128),
-//     rows of 24 blocks, channel planes of 508 blocks;
-//   * act1: pixel (y, x) in slot y*20 + (x ^ ((x >> 2) & 1)), 16-byte channel chunk c at position
-//     c ^ 2((y >> 1) & 1) ^ ((x >> 1) & 1);
-//   * act2: slot y*9 + x, chunk position c ^ ((y >> 1) & 1) ^ (2(x & 1) | ((x >> 1) & 1)).
-// Products accumulate in 32-wide K steps (v2: 16), so outputs match v2 to fp32 rounding, not bit
-// for bit (tests/test_split_gpu.py).
-namespace tsp3 {
-using tsp::NT; using tsp::IN_BYTES;
-constexpr int FRP = 508 * 16;                // frame channel plane (bytes)
-constexpr int OFF_FR = 0;
-constexpr int A1P = 400 * 64;                // one act1 plane
-constexpr int OFF_A1 = 4 * FRP;              // 32512: [buffer 2][hi, lo]
-constexpr int A2P = 81 * 64;                 // one act2 plane
-constexpr int OFF_A2 = OFF_A1 + 4 * A1P;     // 134912: [buffer 2][hi, lo]
-constexpr int OFF_B = OFF_A2 + 4 * A2P;      // 155648: biases conv2, conv3, conv1
-constexpr int OFF_SC = OFF_B + 96 * 4;       // 156032: int8 conv1 row corrections [2][32]
-constexpr int OFF_FLAG = OFF_SC + 64 * 4;    // 156288: frame-ready counter, staging-drained counter
-constexpr int OFF_ST = OFF_FLAG + 16;        // 156304: conv3 output staging [hi, lo][1568] bf16 (CHW)
-constexpr int LDS_BYTES = OFF_ST + 2 * 1568 * 2;   // 162576
-constexpr int NBLK = 4 * 441;                // s2d blocks per frame
-constexpr int PFQ = (NBLK + 255) / 256;      // blocks per C2 thread (7)
-static_assert(LDS_BYTES <= 160 * 1024, "LDS");
-}  // namespace tsp3
-
-__device__ __forceinline__ int a1v3_off(int y, int x, int c) {
-  return (y * 20 + (x ^ ((x >> 2) & 1))) * 64 + ((c ^ (((y >> 1) & 1) << 1) ^ ((x >> 1) & 1)) << 4);
-}
-__device__ __forceinline__ int a2v3_off(int y, int x, int c) {
-  return (y * 9 + x) * 64 + ((c ^ ((y >> 1) & 1) ^ (((x & 1) << 1) | ((x >> 1) & 1))) << 4);
-}
-// s2d block b (channel-major, 21 x 21 per channel) -> its source dword offset in the frame and its
-// LDS offset in the frame image
-__device__ __forceinline__ void fr3_block(int b, int& src, int& dst) {
-  const int ci = b / 441, rem = b - 441 * ci, r = rem / 21, c = rem - 21 * r;
-  src = ci * 7056 + 4 * r * 84 + 4 * c;
-  dst = ci * tsp3::FRP + (r * 24 + c) * 16;
-}
-
-// D2 / D3: depth of the conv2 / conv3 LDS operand rings (K steps in flight)
-template <int D2, int D3>
-__global__ __launch_bounds__(512) void torso_fwd_sp3_kernel(const TSArgs args) {
-  using namespace tsp3;
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  float* lb = (float*)(lds + OFF_B);
-  int* flag = (int*)(lds + OFF_FLAG);
-  int* drained = flag + 1;   // staging copies done (C2 waves, one add per wave per frame)
-  bf16* st = (bf16*)(lds + OFF_ST);
-  // the wave index through readfirstlane: every role / tile decision and its index math is
-  // then scalar (SALU), not repeated per lane on the VALU the conv1 epilogue needs
-  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int l16 = lane & 15, kq = lane >> 4;
-  const int wk = blockIdx.x;
-  int ji = 0;
-#pragma unroll
-  for (int i = 1; i < TS_MAX_JOBS; ++i)
-    if (i < args.njobs && wk >= args.job[i].wbegin) ji = i;
-  const TSJob& J = args.job[ji];
-  const int stride = J.wcount;
-  const int first = wk - J.wbegin;
-  if (first >= stride || first >= J.n) return;
-  const int nf = (J.n - first + stride - 1) / stride;   // frames of this workgroup
-  auto frame_row = [&](int k) -> size_t {
-    const int f = first + k * stride;
-    return J.rows ? (size_t)ld_uniform_i32(J.rows, f) : (size_t)f;
-  };
-
-  // ---- once: W1 digits (all threads; the act1 region is scratch), biases, frame 0, counter
-  const float c1_scale = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(
-      c1_digits(J.w1, J.w1l, tid, lds + OFF_A1, (int*)(lds + OFF_SC), (float*)(lds + OFF_A1 + 3 * 8192)))));
-  if (tid < 96) lb[tid] = tid < 32 ? J.b2[tid] : tid < 64 ? J.b3[tid - 32] : J.b1[tid - 64];
-  if (tid == 0) { *flag = 0; *drained = 0; }
-  {
-    const __amdgpu_buffer_rsrc_t frs = ts_rsrc(args.frames + frame_row(0) * IN_BYTES, IN_BYTES);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int b = tid + 512 * q;
-      if (b < NBLK) {
-        int src, dst;
-        fr3_block(b, src, dst);
-        u32x4 v;
-#pragma unroll
-        for (int dy = 0; dy < 4; ++dy) v[dy] = __builtin_amdgcn_raw_buffer_load_b32(frs, src * 1 + dy * 84, 0, 0) ^ 0x80808080u;
-        *(u32x4*)(lds + OFF_FR + dst) = v;
-      }
-    }
-  }
-  __syncthreads();   // digits + frame 0 + biases in LDS
-  // optional clock stamps of workgroup 0 (r2_torso_sp_trace): [wave][iteration < 16][4] = loop
-  // top, conv3 / frame staging done, conv1 / conv2 done, after the barrier
-  long long* tr = (args.trace && blockIdx.x == 0 && lane == 0) ? args.trace + wave * 16 * 24 : nullptr;
-#define TS3_STAMP(it, k) \
-  if (tr && (it) < 16) tr[(it) * 24 + (k)] = (long long)__builtin_readcyclecounter();
-
-  if (wave >= 4) {
-    // ================================ C1: conv1(f_i) then (next iteration first) conv3(f_{i-2})
-    const int c1 = wave - 4, hc = c1 & 1, grp = c1 >> 1;
-    const int ch0 = 16 * hc + 4 * kq;
-    i32x4_t wd[12];   // W1 digit fragments (kb, d) of channel half hc
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-      for (int d = 0; d < 3; ++d)
-        wd[3 * kb + d] = *(const i32x4_t*)(lds + OFF_A1 + d * 8192 + (16 * hc + l16) * 256 + (4 * kb + kq) * 16);
-    bf16x8 w3h[9], w3l[9];
-#pragma unroll
-    for (int s = 0; s < 9; ++s) {
-      w3h[s] = *(const bf16x8*)(J.w3 + (16 * hc + l16) * 288 + s * 32 + 8 * kq);
-      w3l[s] = *(const bf16x8*)(J.w3l + (16 * hc + l16) * 288 + s * 32 + 8 * kq);
-    }
-    const i32x4_t sc0 = *(const i32x4_t*)(lds + OFF_SC + ch0 * 4);
-    const i32x4_t sc2 = *(const i32x4_t*)(lds + OFF_SC + (32 + ch0) * 4);
-    float b1v[4], b3v[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) { b1v[e] = lb[64 + ch0 + e]; b3v[e] = lb[32 + ch0 + e]; }
-    __syncthreads();   // every C1 wave holds its digits before conv1(f_0) overwrites the scratch
-    const int t_beg = grp ? 13 : 0, t_end = grp ? 25 : 13;
-    // lane-constant parts of the conv1 fragment / epilogue offsets
-    const int fr_lane = OFF_FR + kq * FRP + ((l16 >> 2) * 24 + (l16 & 3)) * 16;
-    // conv3: the act2 operand offsets of both tiles (frame-invariant) and the output pixels
-    int o3[2][9], p3[2];
-    bool ok3[2];
-#pragma unroll
-    for (int tt = 0; tt < 2; ++tt) {
-      const int t = 2 * grp + tt;
-      const int y3 = (t >> 1) * 4 + (l16 >> 2), x3 = (t & 1) * 4 + (l16 & 3);
-      const int yc = min(y3, 6), xc = min(x3, 6);
-#pragma unroll
-      for (int s_ = 0; s_ < 9; ++s_) o3[tt][s_] = a2v3_off(yc + s_ / 3, xc + s_ % 3, kq);
-      p3[tt] = y3 * 7 + x3;
-      ok3[tt] = y3 < 7 && x3 < 7;
-    }
-    for (int i = 0; i < nf + 2; ++i) {
-      TS3_STAMP(i, 0);
-      f32x4 acc3[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-      if (i >= 2 && !(args.dbg & 16384)) {   // (bit 14: timing probe without conv3)
-        // conv3(f_{i-2}): act2 buffer (i-2)&1, two 4x4 tiles of the 7x7 output (accumulators
-        // held until the staging write after conv1)
-        const int k = i - 2;
-        const uint8_t* a2h = lds + OFF_A2 + (k & 1) * 2 * A2P;
-        const uint8_t* a2l = a2h + A2P;
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt) {
-          f32x4& acc = acc3[tt];
-          bf16x8 rh[D3], rl[D3];
-          auto ld = [&](int s, bf16x8& h, bf16x8& l) {
-            h = *(const bf16x8*)(a2h + o3[tt][s]);
-            l = *(const bf16x8*)(a2l + o3[tt][s]);
-          };
-#pragma unroll
-          for (int s = 0; s < D3; ++s) ld(s, rh[s], rl[s]);
-#pragma unroll
-          for (int s = 0; s < 9; ++s) {
-            const bf16x8 h = rh[s % D3], l = rl[s % D3];
-            if (s + D3 < 9) ld(s + D3, rh[s % D3], rl[s % D3]);
-            __builtin_amdgcn_sched_barrier(0);
-            acc = mfma16_x3(w3h[s], w3l[s], h, l, acc);
-          }
-        }
-      }
-      if (i >= 2) {
-        // conv3(f_{i-2}) -> the CHW staging image, once the C2 waves have copied f_{i-3}'s out
-        // (they do so at the start of iteration i, right after staging the frame: by the end of
-        // conv3 this wait is normally satisfied; the accumulators then die before conv1)
-        if (i >= 3) {
-          while (__hip_atomic_load(drained, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 4 * (i - 2))
-            __builtin_amdgcn_s_sleep(1);
-        }
-#pragma unroll
-        for (int tt = 0; tt < 2; ++tt) {
-          if (ok3[tt]) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float v = fmaxf(acc3[tt][e] + b3v[e], 0.f);
-              st[(ch0 + e) * 49 + p3[tt]] = (bf16)v;
-              st[1568 + (ch0 + e) * 49 + p3[tt]] = sp_lo(v);
-            }
-          }
-        }
-      }
-      TS3_STAMP(i, 1);
-      if (i < nf && !(args.dbg & 4096)) {   // (bit 12: timing probe without conv1)
-        if (i >= 1) {   // frame f_i staged by the C2 waves
-          while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < 4 * i)
-            __builtin_amdgcn_s_sleep(1);
-        }
-        uint8_t* a1h = lds + OFF_A1 + (i & 1) * 2 * A1P;
-        uint8_t* a1l = a1h + A1P;
-        const int fidx = first + i * stride;
-        const bool keep_s1 = J.s1 && !(args.dbg & 131072);   // (bit 17: probe without s1 stores)
-        bf16* s1 = keep_s1 ? J.s1 + (size_t)fidx * 400 * 32 : nullptr;
-        bf16* s1l = keep_s1 ? J.s1l + (size_t)fidx * 400 * 32 : nullptr;
-        auto ldb = [&](int t, i32x4_t (&x)[4]) {
-          if (args.dbg & 262144) {   // (bit 18: probe without the fragment loads)
-            x[0] = x[1] = x[2] = x[3] = i32x4_t{t, 1, 2, 3};
-            return;
-          }
-          const int ty = t / 5, tx = t - 5 * ty;
-          const uint8_t* p = lds + fr_lane + (ty * 4 * 24 + tx * 4) * 16;
-          x[0] = *(const i32x4_t*)(p);
-          x[1] = *(const i32x4_t*)(p + 16);
-          x[2] = *(const i32x4_t*)(p + 24 * 16);
-          x[3] = *(const i32x4_t*)(p + 25 * 16);
-        };
-        // Software-pipelined over tiles: the 12 int8 MFMAs of tile t+1 (3 digits x 4 K blocks)
-        // are issued before the epilogue of tile t, and the scheduler interleaves that epilogue's
-        // VALU into the MFMA gaps (sched_group_barrier: 1 MFMA : 2 VALU), so the epilogue -- the
-        // conv1 wave's bottleneck when it followed its own MFMAs -- runs under the matrix pipe.
-        auto mfma12 = [&](const i32x4_t (&b)[4], i32x4_t (&acc)[3]) {
-          acc[0] = sc0;
-          acc[1] = i32x4_t{0, 0, 0, 0};
-          acc[2] = sc2;
-          if (args.dbg & 65536) {   // (bit 16: timing probe, no conv1 MFMAs)
-            acc[1] = b[0] ^ b[1] ^ b[2] ^ b[3];
-            return;
-          }
-#pragma unroll
-          for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-            for (int d = 0; d < 3; ++d)
-              acc[d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(wd[3 * kb + d], b[kb], acc[d], 0, 0, 0);
-        };
-        auto epi = [&](int t, const i32x4_t (&acc)[3]) {
-          const int ty = t / 5, tx = t - 5 * ty;
-          const int y = 4 * ty + (l16 >> 2), x = 4 * tx + (l16 & 3);
-          bf16x4 vh, vl;
-          if (args.dbg & 32768) {   // (bit 15: timing probe, no epilogue math)
-            vh = __builtin_bit_cast(bf16x4, u32x2{(uint32_t)acc[0][0], (uint32_t)acc[1][1]});
-            vl = __builtin_bit_cast(bf16x4, u32x2{(uint32_t)acc[2][2], (uint32_t)acc[0][3]});
-          } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int i0 = acc[0][e];
-            const int i12 = acc[1][e] * 128 + acc[2][e];
-            const float tq = fmaf((float)i12, 1.f / 16384.f, (float)i0);
-            const float v = fmaxf(fmaf(tq, c1_scale, b1v[e]), 0.f);
-            vh[e] = (bf16)v;
-            vl[e] = sp_lo(v);
-          }
-          }
-          const int o = a1v3_off(y, x, ch0 >> 3) + 8 * (kq & 1);
-          *(bf16x4*)(a1h + o) = vh;
-          *(bf16x4*)(a1l + o) = vl;
-          if (s1) {
-            const size_t g = (size_t)(y * 20 + x) * 32 + ch0;
-            *(bf16x4*)(s1 + g) = vh;
-            *(bf16x4*)(s1l + g) = vl;
-          }
-        };
-        auto interleave = [&]() {
-#pragma unroll
-          for (int q = 0; q < 12; ++q) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
-            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);   // 2 VALU
-          }
-        };
-        i32x4_t F0[4], F1[4], A0[3], A1[3];
-        ldb(t_beg, F0);
-        ldb(t_beg + 1, F1);   // t_end - t_beg >= 12: always a valid tile
-        mfma12(F0, A0);
-#pragma unroll 1
-        for (int t = t_beg; t < t_end; t += 2) {
-          // unconditional loads (the last tiles re-read the final one): a prefetch under a branch
-          // made the compiler's lgkmcnt bookkeeping wait for it before the MFMAs
-          TS3_STAMP(i, 4 + (t - t_beg));
-          ldb(min(t + 2, t_end - 1), F0);
-          __builtin_amdgcn_sched_barrier(0);
-          if (t + 1 < t_end) {
-            mfma12(F1, A1);
-            epi(t, A0);
-            interleave();
-          } else {
-            epi(t, A0);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-          if (t + 1 >= t_end) break;
-          TS3_STAMP(i, 5 + (t - t_beg));
-          ldb(min(t + 3, t_end - 1), F1);
-          __builtin_amdgcn_sched_barrier(0);
-          if (t + 2 < t_end) {
-            mfma12(F0, A0);
-            epi(t + 1, A1);
-            interleave();
-          } else {
-            epi(t + 1, A1);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      TS3_STAMP(i, 2);
-      lds_sync();
-      TS3_STAMP(i, 3);
-    }
-  } else {
-    // ================================ C2: stage frame f_i, load f_{i+1}, conv2(f_{i-1})
-    const int c2 = wave, h = c2 & 1, grp = c2 >> 1;
-    const int chc = 16 * h + 4 * kq;
-    bf16x8 w2h[16], w2l[16];
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      w2h[s] = *(const bf16x8*)(J.w2 + (16 * h + l16) * 512 + s * 32 + 8 * kq);
-      w2l[s] = *(const bf16x8*)(J.w2l + (16 * h + l16) * 512 + s * 32 + 8 * kq);
-    }
-    float b2v[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) b2v[e] = lb[chc + e];
-    // frame staging: a (row y, 3-block column group k) pair of all 4 channels per load set --
-    // 12-byte loads (21 dwords a row = 7 x 3: never across a row), each dword to its s2d block
-    // (y >> 2, 3k + m) at row y & 3; channel offsets are immediates.  Pairs t, t + 256, t + 512
-    // (< 588) of thread t: 8-12 loads a frame instead of 28 dword loads
-    constexpr int NPAIR = 84 * 7;
-    int fsrc[3], fdst[3];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int pr = min(tid + 256 * j, NPAIR - 1), y = pr / 7, k = pr - 7 * y;
-      fsrc[j] = y * 84 + 12 * k;
-      fdst[j] = OFF_FR + ((y >> 2) * 24 + 3 * k) * 16 + (y & 3) * 4;
-    }
-    const bool third = tid + 512 < NPAIR;
-    __syncthreads();   // pairs the C1 waves' digit barrier
-    typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
-    u32x3 pf[3][4];
-    // the staged conv3 outputs of frame k (CHW hi / lo, 2 x 196 16-byte chunks) -> global
-    auto drain = [&](int k) {
-      const size_t fo = (size_t)(first + k * stride) * 1568;
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int c = tid + 256 * q;          // chunk: plane c / 196, 8 bf16 each
-        if (c < 392) {
-          const int pl = c >= 196, cc = c - 196 * pl;
-          const u32x4 v = *(const u32x4*)(st + pl * 1568 + cc * 8);
-          if (!(args.dbg & 1024)) *(u32x4*)((pl ? J.out_l : J.out) + fo + cc * 8) = v;
-        }
-      }
-      if (lane == 0) __hip_atomic_fetch_add(drained, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-    for (int i = 0; i < nf + 2; ++i) {
-      TS3_STAMP(i, 0);
-      if (i >= 1 && i < nf) {
-        // frame f_i -> LDS (conv1(f_{i-1}) finished reading the image at the last barrier)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          if (j < 2 || third) {
-#pragma unroll
-            for (int ci = 0; ci < 4; ++ci) {
-              uint32_t* d = (uint32_t*)(lds + fdst[j] + ci * FRP);
-              d[0] = pf[j][ci][0] ^ 0x80808080u;
-              d[4] = pf[j][ci][1] ^ 0x80808080u;
-              d[8] = pf[j][ci][2] ^ 0x80808080u;
-            }
-          }
-        }
-        if (lane == 0) __hip_atomic_fetch_add(flag, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      if (i >= 3) drain(i - 3);
-      // frame f_{i+1} -> registers, issued in three groups between the conv2 tiles (28 dword
-      // loads at once backed the vector-memory queue up into the staging phase the conv1 waves
-      // wait on)
-      const bool ld_next = i + 1 < nf && !(args.dbg & 2048);   // (bit 11: probe without them)
-      const __amdgpu_buffer_rsrc_t frs =
-          ts_rsrc(args.frames + (ld_next ? frame_row(i + 1) : 0) * IN_BYTES, IN_BYTES);
-      auto issue = [&](int j) {
-        if (!ld_next || (j == 2 && !third)) return;
-#pragma unroll
-        for (int ci = 0; ci < 4; ++ci)
-          pf[j][ci] = __builtin_bit_cast(u32x3, __builtin_amdgcn_raw_buffer_load_b96(frs, fsrc[j], ci * 7056, 0));
-      };
-      TS3_STAMP(i, 1);
-      const bool c2_on = i >= 1 && i <= nf && !(args.dbg & 8192);   // (bit 13: without conv2)
-      if (!c2_on) { issue(0); issue(1); issue(2); }
-      if (c2_on) {
-        const int k = i - 1;
-        const uint8_t* a1h = lds + OFF_A1 + (k & 1) * 2 * A1P;
-        const uint8_t* a1l = a1h + A1P;
-        uint8_t* a2h = lds + OFF_A2 + (k & 1) * 2 * A2P;
-        uint8_t* a2l = a2h + A2P;
-        const int fidx = first + k * stride;
-        bf16* s2 = J.s2 ? J.s2 + (size_t)fidx * 81 * 32 : nullptr;
-        bf16* s2l = J.s2 ? J.s2l + (size_t)fidx * 81 * 32 : nullptr;
-#pragma unroll 1
-        for (int tt = 0; tt < 3; ++tt) {
-          const int t = 3 * grp + tt;
-          int y2, x2;
-          bool ok = true;
-          if (t < 4) { y2 = (t >> 1) * 4 + (l16 >> 2); x2 = (t & 1) * 4 + (l16 & 3); }
-          else if (t == 4) { y2 = l16 < 8 ? l16 : 8; x2 = l16 < 8 ? 8 : l16 - 8; }
-          else { y2 = 8; x2 = 8; ok = l16 == 0; }
-          // tap (kh, kw) offset = yo[kh] + xo[kw]: the act1 swizzle splits into a row bit and a
-          // column bit
-          int yo[4], xo[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int y = 2 * y2 + j, x = 2 * x2 + j;
-            yo[j] = y * 1280 + ((((kq >> 1) ^ (y >> 1)) & 1) << 5);
-            xo[j] = ((x ^ ((x >> 2) & 1)) << 6) + ((((kq & 1) ^ (x >> 1)) & 1) << 4);
-          }
-          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-          bf16x8 rh[D2], rl[D2];
-          auto ld = [&](int s, bf16x8& hh, bf16x8& ll) {
-            const int o = yo[s >> 2] + xo[s & 3];
-            hh = *(const bf16x8*)(a1h + o);
-            ll = *(const bf16x8*)(a1l + o);
-          };
-#pragma unroll
-          for (int s = 0; s < D2; ++s) ld(s, rh[s], rl[s]);
-#pragma unroll
-          for (int s = 0; s < 16; ++s) {
-            const bf16x8 hh = rh[s % D2], ll = rl[s % D2];
-            if (s + D2 < 16) ld(s + D2, rh[s % D2], rl[s % D2]);
-            __builtin_amdgcn_sched_barrier(0);
-            acc = mfma16_x3(w2h[s], w2l[s], hh, ll, acc);
-          }
-          if (ok) {
-            bf16x4 vh, vl;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float v = fmaxf(acc[e] + b2v[e], 0.f);
-              vh[e] = (bf16)v;
-              vl[e] = sp_lo(v);
-            }
-            const int o = a2v3_off(y2, x2, chc >> 3) + 8 * (kq & 1);
-            *(bf16x4*)(a2h + o) = vh;
-            *(bf16x4*)(a2l + o) = vl;
-            if (s2) {
-              const size_t g = (size_t)(y2 * 9 + x2) * 32 + chc;
-              *(bf16x4*)(s2 + g) = vh;
-              *(bf16x4*)(s2l + g) = vl;
-            }
-          }
-          if (tt == 0) issue(0);
-          else if (tt == 1) issue(1);
-          else issue(2);
-        }
-      }
-      TS3_STAMP(i, 2);
-      lds_sync();
-      TS3_STAMP(i, 3);
-    }
-    drain(nf - 1);   // the last frame's outputs (staged in iteration nf + 1)
-  }
-#undef TS3_STAMP
-}
-
 static int g_tsp_dbg = 0;
 static long long* g_tsp_trace = nullptr;
 // v2 phase clock stamps of workgroup 0: [wave][frame < 16][5] (loop top, phase A done, barrier,
@@ -1236,12 +490,6 @@ extern "C" int r2_torso_sp_debug(int bits) { g_tsp_dbg = bits; return 0; }
 extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs, int njobs,
                                      int grid, void* stream) {
   if (njobs < 1 || njobs > TS_MAX_JOBS) return -1;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute((const void*)torso_fwd_sp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        tsp::LDS_BYTES);
-    attr_set = true;
-  }
   TSArgs a{};
   a.frames = frames;
   a.dbg = g_tsp_dbg;
@@ -1275,35 +523,14 @@ extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs,
   }
   if (wb > nw) return -3;
   if (grid > wb) grid = wb;
-  if (a.dbg & 8) {   // v1 (A/B timing)
-    hipLaunchKernelGGL(torso_fwd_sp_kernel, dim3(grid), dim3(tsp::NT), tsp::LDS_BYTES,
-                       (hipStream_t)stream, a);
-  } else {
-    static bool attr2 = false;
-    if (!attr2) {
-      hipFuncSetAttribute((const void*)torso_fwd_sp2_kernel<false>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, tsp2::LDS_BYTES);
-      hipFuncSetAttribute((const void*)torso_fwd_sp2_kernel<true>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, tsp2::LDS_BYTES_I8);
-      attr2 = true;
-    }
-    if (a.dbg & 128)   // bf16 split conv1 (the previous v2 path)
-      hipLaunchKernelGGL(torso_fwd_sp2_kernel<false>, dim3(grid), dim3(tsp::NT), tsp2::LDS_BYTES,
-                         (hipStream_t)stream, a);
-    else if (!(a.dbg & 256))   // v2 (int8 conv1, two phases per frame)
-      hipLaunchKernelGGL(torso_fwd_sp2_kernel<true>, dim3(grid), dim3(tsp::NT), tsp2::LDS_BYTES_I8,
-                         (hipStream_t)stream, a);
-    else {   // v3 (2-deep operand rings: 3- / 4-deep measured no faster)
-      static bool attr3 = false;
-      if (!attr3) {
-        hipFuncSetAttribute((const void*)torso_fwd_sp3_kernel<2, 2>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, tsp3::LDS_BYTES);
-        attr3 = true;
-      }
-      hipLaunchKernelGGL((torso_fwd_sp3_kernel<2, 2>), dim3(grid), dim3(tsp::NT), tsp3::LDS_BYTES,
-                         (hipStream_t)stream, a);
-    }
+  static bool attr2 = false;
+  if (!attr2) {
+    hipFuncSetAttribute((const void*)torso_fwd_sp2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        tsp2::LDS_BYTES_I8);
+    attr2 = true;
   }
+  hipLaunchKernelGGL(torso_fwd_sp2_kernel, dim3(grid), dim3(tsp::NT), tsp2::LDS_BYTES_I8,
+                     (hipStream_t)stream, a);
   R2_CHECK_LAUNCH();
   return 0;
 }

@@ -145,6 +145,16 @@ class LearnerConfig:
     # mode (torch.backends.cudnn.benchmark) instead of its immediate-mode heuristics
     conv_autotune: bool = True
     use_graph: bool = True            # capture the whole step in a HIP graph
+    # split precision: the BPTT computes its input gradient dh = dz . W1 itself, inside its
+    # hand-off waits (lstm_persist.hip PTBArgs::dz), instead of the TD launch (td_fuse_dh)
+    bptt_dh: bool = False
+    # split precision: the post-BPTT GEMMs (dW_ih, dW_hh, dW_head1, dX) run on the BPTT launch's
+    # idle workgroups, each K tile as soon as its dgates rows are stored (lstm_persist.hip
+    # g2s_tile_acc helpers), instead of one grouped launch after the BPTT
+    bptt_gemms: bool = False
+    # single-rank step: the weight repack after the optimizer (pack_step) runs on extra
+    # workgroups of the priority tail's launch (replay.hip r2_prio_tail_pack): one launch fewer
+    fuse_pack_tail: bool = True
     save_dir: str = "save"
     # ablation (tools/learn_check.py): ignore the stored recurrent state of every sampled
     # sequence (zeros instead of the actor's (h, c)); with burn_in = 0 the learner has no context

@@ -23,8 +23,9 @@ priority scatters.  Here a step is:
     update    fused centered RMSprop (or Adam) over the flat master buffer, one pack launch
               producing every bf16 kernel layout, target sync as a device-side
               `copy_if_due` (graph-safe)
-    priority  eta-mix refresh of every overlapping sequence, tree repair in two launches (upper
-              levels and the step counter folded into the second)
+    priority  eta-mix refresh of every overlapping sequence + repair of every dirty sum-tree level
+              + the step counter in ONE launch (replay.hip prio_tail_kernel, grid barriers between
+              the levels; the 3-launch form when the grid cannot be resident)
 
 No host synchronisation happens inside a step, so the whole step (minus collectives) is
 captured once into a HIP graph and replayed.
@@ -351,17 +352,32 @@ class LearnerEngine:
             check(k.r2_gather_f32(ptr(self.target), ptr(self.f_index), ptr(self.f32_t), L.f_numel, s), "gather_t")
             torch.add(self.pk_t["b_ih"], self.pk_t["b_hh"], out=self.lstm_b_t)
 
-    def _pack_step(self, interval: int, s, rows_done: bool = False):
-        """rows_done: the optimizer already wrote the row packs and the target master
-        (optim.hip rmsprop_pack_kernel): gather only the packs before layout.bf_rows_begin."""
+    def _pack_args(self, interval: int, rows_done: bool):
+        """r2_pack_step's arguments from the master pointer to lo_off, the step counter excluded
+        (the fused tail takes the counter from its own arguments)."""
         L = self.layout
         n_master, n_bf = (0, L.bf_rows_begin) if rows_done else (L.padded, L.bf_numel)
-        check(kernels().r2_pack_step(ptr(self.master), ptr(self.target), n_master, ptr(self.bf_index),
-                                     ptr(self.bf), ptr(self.bf_t), n_bf, ptr(self.f_index),
-                                     ptr(self.f32), ptr(self.f32_t), L.f_numel,
-                                     L.f_offsets["b_ih"][0], L.f_offsets["b_hh"][0],
-                                     ptr(self.lstm_b), ptr(self.lstm_b_t), L.G, ptr(self.replay.step),
-                                     interval, L.bf_numel if self.sp else 0, s), "pack_step")
+        return (ptr(self.master), ptr(self.target), n_master, ptr(self.bf_index), ptr(self.bf),
+                ptr(self.bf_t), n_bf, ptr(self.f_index), ptr(self.f32), ptr(self.f32_t), L.f_numel,
+                L.f_offsets["b_ih"][0], L.f_offsets["b_hh"][0], ptr(self.lstm_b), ptr(self.lstm_b_t),
+                L.G), (interval, L.bf_numel if self.sp else 0)
+
+    def _pack_step(self, interval: int, s, rows_done: bool = False):
+        """rows_done: the optimizer already wrote the row packs and the target master
+        (optim.hip rmsprop_pack_kernel): gather only the packs before layout.bf_rows_begin.
+        With ``learner.fuse_pack_tail`` on the single-rank step the gather is deferred to the
+        priority tail's launch instead (``_priorities``)."""
+        if self._fuse_pack_tail() and rows_done:
+            self._pack_deferred = (interval, rows_done)
+            return
+        head, tail = self._pack_args(interval, rows_done)
+        check(kernels().r2_pack_step(*head, ptr(self.replay.step), *tail, s), "pack_step")
+
+    def _fuse_pack_tail(self) -> bool:
+        """The weight repack rides on the priority tail's launch (replay.hip r2_prio_tail_pack):
+        single-rank step (the DP step runs the tail before the update), fused tail, GPU."""
+        return (self.cfg.learner.fuse_pack_tail and not self.dp and self.device.type == "cuda"
+                and self.cfg.replay.fused_prio_tail)
 
     def state_dict(self):
         return self.layout.state_dict(self.master)
@@ -671,8 +687,9 @@ class LearnerEngine:
         self._duel_done = False
         self._dh_done = False
         if lc.td_fuse_head_bwd:
-            # + dh = dz @ W1 for the BPTT, on the same launch's MFMAs (16 rows per workgroup)
-            fuse_dh = lc.td_fuse_dh and L.H == 256
+            # + dh = dz @ W1 for the BPTT, on the same launch's MFMAs (16 rows per workgroup) --
+            # unless the BPTT computes it itself (learner.bptt_dh, _dh_in_bptt)
+            fuse_dh = lc.td_fuse_dh and L.H == 256 and not self._dh_in_bptt()
             w1t = ptr(pk["head1T"]) if fuse_dh else 0
             w1t_lo = ptr(self.pk_lo["head1T"]) if fuse_dh and self.sp else 0
             if fuse_fwd:
@@ -687,7 +704,7 @@ class LearnerEngine:
                                   ptr(self.dh) if fuse_dh else 0, L.H, s)
             if rc_ == 0:
                 self._duel_done = True
-                self._dh_done = fuse_dh
+                self._dh_done = fuse_dh or self._dh_in_bptt()
                 return
             if fuse_fwd:   # refused on the host before any launch: separate dueling forward
                 k.r2_td_duel_fwd_set(None)
@@ -696,6 +713,14 @@ class LearnerEngine:
             if self.sp:
                 check(rc_, "td_duel")
         check(k.r2_td_loss(*targs, dp, s), "td_loss")
+
+    def _dh_in_bptt(self) -> bool:
+        """Split precision, hidden 256, head width 256: the BPTT computes its input gradient dh =
+        dz . W1 itself (lstm_persist.hip PTBArgs::dz, 12 MFMAs per wave inside each hand-off wait)
+        instead of the TD launch streaming all of W1^T through each of its workgroups."""
+        lc, L = self.cfg.learner, self.layout
+        return bool(self.sp and lc.bptt_dh and lc.td_fuse_head_bwd and L.H == 256 and 2 * L.HD == 512
+                    and lc.lstm_tag_words and self.device.type == "cuda")
 
     def _backward_core_sp(self):
         """Split-precision backward core: head gradients, dh GEMM, BPTT, weight-gradient + dX
@@ -727,13 +752,67 @@ class LearnerEngine:
                 ptr(pkl["w_hhT"]), ptr(self.dgates), ptr(self.dgates_lo), B, T, Lb, H, ptr(self.ctr),
                 ptr(self.err), ptr(self.ring_b), ptr(self.bias_ws), ptr(self.gate_perm_i32),
                 ptr(L.view(g, "lstm.bias_ih")), ptr(L.view(g, "lstm.bias_hh"))]
-        if side_hg:
-            rc = k.r2_lstm_bwd_tag_sp_hg(*bptt, *hg, s)   # >= 0: bit 0 = head grads done here
-            check(min(rc, 0), "lstm_bwd_tag_sp_hg")
-            if not rc & 1:
-                check(k.r2_head_grads_sp(*hg, s), "head_grads_sp")
+        # the post-BPTT GEMMs (weight gradients + dX) as helper workgroups of the BPTT launch
+        # (learner.bptt_gemms): built before the launch
+        w_jobs, x_job = self._post_bptt_jobs()
+        in_bptt = self._gemms_in_bptt()
+        dz_on = self._dh_in_bptt() and self._duel_done
+
+        def launch(with_gemms: bool) -> int:
+            if dz_on:
+                check(k.r2_lstm_bwd_set_dz(ptr(self.dz), ptr(self.dz_lo), ptr(pk["head1T"]),
+                                           ptr(pkl["head1T"]), 2 * HD), "lstm_bwd_set_dz")
+            if with_gemms:
+                # [dW_ih, dW_hh, dW_head1] (bits 0, 1: read the BPTT's dgates), then dX
+                self._bptt_gemm_descs = np.asarray(
+                    [v for g_ in (w_jobs[2], w_jobs[1], w_jobs[0], x_job) for v in g_.desc()],
+                    dtype=np.int64)
+                k.r2_lstm_bwd_set_gemms(self._bptt_gemm_descs.ctypes.data, 3, 0b011, 1)
+            if side_hg:
+                return k.r2_lstm_bwd_tag_sp_hg(*bptt, *hg, s)   # >= 0: bit 0 = head grads done here
+            return k.r2_lstm_bwd_tag_sp(*bptt, s)
+
+        rc = launch(in_bptt)
+        if in_bptt and rc < 0:      # the helpers' shape rules refused: BPTT alone + the group
+            k.r2_lstm_bwd_set_gemms(None, 0, 0, 0)
+            in_bptt = False
+            rc = launch(False)
+        check(min(rc, 0), "lstm_bwd_tag_sp")
+        if side_hg and not rc & 1:
+            check(k.r2_head_grads_sp(*hg, s), "head_grads_sp")
+        if in_bptt:
+            self._dX = self.dX
+            return
+        if self.cfg.learner.sp_gemm == "fused":
+            sg = self.cfg.learner.sp_group_splits
+            splits = (self._auto_group_splits([w_jobs[2], w_jobs[1], w_jobs[0], x_job]) if sg == "auto"
+                      else [int(v) for v in sg.replace(":", ",").split(",")])
+            self._gemm_sp("group", [w_jobs[2], w_jobs[1], w_jobs[0], x_job], splits,
+                          cfg=-1)
+            self._dX = self.dX
+            return
+        splits = self._group_splits(w_jobs, x_job)
+        if splits:
+            gemm_group([w_jobs[2], w_jobs[1], w_jobs[0], x_job], splits, self.gg_ws, self.gg_tickets)
         else:
-            check(k.r2_lstm_bwd_tag_sp(*bptt, s), "lstm_bwd_tag_sp")
+            gemm(w_jobs[2], w_jobs[1], w_jobs[0])
+            gemm(x_job)
+        self._dX = self.dX
+
+    def _gemms_in_bptt(self) -> bool:
+        """Split precision: the weight-gradient and dX GEMMs run on the BPTT launch's idle
+        workgroups (lstm_persist.hip g2s_tile_acc helpers), each K tile as soon as the BPTT has
+        stored its dgates rows, instead of one grouped launch after it (learner.bptt_gemms)."""
+        lc = self.cfg.learner
+        return bool(self.sp and lc.bptt_gemms and lc.sp_gemm == "fused" and self.device.type == "cuda")
+
+    def _post_bptt_jobs(self):
+        """The post-BPTT GEMMs of the split-precision step: [dW_head1, dW_hh, dW_ih], dX."""
+        B, T, Lb, Ll = self.B, self.T, self.Lb, self.Ll
+        L, pk, pkl = self.layout, self.pk, self.pk_lo
+        H, HD = L.H, L.HD
+        N = Ll * B
+        g = self.grad
         hs, hl = self.hseq["on"], self.hseq_lo["on"]
         h_learn, h_learn_l = hs[Lb:T].reshape(N, H), hl[Lb:T].reshape(N, H)
         if Lb >= 1:
@@ -757,21 +836,7 @@ class LearnerEngine:
                   Gemm(dgT, X, L.view(g, "lstm.weight_ih"), crow=self.gate_perm_i32, a_lo=dgTl, b_lo=Xl)]
         x_job = Gemm(self.dgates, pk["w_ih"], self.dX, a_lo=self.dgates_lo, b_lo=pkl["w_ih"],
                      c_lo=self.dX_lo)
-        if self.cfg.learner.sp_gemm == "fused":
-            sg = self.cfg.learner.sp_group_splits
-            splits = (self._auto_group_splits([w_jobs[2], w_jobs[1], w_jobs[0], x_job]) if sg == "auto"
-                      else [int(v) for v in sg.replace(":", ",").split(",")])
-            self._gemm_sp("group", [w_jobs[2], w_jobs[1], w_jobs[0], x_job], splits,
-                          cfg=-1)
-            self._dX = self.dX
-            return
-        splits = self._group_splits(w_jobs, x_job)
-        if splits:
-            gemm_group([w_jobs[2], w_jobs[1], w_jobs[0], x_job], splits, self.gg_ws, self.gg_tickets)
-        else:
-            gemm(w_jobs[2], w_jobs[1], w_jobs[0])
-            gemm(x_job)
-        self._dX = self.dX
+        return w_jobs, x_job
 
     def _auto_group_splits(self, probs):
         """K splits of the post-BPTT group [dW_head1, dW_hh, dW_ih, dX] on 256 x 256 tiles: the
@@ -1050,6 +1115,14 @@ class LearnerEngine:
 
     def _priorities(self, end: bool = True):
         rp = self.replay
+        deferred = getattr(self, "_pack_deferred", None)
+        self._pack_deferred = None
+        if deferred is not None:
+            head, tail = self._pack_args(*deferred)
+            if end and rp.prio_tail(self.starts, self.B, self.Lb, self.T, end, pack=head + tail):
+                return
+            # refused (shape): the repack as its own launch, then the separate tail
+            check(kernels().r2_pack_step(*head, ptr(rp.step), *tail, stream_handle()), "pack_step")
         if self.cfg.replay.fused_prio_tail and rp.prio_tail(self.starts, self.B, self.Lb, self.T, end):
             return
         rp.refresh_sequences(self.starts, self.B, self.Lb, self.T)

@@ -192,7 +192,7 @@ class HBMReplay:
         return True
 
     def prio_tail(self, starts: torch.Tensor, B: int, upd_lo: int, upd_hi: int,
-                  end_step: bool = True, stream=None) -> bool:
+                  end_step: bool = True, stream=None, pack=None) -> bool:
         """The learner's priority tail in ONE launch (replay.hip prio_tail_kernel): sequence
         priorities of the sampled windows, tree repair of every dirty leaf (grid barriers between
         the levels, the upper levels by the last-arriving workgroup) and, with ``end_step``, the
@@ -201,12 +201,19 @@ class HBMReplay:
         if self.tree.device.type != "cuda":
             return False
         rc = self.cfg.replay
-        r = kernels().r2_prio_tail(
-            ptr(starts), B, ptr(self.is_start), ptr(self.priority), ptr(self.tree),
-            self.tree_offs.ctypes.data, self.tree_sizes.ctypes.data, self.tree_levels, rc.seq_len,
-            upd_lo, upd_hi, self.cap_e, float(rc.eta), ptr(self.dirty), ptr(self.dirty_count),
-            self.max_dirty, ptr(self.prio_sync), ptr(self.step) if end_step else 0,
-            1 if end_step else 0, self._ts(stream))
+        args = (ptr(starts), B, ptr(self.is_start), ptr(self.priority), ptr(self.tree),
+                self.tree_offs.ctypes.data, self.tree_sizes.ctypes.data, self.tree_levels, rc.seq_len,
+                upd_lo, upd_hi, self.cap_e, float(rc.eta), ptr(self.dirty), ptr(self.dirty_count),
+                self.max_dirty, ptr(self.prio_sync), ptr(self.step) if end_step else 0,
+                1 if end_step else 0)
+        if pack is not None:
+            # + the step's weight repack on extra workgroups (replay.hip r2_prio_tail_pack):
+            # ``pack`` = the r2_pack_step arguments between ``step`` and the stream
+            if not end_step:
+                raise ValueError("prio_tail(pack=...) must end the step")
+            r = kernels().r2_prio_tail_pack(*args, *pack, self._ts(stream))
+        else:
+            r = kernels().r2_prio_tail(*args, self._ts(stream))
         if r in (-3, -4):    # shape, or more workgroups than can be resident at once
             return False
         check(r, "prio_tail")

@@ -103,6 +103,10 @@ _SIGS = {
     "r2_lstm_bwd_handoff8": [I],
     "r2_td_duel_fwd_set": [P],
     "r2_prio_tail": [P, I, P, P, P, P, P, I, I, I, I, I, F, P, P, I, P, P, I, P],
+    "r2_lstm_bwd_set_dz": [P, P, P, P, I],
+    "r2_lstm_bwd_set_gemms": [P, I, I, I],
+    "r2_prio_tail_pack": [P, I, P, P, P, P, P, I, I, I, I, I, F, P, P, I, P, P, I,
+                          P, P, I64, P, P, P, I64, P, P, P, I64, I64, I64, P, P, I64, I64, I64, P],
     "r2_td_duel_set_trace": [P],
     "r2_lstm_persist_force_slow": [I],
     "r2_xcc_probe": [P, I, I, I, P],

@@ -77,38 +77,10 @@ if which in ("torso", "both"):
     n_cus = torch.cuda.get_device_properties(0).multi_processor_count
     res["torso_fwd_sp_us_10560"] = timeit(lambda: k.r2_torso_fwd_sp_multi(
         ptr(frames), jobs.ctypes.data, 4, n_cus, stream_handle()))
-    if "ab" in sys.argv:
-        # v3 (debug bit 8) vs v2 (int8 conv1), interleaved, min of the per-round means
-        best = {}
-        for _ in range(5):
-            for bits, name in ((256, "v3"), (256 | 1024, "v3_no_out3"), (256 | 2048, "v3_no_frame_loads"),
-                               (256 | 4096, "v3_no_conv1"), (256 | 8192, "v3_no_conv2"),
-                               (256 | 16384, "v3_no_conv3"), (256 | 4096 | 8192, "v3_no_conv12"), (0, "v2")):
-                k.r2_torso_sp_debug(bits)
-                t = timeit(lambda: k.r2_torso_fwd_sp_multi(ptr(frames), jobs.ctypes.data, 4, n_cus,
-                                                           stream_handle()))
-                best[name] = min(best.get(name, 1e30), t)
-        k.r2_torso_sp_debug(0)
-        res.update({f"torso_{k_}_us": round(v, 1) for k_, v in best.items()})
-    if "probe3" in sys.argv:
-        # v3 per-wave clock stamps of workgroup 0: [wave][iteration][loop top, conv3 / staging done,
-        # conv1 / conv2 done, after the barrier]; mean cycles per segment over iterations 3..12
-        tr = torch.zeros(8 * 16 * 24, dtype=torch.int64, device=DEV)
-        k.r2_torso_sp_trace(ptr(tr))
-        k.r2_torso_sp_debug(256 | int(os.environ.get("SP3_DBG", "0")))
-        k.r2_torso_fwd_sp_multi(ptr(frames), jobs.ctypes.data, 4, n_cus, stream_handle())
-        torch.cuda.synchronize()
-        k.r2_torso_sp_debug(0)
-        k.r2_torso_sp_trace(0)
-        t = tr.view(8, 16, 24).cpu().double()
-        res["v3_conv1_tile_stamps_wave4_it5"] = (t[4, 5, 4:18] - t[4, 5, 1]).tolist()
-        seg = {"a": t[:, 3:13, 1] - t[:, 3:13, 0], "b": t[:, 3:13, 2] - t[:, 3:13, 1],
-               "wait": t[:, 3:13, 3] - t[:, 3:13, 2], "iter": t[:, 4:14, 0] - t[:, 3:13, 0]}
-        res["v3_segments_cycles_per_wave"] = {n: [round(v, 0) for v in x.mean(1).tolist()] for n, x in seg.items()}
     if "probe" in sys.argv:
         # phase costs: skip conv1 / conv2 / conv3 (timing only) etc.; variants interleaved over 7
         # rounds, min of the per-round means (single back-to-back timings drift by +-15 %)
-        variants = ((0, "full"), (128, "bf16_conv1"), (8, "v1"), (1, "no_conv1"), (2, "no_conv2"), (4, "no_conv3"),
+        variants = ((0, "full"), (1, "no_conv1"), (2, "no_conv2"), (4, "no_conv3"),
                     (7, "none"), (16, "no_frame"), (64, "no_save"), (119, "nothing"))
         best = {}
         for _ in range(7):
