@@ -1183,6 +1183,12 @@ struct PTBArgs {
   const bf16* dz_lo;
   const bf16* w1t;
   const bf16* w1t_lo;
+  // per-role clock stamps (r2_lstm_persist_set_debug, probes only): s_memrealtime ticks (100 MHz,
+  // one clock for every CU), 8 words per workgroup: [0] start, [1] end of its work, [2] role (1
+  // recurrence, 2 helper), [3] ticks spent waiting for dgates rows (helpers), [4] dX tiles done,
+  // [5] end of the weight-gradient tile / head-gradient job (helpers); from word 2048: iteration
+  // start stamps of recurrence workgroup (0, 0)
+  long long* dbg;
 };
 #define PT_DZ_K 512                                   // dz row length (2 x head hidden 256)
 #define PT_DZ_SLOT (2 * PT_ROWS * PT_DZ_K * 2)        // one ring slot: 16 rows x 512 x hi/lo = 32 KB
@@ -1215,28 +1221,40 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   int mb, j;
   const int B = a.B, T = a.T, t0 = a.t0, K = T - t0;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  long long* const stamp = a.dbg ? a.dbg + 8 * blockIdx.x : nullptr;
+  if (stamp && tid == 0) stamp[0] = (long long)__builtin_amdgcn_s_memrealtime();
   if (!pl_decode(a.xcd_map, a.MB, NWG, mb, j)) {
     // ================= helper workgroup (4 waves): work beside the recurrence
     if (wave == 4) return;                 // helpers run 256 threads (barriers: surviving waves)
+    long long waited_ticks = 0;
+    int dx_tiles = 0;
     const int b = blockIdx.x, g = b & 7, jj = b >> 3;
     const int h = b - (min(jj, NWG) * a.MB + (jj < NWG ? min(g, a.MB) : 0));   // helper ordinal
     const int nh = (int)gridDim.x - a.MB * NWG;
     const unsigned nbptt = (unsigned)(a.MB * NWG);
     // rows [row_lo, row_hi) (time-major: row = tl * B + b) are stored once BPTT iterations
     // K-1-tl are complete on every recurrence workgroup, for every tl they touch
+    // One lane polls, the workgroup's other waves wait at a barrier: 192 helpers x 4 waves
+    // polling the iteration counters themselves slowed the recurrence's hand-offs 1.8x
+    // (tools/bptt_roles_probe.py).  Called uniformly by all 4 waves.
     auto wait_rows = [&](int row_lo, int row_hi) {
+      const long long w0 = stamp ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
       const int tl_hi = (min(row_hi, K * B) - 1) / B;
-      for (int tl = row_lo / B; tl <= tl_hi; ++tl) {
-        unsigned* w = a.ctr + PT_ITER_OFF + (K - 1 - tl);
-        unsigned spins = 0;
-        while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nbptt) {
-          __builtin_amdgcn_s_sleep(2);
-          if (++spins > PL_SPIN_LIMIT) {
-            __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
+      if (tid == 0) {
+        for (int tl = row_lo / B; tl <= tl_hi; ++tl) {
+          unsigned* w = a.ctr + PT_ITER_OFF + (K - 1 - tl);
+          unsigned spins = 0;
+          while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nbptt) {
+            __builtin_amdgcn_s_sleep(8);
+            if (++spins > PL_SPIN_LIMIT) {
+              __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
           }
         }
       }
+      __builtin_amdgcn_s_barrier();
+      if (stamp) waited_ticks += (long long)__builtin_amdgcn_s_memrealtime() - w0;
     };
     if (SP) {
       // split precision (PTBArgs::gw / gx with hi / lo planes): helpers 0 .. n_wtiles-1 own one
@@ -1259,12 +1277,14 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
         g2s_tile_acc<false, false, 16, 0, 3>(P, tm, tn, pt_dyn, 0, P.K / 32, true,
                                              [&](int kt) { if (wt) wait_rows(32 * kt, 32 * kt + 32); }, acc);
         g2_epilogue_lds(P, tm * 128, tn * 128, wm, wn, lane, acc, pt_dyn);
+        if (stamp && tid == 0) stamp[5] = (long long)__builtin_amdgcn_s_memrealtime();
       } else if (a.hg_on) {   // the head-gradient reduction first (independent of the BPTT)
         const int hx = h - a.n_wtiles, nx = nh - a.n_wtiles;
         const int cbn = (2 * a.hg.HD + 63) / 64;
         for (int it = hx; it < cbn * a.hg.RS * a.hg.NP; it += nx)
           head_grads_body(a.hg, it % cbn, (it / cbn) % a.hg.RS, it / (cbn * a.hg.RS));
       }
+      if (stamp && tid == 0) stamp[5] = (long long)__builtin_amdgcn_s_memrealtime();
       if (a.gx_on) {
         const GemmProb& P = a.gx;
         const int tmn = (P.M + 127) / 128, total = tmn * P.tiles_n;
@@ -1283,6 +1303,7 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
             if (!waited) { wait_rows(128 * tm, 128 * tm + 128); waited = true; }
           }, acc);
           g2_epilogue_lds(P, tm * 128, tn * 128, wm, wn, lane, acc, pt_dyn);
+          ++dx_tiles;
         }
       }
     } else if (h < a.n_wtiles) {
@@ -1315,6 +1336,12 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
                                    [&](int) { wait_rows(128 * tm, 128 * tm + 128); });
         }
       }
+    }
+    if (stamp && tid == 0) {
+      stamp[1] = (long long)__builtin_amdgcn_s_memrealtime();
+      stamp[2] = 2;
+      stamp[3] = waited_ticks;
+      stamp[4] = dx_tiles;
     }
     if (tid == 0) flag = pt_finish(a.ctr, a.MB, (int)gridDim.x, PT_EPOCH_BWD, K) ? 1 : 0;
     __syncthreads();
@@ -1500,8 +1527,10 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
     dz_product(0);
   }
 
+  const bool itrace = a.dbg && mb == 0 && j == 0 && tid == 0;
   for (int k = 0; k < K; ++k) {
     const int t = T - 1 - k;
+    if (itrace && k < 512) a.dbg[2048 + k] = (long long)__builtin_amdgcn_s_memrealtime();
     if (T4 && k > 0) {
       const unsigned want = ((ep & 1u) << 3) | ((unsigned)k & 7u);
       const int slot = (k - 1) & 1;
@@ -1683,6 +1712,10 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     lds_sync();                           // barrier E
+    if (stamp && tid == 0) {
+      stamp[1] = (long long)__builtin_amdgcn_s_memrealtime();
+      stamp[2] = 1;
+    }
   }
   // ---- every wave (compute and I/O): done ticket; the last workgroup sums the bias partials in
   // tile order and clears the counters
@@ -1775,6 +1808,7 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
                             hg_HD, 8, (hg_A + 6) / 7, g_bwd_hg_zr32, g_bwd_hg_dz_lo},
                0};
   args.n_gw = 0; args.gw_wait = 0; args.gx_on = 0; args.n_wtiles = 0;
+  args.dbg = g_pl_dbg;
   int taken = 0, nh = 0;
   if (hg_dva || n_gw > 0 || gx_on) {
     // helpers: every block of the 8 x 32 grid outside the recurrence's groups

@@ -148,10 +148,13 @@ class LearnerConfig:
     # split precision: the BPTT computes its input gradient dh = dz . W1 itself, inside its
     # hand-off waits (lstm_persist.hip PTBArgs::dz), instead of the TD launch (td_fuse_dh)
     bptt_dh: bool = False
-    # split precision: the post-BPTT GEMMs (dW_ih, dW_hh, dW_head1, dX) run on the BPTT launch's
-    # idle workgroups, each K tile as soon as its dgates rows are stored (lstm_persist.hip
-    # g2s_tile_acc helpers), instead of one grouped launch after the BPTT
-    bptt_gemms: bool = False
+    # split precision: post-BPTT GEMMs on the BPTT launch's idle workgroups (lstm_persist.hip
+    # g2s_tile_acc helpers), each tile as soon as the BPTT has stored the dgates rows it reads:
+    # "off" (one grouped launch after the BPTT) | "dx" (dX there, the weight gradients after) |
+    # "all" (dW_ih, dW_hh, dW_head1 and dX there)
+    bptt_gemms: str = "off"
+    # K splits of the weight-gradient group when dX ran on the BPTT's helpers (bptt_gemms = dx)
+    sp_wgrad_splits: int = 7
     # single-rank step: the weight repack after the optimizer (pack_step) runs on extra
     # workgroups of the priority tail's launch (replay.hip r2_prio_tail_pack): one launch fewer
     fuse_pack_tail: bool = True

@@ -755,19 +755,21 @@ class LearnerEngine:
         # the post-BPTT GEMMs (weight gradients + dX) as helper workgroups of the BPTT launch
         # (learner.bptt_gemms): built before the launch
         w_jobs, x_job = self._post_bptt_jobs()
-        in_bptt = self._gemms_in_bptt()
+        in_bptt = self._gemms_in_bptt()      # "" | "dx" | "all"
         dz_on = self._dh_in_bptt() and self._duel_done
 
-        def launch(with_gemms: bool) -> int:
+        def launch(with_gemms: str) -> int:
             if dz_on:
                 check(k.r2_lstm_bwd_set_dz(ptr(self.dz), ptr(self.dz_lo), ptr(pk["head1T"]),
                                            ptr(pkl["head1T"]), 2 * HD), "lstm_bwd_set_dz")
             if with_gemms:
-                # [dW_ih, dW_hh, dW_head1] (bits 0, 1: read the BPTT's dgates), then dX
-                self._bptt_gemm_descs = np.asarray(
-                    [v for g_ in (w_jobs[2], w_jobs[1], w_jobs[0], x_job) for v in g_.desc()],
-                    dtype=np.int64)
-                k.r2_lstm_bwd_set_gemms(self._bptt_gemm_descs.ctypes.data, 3, 0b011, 1)
+                # all: [dW_ih, dW_hh, dW_head1] (bits 0, 1: read the BPTT's dgates), then dX;
+                # dx: dX only
+                wj = (w_jobs[2], w_jobs[1], w_jobs[0]) if with_gemms == "all" else ()
+                self._bptt_gemm_descs = np.asarray([v for g_ in (*wj, x_job) for v in g_.desc()],
+                                                   dtype=np.int64)
+                k.r2_lstm_bwd_set_gemms(self._bptt_gemm_descs.ctypes.data, len(wj),
+                                        0b011 if wj else 0, 1)
             if side_hg:
                 return k.r2_lstm_bwd_tag_sp_hg(*bptt, *hg, s)   # >= 0: bit 0 = head grads done here
             return k.r2_lstm_bwd_tag_sp(*bptt, s)
@@ -775,21 +777,20 @@ class LearnerEngine:
         rc = launch(in_bptt)
         if in_bptt and rc < 0:      # the helpers' shape rules refused: BPTT alone + the group
             k.r2_lstm_bwd_set_gemms(None, 0, 0, 0)
-            in_bptt = False
-            rc = launch(False)
+            in_bptt = ""
+            rc = launch("")
         check(min(rc, 0), "lstm_bwd_tag_sp")
         if side_hg and not rc & 1:
             check(k.r2_head_grads_sp(*hg, s), "head_grads_sp")
-        if in_bptt:
-            self._dX = self.dX
+        self._dX = self.dX
+        if in_bptt == "all":
             return
         if self.cfg.learner.sp_gemm == "fused":
+            probs = [w_jobs[2], w_jobs[1], w_jobs[0]] + ([] if in_bptt else [x_job])
             sg = self.cfg.learner.sp_group_splits
-            splits = (self._auto_group_splits([w_jobs[2], w_jobs[1], w_jobs[0], x_job]) if sg == "auto"
-                      else [int(v) for v in sg.replace(":", ",").split(",")])
-            self._gemm_sp("group", [w_jobs[2], w_jobs[1], w_jobs[0], x_job], splits,
-                          cfg=-1)
-            self._dX = self.dX
+            splits = (self._auto_group_splits(probs) if sg == "auto"
+                      else [int(v) for v in sg.replace(":", ",").split(",")][: len(probs)])
+            self._gemm_sp("group", probs, splits, cfg=-1)
             return
         splits = self._group_splits(w_jobs, x_job)
         if splits:
@@ -797,14 +798,17 @@ class LearnerEngine:
         else:
             gemm(w_jobs[2], w_jobs[1], w_jobs[0])
             gemm(x_job)
-        self._dX = self.dX
 
-    def _gemms_in_bptt(self) -> bool:
-        """Split precision: the weight-gradient and dX GEMMs run on the BPTT launch's idle
-        workgroups (lstm_persist.hip g2s_tile_acc helpers), each K tile as soon as the BPTT has
-        stored its dgates rows, instead of one grouped launch after it (learner.bptt_gemms)."""
+    def _gemms_in_bptt(self) -> str:
+        """Split precision: which post-BPTT GEMMs run on the BPTT launch's idle workgroups
+        (lstm_persist.hip g2s_tile_acc helpers), each tile as soon as the BPTT has stored the
+        dgates rows it reads (learner.bptt_gemms): "" (none), "dx" or "all"."""
         lc = self.cfg.learner
-        return bool(self.sp and lc.bptt_gemms and lc.sp_gemm == "fused" and self.device.type == "cuda")
+        mode = {True: "all", False: "off"}.get(lc.bptt_gemms, lc.bptt_gemms)
+        if mode not in ("off", "dx", "all"):
+            raise ValueError(f"learner.bptt_gemms: {lc.bptt_gemms!r} (off | dx | all)")
+        ok = self.sp and lc.sp_gemm == "fused" and self.device.type == "cuda"
+        return mode if ok and mode != "off" else ""
 
     def _post_bptt_jobs(self):
         """The post-BPTT GEMMs of the split-precision step: [dW_head1, dW_hh, dW_ih], dX."""
@@ -844,9 +848,14 @@ class LearnerEngine:
         config: 80), else 1 (a split's partial-tile write + reduction outweighs 1-3 K steps);
         dX (K = 4H) takes the largest of 4 / 2 ways whose items still fit one round on the CUs.
         Measured: paper 4,4,4,1 (profiles/r04_group_splits_ab.txt: 3,4,4,2 / 3,5,5,2 slower);
-        reference config 1,1,1,4 = 0.2455 ms vs 0.3038 at 4,4,4,1."""
+        reference config 1,1,1,4 = 0.2455 ms vs 0.3038 at 4,4,4,1.  Without dX (it ran on the
+        BPTT's helpers, learner.bptt_gemms = dx) the weight gradients alone split
+        learner.sp_wgrad_splits ways."""
         t = lambda g: -(-g.a.shape[0] // 256) * -(-g.b.shape[1] // 256)   # noqa: E731
         ks_w = -(-probs[0].a.shape[1] // 32)
+        if len(probs) == 3:
+            sw = self.cfg.learner.sp_wgrad_splits if ks_w >= 32 else 1
+            return [sw] * 3
         sw = 4 if ks_w >= 32 else 1
         items = sw * sum(t(g) for g in probs[:3])
         sx = next((c for c in (4, 2) if items + c * t(probs[3]) <= self.n_cus), 1)

@@ -124,9 +124,15 @@ def _oracle64(rp, eng, net, tgt, cfg, mode):
     return _oracle(rp, eng, net, tgt, cfg, mode, torch.float64)
 
 
-@pytest.mark.parametrize("mode,preset", [("fixed", "atari57"), ("shifted", "atari57"),
-                                         ("reference", "atari57"), ("fixed", "dmlab30")])
-def test_engine_fp32_matches_fp64_oracle(mode, preset):
+_FUSED = {"": {}, "dx": {"learner.bptt_gemms": "dx"},
+          "all": {"learner.bptt_dh": True, "learner.bptt_gemms": "all"}}
+
+
+@pytest.mark.parametrize("mode,preset,fused", [("fixed", "atari57", ""), ("shifted", "atari57", ""),
+                                               ("reference", "atari57", ""), ("fixed", "dmlab30", ""),
+                                               ("fixed", "atari57", "dx"), ("fixed", "atari57", "all"),
+                                               ("reference", "atari57", "all")])
+def test_engine_fp32_matches_fp64_oracle(mode, preset, fused):
     """The fp32 (split-precision) learner step against the float64 truth, with plain fp32 PyTorch
     as the yardstick.  With random-init nets the TD error is a small difference of two Q values,
     so every fp32 implementation's gradient error is amplified: fp32 PyTorch itself lands 1e-4 ..
@@ -134,7 +140,7 @@ def test_engine_fp32_matches_fp64_oracle(mode, preset):
     must be within 1e-4 of the truth or no worse than 2x fp32 PyTorch, on the loss, all 18
     gradients and the replay priorities; its forward activations are ~5e-6 off (test below).
     dmlab30 (RGB 3x72x96): the fp32 library torso (ops/torso_lib.py) feeding the split planes."""
-    cfg, rp, eng, net, tgt = _make(mode, preset=preset)
+    cfg, rp, eng, net, tgt = _make(mode, preset=preset, **_FUSED[fused])
     assert eng.sp_lib == (preset == "dmlab30")
     eng._forward_loss()
     eng._backward_core()
@@ -166,14 +172,18 @@ def test_engine_fp32_matches_fp64_oracle(mode, preset):
         assert eng.error_word() == 0 and torch.isfinite(eng.master).all()
 
 
-def test_engine_fp32_matches_fp64_oracle_at_bench_shape():
+@pytest.mark.parametrize("bptt", ["", "dx", "all"])
+def test_engine_fp32_matches_fp64_oracle_at_bench_shape(bptt):
     """The benched step itself (atari57: B=64, burn-in 40 + learn 40, n=5, fixed target) against
     the float64 truth: the 12 LSTM groups (3 chains x 4 batch tiles) placed two per XCD, the
     85-step tagged T4 hand-offs (the 4-bit tags wrap 5 times per launch), the 192x256 split GEMM
     tiles, the full-chip torso grids.  Same bounds as the reduced-shape test; then 5 replays of
-    the captured graph with the persistent kernels' error word still 0."""
+    the captured graph with the persistent kernels' error word still 0.  ``dx``: the dX GEMM runs
+    on the BPTT launch's helper workgroups (learner.bptt_gemms); ``all``: the weight-gradient GEMMs
+    too, and the BPTT computes its input gradient from dz itself (learner.bptt_dh)."""
     over = {"replay.burn_in": 40, "replay.learn": 40, "replay.overlap": 40, "replay.n_step": 5,
             "replay.capacity": 64000}
+    over.update(_FUSED[bptt])
     cfg, rp, eng, net, tgt = _make("fixed", B=64, **over)
     assert (eng.B, eng.Lb, eng.Ll, eng.n, eng.Tn) == (64, 40, 40, 5, 85)
     rp.fill_synthetic(episode_len=200, seed=5)

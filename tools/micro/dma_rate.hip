@@ -2,7 +2,8 @@
 // (164 workgroups of 256 A rows x 256 B rows, hi and lo planes, K = 1568 bf16 = 3136 B per row)
 // streamed through global_load_lds with W bytes of each row per stage (W = 32 / 64 / 128: the
 // 16- / 32- / 64-deep K tiles) and D stages in flight (counted vmcnt).  Nothing is computed; the
-// LDS destination cycles over 64 KB (the bytes are not read).  Prints per-CU GB/s.
+// LDS destination cycles over 64 KB (the bytes are not read).  Prints per-CU GB/s.  The same
+// stream through VGPRs (global_load_dwordx4 + ds_write_b128, two register stages) for comparison.
 //   hipcc --offload-arch=gfx950 -O3 tools/micro/dma_rate.hip -o /tmp/dma_rate && /tmp/dma_rate
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -48,6 +49,63 @@ __global__ __launch_bounds__(512) void k(const uint8_t* A, const uint8_t* Al, co
   vmw<0>();
 }
 
+// the same operand stream through VGPRs: global_load_dwordx4 of stage s+1 issued before the
+// ds_write_b128 of stage s (two register stages)
+template <int W>
+__global__ __launch_bounds__(512) void kr(const uint8_t* A, const uint8_t* Al, const uint8_t* B,
+                                          const uint8_t* Bl, int tiles_n) {
+  extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
+  constexpr int LPR = W / 16, RPI = 64 / LPR, PW = 128 / RPI, NST = KB / W;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+  // wave w: 128 rows of plane w / 2 ([A hi | A lo | B hi | B lo]), rows (w & 1) * 128 + ...
+  const int plane = wave >> 1;
+  const uint8_t* base = plane == 0 ? A : plane == 1 ? Al : plane == 2 ? B : Bl;
+  const int r0 = (plane < 2 ? tm * AR : tn * BR) + (wave & 1) * 128;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(base + (size_t)r0 * KB), 0, 128 * KB, 0x00020000);
+  const int voff = (lane / LPR) * KB + 16 * (lane % LPR);
+  int4 b0[PW], b1[PW];
+  auto ld = [&](int4* b, int s) {
+#pragma unroll
+    for (int i = 0; i < PW; ++i)
+      b[i] = __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + i * RPI * KB, s * W, 0));
+  };
+  auto st = [&](const int4* b, int s) {
+#pragma unroll
+    for (int i = 0; i < PW; ++i)
+      *(int4*)(lds + (((s * PW + wave * PW + i) & 63) * 1024) + lane * 16) = b[i];
+  };
+  ld(b0, 0);
+  for (int s = 0; s < NST; s += 2) {
+    if (s + 1 < NST) ld(b1, s + 1);
+    st(b0, s);
+    if (s + 2 < NST) ld(b0, s + 2);
+    if (s + 1 < NST) st(b1, s + 1);
+  }
+}
+
+template <int W>
+void runr(const uint8_t* A, const uint8_t* Al, const uint8_t* B, const uint8_t* Bl) {
+  const int tiles_n = 4, grid = 41 * 4;
+  hipFuncSetAttribute((const void*)kr<W>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((kr<W>), dim3(grid), dim3(512), 65536, 0, A, Al, B, Bl, tiles_n);
+  hipEventRecord(e0);
+  const int reps = 20;
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((kr<W>), dim3(grid), dim3(512), 65536, 0, A, Al, B, Bl, tiles_n);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms;
+  hipEventElapsedTime(&ms, e0, e1);
+  const double us = ms * 1000.0 / reps;
+  const double bytes = (double)grid * 2 * (AR + BR) * KB;
+  printf("VGPR path W=%3d B/row-stage  2 register stages  %7.1f us  %6.1f GB/s per CU  %5.2f TB/s\n",
+         W, us, bytes / us / 1e3 / grid, bytes / us / 1e6);
+}
+
 template <int W, int D>
 void run(const uint8_t* A, const uint8_t* Al, const uint8_t* B, const uint8_t* Bl) {
   const int tiles_n = 4, grid = 41 * 4;   // 41 row tiles of 256 (of 10560) x 1024 / 256
@@ -87,6 +145,9 @@ int main() {
   run<64, 2>(A, Al, B, Bl);
   run<128, 1>(A, Al, B, Bl);
   run<128, 2>(A, Al, B, Bl);
+  runr<32>(A, Al, B, Bl);
+  runr<64>(A, Al, B, Bl);
+  runr<128>(A, Al, B, Bl);
   hipDeviceSynchronize();
   return 0;
 }
