@@ -133,6 +133,10 @@ class LearnerConfig:
     # K splits of the fused post-BPTT group (dW_ih, dW_hh, dW_head1, dX), or "auto"
     # (learner_engine._auto_group_splits: paper config 4,4,4,1, reference config 1,1,1,4)
     sp_group_splits: str = "auto"
+    # tile config of that group: ops/gemm.py G5_CFGS index, -1 = the launcher's CU model, -2 =
+    # learner_engine._auto_group_splits' choice (paper shape: 128x128, 4-deep 32-K ring)
+    sp_group_cfg: int = -2
+    sp_wgrad_splits: int = 4
     # split GEMMs on gemm6 (gemm_sp.hip: the fragment planes refilled between the three product
     # passes, one barrier per LDS tile; the heads' layer-1 GEMMs join the one-pass kernel too):
     # x-projection 115-129 -> 102-110 us, tools/gemm6_probe.py
@@ -153,8 +157,8 @@ class LearnerConfig:
     # "off" (one grouped launch after the BPTT) | "dx" (dX there, the weight gradients after) |
     # "all" (dW_ih, dW_hh, dW_head1 and dX there)
     bptt_gemms: str = "off"
-    # K splits of the weight-gradient group when dX ran on the BPTT's helpers (bptt_gemms = dx)
-    sp_wgrad_splits: int = 7
+    # (sp_wgrad_splits: K splits of the weight-gradient group when dX ran on the BPTT's helpers,
+    # bptt_gemms = dx)
     # single-rank step: the weight repack after the optimizer (pack_step) runs on extra
     # workgroups of the priority tail's launch (replay.hip r2_prio_tail_pack): one launch fewer
     fuse_pack_tail: bool = True

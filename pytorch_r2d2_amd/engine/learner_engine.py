@@ -787,10 +787,11 @@ class LearnerEngine:
             return
         if self.cfg.learner.sp_gemm == "fused":
             probs = [w_jobs[2], w_jobs[1], w_jobs[0]] + ([] if in_bptt else [x_job])
-            sg = self.cfg.learner.sp_group_splits
-            splits = (self._auto_group_splits(probs) if sg == "auto"
-                      else [int(v) for v in sg.replace(":", ",").split(",")][: len(probs)])
-            self._gemm_sp("group", probs, splits, cfg=-1)
+            sg, cfg = self.cfg.learner.sp_group_splits, self.cfg.learner.sp_group_cfg
+            splits, auto_cfg = self._auto_group_splits(probs)
+            if sg != "auto":
+                splits = [int(v) for v in sg.replace(":", ",").split(",")][: len(probs)]
+            self._gemm_sp("group", probs, splits, cfg=auto_cfg if cfg == -2 else cfg)
             return
         splits = self._group_splits(w_jobs, x_job)
         if splits:
@@ -850,16 +851,24 @@ class LearnerEngine:
         Measured: paper 4,4,4,1 (profiles/r04_group_splits_ab.txt: 3,4,4,2 / 3,5,5,2 slower);
         reference config 1,1,1,4 = 0.2455 ms vs 0.3038 at 4,4,4,1.  Without dX (it ran on the
         BPTT's helpers, learner.bptt_gemms = dx) the weight gradients alone split
-        learner.sp_wgrad_splits ways."""
+        learner.sp_wgrad_splits ways.
+        Returns (splits, tile config for learner.sp_group_cfg = -2).  Round 5
+        (tools/wgrad_probe.py, profiles/r05_wgrad_group_ab.txt): at >= 32 dW K steps the 128x128
+        tile with a 4-deep 32-K ring (G5_CFGS[6]) and splits 3,3,3,1 runs the paper group in
+        97 us vs 113 on 256x256 tiles at 4,4,4,1 (same-box step -1.6 %): the 384 + 260 smaller
+        items balance over the CUs and each split's last-arriver reduction reads 3 x 64 KB, not
+        4 x 256 KB."""
         t = lambda g: -(-g.a.shape[0] // 256) * -(-g.b.shape[1] // 256)   # noqa: E731
         ks_w = -(-probs[0].a.shape[1] // 32)
         if len(probs) == 3:
             sw = self.cfg.learner.sp_wgrad_splits if ks_w >= 32 else 1
-            return [sw] * 3
-        sw = 4 if ks_w >= 32 else 1
+            return [sw] * 3, (6 if ks_w >= 32 else -1)
+        if ks_w >= 32:
+            return [3, 3, 3, 1], 6
+        sw = 1
         items = sw * sum(t(g) for g in probs[:3])
         sx = next((c for c in (4, 2) if items + c * t(probs[3]) <= self.n_cus), 1)
-        return [sw, sw, sw, sx]
+        return [sw, sw, sw, sx], -1
 
     def _gemm_sp(self, site: str, probs, splits=None, cfg: int = -1):
         """Split-precision GEMMs of one call site: the fused one-pass kernel (gemm_sp.hip) with a

@@ -77,6 +77,17 @@ def main():
             err = max(((p.c.double() - r).norm() / r.norm()).item() for p, r in zip(probs, refs))
             out[key] = {"w_us": timeit(run), "w_dx_us": timeit(lambda: run(True)), "relerr": f"{err:.1e}"}
             print(key, json.dumps(out[key]), flush=True)
+    # the whole group on the 128-wide tiles with dX split too
+    for cfg in (1, 6):
+        for s in (2, 3, 4):
+            for sx in (2, 3, 4):
+                def run2(s=s, sx=sx, cfg=cfg):
+                    for p in probs:
+                        p.c.zero_()
+                    gemm_sp(probs + [dx], splits=[s, s, s, sx], cfg=cfg, ws=ws, tickets=tk)
+                key = f"{G5_CFGS[cfg]} s{s} dx s{sx}"
+                out[key] = timeit(run2)
+                print(key, out[key], flush=True)
 
 
 if __name__ == "__main__":
