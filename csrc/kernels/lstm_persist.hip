@@ -1175,10 +1175,13 @@ struct PTBArgs {
   // dz . W1 computed HERE instead of read from dh_ext (the TD launch then skips its fused dh, which
   // streamed all of W1^T through every one of its 160 workgroups: 11 us, tools/td_micro.py).  dz
   // (Tl*B, 512) hi / lo planes (time-major learning rows), w1t = W1^T (H, 512) hi / lo planes.
-  // Each compute wave keeps the W1^T fragments of its K quarter for the workgroup's 16 units in
-  // VGPRs; the I/O wave stages the 16 dz rows of an iteration (32 KB) two iterations ahead into a
-  // 3-slot LDS ring (the dynamic LDS); iteration k+1's product (12 MFMAs per wave) runs right
-  // after iteration k's partial-dh publish, inside the hand-off wait it would otherwise idle in.
+  // dh_ext(t-1) rides on the recurrent hand-off: workgroup j already publishes, at iteration k, its
+  // partial of dh_{t-1} over its 64 dgates columns for all H units; it adds dz_{t-1}[:, 32j, +32]
+  // . W1[32j, +32][:] to that partial (one 16x16x32 K step, 3 passes, per N tile: W1^T fragments
+  // resident, the 16 x 32 dz slice staged with iteration k's operands, 2 KB), so the consumers'
+  // sum over the 16 sources is dh_{t-1} + dh_ext(t-1).  Only dh_ext(T-1) (iteration 0, no
+  // hand-off) is a full-K product: each wave's K quarter for the 16 units, from 32 KB of dz rows
+  // staged once before the loop.
   const bf16* dz;
   const bf16* dz_lo;
   const bf16* w1t;
@@ -1191,8 +1194,12 @@ struct PTBArgs {
   long long* dbg;
 };
 #define PT_DZ_K 512                                   // dz row length (2 x head hidden 256)
-#define PT_DZ_SLOT (2 * PT_ROWS * PT_DZ_K * 2)        // one ring slot: 16 rows x 512 x hi/lo = 32 KB
-#define PT_DZ_LDS (3 * PT_DZ_SLOT)                    // the ring (dynamic LDS of the launch)
+// chunk swizzle of the staged 16 x 32 dz slices: 16-B chunk c of row r at c ^ dzs_f(r).  The
+// ds_read_b128 lane groups of the A fragment ({0-3,12-15,20-27}, ...: rows 0-3 and 12-15 at one
+// chunk, rows 4-11 at the next) then hit 16 distinct 16-B slots of the 256-B bank row
+__device__ __forceinline__ int dzs_f(int r) { return (0x1230 >> (4 * (r >> 2))) & 3; }
+#define PT_DZ_SLOT (2 * PT_ROWS * PT_DZ_K * 2)        // 16 dz rows x 512 x hi/lo = 32 KB
+#define PT_DZ_LDS PT_DZ_SLOT                          // iteration 0's rows (dynamic LDS)
 
 // SP (split precision, split.h): W_hh^T hi / lo fragments, dgates tile kept as hi / lo images for
 // the partial-dh MFMAs (3 passes) and written as hi / lo planes for the weight-gradient GEMMs.
@@ -1216,6 +1223,7 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   __shared__ __attribute__((aligned(1024))) float cl[3][PT_ROWS * PL_UNITS];  // c_t
   __shared__ __attribute__((aligned(1024))) float cpl[3][PT_ROWS * PL_UNITS]; // c_{t-1}
   __shared__ __attribute__((aligned(1024))) float dhl[3][PT_ROWS * PL_UNITS]; // dh_ext
+  __shared__ __attribute__((aligned(1024))) bf16 dzsl[3][2][PT_ROWS * 32];    // dz K slices (a.dz)
   __shared__ int flag;
   extern __shared__ __attribute__((aligned(1024))) uint8_t pt_dyn[];   // helper GEMM LDS ring
   int mb, j;
@@ -1388,12 +1396,22 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
                                        (lds_t*)cpl[s], 16, 0, 0);
       if (a.dh_ext && !a.dz)
         __builtin_amdgcn_global_load_lds(a.dh_ext + (size_t)tl * B * H + hidx, (lds_t*)dhl[s], 16, 0, 0);
+      if (a.dz) {
+        // the dz slice of step t-1 (iteration k's publish): 16 rows x 32 K (this workgroup's
+        // slice) x hi / lo; row r's 16-B chunk c holds global chunk c ^ dzs_f(r) (conflict-free
+        // A-fragment reads); t = t0 has no publish: the previous row stands in
+        const int rr = lane >> 2, bb = min(mb * PT_ROWS + rr, B - 1);
+        const int tlp = max(tl - 1, 0);
+        const size_t o = ((size_t)tlp * B + bb) * PT_DZ_K + 32 * j + 8 * ((lane & 3) ^ dzs_f(rr));
+        __builtin_amdgcn_global_load_lds(a.dz + o, (lds_t*)dzsl[s][0], 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(a.dz_lo + o, (lds_t*)dzsl[s][1], 16, 0, 0);
+      }
     };
     const bool dzon = a.dz != nullptr;
-    auto io_load_dz = [&](int k) {    // dz rows of iteration k -> ring slot k % 3 (32 DMAs)
+    auto io_load_dz = [&](int k) {    // dz rows of iteration k (only k = 0) -> LDS (32 DMAs)
       typedef __attribute__((address_space(3))) void lds_t;
       const int tl = T - 1 - k - t0;
-      uint8_t* slot = pt_dyn + (k % 3) * PT_DZ_SLOT;
+      uint8_t* slot = pt_dyn;
 #pragma unroll
       for (int pl = 0; pl < 2; ++pl)
 #pragma unroll
@@ -1405,7 +1423,7 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
           __builtin_amdgcn_global_load_lds(src, (lds_t*)(slot + (pl * PT_ROWS + r) * 1024), 16, 0, 0);
         }
     };
-    const int nload = (a.dh_ext && !dzon ? 7 : 6) + (dzon ? 32 : 0);   // DMA instructions per iteration
+    const int nload = (a.dh_ext && !dzon ? 7 : 6) + (dzon ? 2 : 0);    // DMA instructions per iteration
     const __amdgpu_buffer_rsrc_t drs = pl_rsrc(a.dgates, (uint32_t)((size_t)K * B * G * 2));
     const __amdgpu_buffer_rsrc_t drsl = pl_rsrc(SP ? a.dgates_lo : a.dgates, (uint32_t)((size_t)K * B * G * 2));
     auto io_store = [&](int k) {      // dgates tile of iteration k (write-through: helpers read it)
@@ -1427,30 +1445,18 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
     };
     io_load(0);
     if (dzon) io_load_dz(0);
-    if (K > 1) {
-      io_load(1);
-      if (dzon) io_load_dz(1);
-    }
+    if (K > 1) io_load(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (dzon) lds_sync();                 // barrier P: dz of iteration 0 landed (compute: dh_ext(0))
     for (int k = 0; k < K; ++k) {
       lds_sync();                         // barrier A_k: operands of k landed
       if (k >= 1) io_store(k - 1);
       const bool more = k + 2 < K;
-      if (more) {
-        io_load(k + 2);
-        if (dzon) io_load_dz(k + 2);
-      }
-      if (dzon) {
-        // dz of iteration k+1 (issued in iteration k-1) must land before barrier B_k: the compute
-        // waves multiply it after B_k.  Everything older than this iteration's loads is waited
-        if (more) asm volatile("s_waitcnt vmcnt(38)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      if (more) io_load(k + 2);
       lds_sync();                         // barrier B_k
       // operands of k+1 (issued in iteration k-1) must land before barrier A_{k+1}
       if (more) {
-        if (nload == 38) asm volatile("s_waitcnt vmcnt(38)" ::: "memory");
+        if (nload == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         else if (nload == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       } else {
@@ -1490,9 +1496,11 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   constexpr int SRC4 = NWG / 4;
   const int cr4 = lane >> 2, cq4 = 4 * (lane & 3), sq = wave;
   const bool crow4_ok = mb * PT_ROWS + cr4 < B;
-  // dh_ext = dz . W1 (a.dz): this wave's K quarter [128 wave, +128) of the 16 units' W1^T rows
+  // dh_ext = dz . W1 (a.dz).  Iteration 0: this wave's K quarter [128 wave, +128) of the 16
+  // units' W1^T rows (w1f); every publish: K slice [32 j, +32) of W1^T for this wave's NTW N tiles
+  // (w1s, B fragments: lane l holds k = 32 j + 8 (l >> 4) .. +7 of unit n)
   const bool dzon = SP && a.dz != nullptr;
-  bf16x8 w1f[4], w1fl[4];
+  bf16x8 w1f[4], w1fl[4], w1s[NTW], w1sl[NTW];
   if (dzon) {
     const bf16* r1 = a.w1t + (size_t)(j * PL_UNITS + (lane & 15)) * PT_DZ_K + 128 * wave + 8 * (lane >> 4);
     const bf16* r1l = a.w1t_lo + (size_t)(j * PL_UNITS + (lane & 15)) * PT_DZ_K + 128 * wave + 8 * (lane >> 4);
@@ -1501,12 +1509,18 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
       w1f[s] = *(const bf16x8*)(r1 + 32 * s);
       w1fl[s] = *(const bf16x8*)(r1l + 32 * s);
     }
+#pragma unroll
+    for (int q = 0; q < NTW; ++q) {
+      const size_t o = (size_t)((H / 4) * wave + 16 * q + (lane & 15)) * PT_DZ_K + 32 * j + 8 * (lane >> 4);
+      w1s[q] = *(const bf16x8*)(a.w1t + o);
+      w1sl[q] = *(const bf16x8*)(a.w1t_lo + o);
+    }
   }
-  // partial dh_ext of iteration kk (this wave's K quarter) -> dxp[kk & 1][wave] (read at kk's
-  // pointwise, after barrier A_kk)
-  float* dxp = (float*)(pt_dyn + PT_DZ_LDS);   // [2][4 waves][16 rows][16 units]
+  // partial dh_ext of iteration 0 (this wave's K quarter) -> dxp[wave] (read at iteration 0's
+  // pointwise, after barrier A_0)
+  float* dxp = (float*)(pt_dyn + PT_DZ_LDS);   // [4 waves][16 rows][16 units]
   auto dz_product = [&](int kk) {
-    const uint8_t* slot = pt_dyn + (kk % 3) * PT_DZ_SLOT;
+    const uint8_t* slot = pt_dyn;
     const int r = lane & 15;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1517,7 +1531,7 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
       const bf16x8 al = *(const bf16x8*)(slot + PT_ROWS * 1024 + o);
       acc = mfma16_x3(ah, al, w1f[s], w1fl[s], acc);
     }
-    float* d = dxp + ((kk & 1) * 4 + wave) * (PT_ROWS * PL_UNITS);
+    float* d = dxp + wave * (PT_ROWS * PL_UNITS);
 #pragma unroll
     for (int e = 0; e < 4; ++e) d[(4 * (lane >> 4) + e) * PL_UNITS + r] = acc[e];
   };
@@ -1604,9 +1618,10 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
     const int s3 = k % 3;
     const int o16 = pt_swz16(prow, ul);
     float dh;
-    if (dzon) {
-      const float* d = dxp + (k & 1) * 4 * (PT_ROWS * PL_UNITS) + prow * PL_UNITS + ul;
-      dh = ((d[0] + d[PT_ROWS * PL_UNITS]) + d[2 * PT_ROWS * PL_UNITS]) + d[3 * PT_ROWS * PL_UNITS];
+    if (dzon) {   // iteration 0: the full-K product; later: inside the hand-off partials
+      const float* d = dxp + prow * PL_UNITS + ul;
+      dh = k == 0 ? ((d[0] + d[PT_ROWS * PL_UNITS]) + d[2 * PT_ROWS * PL_UNITS]) + d[3 * PT_ROWS * PL_UNITS]
+                  : 0.f;
     } else {
       dh = a.dh_ext ? dhl[s3][o16] : 0.f;
     }
@@ -1657,12 +1672,19 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
       }
       const unsigned tag = (ep << 16) | (unsigned)(k + 1);
       const int slot = k & 1;
+      bf16x8 zf, zfl;   // dz_{t-1} slice A fragment (dzon): row l & 15, K chunk l >> 4
+      if (dzon) {
+        const int zr = lane & 15, zo = zr * 32 + 8 * ((lane >> 4) ^ dzs_f(zr));
+        zf = *(const bf16x8*)(dzsl[s3][0] + zo);
+        zfl = *(const bf16x8*)(dzsl[s3][1] + zo);
+      }
 #pragma unroll
       for (int q = 0; q < NTW; ++q) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
         if constexpr (SP) {
           acc = mfma16_x3(a0, a0l, wt[q][0], wtl[q][0], acc);
           acc = mfma16_x3(a1, a1l, wt[q][1], wtl[q][1], acc);
+          if (dzon) acc = mfma16_x3(zf, zfl, w1s[q], w1sl[q], acc);
         } else {
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, wt[q][0], acc, 0, 0, 0);
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, wt[q][1], acc, 0, 0, 0);
@@ -1687,8 +1709,6 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
           }
         }
       }
-      // next iteration's dh_ext, inside the hand-off wait (dz of k+1 landed before barrier B_k)
-      if (dzon) dz_product(k + 1);
     }
   }
     if (a.bias_ws) {
@@ -1849,7 +1869,7 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
   args.dz = g_bwd_dz[0]; args.dz_lo = g_bwd_dz[1]; args.w1t = g_bwd_dz[2]; args.w1t_lo = g_bwd_dz[3];
   for (int i = 0; i < 4; ++i) g_bwd_dz[i] = nullptr;   // one launch per set
   if (args.dz && (!sp || H != 256 || g_pl_bwd8)) return -13;   // split-precision T4 BPTT, H 256 only
-  int dyn_lds = args.dz ? PT_DZ_LDS + 2 * 4 * PT_ROWS * PL_UNITS * 4 : PL_LDS_RESERVE;
+  int dyn_lds = args.dz ? PT_DZ_LDS + 4 * PT_ROWS * PL_UNITS * 4 : PL_LDS_RESERVE;
   if (sp && (args.n_gw || args.gx_on)) dyn_lds = max(dyn_lds, 3 * g2s::ST);   // helper ring
   if (sp && (!args.dgates_lo || H > 256)) return -11;
   if (sp && args.hg_on && (!args.hg.zr32 || !args.hg.dz_lo)) return -12;

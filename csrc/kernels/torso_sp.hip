@@ -62,7 +62,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t ts_rsrc(const void* p, uint32_
 //   * the raw uint8 frame lives in LDS (28 KB): waves 3..7 load frame f+1 into registers at the
 //     start of phase A(f) (nothing else of theirs waits on vmcnt there) and store it in phase B(f);
 //     conv1 reads its B fragments with two conflict-free ds_read_b32 per K step;
-//   * act1 hi / lo unpadded (64 B per pixel) with a row-XOR swizzle (a1_off): the stride-2 conv2
+//   * act1 hi / lo unpadded (64 B per pixel) with a row-XOR swizzle (round 5: the space-to-depth a1_off2): the stride-2 conv2
 //     reads drop from ~2.8 to ~1.8 LDS cycles per group and the image shrinks by 12.8 KB, which is
 //     what makes room for the frame (LDS 159.3 KB);
 //   * conv3 runs on wave 2 alone, both pixel tiles sharing every A fragment, with W3 hi / lo held
@@ -87,9 +87,58 @@ constexpr int PF = (IN_CHUNKS2 + 319) / 320;               // 6 chunks per prefe
 static_assert(LDS_BYTES <= 160 * 1024 && LDS_BYTES_I8 <= 160 * 1024, "LDS");
 }  // namespace tsp2
 
-// act1 image: pixel P, 16-byte chunk c (channels 8c .. 8c+7) -> byte offset in one plane
-__device__ __forceinline__ int a1_off(int P, int c) {
-  return ((P >> 2) << 8) + (((((P & 3) << 2) | c) ^ ((P >> 2) & 15)) << 4);
+// act1 image (one plane): space-to-depth blocks.  Pixel (y, x) of the 20 x 20 map lives in block
+// (y >> 1, x >> 1) (10 x 10 blocks of 2 x 2 pixels = 256 B = one LDS bank row), sub-pixel
+// s = 2 (y & 1) + (x & 1); its 16-byte chunk c (channels 8c .. 8c+7) sits at slot (4 s + c) ^
+// a1_m(block).  A conv2 K step (kh, kw, chunk) reads ONE sub-pixel and chunk in every lane, so the
+// slot is const ^ a1_m(block) and a ds_read_b128 lane group is conflict-free when its 16 output
+// pixels map to 16 distinct a1_m: conv2's lanes take 4 x 4 squares of output pixels (and the
+// column / row left over).  a1_m was searched over the affine family (a by + b bx + c (bx >> 2) +
+// d (by >> 2)) mod 4 per 2-bit half jointly with conv1's epilogue stores (c1_pix order):
+// conv2 reads 1.17 LDS cycles per lane group (round-2 row-XOR layout: 1.83), conv1's 8-byte
+// stores at the 2-way floor of a fixed 8-byte half (profiles/r05_torso_act1_s2d.txt).
+__device__ __forceinline__ int a1_m(int by, int bx) {
+  return (((bx + (by >> 2)) & 3) << 2) | ((by + 2 * bx + (bx >> 2) + 2 * (by >> 2)) & 3);
+}
+// conv1 tile position n (32 per tile, 16 per half) -> act1 pixel: 16-pixel row segments x < 16 of
+// rows 0..19, then the x = 16..19 strip as 4 rows x 4 pixels per half tile (the order that keeps
+// each 16-lane epilogue store group at 2 ways); n >= 400: padding (clamped, not stored)
+__device__ __forceinline__ void c1_pix(int n, int& y, int& x) {
+  n = min(n, tsp::P1 - 1);
+  if (n < 320) {
+    y = n >> 4;
+    x = n & 15;
+  } else {
+    const int j = n - 320;
+    y = 4 * (j >> 4) + ((j >> 2) & 3);
+    x = 16 + (j & 3);
+  }
+}
+__device__ __forceinline__ int a1_off2(int y, int x, int c) {
+  const int by = y >> 1, bx = x >> 1;
+  return ((by * 10 + bx) << 8) + (((((2 * (y & 1) + (x & 1)) << 2) | c) ^ a1_m(by, bx)) << 4);
+}
+// conv2 lane -> output pixel: the 16 lanes of each ds_read_b128 group (l32 in {0-3, 12-15,
+// 20-27} = set 0, the rest = set 1) take one of 6 pixel sets: the four 4 x 4 squares of the 8 x 8
+// corner, the column x = 8 (9 pixels), the row y = 8 (8); lanes past a set's end repeat its last
+// pixel (dup: computed, not stored)
+__device__ __forceinline__ void c2_pixel(int wave, int l32, int& oy, int& ox, bool& dup) {
+  const int g = (l32 >= 4 && l32 < 12) || (l32 >= 16 && l32 < 20) || l32 >= 28;
+  const int i = l32 < 4 ? l32 : l32 < 12 ? l32 - 4 : l32 < 20 ? l32 - 8 : l32 < 28 ? l32 - 12 : l32 - 16;
+  const int S = 2 * wave + g;
+  dup = false;
+  if (S < 4) {
+    oy = 4 * (S >> 1) + (i >> 2);
+    ox = 4 * (S & 1) + (i & 3);
+  } else if (S == 4) {
+    dup = i >= 9;
+    oy = min(i, 8);
+    ox = 8;
+  } else {
+    dup = i >= 8;
+    oy = 8;
+    ox = min(i, 7);
+  }
 }
 
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
@@ -290,20 +339,50 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
       for (int i = 0; i < t1n; ++i) {
         // both 16-pixel halves of the tile: half 1's frame bytes load under half 0's MFMAs
         i32x4_t bx[1][4];
-        auto ldb = [&](int q, i32x4_t (&x)[4]) {
-          const int pc = min((t1b + i) * 32 + 16 * q + l16, P1 - 1);
-          const int oy = pc / 20, ox = pc % 20;
-          const uint8_t* fb = fr + gq * 7056 + 4 * oy * 84 + 4 * ox + oz;
+        // pixel of this lane in half tile q (c1_pix with the half tile's uniform part hoisted):
+        // a row segment (y uniform, x = l16) or a 4 x 4 piece of the x >= 16 strip
+        auto pix = [&](int q, int& oy, int& ox) {
+          const int nb = (t1b + i) * 32 + 16 * q;
+          if (nb < 320) {
+            oy = nb >> 4;
+            ox = l16;
+          } else if (nb < P1) {
+            oy = 4 * ((nb - 320) >> 4) + (l16 >> 2);
+            ox = 16 + (l16 & 3);
+          } else {
+            oy = 19;
+            ox = 19;
+          }
+        };
+        // frame bytes of K blocks [kb0, kb0 + 2): issued in two halves, the second after the first
+        // half's MFMAs of channel half 0 (the reads of K blocks 2, 3 overlap those MFMAs)
+        auto ldb = [&](const uint8_t* fb, int kb0, i32x4_t (&x)[4]) {
 #pragma unroll
-          for (int kb = 0; kb < 4; ++kb)
+          for (int kb = kb0; kb < kb0 + 2; ++kb)
 #pragma unroll
             for (int dy = 0; dy < 4; ++dy)
               x[kb][dy] = (int)*(const uint32_t*)(fb + (kb >> 1) * 336 + (kb & 1) * 4 + dy * 84);
         };
 #pragma unroll 1
         for (int q = 0; q < 2; ++q) {
-          ldb(q, bx[0]);
-          const int p = (t1b + i) * 32 + 16 * q + l16;
+          // frame bytes and the pixel's act1 byte offset with chunk 0 (a1_off2(y, x, 0)); row
+          // segments (uniform y, x = l16) split a1_off2 into uniform and per-lane parts
+          const int nb = (t1b + i) * 32 + 16 * q;
+          const uint8_t* fb;
+          int sbase;
+          if (nb < 320) {
+            const int y = nb >> 4, by = y >> 1, bx = l16 >> 1;
+            fb = fr + gq * 7056 + 4 * l16 + oz + 336 * y;
+            const int m = (((bx + (by >> 2)) & 3) << 2) | ((2 * bx + (bx >> 2) + by + 2 * (by >> 2)) & 3);
+            sbase = ((by * 10 + bx) << 8) + (((m ^ (4 * (l16 & 1))) ^ (8 * (y & 1))) << 4) + 8 * (gq & 1);
+          } else {
+            int py, px;
+            pix(q, py, px);
+            fb = fr + gq * 7056 + 4 * py * 84 + 4 * px + oz;
+            sbase = a1_off2(py, px, 0) + 8 * (gq & 1);
+          }
+          ldb(fb, 0, bx[0]);
+          const bool pst = nb < P1;   // uniform: padding half tiles store nothing
 #pragma unroll
           for (int c = 0; c < 2; ++c) {   // channel halves one after the other (12 acc VGPRs)
             // rows (channels) 16c + 4 gq + e; the -128 shift's row corrections (digit row sums x
@@ -315,14 +394,20 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
             acc[1] = i32x4_t{0, 0, 0, 0};
             acc[2] = *(const i32x4_t*)(sct + 32 + ch0);
 #pragma unroll
-            for (int kb = 0; kb < 4; ++kb)
+            for (int kb = 0; kb < 4; ++kb) {
+              if (c == 0 && kb == 2) {
+                __builtin_amdgcn_sched_barrier(0);
+                ldb(fb, 2, bx[0]);
+                __builtin_amdgcn_sched_barrier(0);
+              }
 #pragma unroll
               for (int d = 0; d < 3; ++d) {
                 const int slot = 12 * c + 3 * kb + d;
                 const i32x4_t a = __builtin_bit_cast(i32x4_t, slot < 16 ? wfh[slot & 15] : wfl[(slot - 16) & 15]);
                 acc[d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bx[0][kb], acc[d], 0, 0, 0);
               }
-            if (p < P1) {
+            }
+            if (pst) {
               // digits 1, 2 merge exactly in int32 (|128 i1 + i2| < 2^30)
               bf16x4 vh, vl;
 #pragma unroll
@@ -334,7 +419,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
                 vh[e] = (bf16)v;
                 vl[e] = sp_lo(v);
               }
-              const int o = a1_off(p, 2 * c + (gq >> 1)) + 8 * (gq & 1);
+              const int o = sbase ^ ((2 * c + (gq >> 1)) << 4);
               *(bf16x4*)(a1h + o) = vh;
               *(bf16x4*)(a1l + o) = vl;
             }
@@ -407,19 +492,27 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
     }
     if (conv2_wave) {
       if (!(args.dbg & 2)) {
-        const int p = wave * 32 + l32;
-        const int pc = p < P2 ? p : P2 - 1;
-        const int oy = pc / 9, ox = pc % 9;
+        int oy, ox;
+        bool dup;
+        c2_pixel(wave, l32, oy, ox, dup);
+        const int p = oy * 9 + ox;
         const bf16* ah = w2h + l32 * 520 + half * 8;
         const bf16* al = w2l + l32 * 520 + half * 8;
-        const int P0 = (2 * oy) * 20 + 2 * ox + oz;
+        // per (kh >> 1, kw >> 1): the block's byte base | (a1_m ^ half) << 4; a K step XORs in its
+        // (sub-pixel, chunk pair) slot -- one VALU per step
+        int vb[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int by = oy + (q >> 1), bx = ox + (q & 1);
+          vb[q] = (((by * 10 + bx) << 8) | ((a1_m(by, bx) ^ half) << 4)) + oz;
+        }
         constexpr int D = 2;
         bf16x8 rah[D], ral[D], rbh[D], rbl[D];
         auto ld = [&](int s, bf16x8& xah, bf16x8& xal, bf16x8& xbh, bf16x8& xbl) {
           const int khkw = s >> 1, kh = khkw >> 2, kw = khkw & 3;
-          int pp;   // computed at the step (not hoisted: 32 live offsets otherwise)
-          asm volatile("v_add_u32 %0, %1, %2" : "=v"(pp) : "v"(P0), "i"(kh * 20 + kw));
-          const int ob = a1_off(pp, (s & 1) * 2 + half);
+          const int q = 2 * (kh >> 1) + (kw >> 1), sub = 2 * (kh & 1) + (kw & 1);
+          int ob;   // computed at the step (not hoisted: 32 live offsets otherwise)
+          asm volatile("v_xor_b32 %0, %1, %2" : "=v"(ob) : "i"(((sub << 2) | ((s & 1) << 1)) << 4), "v"(vb[q]));
           xah = *(const bf16x8*)(ah + s * 16);
           xal = *(const bf16x8*)(al + s * 16);
           xbh = *(const bf16x8*)(a1h + ob);
@@ -448,7 +541,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
           }
         };
         kloop(std::integral_constant<int, C2P>{});
-        if (p < P2) {
+        if (!dup) {
           bf16* d2 = J.s2 ? J.s2 + ((size_t)f * P2 + p) * 32 : nullptr;
           bf16* d2l = J.s2 ? J.s2l + ((size_t)f * P2 + p) * 32 : nullptr;
 #pragma unroll
@@ -476,8 +569,9 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
         bf16* d1 = J.s1 + (size_t)f * P1 * 32;
         bf16* d1l = J.s1l + (size_t)f * P1 * 32;
         for (int i = tid - 192; i < P1 * 4; i += 320) {
-          const int row = i >> 4, pcv = (i & 15) ^ (row & 15);
-          const int P = row * 4 + (pcv >> 2), c = pcv & 3;
+          const int blk = i >> 4, by = blk / 10, bx = blk - 10 * by;
+          const int v = (i & 15) ^ a1_m(by, bx), sub = v >> 2, c = v & 3;
+          const int P = (2 * by + (sub >> 1)) * 20 + 2 * bx + (sub & 1);
           *(bf16x8*)(d1 + P * 32 + c * 8) = *(const bf16x8*)(a1h + i * 16);
           *(bf16x8*)(d1l + P * 32 + c * 8) = *(const bf16x8*)(a1l + i * 16);
         }

@@ -151,7 +151,7 @@ class LearnerConfig:
     use_graph: bool = True            # capture the whole step in a HIP graph
     # split precision: the BPTT computes its input gradient dh = dz . W1 itself, inside its
     # hand-off waits (lstm_persist.hip PTBArgs::dz), instead of the TD launch (td_fuse_dh)
-    bptt_dh: bool = False
+    bptt_dh: bool = True
     # split precision: post-BPTT GEMMs on the BPTT launch's idle workgroups (lstm_persist.hip
     # g2s_tile_acc helpers), each tile as soon as the BPTT has stored the dgates rows it reads:
     # "off" (one grouped launch after the BPTT) | "dx" (dX there, the weight gradients after) |
