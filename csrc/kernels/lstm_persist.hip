@@ -700,7 +700,7 @@ __device__ __forceinline__ int pt_swz16(int r, int col) {      // 16-float rows,
 //    launch of one launch SITE (fixed chain set, one ring, one ctr) advances the epoch by one.
 //    Requirement (the engine keeps it): a ring + ctr pair serves one launch site.
 //  * !T4 (r2_lstm_sp_handoff8(1), A/B probes): {fp32 h[u], 32-bit tag} 8-byte granules.
-template <int H, bool SP, bool T4 = false, bool KQ = false>
+template <int H, bool SP, bool T4 = false>
 __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
   static_assert(!T4 || SP, "T4 is a split-precision hand-off");
   constexpr int G = 4 * H;
@@ -719,13 +719,9 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
   static_assert(CH >= 1 && PT_ROWS * CPR % 256 == 0, "H");
   // LDS: staged h (2 slots), wave-private gate exchange, x-projection ring (3 slots, filled by
   // the I/O wave), per-step outputs (2 slots, drained by the I/O wave)
-  __shared__ __attribute__((aligned(16))) bf16 hin[2][KQ ? 8 : PT_ROWS * HS];
-  __shared__ __attribute__((aligned(16))) bf16 hinl[2][SP && !KQ ? PT_ROWS * HS : 8];   // lo image (SP)
-  __shared__ __attribute__((aligned(16))) float xch[4][KQ ? 4 : PT_ROWS * XS];
-  // KQ: the 4 waves' partial gate tiles, [step & 1][wave][row][XPS] (row stride 68: the partial
-  // stores and the pointwise's reads are conflict-free)
-  constexpr int XPS = 68;
-  __shared__ __attribute__((aligned(16))) float xp[2][4][KQ ? PT_ROWS * XPS : 4];
+  __shared__ __attribute__((aligned(16))) bf16 hin[2][PT_ROWS * HS];
+  __shared__ __attribute__((aligned(16))) bf16 hinl[2][SP ? PT_ROWS * HS : 8];   // lo image (SP)
+  __shared__ __attribute__((aligned(16))) float xch[4][PT_ROWS * XS];
   __shared__ __attribute__((aligned(1024))) float xl[3][PT_ROWS * PL_GCOLS];
   __shared__ __attribute__((aligned(16))) float oc[2][PT_ROWS * PL_UNITS];
   __shared__ __attribute__((aligned(16))) float oh32[2][PT_ROWS * PL_UNITS];
@@ -823,145 +819,6 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
     io_store(T - 1);
     return;
   }
-
-  // ================= compute waves 0..3, K-split layout (KQ): wave w multiplies the K quarter
-  // [H/4 w, +H/4) for all 64 gate columns of the workgroup (4 N tiles = the 4 gates of its 16
-  // units) and polls exactly the h words of its A fragments straight into registers -- no staged
-  // h image, no fragment reads from LDS; the 4 partial gate tiles meet in LDS (xp) at the one
-  // barrier of the step.
-  if constexpr (KQ) {
-    static_assert(SP && T4 && H == 256, "KQ: split-precision T4, H 256");
-    constexpr int KW = H / 4, KSW = KW / 32, NQ = PL_GCOLS / 16;
-    auto woff = [&](int slot, int r, int u_) -> uint32_t {   // T4 word of unit u_, row r
-      return (uint32_t)((((size_t)(chn * 2 + slot) * rows_all + mb * PT_ROWS + r) * H + u_) * 4);
-    };
-    bf16x8 wq[NQ][KSW], wql[NQ][KSW];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q)
-#pragma unroll
-      for (int s = 0; s < KSW; ++s) {
-        const size_t o = ((size_t)j * PL_GCOLS + 16 * q + (lane & 15)) * H + KW * wave + 32 * s + 8 * (lane >> 4);
-        wq[q][s] = *(const bf16x8*)(cd.whh + o);
-        wql[q][s] = *(const bf16x8*)(cd.whh_lo + o);
-      }
-    const int prow = lane >> 2, pu = lane & 3;
-    const int ul = 4 * wave + pu, u = j * PL_UNITS + ul;
-    const int pb = mb * PT_ROWS + prow;
-    const bool pv = pb < B;
-    float creg = cd.c0[(size_t)(pv ? pb : B - 1) * H + u];
-    // A-fragment ownership: row fr (lane & 15), units [KW wave + 32 s + 8 (lane >> 4), +8) per
-    // k-step s = two 16-B chunks of 4 tagged words each
-    const int fr = lane & 15, frb = mb * PT_ROWS + fr;
-    const bool frv = frb < B;
-    const int cu0 = KW * wave + 8 * (lane >> 4);
-    __builtin_amdgcn_s_waitcnt(0);
-    for (int t = 0; t < T; ++t) {
-      bf16x8 ah[KSW], al[KSW];
-      if (t == 0) {
-        const float* h0 = (const float*)cd.h0 + (size_t)(frv ? frb : B - 1) * H;
-#pragma unroll
-        for (int s = 0; s < KSW; ++s) {
-          const f32x4 x0 = *(const f32x4*)(h0 + cu0 + 32 * s), x1 = *(const f32x4*)(h0 + cu0 + 32 * s + 4);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            ah[s][e] = (bf16)x0[e];
-            al[s][e] = sp_lo(x0[e]);
-            ah[s][4 + e] = (bf16)x1[e];
-            al[s][4 + e] = sp_lo(x1[e]);
-          }
-        }
-      } else {
-        const unsigned want = ((ep & 1u) << 3) | ((unsigned)t & 7u);
-        const int slot = (t - 1) & 1;
-        auto ld = [&](int i) -> u32x4 {   // chunk i: k-step i >> 1, 4-unit half i & 1
-          return __builtin_amdgcn_raw_buffer_load_b128(rrs, woff(slot, fr, cu0 + 32 * (i >> 1) + 4 * (i & 1)), 0, 16);
-        };
-        u32x4 v[2 * KSW];
-#pragma unroll
-        for (int i = 0; i < 2 * KSW; ++i) v[i] = ld(i);
-        for (unsigned spins = 0;; ++spins) {
-          bool all = true;
-          bool ok[2 * KSW];
-#pragma unroll
-          for (int i = 0; i < 2 * KSW; ++i) {
-            ok[i] = !frv || ((v[i][0] & 15u) == want && (v[i][1] & 15u) == want &&
-                             (v[i][2] & 15u) == want && (v[i][3] & 15u) == want);
-            all = all && ok[i];
-          }
-          if (all) break;
-          if (spins > PL_SPIN_LIMIT) {
-            __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          asm volatile("" ::: "memory");
-#pragma unroll
-          for (int i = 0; i < 2 * KSW; ++i)
-            if (!ok[i]) v[i] = ld(i);
-        }
-#pragma unroll
-        for (int s = 0; s < KSW; ++s)
-#pragma unroll
-          for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const float f = __uint_as_float(v[2 * s + hf][e] & ~15u);
-              ah[s][4 * hf + e] = (bf16)f;
-              al[s][4 * hf + e] = sp_lo(f);
-            }
-      }
-      // partial gate tiles of this wave's K quarter -> xp[t & 1][wave]: acc[q][e] = gate q of unit
-      // lane & 15, row 4 (lane >> 4) + e
-      {
-        float* xw = xp[t & 1][wave];
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int s = 0; s < KSW; ++s) acc = mfma16_x3(ah[s], al[s], wq[q][s], wql[q][s], acc);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) xw[(4 * (lane >> 4) + e) * XPS + 16 * q + (lane & 15)] = acc[e];
-        }
-      }
-      lds_sync();                                 // barrier t (with the I/O wave)
-      float gp[4];
-      {
-        const float* xr = xl[t % 3];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const float* xq = &xp[t & 1][0][prow * XPS + 16 * g + ul];
-          gp[g] = ((xq[0] + xq[PT_ROWS * XPS]) + xq[2 * PT_ROWS * XPS]) + xq[3 * PT_ROWS * XPS] +
-                  xr[pt_swz64(prow, ul + 16 * g)];
-        }
-      }
-      const float si = sigmoidf_(gp[0]);
-      const float sf = sigmoidf_(gp[1]);
-      const float tg = tanhf_(gp[2]);
-      const float so = sigmoidf_(gp[3]);
-      creg = sf * creg + si * tg;
-      const float hv = so * tanhf_(creg);
-      if (pv) {
-        const uint32_t w = ((__float_as_uint(hv) + 8u) & ~15u) | ((ep & 1u) << 3) | ((unsigned)(t + 1) & 7u);
-        const uint32_t off = woff(t & 1, prow, u);
-        if (fast) __builtin_amdgcn_raw_buffer_store_b32(w, rrs, off, 0, 0);
-        else __builtin_amdgcn_raw_buffer_store_b32(w, rrs, off, 0, 16);
-      }
-      {
-        const int s = t & 1;
-        oc[s][prow * PL_UNITS + ul] = creg;
-        oh32[s][prow * PL_UNITS + ul] = hv;
-        ohs[s][prow * PL_UNITS + ul] = (bf16)hv;
-        ohsl[s][prow * PL_UNITS + ul] = sp_lo(hv);
-        if (save_any) {
-          float* gq = og[s];
-          gq[pt_swz64(prow, ul)] = si;
-          gq[pt_swz64(prow, ul + 16)] = sf;
-          gq[pt_swz64(prow, ul + 32)] = tg;
-          gq[pt_swz64(prow, ul + 48)] = so;
-        }
-      }
-    }
-  } else {
 
   // ================= compute waves 0..3
   auto goff = [&](int slot, int r, int p) -> uint32_t {
@@ -1172,7 +1029,6 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
       }
     }
   }
-  }   // !KQ
 #undef PT_TRACE
   lds_sync();                                     // barrier T: outputs of step T-1 complete
   // the last workgroup to finish advances the epoch (every workgroup read it before any
@@ -1189,9 +1045,6 @@ extern "C" int r2_lstm_tag_ring_bytes(int n_chains, int B, int H) {
 // A/B probe switch: 1 = split-precision forward on the 8-byte {h, tag} granules (previous path)
 static int g_pl_sp8 = 0;
 extern "C" int r2_lstm_sp_handoff8(int v) { g_pl_sp8 = v; return 0; }
-// 1: the split-precision T4 forward at H 256 runs the K-split compute layout (lstm_fwd_tag_kernel KQ)
-static int g_pl_kq = 0;
-extern "C" int r2_lstm_fwd_kq(int v) { g_pl_kq = v; return 0; }
 
 // Same chain layout / ctr as r2_lstm_fwd_persist; ring: r2_lstm_tag_ring_bytes bytes.  bf16: any
 // content.  Split precision (4-bit tagged words): zero- or (-1)-filled at allocation, and one
@@ -1239,15 +1092,7 @@ static int lstm_fwd_tag_launch(const int64_t* chain_ptrs, int words, int n_chain
     switch (H) {
       case 64: PT_T4(64); break;
       case 128: PT_T4(128); break;
-      default:
-        if (g_pl_kq) {
-          hipFuncSetAttribute((const void*)lstm_fwd_tag_kernel<256, true, true, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, PL_LDS_RESERVE);
-          hipLaunchKernelGGL((lstm_fwd_tag_kernel<256, true, true, true>), grid, block, PL_LDS_RESERVE, s, args);
-        } else {
-          PT_T4(256);
-        }
-        break;
+      default: PT_T4(256); break;
     }
 #undef PT_T4
     R2_CHECK_LAUNCH();

@@ -109,9 +109,6 @@ class LearnerConfig:
     # words with a 4-bit tag (lstm_persist.hip T4) -- False = the 8-byte {value, tag} granules
     # (A/B probes; process-wide kernel switch, set by the engine at construction)
     lstm_tag_words: bool = True
-    # split-precision forward at H 256: K-split compute layout (each wave multiplies a K quarter for
-    # all 64 gate columns, its h fragments polled straight into registers; lstm_persist.hip KQ)
-    lstm_fwd_kq: bool = False
     # post-BPTT GEMMs: "group" = weight gradients + dX in one grid (58 us vs 85 separate),
     # "group:a,b,c,d" = with K splits, "separate"
     bwd_gemm: str = "group"

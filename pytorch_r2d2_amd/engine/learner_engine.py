@@ -226,7 +226,6 @@ class LearnerEngine:
         if d.type == "cuda":
             kernels().r2_lstm_sp_handoff8(0 if lc.lstm_tag_words else 1)
             kernels().r2_lstm_bwd_handoff8(0 if lc.lstm_tag_words else 1)
-            kernels().r2_lstm_fwd_kq(1 if lc.lstm_fwd_kq else 0)
         if sp and not (cfg.model.torso == "atari" and d.type == "cuda" and L.H <= 256
                        and lc.lstm_impl == "persistent" and lc.lstm_handoff == "tagged"):
             raise NotImplementedError(
