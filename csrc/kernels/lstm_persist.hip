@@ -739,6 +739,40 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
   const uint32_t ring_bytes = (uint32_t)((size_t)a.groups / MB * 2 * rows_all * GR * 8);
   const __amdgpu_buffer_rsrc_t rrs = pl_rsrc(a.ring, ring_bytes);
   const unsigned ep = __hip_atomic_load(a.ctr + PT_EPOCH_FWD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // I/O wave: x-projection rows of step t -> ring slot t % 3 (LDS-DMA)
+  auto io_load_x = [&](int t) {
+    float* dst = xl[t % 3];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      // LDS chunk (lane & 15) of row r holds global chunk (lane & 15) ^ r (pt_swz64): the
+      // pointwise reads of 16 rows x 4 units then cover 64 distinct banks
+      const int r = 4 * q + (lane >> 4);
+      const int b = min(mb * PT_ROWS + r, B - 1);
+      const float* src = cd.xproj + ((size_t)t * B + b) * G + j * PL_GCOLS + 4 * ((lane & 15) ^ r);
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(dst + q * 256),
+                                       16, 0, 0);
+    }
+  };
+  // the first two steps' x rows load under the XCD rendezvous below (its barrier waits for them)
+  if (wave == 4) {
+    io_load_x(0);
+    if (T > 1) io_load_x(1);
+  }
+  // compute waves: resident W_hh fragments (loaded under the rendezvous too): wave column c
+  // (0..15) = gate c>>2 of unit 4*wave + (c&3), i.e. packed row 16*(c>>2) + 4*wave + (c&3) of
+  // this workgroup's 64
+  bf16x8 wf[KS], wfl[SP ? KS : 1];
+  if (wave < 4) {
+    const int c = lane & 15;
+    const int n = 16 * (c >> 2) + 4 * wave + (c & 3);
+    const size_t o = ((size_t)j * PL_GCOLS + n) * H + 8 * (lane >> 4);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) wf[s] = *(const bf16x8*)(cd.whh + o + 32 * s);
+    if constexpr (SP) {
+#pragma unroll
+      for (int s = 0; s < KS; ++s) wfl[s] = *(const bf16x8*)(cd.whh_lo + o + 32 * s);
+    }
+  }
   const int fast = pl_same_xcd(a.ctr, g, NWG, a.force_slow, a.err, &flag);
   if (fast < 0) return;
   if (a.dbg && tid == 0) {
@@ -751,19 +785,6 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
   if (wave == 4) {
     // ================= I/O wave: x-projection prefetch (2 steps ahead) + output drain.  Its
     // loads and stores never sit in a compute wave's vmcnt queue in front of a granule poll.
-    auto io_load_x = [&](int t) {
-      float* dst = xl[t % 3];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        // LDS chunk (lane & 15) of row r holds global chunk (lane & 15) ^ r (pt_swz64): the
-        // pointwise reads of 16 rows x 4 units then cover 64 distinct banks
-        const int r = 4 * q + (lane >> 4);
-        const int b = min(mb * PT_ROWS + r, B - 1);
-        const float* src = cd.xproj + ((size_t)t * B + b) * G + j * PL_GCOLS + 4 * ((lane & 15) ^ r);
-        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(dst + q * 256),
-                                         16, 0, 0);
-      }
-    };
     auto io_store = [&](int t) {
       const int s = t & 1;
       {
@@ -796,14 +817,9 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
       }
     };
     // x(t) must have landed by barrier t; the 4 DMA loads issued for x(t+2) in step t stay in
-    // flight across barrier t+1 (counted wait: vmcnt retires in order, the stores come first)
-    io_load_x(0);
-    if (T > 1) {
-      io_load_x(1);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // flight across barrier t+1 (counted wait: vmcnt retires in order, the stores come first).
+    // x(0), x(1) were issued before the XCD rendezvous
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_sync();                                   // barrier 0
     for (int t = 0; t < T; ++t) {
       if (t >= 1) io_store(t - 1);
@@ -828,20 +844,6 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
   auto woff = [&](int slot, int r, int u_) -> uint32_t {
     return (uint32_t)((((size_t)(chn * 2 + slot) * rows_all + mb * PT_ROWS + r) * H + u_) * 4);
   };
-  // resident W_hh fragments: wave column c (0..15) = gate c>>2 of unit 4*wave + (c&3), i.e.
-  // packed row 16*(c>>2) + 4*wave + (c&3) of this workgroup's 64
-  bf16x8 wf[KS], wfl[SP ? KS : 1];
-  {
-    const int c = lane & 15;
-    const int n = 16 * (c >> 2) + 4 * wave + (c & 3);
-    const size_t o = ((size_t)j * PL_GCOLS + n) * H + 8 * (lane >> 4);
-#pragma unroll
-    for (int s = 0; s < KS; ++s) wf[s] = *(const bf16x8*)(cd.whh + o + 32 * s);
-    if constexpr (SP) {
-#pragma unroll
-      for (int s = 0; s < KS; ++s) wfl[s] = *(const bf16x8*)(cd.whh_lo + o + 32 * s);
-    }
-  }
   // pointwise ownership: lane = (row prow, unit 4*wave + pu); c lives in a register
   const int prow = lane >> 2, pu = lane & 3;
   const int ul = 4 * wave + pu, u = j * PL_UNITS + ul;
@@ -1369,6 +1371,72 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   const uint32_t ring_bytes = (uint32_t)((size_t)2 * NWG * rows_all * H * 8);
   const __amdgpu_buffer_rsrc_t rrs = pl_rsrc(a.ring, ring_bytes);
   const unsigned ep = __hip_atomic_load(a.ctr + PT_EPOCH_BWD, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // I/O wave operand loads (LDS-DMA into the rings)
+  auto io_load = [&](int k) {       // operands of iteration k (step t = T-1-k) into slot k % 3
+    const int t = T - 1 - k, tl = t - t0, s = k % 3;
+    typedef __attribute__((address_space(3))) void lds_t;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {   // gates: 16 rows x 64 fp32, swizzled (pt_swz64)
+      const int r = 4 * q + (lane >> 4), b = min(mb * PT_ROWS + r, B - 1);
+      __builtin_amdgcn_global_load_lds(a.gates + ((size_t)tl * B + b) * G + j * PL_GCOLS + 4 * ((lane & 15) ^ r),
+                                       (lds_t*)(gl[s] + q * 256), 16, 0, 0);
+    }
+    const int r = lane >> 2, b = min(mb * PT_ROWS + r, B - 1);   // 16-float rows (pt_swz16)
+    const size_t hidx = (size_t)b * H + j * PL_UNITS + 4 * ((lane & 3) ^ (r >> 2));
+    __builtin_amdgcn_global_load_lds(a.c_seq + (size_t)t * B * H + hidx, (lds_t*)cl[s], 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((t == 0 ? a.c0 : a.c_seq + (size_t)(t - 1) * B * H) + hidx,
+                                     (lds_t*)cpl[s], 16, 0, 0);
+    if (a.dh_ext && !a.dz)
+      __builtin_amdgcn_global_load_lds(a.dh_ext + (size_t)tl * B * H + hidx, (lds_t*)dhl[s], 16, 0, 0);
+    if (a.dz) {
+      // the dz slice of step t-1 (iteration k's publish): 16 rows x 32 K (this workgroup's
+      // slice) x hi / lo; row r's 16-B chunk c holds global chunk c ^ dzs_f(r) (conflict-free
+      // A-fragment reads); t = t0 has no publish: the previous row stands in
+      const int rr = lane >> 2, bb = min(mb * PT_ROWS + rr, B - 1);
+      const int tlp = max(tl - 1, 0);
+      const size_t o = ((size_t)tlp * B + bb) * PT_DZ_K + 32 * j + 8 * ((lane & 3) ^ dzs_f(rr));
+      __builtin_amdgcn_global_load_lds(a.dz + o, (lds_t*)dzsl[s][0], 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(a.dz_lo + o, (lds_t*)dzsl[s][1], 16, 0, 0);
+    }
+  };
+  const bool dzon = a.dz != nullptr;
+  auto io_load_dz = [&](int k) {    // dz rows of iteration k (only k = 0) -> LDS (32 DMAs)
+    typedef __attribute__((address_space(3))) void lds_t;
+    const int tl = T - 1 - k - t0;
+    uint8_t* slot = pt_dyn;
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+      for (int r = 0; r < PT_ROWS; ++r) {
+        // row r: 64 chunks of 16 B; LDS chunk i holds global chunk i ^ r (conflict-free
+        // fragment reads of 16 rows at one k)
+        const int b = min(mb * PT_ROWS + r, B - 1);
+        const bf16* src = (pl ? a.dz_lo : a.dz) + ((size_t)tl * B + b) * PT_DZ_K + 8 * ((lane ^ r) & 63);
+        __builtin_amdgcn_global_load_lds(src, (lds_t*)(slot + (pl * PT_ROWS + r) * 1024), 16, 0, 0);
+      }
+  };
+  // the first iterations' operands load under the XCD rendezvous below (its barrier waits for them)
+  if (wave == 4) {
+    io_load(0);
+    if (dzon) io_load_dz(0);
+    if (K > 1) io_load(1);
+  }
+  // compute waves: W_hh^T fragments (loaded under the rendezvous): N tile q of this wave = units
+  // (H/4)*wave + 16*q + (l&15); B[k][n] = Whh_pk[j][k][n]
+  bf16x8 wt[NTW][2], wtl[SP ? NTW : 1][2];
+  if (wave < 4) {
+#pragma unroll
+    for (int q = 0; q < NTW; ++q) {
+      const int n = (H / 4) * wave + 16 * q + (lane & 15);
+      const size_t o = ((size_t)j * H + n) * PL_GCOLS + 8 * (lane >> 4);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) wt[q][s] = *(const bf16x8*)(a.whhT + o + 32 * s);
+      if constexpr (SP) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s) wtl[q][s] = *(const bf16x8*)(a.whhT_lo + o + 32 * s);
+      }
+    }
+  }
   const int fast = pl_same_xcd(a.ctr, mb, NWG, a.force_slow, a.err, &flag);
   if (fast < 0) return;
   auto goff = [&](int slot, int src, int r, int unit) -> uint32_t {
@@ -1380,49 +1448,6 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
 
   if (wave == 4) {
     // ================= I/O wave
-    auto io_load = [&](int k) {       // operands of iteration k (step t = T-1-k) into slot k % 3
-      const int t = T - 1 - k, tl = t - t0, s = k % 3;
-      typedef __attribute__((address_space(3))) void lds_t;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {   // gates: 16 rows x 64 fp32, swizzled (pt_swz64)
-        const int r = 4 * q + (lane >> 4), b = min(mb * PT_ROWS + r, B - 1);
-        __builtin_amdgcn_global_load_lds(a.gates + ((size_t)tl * B + b) * G + j * PL_GCOLS + 4 * ((lane & 15) ^ r),
-                                         (lds_t*)(gl[s] + q * 256), 16, 0, 0);
-      }
-      const int r = lane >> 2, b = min(mb * PT_ROWS + r, B - 1);   // 16-float rows (pt_swz16)
-      const size_t hidx = (size_t)b * H + j * PL_UNITS + 4 * ((lane & 3) ^ (r >> 2));
-      __builtin_amdgcn_global_load_lds(a.c_seq + (size_t)t * B * H + hidx, (lds_t*)cl[s], 16, 0, 0);
-      __builtin_amdgcn_global_load_lds((t == 0 ? a.c0 : a.c_seq + (size_t)(t - 1) * B * H) + hidx,
-                                       (lds_t*)cpl[s], 16, 0, 0);
-      if (a.dh_ext && !a.dz)
-        __builtin_amdgcn_global_load_lds(a.dh_ext + (size_t)tl * B * H + hidx, (lds_t*)dhl[s], 16, 0, 0);
-      if (a.dz) {
-        // the dz slice of step t-1 (iteration k's publish): 16 rows x 32 K (this workgroup's
-        // slice) x hi / lo; row r's 16-B chunk c holds global chunk c ^ dzs_f(r) (conflict-free
-        // A-fragment reads); t = t0 has no publish: the previous row stands in
-        const int rr = lane >> 2, bb = min(mb * PT_ROWS + rr, B - 1);
-        const int tlp = max(tl - 1, 0);
-        const size_t o = ((size_t)tlp * B + bb) * PT_DZ_K + 32 * j + 8 * ((lane & 3) ^ dzs_f(rr));
-        __builtin_amdgcn_global_load_lds(a.dz + o, (lds_t*)dzsl[s][0], 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(a.dz_lo + o, (lds_t*)dzsl[s][1], 16, 0, 0);
-      }
-    };
-    const bool dzon = a.dz != nullptr;
-    auto io_load_dz = [&](int k) {    // dz rows of iteration k (only k = 0) -> LDS (32 DMAs)
-      typedef __attribute__((address_space(3))) void lds_t;
-      const int tl = T - 1 - k - t0;
-      uint8_t* slot = pt_dyn;
-#pragma unroll
-      for (int pl = 0; pl < 2; ++pl)
-#pragma unroll
-        for (int r = 0; r < PT_ROWS; ++r) {
-          // row r: 64 chunks of 16 B; LDS chunk i holds global chunk i ^ r (conflict-free
-          // fragment reads of 16 rows at one k)
-          const int b = min(mb * PT_ROWS + r, B - 1);
-          const bf16* src = (pl ? a.dz_lo : a.dz) + ((size_t)tl * B + b) * PT_DZ_K + 8 * ((lane ^ r) & 63);
-          __builtin_amdgcn_global_load_lds(src, (lds_t*)(slot + (pl * PT_ROWS + r) * 1024), 16, 0, 0);
-        }
-    };
     const int nload = (a.dh_ext && !dzon ? 7 : 6) + (dzon ? 2 : 0);    // DMA instructions per iteration
     const __amdgpu_buffer_rsrc_t drs = pl_rsrc(a.dgates, (uint32_t)((size_t)K * B * G * 2));
     const __amdgpu_buffer_rsrc_t drsl = pl_rsrc(SP ? a.dgates_lo : a.dgates, (uint32_t)((size_t)K * B * G * 2));
@@ -1443,10 +1468,7 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
       if (lane == 0 && K <= PT_ITER_MAX)
         __hip_atomic_fetch_add(a.ctr + PT_ITER_OFF + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
-    io_load(0);
-    if (dzon) io_load_dz(0);
-    if (K > 1) io_load(1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // iterations 0, 1 (issued before the rendezvous)
     if (dzon) lds_sync();                 // barrier P: dz of iteration 0 landed (compute: dh_ext(0))
     for (int k = 0; k < K; ++k) {
       lds_sync();                         // barrier A_k: operands of k landed
@@ -1471,19 +1493,6 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   } else {
 
   // ================= compute waves 0..3
-  // W_hh^T fragments: N tile q of this wave = units (H/4)*wave + 16*q + (l&15); B[k][n] = Whh_pk[j][k][n]
-  bf16x8 wt[NTW][2], wtl[SP ? NTW : 1][2];
-#pragma unroll
-  for (int q = 0; q < NTW; ++q) {
-    const int n = (H / 4) * wave + 16 * q + (lane & 15);
-    const size_t o = ((size_t)j * H + n) * PL_GCOLS + 8 * (lane >> 4);
-#pragma unroll
-    for (int s = 0; s < 2; ++s) wt[q][s] = *(const bf16x8*)(a.whhT + o + 32 * s);
-    if constexpr (SP) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s) wtl[q][s] = *(const bf16x8*)(a.whhT_lo + o + 32 * s);
-    }
-  }
   const int prow = lane >> 2, pu = lane & 3;
   const int ul = 4 * wave + pu;
   const bool pv = mb * PT_ROWS + prow < B;

@@ -57,7 +57,15 @@ def arm(spec: str, reps: int = 3):
         it = d[2048:2048 + 40]
         it = it[it > 0]
         dit = np.diff(it) / 100.0
+        # recurrence workgroup (0, 0) is the one stamping iterations: find it as the recurrence
+        # block whose start is closest before the first iteration stamp
+        rec_start = rec[:, 0]
+        w00 = rec_start[rec_start <= it[0]].max() if len(it) and (rec_start <= it[0]).any() else rec_start.min()
         r = {"span_us": us(blk[blk[:, 2] > 0, 1].max() - t0),
+             "startup_us": us(it[0] - t0) if len(it) else None,
+             "first_iter_us": us(it[1] - it[0]) if len(it) > 1 else None,
+             "after_last_iter_us": us(rec[:, 1].max() - it[-1]) if len(it) else None,
+             "wg00_start_us": us(w00 - t0),
              "recurrence_end_us": us(rec[:, 1].max() - t0),
              "recurrence_start_spread_us": us(rec[:, 0].max() - rec[:, 0].min()),
              "iter_med_us": round(float(np.median(dit)), 3) if len(dit) else None,
