@@ -10,6 +10,7 @@
 // Gradient scale (1/world for DP averaging) and optional global-norm clipping are fused.
 #include "../common.h"
 #include "../pack_step.h"
+#include "../rms_pack.h"
 
 __global__ void rmsprop_centered_kernel(float* __restrict__ p, const float* __restrict__ g,
                                         float* __restrict__ sq, float* __restrict__ ga, int64_t n,
@@ -44,65 +45,11 @@ __global__ void rmsprop_centered_kernel(float* __restrict__ p, const float* __re
   }
 }
 
-// rmsprop_centered_kernel + the row packs (optimizer-side half of the repack, layout.py
-// bf_rows_begin): master float4 q also lands, as bf16 hi (and split-precision lo) planes, at
-// packed position dst4[q] (-1: packed by pack_step_kernel's gather instead); when the target sync
-// is due it writes the target master and the target packs too.  Same arithmetic as
-// rmsprop_centered_kernel (bit-identical master), one HBM pass fewer over the big LSTM / head
-// weights than update-then-gather.
-__global__ void rmsprop_pack_kernel(float* __restrict__ p, const float* __restrict__ g,
-                                    float* __restrict__ sq, float* __restrict__ ga, int64_t n,
-                                    float lr, float alpha, float eps, float gscale,
-                                    const float* __restrict__ clip_sumsq, float max_norm,
-                                    const int* __restrict__ dst4, bf16* __restrict__ bf,
-                                    bf16* __restrict__ bf_t, int64_t lo_off,
-                                    float* __restrict__ target, const int64_t* __restrict__ step,
-                                    int64_t interval) {
-  float scale = gscale;
-  if (clip_sumsq != nullptr && max_norm > 0.f) {
-    const float norm = sqrtf(*clip_sumsq) * gscale;
-    if (norm > max_norm) scale *= max_norm / (norm + 1e-6f);
-  }
-  const bool due = interval <= 1 || ((*step) + 1) % interval == 0;
-  const int64_t n4 = n >> 2;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
-    f32x4 pv = ((f32x4*)p)[i], gv = ((const f32x4*)g)[i];
-    f32x4 sv = ((f32x4*)sq)[i], av = ((f32x4*)ga)[i];
-    const int d = dst4[i];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float gr = gv[e] * scale;
-      sv[e] = alpha * sv[e] + (1.f - alpha) * gr * gr;
-      av[e] = alpha * av[e] + (1.f - alpha) * gr;
-      pv[e] -= lr * gr / (sqrtf(sv[e] - av[e] * av[e]) + eps);
-    }
-    ((f32x4*)p)[i] = pv;
-    ((f32x4*)sq)[i] = sv;
-    ((f32x4*)ga)[i] = av;
-    if (due) ((f32x4*)target)[i] = pv;
-    if (d >= 0) {
-      bf16x4 h, l;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        h[e] = (bf16)pv[e];
-        l[e] = (bf16)(pv[e] - (float)h[e]);
-      }
-      *(bf16x4*)(bf + d) = h;
-      if (lo_off) *(bf16x4*)(bf + lo_off + d) = l;
-      if (due) {
-        *(bf16x4*)(bf_t + d) = h;
-        if (lo_off) *(bf16x4*)(bf_t + lo_off + d) = l;
-      }
-    }
-  }
-  for (int64_t i = (n4 << 2) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
-    const float gr = g[i] * scale;
-    sq[i] = alpha * sq[i] + (1.f - alpha) * gr * gr;
-    ga[i] = alpha * ga[i] + (1.f - alpha) * gr;
-    p[i] -= lr * gr / (sqrtf(sq[i] - ga[i] * ga[i]) + eps);
-    if (due) target[i] = p[i];
-  }
+// rmsprop_centered_kernel + the row packs (rms_pack.h rmsprop_pack_items): same arithmetic
+// (bit-identical master), one HBM pass fewer over the big LSTM / head weights than
+// update-then-gather.
+__global__ void rmsprop_pack_kernel(const RmsPackArgs a) {
+  rmsprop_pack_items(a, blockIdx.x * (int64_t)blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
 }
 
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
@@ -198,11 +145,10 @@ extern "C" int r2_rmsprop_pack(float* p, const float* g, float* sq, float* ga, i
                                float alpha, float eps, float gscale, const float* clip_sumsq,
                                float max_norm, const int* dst4, bf16* bf, bf16* bf_t, int64_t lo_off,
                                float* target, const int64_t* step, int64_t interval, void* stream) {
-  if (((uintptr_t)p | (uintptr_t)g | (uintptr_t)sq | (uintptr_t)ga | (uintptr_t)target) & 15) return -1;
-  if ((((uintptr_t)bf | (uintptr_t)bf_t) & 7) || (lo_off & 3) || !dst4 || !step) return -1;
-  hipLaunchKernelGGL(rmsprop_pack_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream,
-                     p, g, sq, ga, n, lr, alpha, eps, gscale, clip_sumsq, max_norm, dst4, bf, bf_t,
-                     lo_off, target, step, interval);
+  const RmsPackArgs a{p, g, sq, ga, n, lr, alpha, eps, gscale, clip_sumsq, max_norm, dst4, bf, bf_t,
+                      lo_off, target, step, interval};
+  if (!rms_pack_args_ok(a)) return -1;
+  hipLaunchKernelGGL(rmsprop_pack_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, a);
   R2_CHECK_LAUNCH();
   return 0;
 }
