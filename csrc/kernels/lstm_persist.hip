@@ -959,6 +959,9 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
 #pragma unroll
       for (int gi = 0; gi < 4; ++gi) xv[gi] = xr[pt_swz64(prow, ul + 16 * gi)];
     }
+    // every fragment read issued before the first MFMA: the scheduler otherwise interleaves them
+    // just in time and exposes the LDS latency once per k-step pair (7 waits per step)
+    __builtin_amdgcn_sched_barrier(0);
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KS; s += 2) {
