@@ -59,6 +59,7 @@ __device__ __forceinline__ int tree_descend(const float* __restrict__ tree, cons
   const uint64_t ctr = step ? (uint64_t)(*step) : 0ull;
   float u = ((float)b + r2_uniform(seed, ctr, (uint64_t)b)) / (float)B * total;
   int64_t node = 0;
+  float leaf = 0.f;   // the picked leaf's value, already in hand at the last level
   for (int lvl = g.levels - 1; lvl >= 1; --lvl) {
     const int64_t c = node * 64 + lane;
     const float v = (c < g.size[lvl - 1]) ? tree[g.off[lvl - 1] + c] : 0.f;
@@ -76,8 +77,12 @@ __device__ __forceinline__ int tree_descend(const float* __restrict__ tree, cons
     const float pv = __shfl(v, pick, 64);
     u = fminf(fmaxf(u - ex, 0.f), pv * 0.99999f);
     node = node * 64 + pick;
+    leaf = pv;
   }
-  *prob = total > 0.f ? tree[node] / total : 0.f;
+  // leaf == tree[g.off[0] + node] (the level-1 pass loaded it): no dependent re-load of the leaf
+  // on the batch head's critical path
+  if (g.levels == 1) leaf = tree[g.off[0]];
+  *prob = total > 0.f ? leaf / total : 0.f;
   return (int)node;
 }
 
