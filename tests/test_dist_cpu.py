@@ -203,7 +203,7 @@ def test_weight_broadcast_over_actor_rank_group(tmp_path):
 
 def _link_worker(rank, world, port, outdir, slow_rank, rounds, steps):
     """Rank 0: a learner stand-in (2 ms of work per step, polling its record links between steps);
-    ranks 1..: actor stand-ins (2 ms of work per record, ``slow_rank`` 10 ms) that push `rounds`
+    ranks 1..: actor stand-ins (2 ms of work per record, ``slow_rank`` 30 ms) that push `rounds`
     records through a 4-slot LinkSender and take weight snapshots from rank 0 when they arrive."""
     import time
     _init(rank, world, port)
@@ -239,7 +239,7 @@ def _link_worker(rank, world, port, outdir, slow_rank, rounds, steps):
         got = []
         tx = LinkSender(f"rec/{rank}", 0, nb, 4, "cpu")
         wrx = LinkReceiver([f"w/{rank}"], [0], 64, "cpu", lambda i, buf: got.append(int(buf[0])), tag=1)
-        dt = 0.010 if rank == slow_rank else 0.002
+        dt = 0.030 if rank == slow_rank else 0.002
         for r in range(rounds):
             time.sleep(dt)                             # K env steps
             wrx.poll()
@@ -261,9 +261,13 @@ def _link_worker(rank, world, port, outdir, slow_rank, rounds, steps):
 
 def test_async_links_decouple_learner_from_slow_actor(tmp_path):
     """Split-topology transport (parallel/channel.py) over gloo, world 3 (1 learner + 2 actor
-    ranks): with one actor rank 5x slower the learner's step rate stays within 10 % of the run
+    ranks): with one actor rank 15x slower the learner's step rate stays within 30 % of the run
     with two fast actors (it never waits on a record), and every record of every actor arrives
-    exactly once, in order, intact; weight snapshots reach both actors in publication order."""
+    exactly once, in order, intact; weight snapshots reach both actors in publication order.
+    Margin: a learner coupled to the slow actor could not finish its 250 steps before that
+    actor's 60 records (>= 1.8 s, <= ~140 steps/s, under half the decoupled ~250-400 steps/s);
+    the decoupled runs differ only by link-poll overhead (store round trips, CPU load), which
+    moved the ratio to 0.83 with a 10 % bound and a 5x slower actor."""
     rounds, steps = 60, 250
     rates = {}
     # both jobs run at the same time (two worlds of 3), so they see the same background CPU load
@@ -286,4 +290,5 @@ def test_async_links_decouple_learner_from_slow_actor(tmp_path):
         for a in (1, 2):
             ra = torch.load(os.path.join(tmp_path, f"link{a}_{slow}.pt"), weights_only=True)
             assert ra["weights"] and ra["weights"] == sorted(ra["weights"])
-    assert rates[2] >= 0.9 * rates[0], rates
+    print("learner steps/s, fast actors vs one slow actor:", rates)
+    assert rates[2] >= 0.7 * rates[0], rates
