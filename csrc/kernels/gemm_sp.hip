@@ -95,11 +95,37 @@ struct G5Args {
   int item_base[gm::MAXP];
   long long slab_base[gm::MAXP];   // first partial slab (BM x BN fp32) of each problem
   int ticket_base[gm::MAXP];
+  int tiles_m[gm::MAXP];
   int np, total;
   int dbg;   // probe (r2_gemm5_set_mode bits 4-5): 1 = operand staging only, 2 = no staging
+  int order; // item order of K-split problems (g5_coords)
   float* ws;
   unsigned* tickets;
 };
+
+// item -> (tm, tn, ksp).  Blocks take contiguous item ranges per XCD (the remap in the kernels), so
+// the order decides which operand slices one XCD's L2 serves.  Tile-major (tn fastest, then the K
+// split): an XCD's items share A row blocks and stream every B column slice -- right for an
+// unsplit problem whose B is small (dX: W_ih).  order 1, K-split problems: K split slowest, then
+// tn, tm fastest: an XCD's items cover a few (B column slice, K range) pairs against every A row
+// block of that K range, so the big B of a weight gradient (X, h rows: K = B x T) is read by about
+// one XCD instead of by every XCD whose items span its columns
+__device__ __forceinline__ void g5_coords(const G5Args& a, int pi, int S, int item, int& tm,
+                                          int& tn, int& ksp) {
+  const GemmProb& P = a.p[pi];
+  if (a.order && S > 1) {
+    const int tms = a.tiles_m[pi];
+    tm = item % tms;
+    const int r = item / tms;
+    tn = r % P.tiles_n;
+    ksp = r / P.tiles_n;
+  } else {
+    const int tile = item / S;
+    ksp = item % S;
+    tm = tile / P.tiles_n;
+    tn = tile % P.tiles_n;
+  }
+}
 
 // K loop of one item: acc += A[m0.., k] B[k, n0..] over K tiles [kt0, kt1), NS-stage LDS ring,
 // every operand split (A_hi, A_lo, B_hi, B_lo staged; 3 MFMAs per fragment pair)
@@ -362,8 +388,9 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const G5Args a) {
   const GemmProb& P = a.p[pi];
   const int S = a.split[pi];
   const int item = bid - a.item_base[pi];
-  const int tile = item / S, ksp = item % S;
-  const int tm = tile / P.tiles_n, tn = tile % P.tiles_n;
+  int tm, tn, ksp;
+  g5_coords(a, pi, S, item, tm, tn, ksp);
+  const int tile = tm * P.tiles_n + tn;
   const int m0 = tm * BM, n0 = tn * BN;
   const int nk = (P.K + BK - 1) / BK, per = (nk + S - 1) / S;
   const int kt0 = min(nk, ksp * per), kt1 = min(nk, kt0 + per);
@@ -544,8 +571,9 @@ __global__ __launch_bounds__(512) void gemm6_kernel(const G5Args a) {
   const GemmProb& P = a.p[pi];
   const int S = a.split[pi];
   const int item = bid - a.item_base[pi];
-  const int tile = item / S, ksp = item % S;
-  const int tm = tile / P.tiles_n, tn = tile % P.tiles_n;
+  int tm, tn, ksp;
+  g5_coords(a, pi, S, item, tm, tn, ksp);
+  const int tile = tm * P.tiles_n + tn;
   const int m0 = tm * BM, n0 = tn * BN;
   const int nk = (P.K + BK - 1) / BK, per = (nk + S - 1) / S;
   const int kt0 = min(nk, ksp * per), kt1 = min(nk, kt0 + per);
@@ -835,8 +863,9 @@ __global__ __launch_bounds__(512) void gemm7_kernel(const G5Args a) {
   const GemmProb& P = a.p[pi];
   const int S = a.split[pi];
   const int item = bid - a.item_base[pi];
-  const int tile = item / S, ksp = item % S;
-  const int tm = tile / P.tiles_n, tn = tile % P.tiles_n;
+  int tm, tn, ksp;
+  g5_coords(a, pi, S, item, tm, tn, ksp);
+  const int tile = tm * P.tiles_n + tn;
   const int m0 = tm * BM, n0 = tn * BN;
   const int nk = P.K / 16, per = (nk + S - 1) / S;
   const int kt0 = min(nk, ksp * per), kt1 = min(nk, kt0 + per);
@@ -891,11 +920,15 @@ static void g6_kernel_launch(const G5Args& a, hipStream_t s) {
 
 static int g5_il = 1;   // interleaved fragment loads (r2_gemm5_set_mode)
 static int g5_dbg = 0;  // probe bits (G5Args::dbg)
+// K-split-major item order (g5_coords); r2_gemm5_set_mode bit 6 = the tile-major order instead.
+// Group of the paper config (tools/gemm_order_probe.py): 94-103 -> 92-96 us, bitwise-equal output
+static int g5_order = 1;
 extern "C" int r2_gemm5_set_mode(int m) {
   g5_il = m & 1;
   g6_off = (m >> 2) & 1;
   g7_on = (m >> 3) & 1;
   g5_dbg = (m >> 4) & 3;
+  g5_order = !((m >> 6) & 1);
   return 0;
 }
 
@@ -1027,14 +1060,18 @@ extern "C" int r2_gemm5(const int64_t* descs, const int* split, int np, int cfg,
     GemmProb& p = a.p[i];
     p.tiles_n = (p.N + bn - 1) / bn;
     const int t = g5_tiles(p, bm, bn);
+    a.tiles_m[i] = t / p.tiles_n;
     a.item_base[i] = items;
     a.slab_base[i] = slabs;
     a.ticket_base[i] = tks;
     items += t * a.split[i];
     if (a.split[i] > 1) { slabs += (long long)t * a.split[i]; tks += t; }
   }
-  for (int i = np; i < gm::MAXP; ++i) { a.p[i] = a.p[0]; a.split[i] = 1; a.item_base[i] = 1 << 30; }
+  for (int i = np; i < gm::MAXP; ++i) {
+    a.p[i] = a.p[0]; a.split[i] = 1; a.item_base[i] = 1 << 30; a.tiles_m[i] = 1;
+  }
   a.total = items;
+  a.order = g5_order;
   if (slabs * bm * bn * 4 > ws_bytes || tks > n_tickets) return -7;
   hipStream_t s = (hipStream_t)stream;
   // gemm6 (refilled fragment registers) for every configuration; gemm5 under r2_gemm5_set_mode

@@ -141,6 +141,11 @@ class LearnerConfig:
     # passes, one barrier per LDS tile; the heads' layer-1 GEMMs join the one-pass kernel too):
     # x-projection 115-129 -> 102-110 us, tools/gemm6_probe.py
     sp_gemm6: bool = True
+    # item order of K-split split GEMMs (gemm_sp.hip g5_coords): 0 = tile-major, 1 = K split
+    # slowest, tm fastest (a weight gradient's big B operand read by ~one XCD instead of several:
+    # post-BPTT group -2 us in the micro, step -4.5 us on the same box, bitwise-equal results;
+    # profiles/r05_gemm_item_order.txt)
+    sp_gemm_order: int = 1
     # split precision: the dueling head's gradient reduction on the BPTT launch's idle workgroups
     # (r2_lstm_bwd_tag_sp_hg) instead of its own 28 us launch
     sp_head_grads_in_bptt: bool = True

@@ -116,7 +116,10 @@ class LearnerEngine:
                 arr = (ctypes.c_int * 8)(*xcd_cus)
                 kernels().r2_set_xcd_cus(arr)
             kernels().r2_lstm_persist_force_slow(0 if cfg.learner.lstm_xcd_pairs else 2)
-            kernels().r2_gemm5_set_mode(1 | (0 if cfg.learner.sp_gemm6 else 4))
+            # gemm_sp.hip launcher mode: bit 0 interleaved fragment loads, bit 2 gemm5, bit 6 the
+            # tile-major item order instead of the K-split-major one
+            kernels().r2_gemm5_set_mode(1 | (0 if cfg.learner.sp_gemm6 else 4)
+                                        | (0 if cfg.learner.sp_gemm_order else 64))
         if init_module is None:
             torch.manual_seed(cfg.seed)
             init_module = QNet("cpu", m, e)
