@@ -1442,6 +1442,7 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   }
   const int fast = pl_same_xcd(a.ctr, mb, NWG, a.force_slow, a.err, &flag);
   if (fast < 0) return;
+  if (stamp && tid == 0) stamp[6] = (long long)__builtin_amdgcn_s_memrealtime();   // rendezvous done
   auto goff = [&](int slot, int src, int r, int unit) -> uint32_t {
     return (uint32_t)((((size_t)(slot * NWG + src) * rows_all + mb * PT_ROWS + r) * H + unit) * 8);
   };
@@ -1554,6 +1555,7 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   }
 
   const bool itrace = a.dbg && mb == 0 && j == 0 && tid == 0;
+  if (stamp && tid == 0) stamp[7] = (long long)__builtin_amdgcn_s_memrealtime();   // loop entry
   for (int k = 0; k < K; ++k) {
     const int t = T - 1 - k;
     if (itrace && k < 512) a.dbg[2048 + k] = (long long)__builtin_amdgcn_s_memrealtime();

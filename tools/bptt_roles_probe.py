@@ -68,6 +68,11 @@ def arm(spec: str, reps: int = 3):
              "wg00_start_us": us(w00 - t0),
              "recurrence_end_us": us(rec[:, 1].max() - t0),
              "recurrence_start_spread_us": us(rec[:, 0].max() - rec[:, 0].min()),
+             # per recurrence workgroup: start -> XCD rendezvous done -> loop entry (medians)
+             "rendezvous_med_us": us(np.median(rec[:, 6] - rec[:, 0])),
+             "rendezvous_max_us": us((rec[:, 6] - rec[:, 0]).max()),
+             "loop_entry_med_us": us(np.median(rec[:, 7] - rec[:, 0])),
+             "loop_entry_max_us": us((rec[:, 7] - rec[:, 0]).max()),
              "iter_med_us": round(float(np.median(dit)), 3) if len(dit) else None,
              "iter_max_us": round(float(dit.max()), 3) if len(dit) else None,
              "n_helpers": int(len(hlp))}
