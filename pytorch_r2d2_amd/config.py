@@ -146,6 +146,10 @@ class LearnerConfig:
     # post-BPTT group -2 us in the micro, step -4.5 us on the same box, bitwise-equal results;
     # profiles/r05_gemm_item_order.txt)
     sp_gemm_order: int = 1
+    # tile config of the heads' layer-1 split GEMM (ops/gemm.py G5_CFGS index; -1 = the
+    # launcher's CU model, which picks 128x128x64; same-box sweep: -1 0.943 / 0.945, 192x128x64
+    # 0.949 / 0.948, 256x128x32 0.959 / 0.958, 256x256x32 0.990 / 0.989 ms per step)
+    sp_heads_cfg: int = -1
     # split precision: the dueling head's gradient reduction on the BPTT launch's idle workgroups
     # (r2_lstm_bwd_tag_sp_hg) instead of its own 28 us launch
     sp_head_grads_in_bptt: bool = True

@@ -470,7 +470,8 @@ class LearnerEngine:
             probs = [Gemm(h, pk["head1"].t(), zb, a_lo=hl, b_lo=pkl["head1"].t())
                      for (pk, h, zb, _, _), (pkl, hl) in zip(jobs, lo)]
             if self.cfg.learner.sp_gemm6 and self.cfg.learner.sp_gemm == "fused":
-                self._gemm_sp("heads", probs, splits=[0] * len(probs), cfg=-1)   # gemm6
+                self._gemm_sp("heads", probs, splits=[0] * len(probs),
+                              cfg=int(self.cfg.learner.sp_heads_cfg))   # gemm6
             else:
                 gemm(*probs)
             zs = [zb for _, _, zb, _, _ in jobs]
