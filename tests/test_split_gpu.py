@@ -83,6 +83,40 @@ def test_split_gemm_split_output_and_group():
             assert _rel(p.c, r) < 2e-5
 
 
+@pytest.mark.parametrize("splits", [[3, 3, 3, 1], [4, 2, 1, 2]])
+def test_gemm_sp_item_orders_agree(splits):
+    """The fused split GEMM's two item orders (gemm_sp.hip g5_coords: tile-major, and the
+    K-split-major default) on the paper group's shapes: fp32-accurate and bitwise equal (the
+    split-K reduction sums the partial slabs in K order whatever order the items ran in)."""
+    from pytorch_r2d2_amd.ops._lib import kernels
+    from pytorch_r2d2_amd.ops.gemm import gemm_sp
+    g = torch.Generator(device=DEV).manual_seed(11)
+    probs, refs = [], []
+    for (M, N, K, ak) in [(1024, 1568, 2560, 0), (1024, 256, 2560, 0), (512, 256, 2560, 0),
+                          (2560, 1568, 1024, 1)]:
+        x = _op(M, K, 1, g) if ak else _op(K, M, 1, g).t()
+        y = _op(N, K, 0, g).t().contiguous()
+        xh, xl = _split(x)
+        yh, yl = _split(y)
+        probs.append(Gemm(xh, yh, torch.zeros(M, N, device=DEV), a_lo=xl, b_lo=yl))
+        refs.append(x.double() @ y.double())
+    k = kernels()
+    outs = {}
+    try:
+        for mode in (1 | 64, 1):                 # bit 6: tile-major; default: K-split-major
+            k.r2_gemm5_set_mode(mode)
+            for p in probs:
+                p.c.zero_()
+            gemm_sp(probs, splits=splits, cfg=6)
+            torch.cuda.synchronize()
+            outs[mode] = [p.c.clone() for p in probs]
+    finally:
+        k.r2_gemm5_set_mode(1)
+    for a, b, r in zip(outs[1 | 64], outs[1], refs):
+        assert torch.equal(a, b)
+        assert _rel(b, r) < 2e-5
+
+
 def _make(mode, B=16, preset="atari57", dtype="fp32", **kw):
     from pytorch_r2d2_amd.config import get_config
     from pytorch_r2d2_amd.engine.learner_engine import LearnerEngine
