@@ -594,314 +594,9 @@ __global__ __launch_bounds__(512) void gemm6_kernel(const G5Args a) {
   g5_epilogue<BM, BN>(a, P, pi, tile, ksp, S, m0, n0, acc, lds6, tid, wave, lane);
 }
 
-// ============================================================================================
-// gemm7: the split GEMM on a deep LDS-DMA ring (K tiles of 16, v_mfma_f32_32x32x16_bf16).
-//
-// gemm6 stages 32-deep K tiles of all four planes (56-64 KB per tile) into two LDS buffers, so
-// exactly one tile is in flight and every tile ends on a vmcnt(0) + barrier: PMC shows the MFMA
-// pipes ~41 % busy, waves parked 34 % of their cycles (profiles/r03_pmc_gemm6.txt), i.e. the
-// DMA latency of the next tile, not the arithmetic, sets the pace.  Here a tile is 16 deep
-// (28-32 KB) and the ring holds NS of them (4 x 32 KB at 256 x 256, 5 x 28 KB at 192 x 256): the
-// DMA of tile q + NS is issued as soon as tile q's slot is free (mid step q) and has NS - 1 steps
-// to land; the wait before each barrier is a COUNTED vmcnt (this wave's DMAs of the tiles still
-// allowed in flight), never 0 inside the loop.
-//
-//  * 8 waves = 2 (M) x 4 (N); wave tile (BM/2) x (BN/4) as (BM/64) x (BN/128) 32x32 accumulators.
-//    32x32x16 fragments read half the LDS bytes per MFMA FLOP of the 16x16x32 form.
-//  * a plane's k-major stage image is [row][32 B]; global chunk c (8 k) of row r sits in 16-B slot
-//    c ^ ((r >> 3) & 1) (applied through the DMA source address), which makes the fragment reads
-//    (lane = row r0 + (l & 31), chunk l >> 5) conflict-free in every ds_read_b128 lane group.
-//  * the three product passes and the register refill order are gemm6's (A hi.B lo, A hi.B hi,
-//    A lo.B hi); the one barrier per tile follows pass 1 (the tile's last LDS reads).
-//  * the stage's 1-KB DMA blocks (2 (BM + BN) / 32) are dealt to the waves round-robin; a wave
-//    counts only its own (dw = 3 or 4 per tile) in its vmcnt waits.
-//  * k-major A and B only (the x-projection); other layouts stay on gemm6.
-__device__ __forceinline__ void g7_vmwait(int v) {
-  switch (v) {   // wave-uniform: scalar branches outside the MFMA passes
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 13: asm volatile("s_waitcnt vmcnt(13)" ::: "memory"); break;
-    case 14: asm volatile("s_waitcnt vmcnt(14)" ::: "memory"); break;
-    case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-  }
-}
+// (gemm7, a deep LDS-DMA ring of 16-deep K tiles on 32x32x16 MFMAs, was measured slower than gemm6
+// on every shape and removed: profiles/r05_gemm7_deep_ring_rejected.txt)
 
-template <bool AK, bool BKM, int BM, int BN, int NS>
-__device__ __forceinline__ void g7_mainloop(const GemmProb& P, int m0, int n0, int kt0, int kt1,
-                                            uint8_t* lds, int wave, int lane,
-                                            f32x16 (&acc)[BM / 64][BN / 128], int dbg = 0) {
-  constexpr int FM = BM / 64, FN = BN / 128;
-  constexpr int PA = BM * 32, PB = BN * 32, STB = 2 * (PA + PB);
-  constexpr int NBA = BM / 32, NBB = BN / 32, NBLK = 2 * (NBA + NBB);
-  constexpr int DMAX = (NBLK + 7) / 8;
-  static_assert((NS - 1) * DMAX <= 16, "g7_vmwait covers vmcnt <= 16");
-  static_assert((AK || BM % 128 == 0) && (BKM || BN % 128 == 0), "mn-major images are 128-column halves");
-  const int wr = wave >> 2, wc = wave & 3;
-  const int dw = (NBLK - wave + 7) / 8;          // this wave's DMA blocks per tile
-  // per block: plane base (wave-uniform), this lane's element offset at k = 0 and the element
-  // stride of one K tile (16 for a k-major plane, 16 rows for an mn-major one)
-  const bf16* src[DMAX];
-  uint32_t off[DMAX], kst[DMAX];
-#pragma unroll
-  for (int i = 0; i < DMAX; ++i) {
-    const int b0 = wave + 8 * i, b = b0 < NBLK ? b0 : 0;
-    const bool isA = b < 2 * NBA;
-    const int pb = isA ? b % NBA : (b - 2 * NBA) % NBB;
-    const bool lo = isA ? b >= NBA : b >= 2 * NBA + NBB;
-    src[i] = isA ? (lo ? P.A_lo : P.A) : (lo ? P.B_lo : P.B);
-    const bool km = isA ? AK : BKM;
-    const int ld = isA ? P.lda : P.ldb, i0 = isA ? m0 : n0, imax = isA ? P.M : P.N;
-    if (km) {
-      // [row][32 B]: block = 32 rows, lane = (row, 16-B slot); slot s holds chunk s ^ ((r >> 3) & 1)
-      const int r = 32 * pb + (lane >> 1), c = (lane & 1) ^ ((r >> 3) & 1);
-      off[i] = (uint32_t)(min(i0 + r, imax - 1) * ld + 8 * c);
-      kst[i] = 16;
-    } else {
-      // [128-column half][16 k][256 B]: block = 4 k rows of one half; chunk c (8 columns) of
-      // k row kr at slot c ^ 4 (kr & 3) (gemm_tile.h g2_stage / g2_frag)
-      const int h = pb >> 2, kr = 4 * (pb & 3) + (lane >> 4), c = (lane & 15) ^ (4 * (kr & 3));
-      const int col = i0 + 128 * h + 8 * c;
-      off[i] = (uint32_t)(kr * ld + (col < imax ? col : imax - 8));
-      kst[i] = (uint32_t)(16 * ld);
-    }
-  }
-  auto stage = [&](int q) {     // tile q (relative to kt0) into slot q % NS
-    if (dbg & 2) return;        // probe: no staging
-    uint8_t* st = lds + (q % NS) * STB;
-    const uint32_t t = (uint32_t)(kt0 + q);
-#pragma unroll
-    for (int i = 0; i < DMAX; ++i)
-      if (i < dw) g6_dma(src[i] + (off[i] + t * kst[i]), st + (wave + 8 * i) * 1024);
-  };
-  // k-major fragment (row r0 + (l & 31), chunk l >> 5) of a [row][32 B] image, swizzled
-  const int lo_off = (lane & 31) * 32 + 16 * ((lane >> 5) ^ ((lane >> 3) & 1));
-  // mn-major fragment: two transposed 8-byte reads (gemm_tile.h g2_frag, one 16-deep k step)
-  const int mq = (lane >> 2) & 3, mp = lane & 3;
-  const int mn_off = (8 * (lane >> 5) + mq) * 256 + 8 * (mp & 1);
-  const int mn_c = 2 * ((lane >> 4) & 1) + (mp >> 1);
-  auto frag = [&](const uint8_t* pl, int r0, bool km) -> bf16x8 {
-    if (km) return *(const bf16x8*)(pl + r0 * 32 + lo_off);
-    const uint8_t* b0 = pl + (r0 >> 7) * 4096 + mn_off + ((((r0 & 127) >> 3) + mn_c) ^ (4 * mq)) * 16;
-    return gm_tr8((const bf16*)b0, (const bf16*)(b0 + 4 * 256));
-  };
-  bf16x8 ahi[FM], alo[FM], bhi[FN], blo[FN];
-  auto ldA = [&](bf16x8 (&f)[FM], int q, int plane) {
-    const uint8_t* pl = lds + (q % NS) * STB + plane * PA;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) f[i] = frag(pl, wr * (BM / 2) + 32 * i, AK);
-  };
-  auto ldB = [&](bf16x8 (&f)[FN], int q, int plane) {
-    const uint8_t* pl = lds + (q % NS) * STB + 2 * PA + plane * PB;
-#pragma unroll
-    for (int j = 0; j < FN; ++j) f[j] = frag(pl, wc * (BN / 4) + 32 * j, BKM);
-  };
-  const int nkt = kt1 - kt0;
-  if (nkt <= 0) return;
-  const int npro = nkt < NS ? nkt : NS;
-  for (int q = 0; q < npro; ++q) stage(q);
-  g7_vmwait((npro - 1) * dw);                    // tile 0 landed (this wave's part)
-  __builtin_amdgcn_s_barrier();                  // ... every wave's part
-  ldA(ahi, 0, 0);
-  ldB(blo, 0, 1);
-  if (dbg & 1) {   // probe: staging only (same waits and barriers, no fragment reads / MFMAs)
-    for (int q = 0; q + 1 < nkt; ++q) {
-      const int allow = (q + NS - 1 < nkt - 1 ? q + NS - 1 : nkt - 1) - (q + 1);
-      g7_vmwait(allow * dw);
-      __builtin_amdgcn_s_barrier();
-      if (q + NS < nkt) stage(q + NS);
-    }
-    return;
-  }
-  for (int q = 0; q < nkt; ++q) {
-    const bool more = q + 1 < nkt;
-    // pass 1: A hi x B lo; this tile's A lo / B hi arrive.  The first fragment row's MFMAs go
-    // out before the reads (pinned): issued ahead of them, the reads made the compiler's wait
-    // for the OLD operands (lgkmcnt, in order) also wait for the new reads
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[0][j] = mfma32(ahi[0], blo[j], acc[0][j]);
-    __builtin_amdgcn_sched_barrier(0);
-    ldA(alo, q, 1);
-    ldB(bhi, q, 0);
-#pragma unroll
-    for (int i = 1; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = mfma32(ahi[i], blo[j], acc[i][j]);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    if (more) {
-      // tile q+1 landed: of the tiles issued (up to min(q + NS - 1, nkt - 1)) all after q+1 may
-      // stay in flight; every wave past its reads of tile q (lgkmcnt) -> its slot is free
-      const int allow = (q + NS - 1 < nkt - 1 ? q + NS - 1 : nkt - 1) - (q + 1);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      g7_vmwait(allow * dw);
-      __builtin_amdgcn_s_barrier();
-      if (q + NS < nkt) stage(q + NS);
-    }
-    // pass 2: A hi x B hi; B lo <- tile q+1
-    if (more) ldB(blo, q + 1, 1);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = mfma32(ahi[i], bhi[j], acc[i][j]);
-    __builtin_amdgcn_s_setprio(0);
-    if (more) g6_mix<FN, FM * FN>(); else g6_mix<0, FM * FN>();
-    // pass 3: A lo x B hi; A hi <- tile q+1
-    if (more) ldA(ahi, q + 1, 0);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = mfma32(alo[i], bhi[j], acc[i][j]);
-    __builtin_amdgcn_s_setprio(0);
-    if (more) g6_mix<FM, FM * FN>(); else g6_mix<0, FM * FN>();
-  }
-}
-
-// gemm5's epilogue for the 32x32 accumulator layout: acc[i][j][r] = tile[wr*(BM/2) + 32i + (r&3)
-// + 8(r>>2) + 4(l>>5)][wc*(BN/4) + 32j + (l&31)]; 64 rows per LDS pass (row i of both wave rows)
-template <int BM, int BN>
-__device__ __forceinline__ void g7_epilogue(const G5Args& a, const GemmProb& P, int pi, int tile,
-                                            int ksp, int S, int m0, int n0,
-                                            const f32x16 (&acc)[BM / 64][BN / 128], uint8_t* lds7,
-                                            int tid, int wave, int lane) {
-  constexpr int FM = BM / 64, FN = BN / 128;
-  constexpr int LS = BN + 16;
-  const int wr = wave >> 2, wc = wave & 3;
-  int& last = *(int*)(lds7 + 64 * LS * 4);
-  float* L = (float*)lds7;
-  const int l32 = lane & 31, h = lane >> 5;
-  const bool vec = ((uintptr_t)P.C % 16 == 0) && (P.ldc % 4 == 0);
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.ws, 0, 0x7fffffff, 0x00020000);
-  const long long slab0 = a.slab_base[pi] + (long long)tile * S;
-  auto soff = [&](int s, int r, int c) {
-    return (uint32_t)((((slab0 + s) * BM + r) * BN + c) * 4);
-  };
-  auto put = [&](int p) {
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r)
-        L[(wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * LS + wc * (BN / 4) + 32 * j + l32] = acc[p][j][r];
-  };
-  if (S > 1) {
-#pragma unroll
-    for (int p = 0; p < FM; ++p) {
-      __builtin_amdgcn_s_barrier();
-      put(p);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      for (int q = tid; q < 64 * (BN / 4); q += 512) {
-        const int lr = q / (BN / 4), cc = (q % (BN / 4)) * 4;
-        const int r = (lr >> 5) * (BM / 2) + 32 * p + (lr & 31);
-        const f32x4 v = *(const f32x4*)(L + lr * LS + cc);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, soff(ksp, r, cc), 0, 16);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    unsigned* tk = a.tickets + a.ticket_base[pi] + tile;
-    if (tid == 0)
-      last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(S - 1);
-    __syncthreads();
-    if (!last) return;
-    for (int q = tid; q < BM * (BN / 4); q += 512) {
-      const int r = q / (BN / 4), cc = (q % (BN / 4)) * 4;
-      const int row = m0 + r, col = n0 + cc;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      for (int s = 0; s < S; ++s)
-        v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, soff(s, r, cc), 0, 16));
-      if (row < P.M && col < P.N) g5_emit(P, row, col, v, vec);
-    }
-    if (tid == 0) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-#pragma unroll
-  for (int p = 0; p < FM; ++p) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    put(p);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-#pragma unroll 2
-    for (int q = tid; q < 64 * (BN / 4); q += 512) {
-      const int lr = q / (BN / 4), cc = (q % (BN / 4)) * 4;
-      const int row = m0 + (lr >> 5) * (BM / 2) + 32 * p + (lr & 31);
-      const int col = n0 + cc;
-      if (row >= P.M || col >= P.N) continue;
-      g5_emit(P, row, col, *(const f32x4*)(L + lr * LS + cc), vec);
-    }
-  }
-}
-
-template <bool BKM, int BM, int BN, int NS>
-__global__ __launch_bounds__(512) void gemm7_kernel(const G5Args a) {
-  constexpr int FM = BM / 64, FN = BN / 128;
-  extern __shared__ __attribute__((aligned(1024))) uint8_t lds7[];
-  int bid;
-  {
-    const int b = blockIdx.x, x = b & 7, qn = a.total >> 3, r = a.total & 7;
-    bid = (x < r ? x * (qn + 1) : r * (qn + 1) + (x - r) * qn) + (b >> 3);
-  }
-  int pi = 0;
-#pragma unroll
-  for (int i = 1; i < gm::MAXP; ++i)
-    if (i < a.np && bid >= a.item_base[i]) pi = i;
-  const GemmProb& P = a.p[pi];
-  const int S = a.split[pi];
-  const int item = bid - a.item_base[pi];
-  int tm, tn, ksp;
-  g5_coords(a, pi, S, item, tm, tn, ksp);
-  const int tile = tm * P.tiles_n + tn;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int nk = P.K / 16, per = (nk + S - 1) / S;
-  const int kt0 = min(nk, ksp * per), kt1 = min(nk, kt0 + per);
-  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  f32x16 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-  if constexpr (BM % 128 == 0) {
-    if (P.a_kmajor) g7_mainloop<true, BKM, BM, BN, NS>(P, m0, n0, kt0, kt1, lds7, wave, lane, acc, a.dbg);
-    else g7_mainloop<false, BKM, BM, BN, NS>(P, m0, n0, kt0, kt1, lds7, wave, lane, acc, a.dbg);
-  } else {
-    g7_mainloop<true, BKM, BM, BN, NS>(P, m0, n0, kt0, kt1, lds7, wave, lane, acc, a.dbg);
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();            // every wave past its last LDS read / DMA before the epilogue
-  g7_epilogue<BM, BN>(a, P, pi, tile, ksp, S, m0, n0, acc, lds7, tid, wave, lane);
-}
-
-template <bool BKM, int BM, int BN, int NS>
-static void g7_kernel_launch(const G5Args& a, hipStream_t s) {
-  constexpr int LDS = NS * 2 * (BM + BN) * 32;
-  static_assert(LDS <= 160 * 1024 && 64 * (BN + 16) * 4 + 4 <= LDS, "LDS");
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)gemm7_kernel<BKM, BM, BN, NS>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    attr = true;
-  }
-  hipLaunchKernelGGL((gemm7_kernel<BKM, BM, BN, NS>), dim3(a.total), dim3(512), LDS, s, a);
-}
-
-static int g7_on = 0;    // r2_gemm5_set_mode bit 3: k-major launches on gemm7
 
 static int g6_off = 0;   // r2_gemm5_set_mode bit 2: every launch on gemm5
 
@@ -926,7 +621,6 @@ static int g5_order = 1;
 extern "C" int r2_gemm5_set_mode(int m) {
   g5_il = m & 1;
   g6_off = (m >> 2) & 1;
-  g7_on = (m >> 3) & 1;
   g5_dbg = (m >> 4) & 3;
   g5_order = !((m >> 6) & 1);
   return 0;
@@ -1078,23 +772,6 @@ extern "C" int r2_gemm5(const int64_t* descs, const int* split, int np, int cfg,
   // bit 2 or the probe bits.  gemm6's fast staging (k-major A and B, BK 32) has no K tail.
   bool k32 = true;
   for (int i = 0; i < np; ++i) k32 = k32 && a.p[i].K % 32 == 0;
-  // gemm7 (deep DMA ring, 16-deep K tiles): K % 16 == 0, the 192 x 256 (k-major A) and
-  // 256 x 256 tiles; an mn-major operand's extent a multiple of 8 (whole 16-B chunks)
-  bool g7ok = g7_on && (cfg == 3 || (cfg == 7 && all_k));
-  for (int i = 0; i < np; ++i) {
-    const GemmProb& p = a.p[i];
-    g7ok = g7ok && p.K % 16 == 0 && (p.a_kmajor || p.M % 8 == 0) && (p.b_kmajor || p.N % 8 == 0);
-  }
-  if (g7ok) {
-    switch (cfg * 2 + bkm) {
-      case 6: g7_kernel_launch<false, 256, 256, 4>(a, s); break;
-      case 7: g7_kernel_launch<true, 256, 256, 4>(a, s); break;
-      case 14: g7_kernel_launch<false, 192, 256, 5>(a, s); break;
-      default: g7_kernel_launch<true, 192, 256, 5>(a, s); break;
-    }
-    R2_CHECK_LAUNCH();
-    return cfg;
-  }
   if (!g6_off && !a.dbg && (k32 || !(bkm && all_k))) {
     switch (cfg * 2 + bkm) {
       case 0: g6_kernel_launch<false, 192, 128, 64>(a, s); break;
