@@ -229,7 +229,6 @@ __device__ __forceinline__ void c1_frags(const uint8_t* dig, int lane, bf16x8 (&
 __constant__ int c_s2_begin[8] = {0, 2, 4, 4, 6, 8, 10, 11};
 __constant__ int c_s2_count[8] = {2, 2, 0, 2, 2, 2, 1, 2};
 
-template <int C2P>
 __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
   using namespace tsp2;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -521,26 +520,15 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
 #pragma unroll
         for (int s = 0; s < D; ++s) ld(s, rah[s], ral[s], rbh[s], rbl[s]);
         f32x16 acc = {};
-        // C2P 0: the conv2 K loop; probe instances (r2_torso_sp_debug bits 9 / 10): 1 = MFMAs on the
-        // first two steps' operands (no LDS reads after them), 2 = the LDS reads with ONE MFMA per
-        // step instead of three
-        auto kloop = [&](auto mode) {
-          constexpr int MODE = decltype(mode)::value;
+        // the conv2 K loop (its LDS reads cost ~25 us of the launch against MFMAs alone, measured
+        // with probe instances that are gone now: profiles/r05_torso_act1_s2d.txt)
 #pragma unroll
-          for (int s = 0; s < 32; ++s) {
-            const bf16x8 xah = rah[s % D], xal = ral[s % D], xbh = rbh[s % D], xbl = rbl[s % D];
-            if (s + D < 32 && MODE != 1) ld(s + D, rah[s % D], ral[s % D], rbh[s % D], rbl[s % D]);
-            __builtin_amdgcn_sched_barrier(0);
-            if constexpr (MODE == 2)
-              acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                  __builtin_bit_cast(bf16x8, __builtin_bit_cast(u32x4, xah) ^ __builtin_bit_cast(u32x4, xal)),
-                  __builtin_bit_cast(bf16x8, __builtin_bit_cast(u32x4, xbh) ^ __builtin_bit_cast(u32x4, xbl)),
-                  acc, 0, 0, 0);
-            else
-              acc = mfma32_x3(xah, xal, xbh, xbl, acc);
-          }
-        };
-        kloop(std::integral_constant<int, C2P>{});
+        for (int s = 0; s < 32; ++s) {
+          const bf16x8 xah = rah[s % D], xal = ral[s % D], xbh = rbh[s % D], xbl = rbl[s % D];
+          if (s + D < 32) ld(s + D, rah[s % D], ral[s % D], rbh[s % D], rbl[s % D]);
+          __builtin_amdgcn_sched_barrier(0);
+          acc = mfma32_x3(xah, xal, xbh, xbl, acc);
+        }
         if (!dup) {
           bf16* d2 = J.s2 ? J.s2 + ((size_t)f * P2 + p) * 32 : nullptr;
           bf16* d2l = J.s2 ? J.s2l + ((size_t)f * P2 + p) * 32 : nullptr;
@@ -593,7 +581,7 @@ static long long* g_tsp_trace = nullptr;
 // phase B done, barrier), s_memrealtime-free cycle counter
 extern "C" int r2_torso_sp_trace(long long* p) { g_tsp_trace = p; return 0; }
 // timing probes only (tools/sp_micro.py): bit 0 skips conv1, bit 1 conv2, bit 2 conv3, bit 4 the
-// next-frame staging, bit 6 the act1 save; bits 9 / 10 the conv2 probe instances
+// next-frame staging, bit 6 the act1 save
 extern "C" int r2_torso_sp_debug(int bits) { g_tsp_dbg = bits; return 0; }
 
 extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs, int njobs,
@@ -634,24 +622,12 @@ extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs,
   if (grid > wb) grid = wb;
   static bool attr2 = false;
   if (!attr2) {
-    hipFuncSetAttribute((const void*)torso_fwd_sp2_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        tsp2::LDS_BYTES_I8);
-    hipFuncSetAttribute((const void*)torso_fwd_sp2_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        tsp2::LDS_BYTES_I8);
-    hipFuncSetAttribute((const void*)torso_fwd_sp2_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipFuncSetAttribute((const void*)torso_fwd_sp2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                         tsp2::LDS_BYTES_I8);
     attr2 = true;
   }
-  // bits 9 / 10: the conv2 probe instances (timing only, outputs garbage)
-  if (a.dbg & 512)
-    hipLaunchKernelGGL(torso_fwd_sp2_kernel<1>, dim3(grid), dim3(tsp::NT), tsp2::LDS_BYTES_I8,
-                       (hipStream_t)stream, a);
-  else if (a.dbg & 1024)
-    hipLaunchKernelGGL(torso_fwd_sp2_kernel<2>, dim3(grid), dim3(tsp::NT), tsp2::LDS_BYTES_I8,
-                       (hipStream_t)stream, a);
-  else
-    hipLaunchKernelGGL(torso_fwd_sp2_kernel<0>, dim3(grid), dim3(tsp::NT), tsp2::LDS_BYTES_I8,
-                       (hipStream_t)stream, a);
+  hipLaunchKernelGGL(torso_fwd_sp2_kernel, dim3(grid), dim3(tsp::NT), tsp2::LDS_BYTES_I8,
+                     (hipStream_t)stream, a);
   R2_CHECK_LAUNCH();
   return 0;
 }

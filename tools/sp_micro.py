@@ -82,8 +82,6 @@ if which in ("torso", "both"):
         # rounds, min of the per-round means (single back-to-back timings drift by +-15 %)
         variants = ((0, "full"), (1, "no_conv1"), (2, "no_conv2"), (4, "no_conv3"),
                     (7, "none"), (16, "no_frame"), (64, "no_save"), (119, "nothing"),
-                    (512, "conv2_mfma_only"), (1024, "conv2_reads_only"),
-                    (512 | 1 | 4, "conv2_mfma_only_alone"), (1024 | 1 | 4, "conv2_reads_only_alone"),
                     (1 | 4, "conv2_alone"))
         best = {}
         for _ in range(7):
