@@ -539,6 +539,8 @@ static bool pl_xcd_fit(int xcd_map, int groups, int nwg, bool full = false) {
 }
 
 static long long* g_pl_dbg = nullptr;
+static long long* g_pl_fwd_stamps = nullptr;   // tagged forward: >= 4 x grid words
+extern "C" int r2_lstm_fwd_set_stamps(long long* p) { g_pl_fwd_stamps = p; return 0; }
 static int g_pl_slow = 0;
 extern "C" int r2_lstm_persist_set_debug(long long* p) { g_pl_dbg = p; return 0; }
 static int g_pl_nomap2 = 0;
@@ -663,6 +665,7 @@ struct PTArgs {
   unsigned* ctr;
   unsigned* err;
   long long* dbg;
+  long long* stamps;   // optional per-workgroup startup stamps (4 per block of the grid)
   void* ring;     // (chains, 2, MB*16, H/2) granules
   int MB, groups, xcd_map, force_slow;
 };
@@ -731,6 +734,10 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
   __shared__ int flag;
   int g, j;
   if (!pl_decode(a.xcd_map, a.groups, NWG, g, j)) return;
+  // per-workgroup clock stamps (r2_lstm_fwd_set_stamps, tools/lstm_startup_probe.py): stamps[4 b +
+  // {0 start, 1 rendezvous done, 2 compute loop entry, 3 end}] (s_memrealtime, 100 MHz)
+  long long* const wst = a.stamps ? a.stamps + 4 * blockIdx.x : nullptr;
+  if (wst && threadIdx.x == 0) wst[0] = (long long)__builtin_amdgcn_s_memrealtime();
   const int MB = a.MB, mb = g % MB, chn = g / MB;
   const PChain& cd = a.ch[chn];
   const int B = a.B, T = a.T;
@@ -775,6 +782,7 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
   }
   const int fast = pl_same_xcd(a.ctr, g, NWG, a.force_slow, a.err, &flag);
   if (fast < 0) return;
+  if (wst && tid == 0) wst[1] = (long long)__builtin_amdgcn_s_memrealtime();
   if (a.dbg && tid == 0) {
     unsigned x;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
@@ -857,6 +865,7 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
   const bool trace = a.dbg && g == 0 && j == 0 && tid == 0;
 #define PT_TRACE(k) \
   if (trace && t < 32) a.dbg[t * 8 + (k)] = clock64();
+  if (wst && tid == 0) wst[2] = (long long)__builtin_amdgcn_s_memrealtime();
 
   for (int t = 0; t < T; ++t) {
     PT_TRACE(0);
@@ -1036,6 +1045,7 @@ __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
   }
 #undef PT_TRACE
   lds_sync();                                     // barrier T: outputs of step T-1 complete
+  if (wst && tid == 0) wst[3] = (long long)__builtin_amdgcn_s_memrealtime();
   // the last workgroup to finish advances the epoch (every workgroup read it before any
   // finished) and clears the counters
   if (tid == 0) pt_finish(a.ctr, a.groups, a.groups * NWG, PT_EPOCH_FWD);
@@ -1078,6 +1088,7 @@ static int lstm_fwd_tag_launch(const int64_t* chain_ptrs, int words, int n_chain
     if (SP && (!ch.whh_lo || !ch.h_seq_lo)) return -5;
   }
   args.B = B; args.T = T; args.ctr = ctr; args.err = err; args.dbg = g_pl_dbg; args.ring = ring;
+  args.stamps = g_pl_fwd_stamps;
   // group -> XCD placement (workgroup b runs on XCD b % 8): one group per XCD up to 8 groups,
   // two per XCD up to 16 (the fixed-target step's 3 chains x 4 batch tiles = 12 groups), so a
   // group's h hand-off stays in one XCD's L2 (pl_same_xcd: plain stores, L2-hit polls) instead

@@ -99,6 +99,7 @@ _SIGS = {
     "r2_torso_bwd_set_debug": [P],
     "r2_torso_fwd_set_debug": [P],
     "r2_lstm_persist_set_debug": [P],
+    "r2_lstm_fwd_set_stamps": [P],
     "r2_lstm_sp_handoff8": [I],
     "r2_lstm_bwd_handoff8": [I],
     "r2_td_duel_fwd_set": [P],
