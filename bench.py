@@ -142,6 +142,10 @@ def main(argv=None):
         dist.barrier()
     dt = time.perf_counter() - t0
     err = eng.error_word()
+    hoisted = None
+    if getattr(eng, "hoist", False):   # target-net frames the last step's side launch computed
+        n_tg = (eng.Tn - eng.t_lo_tg) * eng.B
+        hoisted = [min(int(eng.tq[0].item()), n_tg), n_tg]
     if world > 1:
         tt = torch.tensor([dt, float(err)], device=device, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -190,6 +194,9 @@ def main(argv=None):
                 "parallelism": "dp%d" % world + ("-shared-gpu-gloo-rehearsal" if shared else "")
                                + ("-forced-dp-rehearsal" if args.force_dp and world == 1 else ""),
                 "hip_graph": bool(use_graph),
+                # step k's priority tail, step k+1's sample and part of its target-net torso
+                # run on a side stream beside step k's BPTT (learner.hoist; bit-identical)
+                "hoisted_step": bool(getattr(eng, "hoist", False)),
                 "dp_graph": ("one graph, RCCL captured" if getattr(eng, "_one_dp_graph", False)
                              else "segment graphs") if eng.dp else None,
             },
@@ -201,6 +208,8 @@ def main(argv=None):
         }
         if phases is not None:
             out["phases_ms"] = phases
+        if hoisted is not None:
+            out["hoisted_target_frames"] = hoisted
         print(json.dumps(out), flush=True)
     if use_pg:
         dist.destroy_process_group()

@@ -32,7 +32,6 @@
 #include "../common.h"
 #include "../split.h"
 #include "../gradsum.h"
-#include "../gemm_tile.h"
 
 #define PL_UNITS 16
 #define PL_GCOLS 64
@@ -56,14 +55,7 @@
 #define PT_MEMSET_WORDS (PL_CTR_WORDS + 32)
 #define PT_EPOCH_FWD (PL_CTR_WORDS + 32)
 #define PT_EPOCH_BWD (PL_CTR_WORDS + 64)
-// BPTT progress for helper workgroups: word k counts the recurrence workgroups whose dgates of
-// iteration k are stored (exact per-iteration counts: a sum over iterations would let a fast
-// group hide a slow one); reset by the last workgroup
-// dX tile queue of the BPTT's split-precision helpers (atomic dequeue; reset by the last workgroup)
-#define PT_DXQ_OFF (PL_CTR_WORDS + 96)
-#define PT_ITER_OFF (PL_CTR_WORDS + 128)
-#define PT_ITER_MAX 512
-#define PT_CTR_WORDS (PL_CTR_WORDS + 128 + PT_ITER_MAX)
+#define PT_CTR_WORDS (PL_CTR_WORDS + 96)
 
 struct PChain {
   const float* xproj;  // (T, B, G) packed, chain-local time
@@ -643,8 +635,7 @@ extern "C" int r2_lstm_bwd_persist(const float* dh_ext, const float* gates, cons
 // advances the launch epoch and returns the counter words (XCD masks / arrivals of `groups`
 // groups, the done ticket) to zero, so the next launch needs no memset node.  Returns true in the
 // last workgroup.
-__device__ __forceinline__ bool pt_finish(unsigned* ctr, int groups, int total_wgs, int epoch_off,
-                                          int n_iter = 0) {
+__device__ __forceinline__ bool pt_finish(unsigned* ctr, int groups, int total_wgs, int epoch_off) {
   const unsigned done = __hip_atomic_fetch_add(ctr + PT_DONE_OFF, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (done != (unsigned)total_wgs - 1) return false;
   for (int g = 0; g < groups; ++g) {
@@ -652,9 +643,6 @@ __device__ __forceinline__ bool pt_finish(unsigned* ctr, int groups, int total_w
     __hip_atomic_store(ctr + PL_OFF_ARRIVE + g * PL_CTR_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __hip_atomic_store(ctr + PT_DONE_OFF, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(ctr + PT_DXQ_OFF, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  for (int k = 0; k < n_iter; ++k)
-    __hip_atomic_store(ctr + PT_ITER_OFF + k, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_fetch_add(ctr + epoch_off, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return true;
 }
@@ -1176,14 +1164,12 @@ struct PTBArgs {
   // optional side job for the idle workgroups (groups >= MB of the XCD map, i.e. XCDs the
   // recurrence does not use): the dueling head's gradient reduction, (CB x 8) work items
   HeadGradArgs hg;
-  int hg_on;
-  // optional GEMMs beside the recurrence, on helper workgroups (the grid grows to 8 x 32):
-  // gw[0..n_gw) weight-gradient problems (mn-major A and B, K = the time-major learning rows;
-  // bit i of gw_wait: problem i reads dgates and waits for the BPTT per 64-row K tile),
-  // gx = dX (rows = time-major learning rows, waits per 128-row tile), when gx_on.
-  GemmProb gw[3];
-  int n_gw, gw_wait, gx_on, n_wtiles;
-  GemmProb gx;
+  int hg_on, hg_wgs;    // hg_wgs: helpers that take head-gradient items (the rest leave at once)
+  // optional stop word (r2_lstm_bwd_set_stop): workgroup (0, 0) stores 0 at iteration 0 and 1 at
+  // iteration stop_at -- the hoisted target-net torso frames beside this launch (torso_sp.hip
+  // qmode 1) stop taking frames then, so they end about when the recurrence does
+  unsigned* stop;
+  int stop_at, pad2_;
   // split precision (the _sp launcher): W_hh^T lo plane; dgates lo plane out
   const bf16* whhT_lo;
   bf16* dgates_lo;
@@ -1250,124 +1236,25 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   if (!pl_decode(a.xcd_map, a.MB, NWG, mb, j)) {
     // ================= helper workgroup (4 waves): work beside the recurrence
     if (wave == 4) return;                 // helpers run 256 threads (barriers: surviving waves)
-    long long waited_ticks = 0;
-    int dx_tiles = 0;
     const int b = blockIdx.x, g = b & 7, jj = b >> 3;
     const int h = b - (min(jj, NWG) * a.MB + (jj < NWG ? min(g, a.MB) : 0));   // helper ordinal
     const int nh = (int)gridDim.x - a.MB * NWG;
-    const unsigned nbptt = (unsigned)(a.MB * NWG);
-    // rows [row_lo, row_hi) (time-major: row = tl * B + b) are stored once BPTT iterations
-    // K-1-tl are complete on every recurrence workgroup, for every tl they touch
-    // One lane polls, the workgroup's other waves wait at a barrier: 192 helpers x 4 waves
-    // polling the iteration counters themselves slowed the recurrence's hand-offs 1.8x
-    // (tools/bptt_roles_probe.py).  Called uniformly by all 4 waves.
-    auto wait_rows = [&](int row_lo, int row_hi) {
-      const long long w0 = stamp ? (long long)__builtin_amdgcn_s_memrealtime() : 0;
-      const int tl_hi = (min(row_hi, K * B) - 1) / B;
-      if (tid == 0) {
-        for (int tl = row_lo / B; tl <= tl_hi; ++tl) {
-          unsigned* w = a.ctr + PT_ITER_OFF + (K - 1 - tl);
-          unsigned spins = 0;
-          while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nbptt) {
-            __builtin_amdgcn_s_sleep(8);
-            if (++spins > PL_SPIN_LIMIT) {
-              __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              break;
-            }
-          }
-        }
-      }
-      __builtin_amdgcn_s_barrier();
-      if (stamp) waited_ticks += (long long)__builtin_amdgcn_s_memrealtime() - w0;
-    };
-    if (SP) {
-      // split precision (PTBArgs::gw / gx with hi / lo planes): helpers 0 .. n_wtiles-1 own one
-      // weight-gradient tile each for the whole BPTT, all three products per 32-row K tile in
-      // BPTT order (g2s_tile_acc: each K tile as soon as its dgates rows are stored); every helper
-      // then dequeues dX tiles, latest rows (first produced) first
-      const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-      if (h < a.n_wtiles) {
-        int item = h, pi = 0;
-        while (pi + 1 < a.n_gw) {
-          const int nt = a.gw[pi].tiles_n * ((a.gw[pi].M + 127) / 128);
-          if (item < nt) break;
-          item -= nt;
-          ++pi;
-        }
-        const GemmProb& P = a.gw[pi];
-        const bool wt = (a.gw_wait >> pi) & 1;
-        const int tm = item / P.tiles_n, tn = item % P.tiles_n;
-        f32x16 acc[2][2] = {};
-        g2s_tile_acc<false, false, 16, 0, 3>(P, tm, tn, pt_dyn, 0, P.K / 32, true,
-                                             [&](int kt) { if (wt) wait_rows(32 * kt, 32 * kt + 32); }, acc);
-        g2_epilogue_lds(P, tm * 128, tn * 128, wm, wn, lane, acc, pt_dyn);
-        if (stamp && tid == 0) stamp[5] = (long long)__builtin_amdgcn_s_memrealtime();
-      } else if (a.hg_on) {   // the head-gradient reduction first (independent of the BPTT)
-        const int hx = h - a.n_wtiles, nx = nh - a.n_wtiles;
-        const int cbn = (2 * a.hg.HD + 63) / 64;
-        for (int it = hx; it < cbn * a.hg.RS * a.hg.NP; it += nx)
-          head_grads_body(a.hg, it % cbn, (it / cbn) % a.hg.RS, it / (cbn * a.hg.RS));
-      }
-      if (stamp && tid == 0) stamp[5] = (long long)__builtin_amdgcn_s_memrealtime();
-      if (a.gx_on) {
-        const GemmProb& P = a.gx;
-        const int tmn = (P.M + 127) / 128, total = tmn * P.tiles_n;
-        __shared__ int dxq;
-        for (;;) {
-          if (tid == 0)
-            dxq = (int)__hip_atomic_fetch_add(a.ctr + PT_DXQ_OFF, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __builtin_amdgcn_s_barrier();
-          const int it = dxq;
-          __builtin_amdgcn_s_barrier();
-          if (it >= total) break;
-          const int tm = tmn - 1 - it / P.tiles_n, tn = it % P.tiles_n;
-          f32x16 acc[2][2] = {};
-          bool waited = false;
-          g2s_tile_acc<true, false, 16, 0, 3>(P, tm, tn, pt_dyn, 0, P.K / 32, false, [&](int) {
-            if (!waited) { wait_rows(128 * tm, 128 * tm + 128); waited = true; }
-          }, acc);
-          g2_epilogue_lds(P, tm * 128, tn * 128, wm, wn, lane, acc, pt_dyn);
-          ++dx_tiles;
-        }
-      }
-    } else if (h < a.n_wtiles) {
-      // one weight-gradient tile, K tiles in BPTT order (latest time step first)
-      int item = h, pi = 0;
-      while (pi + 1 < a.n_gw) {
-        const int nt = a.gw[pi].tiles_n * ((a.gw[pi].M + 127) / 128);
-        if (item < nt) break;
-        item -= nt;
-        ++pi;
-      }
-      const GemmProb& P = a.gw[pi];
-      const bool wt = (a.gw_wait >> pi) & 1;
-      g2_tile<false, false, 16>(P, item / P.tiles_n, item % P.tiles_n, pt_dyn, true,
-                                [&](int kt) { if (wt) wait_rows(64 * kt, 64 * kt + 64); });
-    } else {
-      const int hx = h - a.n_wtiles, nx = nh - a.n_wtiles;
-      if (a.hg_on) {
-        const int cbn = (2 * a.hg.HD + 63) / 64;
-        for (int it = hx; it < cbn * a.hg.RS * a.hg.NP; it += nx)
-          head_grads_body(a.hg, it % cbn, (it / cbn) % a.hg.RS, it / (cbn * a.hg.RS));
-      }
-      if (a.gx_on) {
-        // dX tiles, latest rows (first produced) first
-        const GemmProb& P = a.gx;
-        const int tmn = (P.M + 127) / 128, total = tmn * P.tiles_n;
-        for (int it = hx; it < total; it += nx) {
-          const int tm = tmn - 1 - it / P.tiles_n, tn = it % P.tiles_n;
-          g2_tile<true, false, 16>(P, tm, tn, pt_dyn, false,
-                                   [&](int) { wait_rows(128 * tm, 128 * tm + 128); });
-        }
-      }
+    // the dueling head's gradient reduction (independent of the BPTT) on the first a.hg_wgs
+    // helpers; the others leave at once and free their CUs (the hoisted target-net torso frames
+    // of the next step run there, engine/learner_engine.py).  Round 5's GEMM helpers (dX / weight
+    // gradients on these workgroups) slowed the recurrence in every arm and are gone
+    // (profiles/r05_bptt_helpers_roles.txt).
+    if (a.hg_on && h < min(nh, a.hg_wgs)) {
+      const int nx = min(nh, a.hg_wgs);
+      const int cbn = (2 * a.hg.HD + 63) / 64;
+      for (int it = h; it < cbn * a.hg.RS * a.hg.NP; it += nx)
+        head_grads_body(a.hg, it % cbn, (it / cbn) % a.hg.RS, it / (cbn * a.hg.RS));
     }
     if (stamp && tid == 0) {
       stamp[1] = (long long)__builtin_amdgcn_s_memrealtime();
       stamp[2] = 2;
-      stamp[3] = waited_ticks;
-      stamp[4] = dx_tiles;
     }
-    if (tid == 0) flag = pt_finish(a.ctr, a.MB, (int)gridDim.x, PT_EPOCH_BWD, K) ? 1 : 0;
+    if (tid == 0) flag = pt_finish(a.ctr, a.MB, (int)gridDim.x, PT_EPOCH_BWD) ? 1 : 0;
     __syncthreads();
     if (flag && a.bias_ws) {
       for (int c = tid; c < G; c += 256) {
@@ -1479,10 +1366,6 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
         }
       }
     };
-    auto io_progress = [&](int k) {    // after this wave's dgates stores of iteration k completed
-      if (lane == 0 && K <= PT_ITER_MAX)
-        __hip_atomic_fetch_add(a.ctr + PT_ITER_OFF + k, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // iterations 0, 1 (issued before the rendezvous)
     if (dzon) lds_sync();                 // barrier P: dz of iteration 0 landed (compute: dh_ext(0))
     for (int k = 0; k < K; ++k) {
@@ -1499,12 +1382,10 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      if (k >= 1) io_progress(k - 1);    // the stores of iteration k-1 are complete
     }
     lds_sync();                           // barrier E: dgates of the last iteration complete
     io_store(K - 1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    io_progress(K - 1);
   } else {
 
   // ================= compute waves 0..3
@@ -1567,9 +1448,14 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
 
   const bool itrace = a.dbg && mb == 0 && j == 0 && tid == 0;
   if (stamp && tid == 0) stamp[7] = (long long)__builtin_amdgcn_s_memrealtime();   // loop entry
+  const bool stopper = a.stop && mb == 0 && j == 0 && tid == 0;
   for (int k = 0; k < K; ++k) {
     const int t = T - 1 - k;
     if (itrace && k < 512) a.dbg[2048 + k] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (stopper) {
+      if (k == 0) __hip_atomic_store(a.stop, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (k == a.stop_at) __hip_atomic_store(a.stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (T4 && k > 0) {
       const unsigned want = ((ep & 1u) << 3) | ((unsigned)k & 7u);
       const int slot = (k - 1) & 1;
@@ -1765,7 +1651,7 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   // ---- every wave (compute and I/O): done ticket; the last workgroup sums the bias partials in
   // tile order and clears the counters
   lds_sync();                             // barrier F: the I/O wave's last stores + progress done
-  if (tid == 0) flag = pt_finish(a.ctr, a.MB, (int)gridDim.x, PT_EPOCH_BWD, K) ? 1 : 0;
+  if (tid == 0) flag = pt_finish(a.ctr, a.MB, (int)gridDim.x, PT_EPOCH_BWD) ? 1 : 0;
   lds_sync();                             // barrier G
   if (flag && a.bias_ws && tid < 256) {
     for (int c = tid; c < G; c += 256) {
@@ -1779,32 +1665,25 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
   }
 }
 
-// lo planes handed from r2_lstm_bwd_tag_sp to the shared launcher body (host-side, per call)
-static const bf16* g_bwd_whhT_lo = nullptr;
-// split-precision head-gradient side job operands (r2_lstm_bwd_tag_sp_hg): zr fp32, dz lo plane
-static const float* g_bwd_hg_zr32 = nullptr;
-static const bf16* g_bwd_hg_dz_lo = nullptr;
-static bf16* g_bwd_dgates_lo = nullptr;
-
-// split-precision helper GEMMs (PTBArgs::gw / gx): problems for the next r2_lstm_bwd_tag_sp*
-// call on this host thread (consumed by it): n_gw weight-gradient descriptors then (gx_on) dX
-static thread_local const int64_t* g_bwd_gemms = nullptr;
-static thread_local int g_bwd_n_gw = 0, g_bwd_gw_wait = 0, g_bwd_gx_on = 0;
-extern "C" int r2_lstm_bwd_set_gemms(const int64_t* descs, int n_gw, int gw_wait, int gx_on) {
-  g_bwd_gemms = descs;
-  g_bwd_n_gw = descs ? n_gw : 0;
-  g_bwd_gw_wait = gw_wait;
-  g_bwd_gx_on = descs ? gx_on : 0;
-  return 0;
-}
-
 // in-BPTT dh_ext (PTBArgs::dz): operands for the next r2_lstm_bwd_tag_sp* call on this host
-// thread (consumed by it); dz / w1t hi / lo planes, row length PT_DZ_K
+// thread; dz / w1t hi / lo planes, row length PT_DZ_K.  The launcher copies and clears them on
+// entry, before any check, so a refused call never leaves them armed for a later one.
 static thread_local const bf16* g_bwd_dz[4] = {nullptr, nullptr, nullptr, nullptr};
 extern "C" int r2_lstm_bwd_set_dz(const bf16* dz, const bf16* dz_lo, const bf16* w1t,
                                   const bf16* w1t_lo, int kd) {
   if (dz && (!dz_lo || !w1t || !w1t_lo || kd != PT_DZ_K)) return -1;
   g_bwd_dz[0] = dz; g_bwd_dz[1] = dz_lo; g_bwd_dz[2] = w1t; g_bwd_dz[3] = w1t_lo;
+  return 0;
+}
+// stop word for the next r2_lstm_bwd_tag* call on this host thread (PTBArgs::stop), and the number
+// of helpers that take head-gradient items (0 = all of them); consumed (cleared) on entry like dz
+static thread_local unsigned* g_bwd_stop = nullptr;
+static thread_local int g_bwd_stop_at = 0, g_bwd_hg_wgs = 0;
+extern "C" int r2_lstm_bwd_set_stop(unsigned* stop, int stop_at, int hg_wgs) {
+  if (stop_at < 0 || hg_wgs < 0) return -1;
+  g_bwd_stop = stop;
+  g_bwd_stop_at = stop_at;
+  g_bwd_hg_wgs = hg_wgs;
   return 0;
 }
 
@@ -1829,16 +1708,22 @@ extern "C" int r2_lstm_bwd_tag_hg_ok(int B, int H, int HD) {
 }
 
 // hg_*: optional head-gradient job (gradsum.hip r2_head_grads operands); pass dva = null for none,
-// and only when r2_lstm_bwd_tag_hg_ok(B, H, HD).
-extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const float* c_seq,
-                               const float* c0, const bf16* whhT, bf16* dgates, int B, int T,
-                               int t0, int H, unsigned* ctr, unsigned* err, void* ring,
-                               float* bias_ws, const int* perm, float* db1, float* db2,
-                               const float* hg_dva, const bf16* hg_zr, const bf16* hg_dz,
+// and only when r2_lstm_bwd_tag_hg_ok(B, H, HD).  Returns bit 0 = head gradients done here.
+static int lstm_bwd_tag_launch(const float* dh_ext, const float* gates, const float* c_seq,
+                               const float* c0, const bf16* whhT, const bf16* whhT_lo, bf16* dgates,
+                               bf16* dgates_lo, int B, int T, int t0, int H, unsigned* ctr,
+                               unsigned* err, void* ring, float* bias_ws, const int* perm, float* db1,
+                               float* db2, const float* hg_dva, const bf16* hg_zr,
+                               const float* hg_zr32, const bf16* hg_dz, const bf16* hg_dz_lo,
                                float* hg_gw2, float* hg_gb2, float* hg_gb1, int hg_N, int hg_A,
-                               int hg_HD, float* hg_ws, unsigned* hg_ticket,
-                               const int64_t* gemm_descs, int n_gw, int gw_wait, int gx_on,
-                               void* stream) {
+                               int hg_HD, float* hg_ws, unsigned* hg_ticket, void* stream) {
+  // host-thread state of this call (set_dz / set_stop), cleared before any check
+  const bf16* dz[4] = {g_bwd_dz[0], g_bwd_dz[1], g_bwd_dz[2], g_bwd_dz[3]};
+  for (int i = 0; i < 4; ++i) g_bwd_dz[i] = nullptr;
+  unsigned* const stop = g_bwd_stop;
+  const int stop_at = g_bwd_stop_at, hg_wgs = g_bwd_hg_wgs;
+  g_bwd_stop = nullptr;
+  g_bwd_stop_at = g_bwd_hg_wgs = 0;
   if (B < 1 || T < 1 || t0 < 0 || t0 >= T) return -1;
   if (H != 64 && H != 128 && H != 256 && H != 512) return -2;
   const int MB = (B + PT_ROWS - 1) / PT_ROWS, nwg = H / PL_UNITS;
@@ -1847,57 +1732,37 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
       T - t0 >= 65535) return -4;
   const int xmap = MB <= 8 && nwg <= 32 && pl_xcd_fit(1, MB, nwg);
   if (bias_ws && (!perm || !db1)) return -1;
+  const bool sp = whhT_lo != nullptr;
+  if (sp && (!dgates_lo || H > 256)) return -11;
   PTBArgs args{dh_ext, gates, c_seq, c0, whhT, dgates, ring, B, T, t0, ctr, err, MB, xmap, g_pl_slow, 0,
                bias_ws, perm, db1, db2,
                HeadGradArgs{hg_dva, hg_zr, hg_dz, hg_gw2, hg_gb2, hg_gb1, hg_ws, hg_ticket, hg_N, hg_A,
-                            hg_HD, 8, (hg_A + 6) / 7, g_bwd_hg_zr32, g_bwd_hg_dz_lo},
-               0};
-  args.n_gw = 0; args.gw_wait = 0; args.gx_on = 0; args.n_wtiles = 0;
+                            hg_HD, 8, (hg_A + 6) / 7, hg_zr32, hg_dz_lo},
+               0, 0};
+  args.stop = stop;
+  args.stop_at = stop_at;
   args.dbg = g_pl_dbg;
   int taken = 0, nh = 0;
-  if (hg_dva || n_gw > 0 || gx_on) {
+  if (hg_dva) {
     // helpers: every block of the 8 x 32 grid outside the recurrence's groups
-    if (!xmap || nwg > 32 || T - t0 > PT_ITER_MAX || !pl_xcd_fit(1, MB, nwg, true)) return -6;
+    if (!xmap || nwg > 32 || !pl_xcd_fit(1, MB, nwg, true)) return -6;
     nh = 8 * 32 - MB * nwg;
-    int nw = 0, nx = 0;
-    if (n_gw < 0 || n_gw > 3) return -7;
-    for (int i = 0; i < n_gw + (gx_on ? 1 : 0); ++i) {
-      GemmProb& p = i < n_gw ? args.gw[i] : args.gx;
-      const int rc = gemm_parse_desc(gemm_descs + GEMM_DESC * i, p);
-      if (rc) return -20 + rc;
-      if (g_bwd_whhT_lo) {        // split precision: both operands split (g2s_tile_acc)
-        if (p.npass != 3 || p.K % 32) return -11;
-      } else {
-        if (p.npass > 1 || p.C_lo) return -11;   // helpers: bf16 operands only
-        if (p.K % 64) return -8;
-      }
-      const bool is_x = i == n_gw;
-      if (is_x ? (!p.a_kmajor || p.b_kmajor) : (p.a_kmajor || p.b_kmajor)) return -9;
-      const int tiles = p.tiles_n * ((p.M + 127) / 128);
-      if (is_x) nx = tiles; else nw += tiles;
-    }
-    const int hgi = hg_dva ? ((2 * hg_HD + 63) / 64) * 8 * ((hg_A + 6) / 7) : 0;
-    if (nw >= nh || (hgi + nx > 0 && nh - nw < 16)) return -10;   // too few helpers
-    if (hg_dva) {
-      if (hg_A > 63 || ((2 * hg_HD + 63) / 64) * ((hg_A + 6) / 7) > 32 || hg_N < 1 || hg_HD % 64)
-        return -5;
-      args.hg_on = 1;
-      taken |= 1;
-    }
-    args.n_gw = n_gw; args.gw_wait = gw_wait; args.n_wtiles = nw; args.gx_on = gx_on;
-    if (n_gw) taken |= 2;
-    if (gx_on) taken |= 4;
+    if (nh < 16) return -10;   // too few helpers
+    if (hg_A > 63 || ((2 * hg_HD + 63) / 64) * ((hg_A + 6) / 7) > 32 || hg_N < 1 || hg_HD % 64)
+      return -5;
+    if (sp && (!hg_zr32 || !hg_dz_lo)) return -12;
+    args.hg_on = 1;
+    args.hg_wgs = hg_wgs > 0 ? hg_wgs : nh;
+    taken |= 1;
   }
-  args.whhT_lo = g_bwd_whhT_lo;
-  args.dgates_lo = g_bwd_dgates_lo;
-  const bool sp = g_bwd_whhT_lo != nullptr;
-  args.dz = g_bwd_dz[0]; args.dz_lo = g_bwd_dz[1]; args.w1t = g_bwd_dz[2]; args.w1t_lo = g_bwd_dz[3];
-  for (int i = 0; i < 4; ++i) g_bwd_dz[i] = nullptr;   // one launch per set
+  args.whhT_lo = whhT_lo;
+  args.dgates_lo = dgates_lo;
+  args.dz = dz[0]; args.dz_lo = dz[1]; args.w1t = dz[2]; args.w1t_lo = dz[3];
   if (args.dz && (!sp || H != 256 || g_pl_bwd8)) return -13;   // split-precision T4 BPTT, H 256 only
-  int dyn_lds = args.dz ? PT_DZ_LDS + 4 * PT_ROWS * PL_UNITS * 4 : PL_LDS_RESERVE;
-  if (sp && (args.n_gw || args.gx_on)) dyn_lds = max(dyn_lds, 3 * g2s::ST);   // helper ring
-  if (sp && (!args.dgates_lo || H > 256)) return -11;
-  if (sp && args.hg_on && (!args.hg.zr32 || !args.hg.dz_lo)) return -12;
+  // one workgroup per CU (the PL_LDS_RESERVE rule, comment at its definition): the dz path's own
+  // dynamic LDS (iteration 0's dz rows + the dh partials) is smaller than the reserve
+  const int dyn_lds = args.dz ? max(PL_LDS_RESERVE, PT_DZ_LDS + 4 * PT_ROWS * PL_UNITS * 4)
+                              : PL_LDS_RESERVE;
   hipStream_t s = (hipStream_t)stream;   // counters are left zeroed by the previous launch
   dim3 grid(nh ? 256 : (xmap ? 8 * nwg : MB * nwg)), block(320);
 #define R2_BWD_LAUNCH1(HH, SPP, T4)                                                            \
@@ -1928,28 +1793,34 @@ extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const fl
 #undef R2_BWD_LAUNCH
 #undef R2_BWD_LAUNCH1
   R2_CHECK_LAUNCH();
-  return taken;   // bit 0: head grads, 1: weight grads, 2: dX done here
+  return taken;
+}
+
+extern "C" int r2_lstm_bwd_tag(const float* dh_ext, const float* gates, const float* c_seq,
+                               const float* c0, const bf16* whhT, bf16* dgates, int B, int T,
+                               int t0, int H, unsigned* ctr, unsigned* err, void* ring,
+                               float* bias_ws, const int* perm, float* db1, float* db2,
+                               const float* hg_dva, const bf16* hg_zr, const bf16* hg_dz,
+                               float* hg_gw2, float* hg_gb2, float* hg_gb1, int hg_N, int hg_A,
+                               int hg_HD, float* hg_ws, unsigned* hg_ticket, void* stream) {
+  return lstm_bwd_tag_launch(dh_ext, gates, c_seq, c0, whhT, nullptr, dgates, nullptr, B, T, t0, H,
+                             ctr, err, ring, bias_ws, perm, db1, db2, hg_dva, hg_zr, nullptr, hg_dz,
+                             nullptr, hg_gw2, hg_gb2, hg_gb1, hg_N, hg_A, hg_HD, hg_ws, hg_ticket,
+                             stream);
 }
 
 // Split precision: the same launch with W_hh^T given as hi / lo planes and dgates written as hi /
-// lo planes (no helper jobs).  Same argument list as r2_lstm_bwd_tag plus the two lo pointers.
+// lo planes (no side job).  Same argument list as r2_lstm_bwd_tag plus the two lo pointers.
 extern "C" int r2_lstm_bwd_tag_sp(const float* dh_ext, const float* gates, const float* c_seq,
                                   const float* c0, const bf16* whhT, const bf16* whhT_lo,
                                   bf16* dgates, bf16* dgates_lo, int B, int T, int t0, int H,
                                   unsigned* ctr, unsigned* err, void* ring, float* bias_ws,
                                   const int* perm, float* db1, float* db2, void* stream) {
   if (!whhT_lo || !dgates_lo) return -5;
-  g_bwd_whhT_lo = whhT_lo;
-  g_bwd_dgates_lo = dgates_lo;
-  const int64_t* gd = g_bwd_gemms;
-  const int ngw = g_bwd_n_gw, gww = g_bwd_gw_wait, gx = g_bwd_gx_on;
-  g_bwd_gemms = nullptr; g_bwd_n_gw = g_bwd_gw_wait = g_bwd_gx_on = 0;
-  const int rc = r2_lstm_bwd_tag(dh_ext, gates, c_seq, c0, whhT, dgates, B, T, t0, H, ctr, err, ring,
-                                 bias_ws, perm, db1, db2, nullptr, nullptr, nullptr, nullptr, nullptr,
-                                 nullptr, 0, 0, 0, nullptr, nullptr, gd, ngw, gww, gx, stream);
-  g_bwd_whhT_lo = nullptr;
-  g_bwd_dgates_lo = nullptr;
-  return rc;
+  return lstm_bwd_tag_launch(dh_ext, gates, c_seq, c0, whhT, whhT_lo, dgates, dgates_lo, B, T, t0, H,
+                             ctr, err, ring, bias_ws, perm, db1, db2, nullptr, nullptr, nullptr,
+                             nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, nullptr, nullptr,
+                             stream);
 }
 
 // Split precision with the dueling head's gradient reduction on the launch's idle workgroups
@@ -1964,21 +1835,10 @@ extern "C" int r2_lstm_bwd_tag_sp_hg(const float* dh_ext, const float* gates, co
                                      float* hg_gw2, float* hg_gb2, float* hg_gb1, int hg_N, int hg_A,
                                      int hg_HD, float* hg_ws, unsigned* hg_ticket, void* stream) {
   if (!whhT_lo || !dgates_lo || !hg_zr32 || !hg_dz_lo) return -5;
-  g_bwd_whhT_lo = whhT_lo;
-  g_bwd_dgates_lo = dgates_lo;
-  g_bwd_hg_zr32 = hg_zr32;
-  g_bwd_hg_dz_lo = hg_dz_lo;
-  const int64_t* gd = g_bwd_gemms;
-  const int ngw = g_bwd_n_gw, gww = g_bwd_gw_wait, gx = g_bwd_gx_on;
-  g_bwd_gemms = nullptr; g_bwd_n_gw = g_bwd_gw_wait = g_bwd_gx_on = 0;
-  const int rc = r2_lstm_bwd_tag(dh_ext, gates, c_seq, c0, whhT, dgates, B, T, t0, H, ctr, err, ring,
-                                 bias_ws, perm, db1, db2, hg_dva, nullptr, hg_dz, hg_gw2, hg_gb2,
-                                 hg_gb1, hg_N, hg_A, hg_HD, hg_ws, hg_ticket, gd, ngw, gww, gx, stream);
-  g_bwd_whhT_lo = nullptr;
-  g_bwd_dgates_lo = nullptr;
-  g_bwd_hg_zr32 = nullptr;
-  g_bwd_hg_dz_lo = nullptr;
-  return rc;
+  return lstm_bwd_tag_launch(dh_ext, gates, c_seq, c0, whhT, whhT_lo, dgates, dgates_lo, B, T, t0, H,
+                             ctr, err, ring, bias_ws, perm, db1, db2, hg_dva, nullptr, hg_zr32, hg_dz,
+                             hg_dz_lo, hg_gw2, hg_gb2, hg_gb1, hg_N, hg_A, hg_HD, hg_ws, hg_ticket,
+                             stream);
 }
 
 extern "C" int r2_lstm_persist_ctr_words() { return PT_CTR_WORDS; }

@@ -118,11 +118,18 @@ struct SampleBatchArgs {
   int off[3];
   int B, Tn, cap_e, H, nstate;
   int h_f32;      // split-precision learner: h out as fp32 (the h pointers are float*)
+  // optional: the hoisted torso's frame-queue words (torso_sp.hip TSJob::q [0], [1]) zeroed for
+  // the launches of the step this sample feeds
+  unsigned* qreset;
 };
 
 __global__ __launch_bounds__(256) void sample_batch_kernel(const SampleBatchArgs a) {
   __shared__ int s_start;
   const int b = blockIdx.x, tid = threadIdx.x;
+  if (a.qreset && b == 0 && tid == 0) {
+    __hip_atomic_store(a.qreset, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.qreset + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (tid < 64) {
     float prob;
     const int node = tree_descend(a.tree, a.g, a.B, b, a.seed, a.step, tid, &prob);
@@ -561,9 +568,11 @@ static int sample_batch_launch(const float* tree, const int64_t* offs, const int
                                int levels, int B, uint64_t seed, const int64_t* step, int* starts,
                                float* probs, int* rows, int Tn, int cap_e, int H, int nstate,
                                const int64_t* hs, const int* off, const int64_t* h,
-                               const int64_t* c, int h_f32, void* stream) {
+                               const int64_t* c, int h_f32, void* stream,
+                               unsigned* qreset = nullptr) {
   if (levels < 2 || levels > TREE_MAX_LEVELS || nstate < 0 || nstate > 3 || B < 1) return -1;
   SampleBatchArgs a;
+  a.qreset = qreset;
   a.tree = tree; a.g = make_geom(offs, sizes, levels); a.seed = seed; a.step = step;
   a.starts = starts; a.probs = probs; a.rows = rows;
   for (int j = 0; j < 3; ++j) {
@@ -596,6 +605,16 @@ extern "C" int r2_sample_batch_f32h(const float* tree, const int64_t* offs, cons
                                     const int64_t* h, const int64_t* c, void* stream) {
   return sample_batch_launch(tree, offs, sizes, levels, B, seed, step, starts, probs, rows, Tn,
                              cap_e, H, nstate, hs, off, h, c, 1, stream);
+}
+
+// r2_sample_batch(_f32h) that also zeroes the hoisted torso's frame-queue words qreset[0..1]
+extern "C" int r2_sample_batch_q(const float* tree, const int64_t* offs, const int64_t* sizes,
+                                 int levels, int B, uint64_t seed, const int64_t* step, int* starts,
+                                 float* probs, int* rows, int Tn, int cap_e, int H, int nstate,
+                                 const int64_t* hs, const int* off, const int64_t* h,
+                                 const int64_t* c, int h_f32, unsigned* qreset, void* stream) {
+  return sample_batch_launch(tree, offs, sizes, levels, B, seed, step, starts, probs, rows, Tn,
+                             cap_e, H, nstate, hs, off, h, c, h_f32, stream, qreset);
 }
 
 extern "C" int r2_tree_rebuild(float* tree, const int64_t* offs, const int64_t* sizes, int levels,

@@ -41,14 +41,34 @@ struct TSJob {
   bf16* out; bf16* out_l;          // (n, 1568) hi / lo planes
   bf16* s1; bf16* s1l;             // optional (n, 400, 32) channels-last act1 hi / lo
   bf16* s2; bf16* s2l;             // optional (n, 81, 32)
-  int n, wbegin, wcount, keep;     // keep: 0 (opaque to the compiler)
+  // frame queue (job words 17 / 18; null = the static grid-stride deal).  qmode 1 (the hoisted
+  // target-net frames beside the BPTT): frames q[0]++ until q[0] >= n or the stop word q[2] is set;
+  // qmode 2 (the same job's remainder in the next step's launch): frames min(q[0], n) + q[1]++.
+  // A grabbed frame is always finished, so [0, min(q[0], n)) is done once the qmode-1 launch ends.
+  unsigned* q;
+  int n, wbegin, wcount, qmode;
 };
 struct TSArgs {
   const uint8_t* frames;
   TSJob job[TS_MAX_JOBS];
-  int njobs, dbg, pad_[2];   // dbg: timing-probe bits (r2_torso_sp_debug), 0 in production
+  int njobs, dbg;            // dbg: timing-probe bits (r2_torso_sp_debug), 0 in production
+  int dyn, pad_;             // dyn: workgroups dealt on the device (a qmode-2 job's size is q-dependent)
   long long* trace;          // optional per-phase clock stamps (r2_torso_sp_trace), null in production
 };
+
+// Frame of a queue job (one thread): qmode 1 stops at the stop word, qmode 2 continues after the
+// qmode-1 launch's frames.  n when the job is exhausted.
+__device__ __forceinline__ int ts_grab(const TSJob& J) {
+  unsigned* q = J.q;
+  if (J.qmode == 1) {
+    if (__hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return J.n;
+    const unsigned g = __hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return g < (unsigned)J.n ? (int)g : J.n;
+  }
+  const unsigned base = min(__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), (unsigned)J.n);
+  const unsigned g = base + __hip_atomic_fetch_add(q + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return g < (unsigned)J.n ? (int)g : J.n;
+}
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t ts_rsrc(const void* p, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, bytes, 0x00020000);
@@ -244,15 +264,75 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int half = lane >> 5, l32 = lane & 31;
   const int wk = blockIdx.x;
-  int ji = 0;
+  int ji = 0, wbeg = 0, wcnt = 0;
+  if (args.dyn) {
+    // the host's deal (r2_torso_fwd_sp_multi) with a qmode-2 job counted at its remaining frames
+    // n - min(q[0], n): every workgroup computes the same table from the same words
+    int ne[TS_MAX_JOBS];
+    int64_t total = 0;
 #pragma unroll
-  for (int i = 1; i < TS_MAX_JOBS; ++i)
-    if (i < args.njobs && wk >= args.job[i].wbegin) ji = i;
+    for (int i = 0; i < TS_MAX_JOBS; ++i) {
+      const TSJob& Ji = args.job[i];
+      int v = i < args.njobs ? Ji.n : 0;
+      if (i < args.njobs && Ji.qmode == 2)
+        v -= (int)min(__hip_atomic_load(Ji.q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), (unsigned)Ji.n);
+      ne[i] = v;
+      total += v;
+    }
+    const int nw = gridDim.x;
+    int wb = 0, left = 0;
+#pragma unroll
+    for (int i = 0; i < TS_MAX_JOBS; ++i) left += ne[i] > 0;
+    int64_t seen = 0;
+    ji = -1;
+#pragma unroll
+    for (int i = 0; i < TS_MAX_JOBS; ++i) {
+      if (ne[i] <= 0) continue;
+      --left;   // non-empty jobs after this one: each keeps at least one workgroup (nw >= njobs)
+      seen += ne[i];
+      int end = (int)((seen * nw + total - 1) / total);
+      end = min(end, nw - left);
+      const int cnt = min(max(end - wb, 1), ne[i]);
+      if (wk >= wb && wk < wb + cnt) {
+        ji = i;
+        wbeg = wb;
+        wcnt = cnt;
+      }
+      wb += cnt;
+    }
+    if (ji < 0) return;
+  } else {
+#pragma unroll
+    for (int i = 1; i < TS_MAX_JOBS; ++i)
+      if (i < args.njobs && wk >= args.job[i].wbegin) ji = i;
+    wbeg = args.job[ji].wbegin;
+    wcnt = args.job[ji].wcount;
+  }
   const TSJob& J = args.job[ji];
-  const int stride = J.wcount;
-  if (wk - J.wbegin >= stride) return;
+  const int stride = wcnt;
+  if (wk - wbeg >= stride) return;
   const int n_frames = J.n;
-  int f = wk - J.wbegin;
+  const bool qjob = J.q != nullptr;
+  __shared__ int s_q[4];
+  int f = wk - wbeg;
+  int row_f = 0, row_q1 = 0, f_q1 = 0;
+  if (qjob) {
+    // first two frames of this workgroup from the queue (before any setup: a workgroup that
+    // finds the queue empty or stopped leaves at once)
+    if (tid == 0) {
+      const int g0 = ts_grab(J);
+      const int g1 = g0 < n_frames ? ts_grab(J) : n_frames;
+      s_q[0] = g0;
+      s_q[1] = g1;
+      s_q[2] = g0 < n_frames ? (J.rows ? J.rows[g0] : g0) : 0;
+      s_q[3] = g1 < n_frames ? (J.rows ? J.rows[g1] : g1) : 0;
+    }
+    __syncthreads();
+    f = __builtin_amdgcn_readfirstlane(s_q[0]);
+    f_q1 = __builtin_amdgcn_readfirstlane(s_q[1]);
+    row_f = __builtin_amdgcn_readfirstlane(s_q[2]);
+    row_q1 = __builtin_amdgcn_readfirstlane(s_q[3]);
+  }
   if (f >= n_frames) return;
   const bool conv3_wave = wave == 2, conv2_wave = wave < 3, pf_wave = wave >= 3;
   const int t5 = tid - 192;   // prefetch thread index (waves 3..7)
@@ -288,7 +368,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
     *(bf16x8*)(w3t + pl * 2048 + (r * 32 + c * 8) * 2) = *(const bf16x8*)((pl ? J.w3l : J.w3) + r * 288 + 256 + c * 8);
   }
   {
-    const size_t row = J.rows ? (size_t)ld_uniform_i32(J.rows, f) : (size_t)f;
+    const size_t row = qjob ? (size_t)row_f : J.rows ? (size_t)ld_uniform_i32(J.rows, f) : (size_t)f;
     const u32x4* src = (const u32x4*)(args.frames + row * IN_BYTES);
     // int8 conv1 reads the frame as (byte - 128): the shift is applied once here / at the
     // phase-B store, not per conv1 lane per K step (16 XORs per 16-pixel half tile)
@@ -296,7 +376,11 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
     for (int c = tid; c < IN_CHUNKS2; c += NT) ((u32x4*)fr)[c] = src[c] ^ sh;
   }
   const int t1b = c_s2_begin[wave], t1n = c_s2_count[wave];
-  int row_nx = f + stride < n_frames ? (J.rows ? ld_uniform_i32(J.rows, f + stride) : f + stride) : 0;
+  int row_nx = qjob ? row_q1
+               : f + stride < n_frames ? (J.rows ? ld_uniform_i32(J.rows, f + stride) : f + stride) : 0;
+  // queue jobs: the next frame (fn) is known one iteration ahead; the one after (fnn) is grabbed
+  // during phase B by wave 3's first lane (it only stores its share of the prefetched frame there)
+  int f_nx = qjob ? f_q1 : f + stride;
   __syncthreads();
 
   int fprev = -1;
@@ -307,9 +391,9 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
   for (;;) {
     TS2_STAMP(0);
     const bool have = f < n_frames;
-    const int fn = f + stride;
-    const int fnn = fn + stride;
-    const int row_nn = fnn < n_frames ? (J.rows ? ld_uniform_i32(J.rows, fnn) : fnn) : 0;
+    const int fn = f_nx;
+    int fnn = fn + stride;
+    int row_nn = (!qjob && fnn < n_frames) ? (J.rows ? ld_uniform_i32(J.rows, fnn) : fnn) : 0;
     // a per-iteration zero: keeps the lane-constant LDS offsets of the MFMA loops from being
     // hoisted out of the frame loop (32+ VGPRs held across every phase otherwise)
     int oz;
@@ -489,6 +573,11 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
           ((u32x4*)fr)[c] = __builtin_bit_cast(u32x4, wfl[8 + q]) ^ 0x80808080u;
       }
     }
+    if (qjob && tid == 192) {   // fnn of a queue job and its row, read after the barrier below
+      const int g = fn < n_frames ? ts_grab(J) : n_frames;
+      s_q[0] = g;
+      s_q[1] = g < n_frames ? (J.rows ? J.rows[g] : g) : 0;
+    }
     if (conv2_wave) {
       if (!(args.dbg & 2)) {
         int oy, ox;
@@ -569,8 +658,13 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
     lds_sync();
     TS2_STAMP(4);
     ++it_dbg;
+    if (qjob) {
+      fnn = __builtin_amdgcn_readfirstlane(s_q[0]);
+      row_nn = __builtin_amdgcn_readfirstlane(s_q[1]);
+    }
     fprev = f;
     f = fn;
+    f_nx = fnn;
     row_nx = row_nn;
   }
 }
@@ -614,12 +708,19 @@ extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs,
     J.w3 = (const bf16*)p[8]; J.w3l = (const bf16*)p[9]; J.b3 = (const float*)p[10];
     J.out = (bf16*)p[11]; J.out_l = (bf16*)p[12];
     J.s1 = (bf16*)p[13]; J.s1l = (bf16*)p[14]; J.s2 = (bf16*)p[15]; J.s2l = (bf16*)p[16];
+    J.q = (unsigned*)p[17];
+    J.qmode = J.q ? (int)p[18] : 0;
     if (!J.w1l || !J.w2l || !J.w3l || !J.out_l || (J.s1 && !J.s1l) || (J.s2 && !J.s2l)) return -4;
-    J.wbegin = wb; J.wcount = cnt; J.keep = 0;
+    // queue jobs: no activation saves (the saved frames are indexed by launch order), mode 1 / 2
+    if (J.q && (J.s1 || J.s2 || (J.qmode != 1 && J.qmode != 2))) return -5;
+    if (J.qmode == 2) a.dyn = 1;
+    J.wbegin = wb; J.wcount = cnt;
     wb += cnt;
   }
   if (wb > nw) return -3;
-  if (grid > wb) grid = wb;
+  // the device-side deal (dyn) may give every workgroup of the grid a job: keep the whole grid
+  if (grid > wb && !a.dyn) grid = wb;
+  if (a.dyn && grid < a.njobs) return -3;
   static bool attr2 = false;
   if (!attr2) {
     hipFuncSetAttribute((const void*)torso_fwd_sp2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,

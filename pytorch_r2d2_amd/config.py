@@ -136,7 +136,6 @@ class LearnerConfig:
     # tile config of that group: ops/gemm.py G5_CFGS index, -1 = the launcher's CU model, -2 =
     # learner_engine._auto_group_splits' choice (paper shape: 128x128, 4-deep 32-K ring)
     sp_group_cfg: int = -2
-    sp_wgrad_splits: int = 4
     # split GEMMs on gemm6 (gemm_sp.hip: the fragment planes refilled between the three product
     # passes, one barrier per LDS tile; the heads' layer-1 GEMMs join the one-pass kernel too):
     # x-projection 115-129 -> 102-110 us, tools/gemm6_probe.py
@@ -161,13 +160,23 @@ class LearnerConfig:
     # split precision: the BPTT computes its input gradient dh = dz . W1 itself, inside its
     # hand-off waits (lstm_persist.hip PTBArgs::dz), instead of the TD launch (td_fuse_dh)
     bptt_dh: bool = True
-    # split precision: post-BPTT GEMMs on the BPTT launch's idle workgroups (lstm_persist.hip
-    # g2s_tile_acc helpers), each tile as soon as the BPTT has stored the dgates rows it reads:
-    # "off" (one grouped launch after the BPTT) | "dx" (dX there, the weight gradients after) |
-    # "all" (dW_ih, dW_hh, dW_head1 and dX there)
-    bptt_gemms: str = "off"
-    # (sp_wgrad_splits: K splits of the weight-gradient group when dX ran on the BPTT's helpers,
-    # bptt_gemms = dx)
+    # (round 5's post-BPTT GEMMs on the BPTT launch's idle workgroups -- learner.bptt_gemms --
+    # slowed the recurrence in every arm and were removed: profiles/r05_bptt_helpers_roles.txt)
+    # Single-rank split-precision step, software-pipelined over two steps (learner_engine.py
+    # "hoisted step"): right after step k's TD launch a side stream runs step k's priority tail,
+    # step k+1's sample and step k+1's target-network torso frames on the CUs the BPTT leaves
+    # free (a frame queue the next step's torso launch finishes); bit-identical to the plain step
+    hoist: bool = True
+    # the BPTT raises the side torso's stop word this many iterations before its last one (the
+    # side workgroups finish the frame in hand and the one already taken: ~1.5 frames)
+    hoist_stop_lead: int = 5
+    # BPTT helper workgroups that take the dueling head's gradient reduction items in the hoisted
+    # step (0 = all 192); the others leave at once so the side torso gets their CUs
+    hoist_hg_wgs: int = 0
+    # workgroups of the side torso launch (0 = the CUs outside the BPTT recurrence's groups)
+    hoist_grid: int = 0
+    # A/B probe: False = the side stream runs only the priority tail and the next sample
+    hoist_torso: bool = True
     # single-rank step: the weight repack after the optimizer (pack_step) runs on extra
     # workgroups of the priority tail's launch (replay.hip r2_prio_tail_pack): one launch fewer
     fuse_pack_tail: bool = True

@@ -130,20 +130,27 @@ class HBMReplay:
                                ptr(out_prob), self._ts(stream)), "tree_sample")
 
     def sample_batch(self, B: int, out_idx: torch.Tensor, out_prob: torch.Tensor,
-                     rows: torch.Tensor, Tn: int, states, stream=None, h_f32: bool = False) -> None:
+                     rows: torch.Tensor, Tn: int, states, stream=None, h_f32: bool = False,
+                     qreset: Optional[torch.Tensor] = None) -> None:
         """One launch (replay.hip sample_batch_kernel): sample B sequence starts, write the
         time-major row list ``rows[t*B + b]`` (t < Tn) and gather stored states.  ``states``:
-        up to 3 ``(hs_cs, offset, h_out (B,H) bf16 -- fp32 with h_f32 --, c_out f32 (B,H))``."""
+        up to 3 ``(hs_cs, offset, h_out (B,H) bf16 -- fp32 with h_f32 --, c_out f32 (B,H))``.
+        ``qreset``: the hoisted target torso's frame-queue words, zeroed by the same launch
+        (learner_engine.py, learner.hoist)."""
         hs = np.asarray([ptr(s[0]) for s in states] + [0], dtype=np.int64)
         off = np.asarray([int(s[1]) for s in states] + [0], dtype=np.int32)
         h = np.asarray([ptr(s[2]) for s in states] + [0], dtype=np.int64)
         c = np.asarray([ptr(s[3]) for s in states] + [0], dtype=np.int64)
+        base = (ptr(self.tree), self.tree_offs.ctypes.data, self.tree_sizes.ctypes.data,
+                self.tree_levels, B, self.seed, ptr(self.step), ptr(out_idx), ptr(out_prob), ptr(rows),
+                Tn, self.cap_e, self.H, len(states), hs.ctypes.data, off.ctypes.data, h.ctypes.data,
+                c.ctypes.data)
+        if qreset is not None:
+            check(kernels().r2_sample_batch_q(*base, int(h_f32), ptr(qreset), self._ts(stream)),
+                  "sample_batch_q")
+            return
         fn = kernels().r2_sample_batch_f32h if h_f32 else kernels().r2_sample_batch
-        check(fn(
-            ptr(self.tree), self.tree_offs.ctypes.data, self.tree_sizes.ctypes.data,
-            self.tree_levels, B, self.seed, ptr(self.step), ptr(out_idx), ptr(out_prob), ptr(rows),
-            Tn, self.cap_e, self.H, len(states), hs.ctypes.data, off.ctypes.data, h.ctypes.data,
-            c.ctypes.data, self._ts(stream)), "sample_batch")
+        check(fn(*base, self._ts(stream)), "sample_batch")
 
     def rebuild_tree(self, stream=None) -> None:
         k = kernels()

@@ -65,6 +65,7 @@ _SIGS = {
     "r2_make_rows": [P, I, I, I, I, P, P],
     "r2_sample_batch": [P, P, P, I, I, U64, P, P, P, P, I, I, I, I, P, P, P, P, P],
     "r2_sample_batch_f32h": [P, P, P, I, I, U64, P, P, P, P, I, I, I, I, P, P, P, P, P],
+    "r2_sample_batch_q": [P, P, P, I, I, U64, P, P, P, P, I, I, I, I, P, P, P, P, I, P, P],
     "r2_torso_fwd_sp_multi": [P, P, I, I, P],
     "r2_torso_sp_debug": [I],
     "r2_torso_sp_trace": [P],
@@ -105,7 +106,7 @@ _SIGS = {
     "r2_td_duel_fwd_set": [P],
     "r2_prio_tail": [P, I, P, P, P, P, P, I, I, I, I, I, F, P, P, I, P, P, I, P],
     "r2_lstm_bwd_set_dz": [P, P, P, P, I],
-    "r2_lstm_bwd_set_gemms": [P, I, I, I],
+    "r2_lstm_bwd_set_stop": [P, I, I],
     "r2_prio_tail_pack": [P, I, P, P, P, P, P, I, I, I, I, I, F, P, P, I, P, P, I,
                           P, P, I64, P, P, P, I64, P, P, P, I64, I64, I64, P, P, I64, I64, I64, P],
     "r2_td_duel_set_trace": [P],
@@ -119,7 +120,7 @@ _SIGS = {
     "r2_lstm_fwd_tag": [P, I, I, I, I, P, P, P, P],
     "r2_lstm_tag_ring_bytes": [I, I, I],
     "r2_lstm_bwd_tag": [P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P, P,
-                        P, P, P, P, P, P, I, I, I, P, P, P, I, I, I, P],
+                        P, P, P, P, P, P, I, I, I, P, P, P],
     "r2_lstm_bwd_tag_hg_ok": [I, I, I],
     "r2_lstm_bwd_tag_ring_bytes": [I, I],
     "r2_lstm_bwd_persist": [P, P, P, P, P, P, P, I, I, I, I, P, P, P],
