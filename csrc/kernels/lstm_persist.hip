@@ -95,6 +95,11 @@ __device__ __forceinline__ bool pl_decode(int xcd_map, int groups, int nwg, int&
     const int l = b >> 3;
     g = (b & 7) + 8 * (l / nwg);
     j = l % nwg;
+  } else if (xcd_map == 3) {   // packed pairs: groups 2x, 2x+1 on XCD x (x < groups / 2), so
+    // whole XCDs stay free (the hoisted target torso beside the BPTT); blocks b = 8 l + x
+    const int l = b >> 3, slot = l / nwg;
+    g = slot < 2 ? 2 * (b & 7) + slot : groups;
+    j = l % nwg;
   } else if (xcd_map) { g = b & 7; j = b >> 3; }
   else { g = b / nwg; j = b % nwg; }
   return g < groups && j < nwg;
@@ -523,7 +528,8 @@ extern "C" int r2_get_num_cus() { return g_num_cus; }
 // hosts helper workgroups that take part in the launch)
 static bool pl_xcd_fit(int xcd_map, int groups, int nwg, bool full = false) {
   for (int x = 0; x < 8; ++x) {
-    const int n = (x < groups ? 1 : 0) + (xcd_map == 2 && x + 8 < groups ? 1 : 0);
+    const int n = xcd_map == 3 ? min(max(groups - 2 * x, 0), 2)
+                               : (x < groups ? 1 : 0) + (xcd_map == 2 && x + 8 < groups ? 1 : 0);
     if (n == 0) continue;
     if (n * nwg > g_xcd_cus[x] || (full && g_xcd_cus[x] < 32)) return false;
   }
@@ -1237,7 +1243,13 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
     // ================= helper workgroup (4 waves): work beside the recurrence
     if (wave == 4) return;                 // helpers run 256 threads (barriers: surviving waves)
     const int b = blockIdx.x, g = b & 7, jj = b >> 3;
-    const int h = b - (min(jj, NWG) * a.MB + (jj < NWG ? min(g, a.MB) : 0));   // helper ordinal
+    int h;   // helper ordinal: blocks before b that are not recurrence blocks
+    if (a.xcd_map == 3) {
+      const int xr = (a.MB + 1) / 2, lr = 2 * NWG;   // recurrence rows l < lr on XCDs x < xr
+      h = jj < lr ? jj * (8 - xr) + (g - xr) : lr * (8 - xr) + (jj - lr) * 8 + g;
+    } else {
+      h = b - (min(jj, NWG) * a.MB + (jj < NWG ? min(g, a.MB) : 0));
+    }
     const int nh = (int)gridDim.x - a.MB * NWG;
     // the dueling head's gradient reduction (independent of the BPTT) on the first a.hg_wgs
     // helpers; the others leave at once and free their CUs (the hoisted target-net torso frames
@@ -1687,6 +1699,10 @@ extern "C" int r2_lstm_bwd_set_stop(unsigned* stop, int stop_at, int hg_wgs) {
   return 0;
 }
 
+// BPTT placement: 1 = recurrence groups packed two per XCD (PTBArgs xcd_map 3), 0 = one per XCD
+static int g_bwd_pairs = 0;
+extern "C" int r2_lstm_bwd_xcd_pairs(int v) { g_bwd_pairs = v; return 0; }
+
 // A/B probe switch: 1 = the BPTT on 8-byte {partial, tag} granules (the previous hand-off)
 static int g_pl_bwd8 = 0;
 extern "C" int r2_lstm_bwd_handoff8(int v) { g_pl_bwd8 = v; return 0; }
@@ -1730,7 +1746,9 @@ static int lstm_bwd_tag_launch(const float* dh_ext, const float* gates, const fl
   if (MB * nwg > g_num_cus || MB > PL_MAX_GROUPS) return -3;
   if ((size_t)T * B * (size_t)(4 * H) * 4 >= (1ull << 32) || r2_lstm_bwd_tag_ring_bytes(B, H) < 0 ||
       T - t0 >= 65535) return -4;
-  const int xmap = MB <= 8 && nwg <= 32 && pl_xcd_fit(1, MB, nwg);
+  // map 3 (r2_lstm_bwd_xcd_pairs): the recurrence packed two groups per XCD, else one per XCD
+  int xmap = MB <= 8 && nwg <= 32 && pl_xcd_fit(1, MB, nwg) ? 1 : 0;
+  if (g_bwd_pairs && MB <= 16 && 2 * nwg <= 32 && pl_xcd_fit(3, MB, nwg, true)) xmap = 3;
   if (bias_ws && (!perm || !db1)) return -1;
   const bool sp = whhT_lo != nullptr;
   if (sp && (!dgates_lo || H > 256)) return -11;
@@ -1745,14 +1763,18 @@ static int lstm_bwd_tag_launch(const float* dh_ext, const float* gates, const fl
   int taken = 0, nh = 0;
   if (hg_dva) {
     // helpers: every block of the 8 x 32 grid outside the recurrence's groups
-    if (!xmap || nwg > 32 || !pl_xcd_fit(1, MB, nwg, true)) return -6;
+    if (!xmap || nwg > 32 || !pl_xcd_fit(xmap, MB, nwg, true)) return -6;
     nh = 8 * 32 - MB * nwg;
     if (nh < 16) return -10;   // too few helpers
     if (hg_A > 63 || ((2 * hg_HD + 63) / 64) * ((hg_A + 6) / 7) > 32 || hg_N < 1 || hg_HD % 64)
       return -5;
     if (sp && (!hg_zr32 || !hg_dz_lo)) return -12;
     args.hg_on = 1;
-    args.hg_wgs = hg_wgs > 0 ? hg_wgs : nh;
+    args.hg_wgs = hg_wgs > 0 ? min(hg_wgs, nh) : nh;
+    // row splits: one item per head-gradient helper (8 column blocks x NP passes x RS), so the
+    // helpers finish early and free their CUs (RS 8 left 64 helpers on 320-row items until ~55 us)
+    const int cbn = (2 * hg_HD + 63) / 64;
+    args.hg.RS = max(1, min(32, args.hg_wgs / (cbn * args.hg.NP)));
     taken |= 1;
   }
   args.whhT_lo = whhT_lo;
@@ -1764,7 +1786,7 @@ static int lstm_bwd_tag_launch(const float* dh_ext, const float* gates, const fl
   const int dyn_lds = args.dz ? max(PL_LDS_RESERVE, PT_DZ_LDS + 4 * PT_ROWS * PL_UNITS * 4)
                               : PL_LDS_RESERVE;
   hipStream_t s = (hipStream_t)stream;   // counters are left zeroed by the previous launch
-  dim3 grid(nh ? 256 : (xmap ? 8 * nwg : MB * nwg)), block(320);
+  dim3 grid(nh ? 256 : (xmap == 3 ? 16 * nwg : xmap ? 8 * nwg : MB * nwg)), block(320);
 #define R2_BWD_LAUNCH1(HH, SPP, T4)                                                            \
   do {                                                                                         \
     hipFuncSetAttribute((const void*)lstm_bwd_tag_kernel<HH, SPP, T4>,                         \

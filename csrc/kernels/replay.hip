@@ -51,18 +51,29 @@ __device__ __forceinline__ float wave_incl_scan(float v, int lane) {
 
 // ---- sampling: one wave per sample, stratified over [0, total).  Returns the leaf (row) and
 // sets *prob = leaf / total (lane 0's value is the one to use).
+// COH: the tree (and the step counter) were written earlier in the SAME launch by workgroups on
+// other XCDs (prio_tail_kernel's fused sample): agent-scope loads, never a stale L2 line.
+template <bool COH = false>
 __device__ __forceinline__ int tree_descend(const float* __restrict__ tree, const TreeGeom& g,
                                             int B, int b, uint64_t seed,
                                             const int64_t* __restrict__ step, int lane,
                                             float* prob) {
-  const float total = tree[g.off[g.levels - 1]];
-  const uint64_t ctr = step ? (uint64_t)(*step) : 0ull;
+  auto ld = [&](int64_t i) -> float {
+    if constexpr (COH) return __hip_atomic_load(tree + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return tree[i];
+  };
+  const float total = ld(g.off[g.levels - 1]);
+  uint64_t ctr = 0ull;
+  if (step) {
+    if constexpr (COH) ctr = (uint64_t)__hip_atomic_load(step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else ctr = (uint64_t)(*step);
+  }
   float u = ((float)b + r2_uniform(seed, ctr, (uint64_t)b)) / (float)B * total;
   int64_t node = 0;
   float leaf = 0.f;   // the picked leaf's value, already in hand at the last level
   for (int lvl = g.levels - 1; lvl >= 1; --lvl) {
     const int64_t c = node * 64 + lane;
-    const float v = (c < g.size[lvl - 1]) ? tree[g.off[lvl - 1] + c] : 0.f;
+    const float v = (c < g.size[lvl - 1]) ? ld(g.off[lvl - 1] + c) : 0.f;
     const float incl = wave_incl_scan(v, lane);
     const float excl = incl - v;
     const unsigned long long hit = __ballot(incl > u && v > 0.f);
@@ -81,7 +92,7 @@ __device__ __forceinline__ int tree_descend(const float* __restrict__ tree, cons
   }
   // leaf == tree[g.off[0] + node] (the level-1 pass loaded it): no dependent re-load of the leaf
   // on the batch head's critical path
-  if (g.levels == 1) leaf = tree[g.off[0]];
+  if (g.levels == 1) leaf = ld(g.off[0]);
   *prob = total > 0.f ? leaf / total : 0.f;
   return (int)node;
 }
@@ -123,16 +134,19 @@ struct SampleBatchArgs {
   unsigned* qreset;
 };
 
-__global__ __launch_bounds__(256) void sample_batch_kernel(const SampleBatchArgs a) {
+// sequence b of the batch, one 256-thread workgroup (sample_batch_kernel, and prio_tail_kernel's
+// fused sample with COH)
+template <bool COH>
+__device__ __forceinline__ void sample_one(const SampleBatchArgs& a, int b) {
   __shared__ int s_start;
-  const int b = blockIdx.x, tid = threadIdx.x;
+  const int tid = threadIdx.x;
   if (a.qreset && b == 0 && tid == 0) {
     __hip_atomic_store(a.qreset, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(a.qreset + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (tid < 64) {
     float prob;
-    const int node = tree_descend(a.tree, a.g, a.B, b, a.seed, a.step, tid, &prob);
+    const int node = tree_descend<COH>(a.tree, a.g, a.B, b, a.seed, a.step, tid, &prob);
     if (tid == 0) {
       a.starts[b] = node;
       a.probs[b] = prob;
@@ -150,6 +164,11 @@ __global__ __launch_bounds__(256) void sample_batch_kernel(const SampleBatchArgs
       a.c[j][(size_t)b * a.H + k] = src[a.H + k];
     }
   }
+  __syncthreads();   // s_start is reused by the next sequence of this workgroup
+}
+
+__global__ __launch_bounds__(256) void sample_batch_kernel(const SampleBatchArgs a) {
+  sample_one<false>(a, blockIdx.x);
 }
 
 // ---- rebuild one level from its children (full pass; used after bulk fills)
@@ -342,6 +361,34 @@ __device__ __forceinline__ void prio_grid_barrier(unsigned* ctr, unsigned target
   __syncthreads();
 }
 
+// prio_tail_kernel's fused sample (below): wait for the tree, sample this workgroup's sequences,
+// the last sampler clears the flag words
+__device__ __forceinline__ void prio_tail_sample(const SampleBatchArgs& sb, unsigned* sync, int nprio) {
+  __shared__ int last_s;
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(sync + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 22)) {
+        __hip_atomic_fetch_or(sync + 3, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  for (int b = blockIdx.x; b < sb.B; b += nprio) sample_one<true>(sb, b);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last_s = __hip_atomic_fetch_add(sync + 5, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             (unsigned)nprio - 1;
+  __syncthreads();
+  if (last_s && threadIdx.x == 0) {
+    __hip_atomic_store(sync + 4, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(sync + 5, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // ---- the learner's whole priority tail in ONE launch (seqprio_refresh + tree_update_level(0)
 // + tree_update_tail): refresh of the sampled windows' sequence priorities (leaves), grid
 // barrier, level-0 repair of the dirty list, grid barrier, level-1 repair, arrival ticket, and
@@ -355,12 +402,19 @@ __device__ __forceinline__ void prio_grid_barrier(unsigned* ctr, unsigned target
 // pack_step_kernel launch) beside the tail; they take no part in the two grid barriers (target
 // nprio) and arrive on the final ticket like the tail's workgroups, so the step counter -- which
 // their target-sync test reads -- advances only after every one of them has read it.
+//
+// Optional fused sample (r2_prio_tail_sample, the hoisted learner step: the NEXT step's batch from
+// the repaired tree, the former sample_batch_kernel launch): the last arriver publishes the step
+// counter and the top levels write-through, then raises sync[4]; the nprio tail workgroups wait
+// for it and sample sequences b = blockIdx.x, +nprio, ... with agent-scope tree loads (the levels
+// were written by workgroups on other XCDs in this launch); the last of them (ticket sync[5])
+// clears sync[4..5].  sync[3] bit 1: that wait timed out.
 __global__ __launch_bounds__(256) void prio_tail_kernel(
     const int* __restrict__ starts, const uint8_t* __restrict__ is_start,
     const float* __restrict__ priority, float* __restrict__ tree, TreeGeom g, int T, int upd_lo,
     int upd_hi, int cap_e, float eta, int* __restrict__ dirty, int* __restrict__ count,
     int max_dirty, unsigned* __restrict__ sync, int64_t* __restrict__ step, int reset_count,
-    int nprio, const PackStepArgs pk) {
+    int nprio, const PackStepArgs pk, const SampleBatchArgs sb) {
   __shared__ int last;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   if ((int)blockIdx.x >= nprio) {
@@ -393,7 +447,11 @@ __global__ __launch_bounds__(256) void prio_tail_kernel(
     last = __hip_atomic_fetch_add(sync + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
            gridDim.x - 1;
   __syncthreads();
-  if (!last) return;
+  const bool sampler = sb.B > 0 && (int)blockIdx.x < nprio;
+  if (!last) {
+    if (sampler) prio_tail_sample(sb, sync, nprio);
+    return;
+  }
   // levels 3.. recomputed by this workgroup alone: level 2 comes from memory (the other
   // workgroups' sc1 stores), every level above from the LDS copy of the one below it -- one
   // memory round trip for the whole top of the tree instead of one per level (the stores still
@@ -423,9 +481,19 @@ __global__ __launch_bounds__(256) void prio_tail_kernel(
     sync[0] = 0u;
     sync[1] = 0u;
     sync[2] = 0u;
-    if (step) *step += 1;
+    if (step) {
+      if (sb.B > 0)   // read by the fused sample's workgroups on other XCDs: write-through
+        __hip_atomic_store(step, *step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        *step += 1;
+    }
     if (reset_count) *count = 0;
+    if (sb.B > 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(sync + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
+  if (sampler) prio_tail_sample(sb, sync, nprio);
 }
 
 // ---- mark new sequence starts (actor side): set flag, compute eta-mix, append dirty
@@ -564,13 +632,12 @@ extern "C" int r2_tree_sample(const float* tree, const int64_t* offs, const int6
   return 0;
 }
 
-static int sample_batch_launch(const float* tree, const int64_t* offs, const int64_t* sizes,
-                               int levels, int B, uint64_t seed, const int64_t* step, int* starts,
-                               float* probs, int* rows, int Tn, int cap_e, int H, int nstate,
-                               const int64_t* hs, const int* off, const int64_t* h,
-                               const int64_t* c, int h_f32, void* stream,
-                               unsigned* qreset = nullptr) {
-  if (levels < 2 || levels > TREE_MAX_LEVELS || nstate < 0 || nstate > 3 || B < 1) return -1;
+static SampleBatchArgs make_sample_args(const float* tree, const int64_t* offs, const int64_t* sizes,
+                                        int levels, int B, uint64_t seed, const int64_t* step,
+                                        int* starts, float* probs, int* rows, int Tn, int cap_e, int H,
+                                        int nstate, const int64_t* hs, const int* off,
+                                        const int64_t* h, const int64_t* c, int h_f32,
+                                        unsigned* qreset) {
   SampleBatchArgs a;
   a.qreset = qreset;
   a.tree = tree; a.g = make_geom(offs, sizes, levels); a.seed = seed; a.step = step;
@@ -582,6 +649,18 @@ static int sample_batch_launch(const float* tree, const int64_t* offs, const int
     a.off[j] = j < nstate ? off[j] : 0;
   }
   a.B = B; a.Tn = Tn; a.cap_e = cap_e; a.H = H; a.nstate = nstate; a.h_f32 = h_f32;
+  return a;
+}
+
+static int sample_batch_launch(const float* tree, const int64_t* offs, const int64_t* sizes,
+                               int levels, int B, uint64_t seed, const int64_t* step, int* starts,
+                               float* probs, int* rows, int Tn, int cap_e, int H, int nstate,
+                               const int64_t* hs, const int* off, const int64_t* h,
+                               const int64_t* c, int h_f32, void* stream,
+                               unsigned* qreset = nullptr) {
+  if (levels < 2 || levels > TREE_MAX_LEVELS || nstate < 0 || nstate > 3 || B < 1) return -1;
+  const SampleBatchArgs a = make_sample_args(tree, offs, sizes, levels, B, seed, step, starts, probs,
+                                             rows, Tn, cap_e, H, nstate, hs, off, h, c, h_f32, qreset);
   hipLaunchKernelGGL(sample_batch_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, a);
   R2_CHECK_LAUNCH();
   return 0;
@@ -708,7 +787,8 @@ static int prio_tail_launch(const int* starts, int B, const uint8_t* is_start, c
                             float* tree, const int64_t* offs, const int64_t* sizes, int levels,
                             int T, int upd_lo, int upd_hi, int cap_e, float eta, int* dirty,
                             int* count, int max_dirty, unsigned* sync, int64_t* step,
-                            int reset_count, const PackStepArgs* pk, void* stream) {
+                            int reset_count, const PackStepArgs* pk, void* stream,
+                            const SampleBatchArgs* sb = nullptr) {
   if (upd_hi - upd_lo + T - 1 > 2048) return -2;
   if (B <= 0 || B > 256) return -3;
   {   // every workgroup must be resident at once (grid barriers): B <= CUs x blocks per CU
@@ -723,14 +803,19 @@ static int prio_tail_launch(const int* starts, int B, const uint8_t* is_start, c
     if (sizes[l - 1] > 64 * 64) return -3;
   TreeGeom g = make_geom(offs, sizes, levels);
   PackStepArgs none{};
+  SampleBatchArgs no_sample{};
+  no_sample.B = 0;
   int grid = B;
   if (pk) {
     if (!pack_step_args_ok(*pk) || !step) return -5;
     grid += PRIO_PACK_BLOCKS;
   }
+  // the fused sample: its own tree (the same), every tail workgroup resident (checked above), no
+  // pack workgroups (their late arrival would hold the samplers' wait)
+  if (sb && (pk || sb->tree != tree)) return -5;
   hipLaunchKernelGGL(prio_tail_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, starts, is_start,
                      priority, tree, g, T, upd_lo, upd_hi, cap_e, eta, dirty, count, max_dirty, sync,
-                     step, reset_count, B, pk ? *pk : none);
+                     step, reset_count, B, pk ? *pk : none, sb ? *sb : no_sample);
   R2_CHECK_LAUNCH();
   return 0;
 }
@@ -810,4 +895,23 @@ extern "C" int r2_step_end(int64_t* step, int* count, void* stream) {
   hipLaunchKernelGGL(step_end_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, step, count);
   R2_CHECK_LAUNCH();
   return 0;
+}
+
+// r2_prio_tail (ending the step: step counter + 1) + the NEXT step's sample (r2_sample_batch_q
+// arguments, the same tree and step counter) in one launch: the hoisted learner step's side
+// branch (engine/learner_engine.py).  sync: 6 zeroed uints.
+extern "C" int r2_prio_tail_sample(const int* starts, int B, const uint8_t* is_start,
+                                   const float* priority, float* tree, const int64_t* offs,
+                                   const int64_t* sizes, int levels, int T, int upd_lo, int upd_hi,
+                                   int cap_e, float eta, int* dirty, int* count, int max_dirty,
+                                   unsigned* sync, int64_t* step, uint64_t seed, int* s_starts,
+                                   float* s_probs, int* s_rows, int Tn, int H, int nstate,
+                                   const int64_t* hs, const int* off, const int64_t* h,
+                                   const int64_t* c, int h_f32, unsigned* qreset, void* stream) {
+  if (!step || nstate < 0 || nstate > 3) return -1;
+  const SampleBatchArgs sb = make_sample_args(tree, offs, sizes, levels, B, seed, step, s_starts,
+                                              s_probs, s_rows, Tn, cap_e, H, nstate, hs, off, h, c,
+                                              h_f32, qreset);
+  return prio_tail_launch(starts, B, is_start, priority, tree, offs, sizes, levels, T, upd_lo, upd_hi,
+                          cap_e, eta, dirty, count, max_dirty, sync, step, 1, nullptr, stream, &sb);
 }

@@ -177,6 +177,11 @@ class LearnerConfig:
     hoist_grid: int = 0
     # A/B probe: False = the side stream runs only the priority tail and the next sample
     hoist_torso: bool = True
+    # the side branch's priority tail and next-step sample in one launch (r2_prio_tail_sample)
+    hoist_fuse_sample: bool = True
+    # BPTT recurrence groups packed two per XCD (lstm_persist.hip xcd_map 3): whole XCDs free
+    # for the hoisted torso frames, whose L2 traffic then stays off the recurrence's hand-offs
+    bptt_xcd_pairs: bool = True
     # single-rank step: the weight repack after the optimizer (pack_step) runs on extra
     # workgroups of the priority tail's launch (replay.hip r2_prio_tail_pack): one launch fewer
     fuse_pack_tail: bool = True

@@ -116,6 +116,7 @@ class LearnerEngine:
                 arr = (ctypes.c_int * 8)(*xcd_cus)
                 kernels().r2_set_xcd_cus(arr)
             kernels().r2_lstm_persist_force_slow(0 if cfg.learner.lstm_xcd_pairs else 2)
+            kernels().r2_lstm_bwd_xcd_pairs(1 if cfg.learner.bptt_xcd_pairs else 0)
             # gemm_sp.hip launcher mode: bit 0 interleaved fragment loads, bit 2 gemm5, bit 6 the
             # tile-major item order instead of the K-split-major one
             kernels().r2_gemm5_set_mode(1 | (0 if cfg.learner.sp_gemm6 else 4)
@@ -451,19 +452,26 @@ class LearnerEngine:
         rp, B = self.replay, self.B
         nxt = 1 - self._cur
         with torch.cuda.stream(side):
-            if not rp.prio_tail(self.starts, B, self.Lb, self.T, True):
-                rp.refresh_sequences(self.starts, B, self.Lb, self.T)
-                if not rp.update_tree_and_end_step(True):
-                    rp.update_tree()
-                    rp.step_end()
-            self._sample(set_idx=nxt, qreset=self.tq)
+            # one launch: the tail ends the step (counter + 1) and samples the next batch from the
+            # repaired tree (replay.hip r2_prio_tail_sample); else the separate launches
+            S, states = self._sample_dst(nxt)
+            if not (self.cfg.learner.hoist_fuse_sample and rp.prio_tail_sample(
+                    self.starts, B, self.Lb, self.T, S["starts"], S["probs"], S["rows"], self.Tn,
+                    states, self.sp, self.tq)):
+                if not rp.prio_tail(self.starts, B, self.Lb, self.T, True):
+                    rp.refresh_sequences(self.starts, B, self.Lb, self.T)
+                    if not rp.update_tree_and_end_step(True):
+                        rp.update_tree()
+                        rp.step_end()
+                self._sample(set_idx=nxt, qreset=self.tq)
             if torso:
                 lc = self.cfg.learner
                 rows = self._sets[nxt]["rows"][self.t_lo_tg * B:]
                 job = self._torso_job_sp(self.pk_t, self.pk_t_lo, rows, self.X_tg, self.X_tg_lo, qmode=1)
                 arr = np.asarray([job], dtype=np.int64)
                 self._side_job = arr      # (the launcher copies it into the kernel arguments)
-                grid = int(lc.hoist_grid) or max(1, self.n_cus - self._bptt_groups_wgs())
+                grid = int(lc.hoist_grid) or (self.n_cus if lc.bptt_xcd_pairs
+                                              else max(1, self.n_cus - self._bptt_groups_wgs()))
                 check(kernels().r2_torso_fwd_sp_multi(ptr(rp.frames), arr.ctypes.data, 1, grid,
                                                       stream_handle(side)), "torso_fwd_sp (hoisted)")
         return side
@@ -660,17 +668,11 @@ class LearnerEngine:
         (replay_memory.py:224-262: multinomial over a host scan + per-row Python gathers).
         ``set_idx``: write that sample set (the hoisted step samples the next step's batch into
         the other set); ``qreset``: also zero the hoisted torso's frame-queue words."""
-        B, Tn, n = self.B, self.Tn, self.n
+        B, Tn = self.B, self.Tn
         rp = self.replay
         if qreset is None and self.hoist:
             qreset = self.tq     # the torso launch after this sample takes every target frame
-        S = self._sets[self._cur if set_idx is None else set_idx]
-        h0, c0 = S["h0"], S["c0"]
-        st_off = {"on": 0, "tg": 0 if self.mode == "shifted" else n, "nx": n}
-        states = [(rp.hs_cs, 0, h0["on"], c0["on"]),
-                  (rp.target_hs_cs, st_off["tg"], h0["tg"], c0["tg"])]
-        if self.mode == "fixed":
-            states.append((rp.hs_cs, n, h0["nx"], c0["nx"]))
+        S, states = self._sample_dst(self._cur if set_idx is None else set_idx)
         rp.sample_batch(B, S["starts"], S["probs"], S["rows"], Tn, states, h_f32=self.sp,
                         qreset=qreset)
         if self.cfg.learner.zero_stored_state:     # ablation: no stored recurrent state
@@ -685,6 +687,19 @@ class LearnerEngine:
             else:
                 from ..parallel.sharded_replay import local_stats
                 local_stats(root, rp.n_valid, self.probs, out=self.dp_send)
+
+    def _sample_dst(self, i: int):
+        """Sample set ``i`` and the stored-state gathers (hs_cs, row offset, h out, c out) of its
+        chains."""
+        rp, n = self.replay, self.n
+        S = self._sets[i]
+        h0, c0 = S["h0"], S["c0"]
+        st_off = {"on": 0, "tg": 0 if self.mode == "shifted" else n, "nx": n}
+        states = [(rp.hs_cs, 0, h0["on"], c0["on"]),
+                  (rp.target_hs_cs, st_off["tg"], h0["tg"], c0["tg"])]
+        if self.mode == "fixed":
+            states.append((rp.hs_cs, n, h0["nx"], c0["nx"]))
+        return S, states
 
     def _gather_dp(self):
         """The step's one extra collective (DP global sampling): 3 floats per rank."""

@@ -87,8 +87,9 @@ class HBMReplay:
         self.step = torch.zeros(1, dtype=torch.int64, device=d)
         # arrival ticket of the fused tree repair (allocated before any graph capture)
         self.tree_ticket = torch.zeros(1, dtype=torch.int32, device=d) if d.type == "cuda" else None
-        # prio_tail_kernel: two grid-barrier counters, the arrival ticket, an error word
-        self.prio_sync = torch.zeros(4, dtype=torch.int32, device=d) if d.type == "cuda" else None
+        # prio_tail_kernel: two grid-barrier counters, the arrival ticket, an error word, and the
+        # fused sample's tree-ready flag + sampler ticket (r2_prio_tail_sample)
+        self.prio_sync = torch.zeros(8, dtype=torch.int32, device=d) if d.type == "cuda" else None
         self.seed = int(cfg.seed) * 0x9E3779B1 + 12345
         self.heads = np.zeros(n_sub, dtype=np.int64)   # per-sub-ring write heads (host mirror)
         self.total_written = 0
@@ -224,6 +225,30 @@ class HBMReplay:
         if r in (-3, -4):    # shape, or more workgroups than can be resident at once
             return False
         check(r, "prio_tail")
+        return True
+
+    def prio_tail_sample(self, starts: torch.Tensor, B: int, upd_lo: int, upd_hi: int, out_idx,
+                         out_prob, rows, Tn: int, states, h_f32: bool, qreset, stream=None) -> bool:
+        """prio_tail (ending the step) + the NEXT step's sample_batch in ONE launch (replay.hip
+        r2_prio_tail_sample): the sample waits for the repaired tree inside the launch.  Same
+        arguments as prio_tail + sample_batch; False (nothing launched) when the shape refuses."""
+        if self.tree.device.type != "cuda":
+            return False
+        rc = self.cfg.replay
+        hs = np.asarray([ptr(s_[0]) for s_ in states] + [0], dtype=np.int64)
+        off = np.asarray([int(s_[1]) for s_ in states] + [0], dtype=np.int32)
+        h = np.asarray([ptr(s_[2]) for s_ in states] + [0], dtype=np.int64)
+        c = np.asarray([ptr(s_[3]) for s_ in states] + [0], dtype=np.int64)
+        r = kernels().r2_prio_tail_sample(
+            ptr(starts), B, ptr(self.is_start), ptr(self.priority), ptr(self.tree),
+            self.tree_offs.ctypes.data, self.tree_sizes.ctypes.data, self.tree_levels, rc.seq_len,
+            upd_lo, upd_hi, self.cap_e, float(rc.eta), ptr(self.dirty), ptr(self.dirty_count),
+            self.max_dirty, ptr(self.prio_sync), ptr(self.step), self.seed, ptr(out_idx),
+            ptr(out_prob), ptr(rows), Tn, self.H, len(states), hs.ctypes.data, off.ctypes.data,
+            h.ctypes.data, c.ctypes.data, int(h_f32), ptr(qreset), self._ts(stream))
+        if r in (-3, -4):
+            return False
+        check(r, "prio_tail_sample")
         return True
 
     def reset_dirty(self, stream=None) -> None:

@@ -107,6 +107,9 @@ _SIGS = {
     "r2_prio_tail": [P, I, P, P, P, P, P, I, I, I, I, I, F, P, P, I, P, P, I, P],
     "r2_lstm_bwd_set_dz": [P, P, P, P, I],
     "r2_lstm_bwd_set_stop": [P, I, I],
+    "r2_lstm_bwd_xcd_pairs": [I],
+    "r2_prio_tail_sample": [P, I, P, P, P, P, P, I, I, I, I, I, F, P, P, I, P, P, U64, P, P, P, I,
+                            I, I, P, P, P, P, I, P, P],
     "r2_prio_tail_pack": [P, I, P, P, P, P, P, I, I, I, I, I, F, P, P, I, P, P, I,
                           P, P, I64, P, P, P, I64, P, P, P, I64, I64, I64, P, P, I64, I64, I64, P],
     "r2_td_duel_set_trace": [P],

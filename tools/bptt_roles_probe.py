@@ -1,12 +1,14 @@
 """Per-role clock stamps of the fp32 BPTT launch (lstm_persist.hip lstm_bwd_tag_kernel, PTBArgs::dbg)
 at the bench config, one eager engine step per arm, arms as learner.* override sets:
 
-    python tools/bptt_roles_probe.py off bptt_gemms=dx bptt_gemms=all,bptt_dh=1 ...
+    python tools/bptt_roles_probe.py hoist=0 hoist_torso=0 off hoist_hg_wgs=64 ...
 
 Per arm: launch span (first workgroup start -> last workgroup end), the recurrence's end (its
-last workgroup), the helpers' end, the median / max BPTT iteration of recurrence workgroup (0, 0),
-the helpers' mean time blocked on dgates rows, and dX tiles per helper.  Times in us
-(s_memrealtime, 100 MHz, one clock for the chip).
+last workgroup), the helpers' end (head-gradient reduction), the median / max BPTT iteration of
+recurrence workgroup (0, 0) and the medians of its first / middle / last 10 iterations (round 6:
+in the hoisted step the side branch's priority tail + sample run beside the first ~15
+iterations, its torso frames beside the rest).  Times in us (s_memrealtime, 100 MHz, one clock
+for the chip).
 """
 import json
 import os
@@ -75,20 +77,20 @@ def arm(spec: str, reps: int = 3):
              "loop_entry_max_us": us((rec[:, 7] - rec[:, 0]).max()),
              "iter_med_us": round(float(np.median(dit)), 3) if len(dit) else None,
              "iter_max_us": round(float(dit.max()), 3) if len(dit) else None,
+             "iter_med_first10": round(float(np.median(dit[:10])), 3) if len(dit) >= 30 else None,
+             "iter_med_mid10": round(float(np.median(dit[10:20])), 3) if len(dit) >= 30 else None,
+             "iter_med_last10": round(float(np.median(dit[-10:])), 3) if len(dit) >= 30 else None,
              "n_helpers": int(len(hlp))}
         if len(hlp):
             r.update({"helpers_end_us": us(hlp[:, 1].max() - t0),
-                      "helpers_first_job_end_us": us(hlp[:, 5].max() - t0) if hlp[:, 5].max() else None,
-                      "helper_rows_wait_mean_us": us(hlp[:, 3].mean()),
-                      "dx_tiles_total": int(hlp[:, 4].sum()),
-                      "dx_tiles_max_per_helper": int(hlp[:, 4].max())})
+                      "helpers_end_med_us": us(np.median(hlp[:, 1]) - t0)})
         out.append(r)
     err = eng.error_word()
     return {"arm": spec, "error_word": int(err), "runs": out}
 
 
 def main():
-    arms = sys.argv[1:] or ["off", "bptt_gemms=dx"]
+    arms = sys.argv[1:] or ["hoist=0", "hoist_torso=0", "off"]
     for a in arms:
         print(json.dumps(arm(a)), flush=True)
 
