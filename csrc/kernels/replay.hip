@@ -269,13 +269,12 @@ __device__ __forceinline__ void seqprio_refresh_wg(const int* __restrict__ start
                                                    float* __restrict__ leaves, int T, int upd_lo,
                                                    int upd_hi, int cap_e, float eta,
                                                    int* __restrict__ dirty, int* __restrict__ count,
-                                                   int max_dirty) {
+                                                   int max_dirty, const int b) {
   constexpr int MAXC = 2048;     // host checks the candidate range fits
   __shared__ int list[MAXC];
   __shared__ int n_list;
   __shared__ int dbase;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int b = blockIdx.x;
   if (threadIdx.x == 0) n_list = 0;
   __syncthreads();
   const int sb = starts[b];
@@ -333,7 +332,7 @@ __global__ void seqprio_refresh_kernel(const int* __restrict__ starts, int B,
                                        int max_dirty) {
   (void)B;
   seqprio_refresh_wg<false>(starts, is_start, priority, leaves, T, upd_lo, upd_hi, cap_e, eta,
-                            dirty, count, max_dirty);
+                            dirty, count, max_dirty, blockIdx.x);
 }
 
 // pack workgroups of r2_prio_tail_pack (grid-stride over ~115k items of the fp32 paper config)
@@ -363,7 +362,8 @@ __device__ __forceinline__ void prio_grid_barrier(unsigned* ctr, unsigned target
 
 // prio_tail_kernel's fused sample (below): wait for the tree, sample this workgroup's sequences,
 // the last sampler clears the flag words
-__device__ __forceinline__ void prio_tail_sample(const SampleBatchArgs& sb, unsigned* sync, int nprio) {
+__device__ __forceinline__ void prio_tail_sample(const SampleBatchArgs& sb, unsigned* sync, int nprio,
+                                                 int role) {
   __shared__ int last_s;
   if (threadIdx.x == 0) {
     unsigned spins = 0;
@@ -376,7 +376,7 @@ __device__ __forceinline__ void prio_tail_sample(const SampleBatchArgs& sb, unsi
     }
   }
   __syncthreads();
-  for (int b = blockIdx.x; b < sb.B; b += nprio) sample_one<true>(sb, b);
+  for (int b = role; b < sb.B; b += nprio) sample_one<true>(sb, b);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0)
@@ -414,22 +414,33 @@ __global__ __launch_bounds__(256) void prio_tail_kernel(
     const float* __restrict__ priority, float* __restrict__ tree, TreeGeom g, int T, int upd_lo,
     int upd_hi, int cap_e, float eta, int* __restrict__ dirty, int* __restrict__ count,
     int max_dirty, unsigned* __restrict__ sync, int64_t* __restrict__ step, int reset_count,
-    int nprio, const PackStepArgs pk, const SampleBatchArgs sb) {
+    int nprio, int npart, int skip, const PackStepArgs pk, const SampleBatchArgs sb) {
   __shared__ int last;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  if ((int)blockIdx.x >= nprio) {
-    const int64_t pb = blockIdx.x - nprio, npb = gridDim.x - nprio;
+  // role of this block among the npart participants.  skip > 0 (the hoisted step): blocks b with
+  // b % 8 < skip -- placed on the XCDs that hold the BPTT recurrence beside this launch -- sit it
+  // out, so no tail workgroup shares a CU with a recurrence workgroup (the placement only moves
+  // work; the roles, and so the results, do not depend on it)
+  int role = blockIdx.x;
+  if (skip) {
+    const int x = blockIdx.x & 7;
+    if (x < skip) return;
+    role = (blockIdx.x >> 3) * (8 - skip) + x - skip;
+  }
+  if (role >= npart) return;
+  if (role >= nprio) {
+    const int64_t pb = role - nprio, npb = npart - nprio;
     pack_step_items(pk, pb * blockDim.x + threadIdx.x, npb * blockDim.x);
   } else {
     const int nwaves = nprio * nw;
     seqprio_refresh_wg<true>(starts, is_start, priority, tree, T, upd_lo, upd_hi, cap_e, eta, dirty,
-                             count, max_dirty);
+                             count, max_dirty, role);
     prio_grid_barrier(sync + 0, nprio, sync + 3);
     const int n = min(__hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), max_dirty);
     for (int lvl = 0; lvl < 2; ++lvl) {
       const float* child = tree + g.off[lvl];
       float* parent = tree + g.off[lvl + 1];
-      for (int e = blockIdx.x * nw + wave; e < n; e += nwaves) {
+      for (int e = role * nw + wave; e < n; e += nwaves) {
         const int64_t p = ((int64_t)__hip_atomic_load(dirty + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                           >> (6 * (lvl + 1));
         const int64_t c = p * 64 + lane;
@@ -445,11 +456,11 @@ __global__ __launch_bounds__(256) void prio_tail_kernel(
   __syncthreads();
   if (threadIdx.x == 0)
     last = __hip_atomic_fetch_add(sync + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-           gridDim.x - 1;
+           (unsigned)npart - 1;
   __syncthreads();
-  const bool sampler = sb.B > 0 && (int)blockIdx.x < nprio;
+  const bool sampler = sb.B > 0 && role < nprio;
   if (!last) {
-    if (sampler) prio_tail_sample(sb, sync, nprio);
+    if (sampler) prio_tail_sample(sb, sync, nprio, role);
     return;
   }
   // levels 3.. recomputed by this workgroup alone: level 2 comes from memory (the other
@@ -493,7 +504,7 @@ __global__ __launch_bounds__(256) void prio_tail_kernel(
       __hip_atomic_store(sync + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  if (sampler) prio_tail_sample(sb, sync, nprio);
+  if (sampler) prio_tail_sample(sb, sync, nprio, role);
 }
 
 // ---- mark new sequence starts (actor side): set flag, compute eta-mix, append dirty
@@ -788,7 +799,7 @@ static int prio_tail_launch(const int* starts, int B, const uint8_t* is_start, c
                             int T, int upd_lo, int upd_hi, int cap_e, float eta, int* dirty,
                             int* count, int max_dirty, unsigned* sync, int64_t* step,
                             int reset_count, const PackStepArgs* pk, void* stream,
-                            const SampleBatchArgs* sb = nullptr) {
+                            const SampleBatchArgs* sb = nullptr, int skip = 0) {
   if (upd_hi - upd_lo + T - 1 > 2048) return -2;
   if (B <= 0 || B > 256) return -3;
   {   // every workgroup must be resident at once (grid barriers): B <= CUs x blocks per CU
@@ -813,9 +824,12 @@ static int prio_tail_launch(const int* starts, int B, const uint8_t* is_start, c
   // the fused sample: its own tree (the same), every tail workgroup resident (checked above), no
   // pack workgroups (their late arrival would hold the samplers' wait)
   if (sb && (pk || sb->tree != tree)) return -5;
+  if (skip < 0 || skip > 4) return -1;
+  const int npart = grid;
+  if (skip) grid = (npart + 8 - skip - 1) / (8 - skip) * 8;
   hipLaunchKernelGGL(prio_tail_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, starts, is_start,
                      priority, tree, g, T, upd_lo, upd_hi, cap_e, eta, dirty, count, max_dirty, sync,
-                     step, reset_count, B, pk ? *pk : none, sb ? *sb : no_sample);
+                     step, reset_count, B, npart, skip, pk ? *pk : none, sb ? *sb : no_sample);
   R2_CHECK_LAUNCH();
   return 0;
 }
@@ -907,11 +921,13 @@ extern "C" int r2_prio_tail_sample(const int* starts, int B, const uint8_t* is_s
                                    unsigned* sync, int64_t* step, uint64_t seed, int* s_starts,
                                    float* s_probs, int* s_rows, int Tn, int H, int nstate,
                                    const int64_t* hs, const int* off, const int64_t* h,
-                                   const int64_t* c, int h_f32, unsigned* qreset, void* stream) {
+                                   const int64_t* c, int h_f32, unsigned* qreset, int skip_xcds,
+                                   void* stream) {
   if (!step || nstate < 0 || nstate > 3) return -1;
   const SampleBatchArgs sb = make_sample_args(tree, offs, sizes, levels, B, seed, step, s_starts,
                                               s_probs, s_rows, Tn, cap_e, H, nstate, hs, off, h, c,
                                               h_f32, qreset);
   return prio_tail_launch(starts, B, is_start, priority, tree, offs, sizes, levels, T, upd_lo, upd_hi,
-                          cap_e, eta, dirty, count, max_dirty, sync, step, 1, nullptr, stream, &sb);
+                          cap_e, eta, dirty, count, max_dirty, sync, step, 1, nullptr, stream, &sb,
+                          skip_xcds);
 }

@@ -26,6 +26,21 @@ struct RmsPackArgs {
   float* target;
   const int64_t* step;
   int64_t interval;
+  // optional full repack (r2_rmsprop_pack_all: no pack_step launch after the update).  Quads
+  // q >= xq0 carry per-element destinations: xA / xB = up to two bf16 prefix-pack slots (conv
+  // layouts, W_hh^T, W1^T; -1 none), xF = the fp32 gather slot (-1 none), indexed q - xq0.  The
+  // bias_ih quads [bq0, bq0 + G/4) are updated together with their bias_hh partners (+G/4), so
+  // one thread forms the packed LSTM bias lstm_b[binv[k]] = b_ih[k] + b_hh[k] from both new values
+  // (pack_step.h's gather order and rounding).
+  int64_t xq0, bq0, G;
+  const int4* xA;
+  const int4* xB;
+  const int4* xF;
+  const int* binv;
+  float* f32;
+  float* f32_t;
+  float* lstm_b;
+  float* lstm_b_t;
 };
 
 __device__ __forceinline__ void rmsprop_pack_items(const RmsPackArgs& a, int64_t first, int64_t stride) {
@@ -41,10 +56,13 @@ __device__ __forceinline__ void rmsprop_pack_items(const RmsPackArgs& a, int64_t
   float* __restrict__ ga = a.ga;
   const bool due = a.interval <= 1 || ((*a.step) + 1) % a.interval == 0;
   const int64_t n = a.n, n4 = n >> 2;
-  for (int64_t i = first; i < n4; i += stride) {
-    f32x4 pv = ((f32x4*)p)[i], gv = ((const f32x4*)g)[i];
-    f32x4 sv = ((f32x4*)sq)[i], av = ((f32x4*)ga)[i];
-    const int d = a.dst4[i];
+  const bool full = a.xA != nullptr;
+  const int64_t gq = a.G >> 2;
+  // quad q: update, row pack (dst4), and (full) the per-element prefix / fp32 destinations
+  auto quad = [&](int64_t q) -> f32x4 {
+    f32x4 pv = ((f32x4*)p)[q], gv = ((const f32x4*)g)[q];
+    f32x4 sv = ((f32x4*)sq)[q], av = ((f32x4*)ga)[q];
+    const int d = a.dst4[q];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float gr = gv[e] * scale;
@@ -52,10 +70,10 @@ __device__ __forceinline__ void rmsprop_pack_items(const RmsPackArgs& a, int64_t
       av[e] = alpha * av[e] + (1.f - alpha) * gr;
       pv[e] -= lr * gr / (sqrtf(sv[e] - av[e] * av[e]) + eps);
     }
-    ((f32x4*)p)[i] = pv;
-    ((f32x4*)sq)[i] = sv;
-    ((f32x4*)ga)[i] = av;
-    if (due) ((f32x4*)a.target)[i] = pv;
+    ((f32x4*)p)[q] = pv;
+    ((f32x4*)sq)[q] = sv;
+    ((f32x4*)ga)[q] = av;
+    if (due) ((f32x4*)a.target)[q] = pv;
     if (d >= 0) {
       bf16x4 h, l;
 #pragma unroll
@@ -68,6 +86,52 @@ __device__ __forceinline__ void rmsprop_pack_items(const RmsPackArgs& a, int64_t
       if (due) {
         *(bf16x4*)(a.bf_t + d) = h;
         if (a.lo_off) *(bf16x4*)(a.bf_t + a.lo_off + d) = l;
+      }
+    }
+    if (full && q >= a.xq0) {
+      const int4 xa = a.xA[q - a.xq0], xb = a.xB[q - a.xq0], xf = a.xF[q - a.xq0];
+      const int sa[4] = {xa.x, xa.y, xa.z, xa.w}, sb[4] = {xb.x, xb.y, xb.z, xb.w};
+      const int sf[4] = {xf.x, xf.y, xf.z, xf.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bf16 h = (bf16)pv[e];
+        const bf16 l = (bf16)(pv[e] - (float)h);
+        if (sa[e] >= 0) {
+          a.bf[sa[e]] = h;
+          if (a.lo_off) a.bf[sa[e] + a.lo_off] = l;
+          if (due) {
+            a.bf_t[sa[e]] = h;
+            if (a.lo_off) a.bf_t[sa[e] + a.lo_off] = l;
+          }
+        }
+        if (sb[e] >= 0) {
+          a.bf[sb[e]] = h;
+          if (a.lo_off) a.bf[sb[e] + a.lo_off] = l;
+          if (due) {
+            a.bf_t[sb[e]] = h;
+            if (a.lo_off) a.bf_t[sb[e] + a.lo_off] = l;
+          }
+        }
+        if (sf[e] >= 0) {
+          a.f32[sf[e]] = pv[e];
+          if (due) a.f32_t[sf[e]] = pv[e];
+        }
+      }
+    }
+    return pv;
+  };
+  for (int64_t i = first; i < n4; i += stride) {
+    if (full && i >= a.bq0 + gq && i < a.bq0 + 2 * gq) continue;   // bias_hh: with its partner
+    const f32x4 pv = quad(i);
+    if (full && i >= a.bq0 && i < a.bq0 + gq) {
+      const f32x4 ph = quad(i + gq);
+      const int k0 = (int)(i - a.bq0) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int j = a.binv[k0 + e];
+        const float b = pv[e] + ph[e];
+        a.lstm_b[j] = b;
+        if (due) a.lstm_b_t[j] = b;
       }
     }
   }

@@ -179,6 +179,8 @@ class LearnerConfig:
     hoist_torso: bool = True
     # the side branch's priority tail and next-step sample in one launch (r2_prio_tail_sample)
     hoist_fuse_sample: bool = True
+    # where the side branch joins the main stream: "bwd" (before the conv backward) | "end"
+    hoist_join: str = "bwd"
     # BPTT recurrence groups packed two per XCD (lstm_persist.hip xcd_map 3): whole XCDs free
     # for the hoisted torso frames, whose L2 traffic then stays off the recurrence's hand-offs
     bptt_xcd_pairs: bool = True

@@ -184,6 +184,16 @@ class LearnerEngine:
         self.graph = None
         self.stats: Dict[str, float] = {}
         self._alloc()
+        # hoisted step: the optimizer writes EVERY packed layout itself (r2_rmsprop_pack_all; the
+        # pack_step launch is gone from the step's tail)
+        self._rms_all = None
+        if self.hoist and self.row_dst4 is not None:
+            t = L.rms_scatter_tables()
+            if t is not None:
+                xq0, xA, xB, xF, bq0, binv = t
+                self._rms_all = dict(xq0=xq0, bq0=bq0, xA=torch.from_numpy(xA).to(d),
+                                     xB=torch.from_numpy(xB).to(d), xF=torch.from_numpy(xF).to(d),
+                                     binv=torch.from_numpy(binv).to(d))
         self._pack(always=True)
         if d.type == "cuda":
             torch.cuda.synchronize(d)
@@ -457,7 +467,7 @@ class LearnerEngine:
             S, states = self._sample_dst(nxt)
             if not (self.cfg.learner.hoist_fuse_sample and rp.prio_tail_sample(
                     self.starts, B, self.Lb, self.T, S["starts"], S["probs"], S["rows"], self.Tn,
-                    states, self.sp, self.tq)):
+                    states, self.sp, self.tq, skip_xcds=self._bptt_xcds())):
                 if not rp.prio_tail(self.starts, B, self.Lb, self.T, True):
                     rp.refresh_sequences(self.starts, B, self.Lb, self.T)
                     if not rp.update_tree_and_end_step(True):
@@ -475,6 +485,13 @@ class LearnerEngine:
                 check(kernels().r2_torso_fwd_sp_multi(ptr(rp.frames), arr.ctypes.data, 1, grid,
                                                       stream_handle(side)), "torso_fwd_sp (hoisted)")
         return side
+
+    def _bptt_xcds(self) -> int:
+        """XCDs 0 .. n-1 hold the BPTT recurrence when it is packed two groups per XCD
+        (learner.bptt_xcd_pairs; lstm_persist.hip xcd_map 3), else 0."""
+        if not self.cfg.learner.bptt_xcd_pairs or self.layout.H // UNITS != 16:
+            return 0
+        return min(4, (-(-self.B // 16) + 1) // 2)
 
     def _bptt_groups_wgs(self) -> int:
         """Workgroups of the BPTT recurrence (batch tiles x hidden / 16)."""
@@ -499,9 +516,13 @@ class LearnerEngine:
         # when the side branch was captured first)
         self._backward_core()
         side = self._hoist_side(torso=not due and self.cfg.learner.hoist_torso, after_td=after_td)
-        main.wait_stream(side)   # joined before the conv backward: the side branch ends with the BPTT
+        end_join = self.cfg.learner.hoist_join == "end"
+        if not end_join:
+            main.wait_stream(side)   # before the conv backward: the side branch ends with the BPTT
         self._seg_torso()
         self._update()
+        if end_join:
+            main.wait_stream(side)
 
     def _hoist_step(self):
         k = self.steps_done
@@ -1243,6 +1264,19 @@ class LearnerEngine:
                             float(lc.lr), float(lc.adam_betas[0]), float(lc.adam_betas[1]),
                             float(lc.eps), gscale, ptr(self.replay.step), clip,
                             float(lc.grad_clip), s), "adam")
+        elif self._rms_all is not None:
+            # the update writes every packed layout and, when due, the target master and packs
+            r = self._rms_all
+            check(k.r2_rmsprop_pack_all(ptr(self.master), ptr(self.grad), ptr(self.opt_a),
+                                        ptr(self.opt_b), n, float(lc.lr), float(lc.rms_alpha),
+                                        float(lc.eps), gscale, clip, float(lc.grad_clip),
+                                        ptr(self.row_dst4), ptr(self.bf), ptr(self.bf_t),
+                                        L.bf_numel if self.sp else 0, ptr(self.target),
+                                        ptr(self.replay.step), self._baked_interval(), r["xq0"],
+                                        ptr(r["xA"]), ptr(r["xB"]), ptr(r["xF"]), r["bq0"], L.G,
+                                        ptr(r["binv"]), ptr(self.f32), ptr(self.f32_t),
+                                        ptr(self.lstm_b), ptr(self.lstm_b_t), s), "rmsprop_pack_all")
+            return
         elif self.row_dst4 is not None:
             # the update writes the row packs (w_ih / w_hh / head1) and, when due, the target
             # master itself; the pack launch below gathers the rest

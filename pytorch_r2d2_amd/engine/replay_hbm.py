@@ -228,10 +228,13 @@ class HBMReplay:
         return True
 
     def prio_tail_sample(self, starts: torch.Tensor, B: int, upd_lo: int, upd_hi: int, out_idx,
-                         out_prob, rows, Tn: int, states, h_f32: bool, qreset, stream=None) -> bool:
+                         out_prob, rows, Tn: int, states, h_f32: bool, qreset, skip_xcds: int = 0,
+                         stream=None) -> bool:
         """prio_tail (ending the step) + the NEXT step's sample_batch in ONE launch (replay.hip
         r2_prio_tail_sample): the sample waits for the repaired tree inside the launch.  Same
-        arguments as prio_tail + sample_batch; False (nothing launched) when the shape refuses."""
+        arguments as prio_tail + sample_batch; False (nothing launched) when the shape refuses.
+        ``skip_xcds``: keep the launch's workgroups off the first XCDs (the BPTT recurrence's,
+        lstm_persist.hip xcd_map 3) -- placement only, same results."""
         if self.tree.device.type != "cuda":
             return False
         rc = self.cfg.replay
@@ -245,7 +248,7 @@ class HBMReplay:
             upd_lo, upd_hi, self.cap_e, float(rc.eta), ptr(self.dirty), ptr(self.dirty_count),
             self.max_dirty, ptr(self.prio_sync), ptr(self.step), self.seed, ptr(out_idx),
             ptr(out_prob), ptr(rows), Tn, self.H, len(states), hs.ctypes.data, off.ctypes.data,
-            h.ctypes.data, c.ctypes.data, int(h_f32), ptr(qreset), self._ts(stream))
+            h.ctypes.data, c.ctypes.data, int(h_f32), ptr(qreset), int(skip_xcds), self._ts(stream))
         if r in (-3, -4):
             return False
         check(r, "prio_tail_sample")

@@ -77,6 +77,8 @@ _SIGS = {
     "r2_step_end": [P, P, P],
     "r2_rmsprop_centered": [P, P, P, P, I64, F, F, F, F, P, F, P],
     "r2_rmsprop_pack": [P, P, P, P, I64, F, F, F, F, P, F, P, P, P, I64, P, P, I64, P],
+    "r2_rmsprop_pack_all": [P, P, P, P, I64, F, F, F, F, P, F, P, P, P, I64, P, P, I64, I64, P, P, P,
+                            I64, I64, P, P, P, P, P, P],
     "r2_adam": [P, P, P, P, I64, F, F, F, F, F, P, P, F, P],
     "r2_sumsq": [P, I64, P, P],
     "r2_pack_bf16": [P, P, P, I64, P],
@@ -109,7 +111,7 @@ _SIGS = {
     "r2_lstm_bwd_set_stop": [P, I, I],
     "r2_lstm_bwd_xcd_pairs": [I],
     "r2_prio_tail_sample": [P, I, P, P, P, P, P, I, I, I, I, I, F, P, P, I, P, P, U64, P, P, P, I,
-                            I, I, P, P, P, P, I, P, P],
+                            I, I, P, P, P, P, I, P, I, P],
     "r2_prio_tail_pack": [P, I, P, P, P, P, P, I, I, I, I, I, F, P, P, I, P, P, I,
                           P, P, I64, P, P, P, I64, P, P, P, I64, I64, I64, P, P, I64, I64, I64, P],
     "r2_td_duel_set_trace": [P],

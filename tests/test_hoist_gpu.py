@@ -25,10 +25,16 @@ def _engine(hoist, B=64, interval=3, graph=True, **kw):
 
 
 def _state(rp, eng):
-    return {"master": eng.master, "target": eng.target, "opt_a": eng.opt_a, "opt_b": eng.opt_b,
-            "bf": eng.bf, "bf_t": eng.bf_t, "f32": eng.f32, "f32_t": eng.f32_t,
-            "lstm_b": eng.lstm_b, "lstm_b_t": eng.lstm_b_t, "priority": rp.priority,
-            "tree": rp.tree, "step": rp.step, "loss": eng.loss}
+    # the packed layouts by name (their alignment padding is never read and not compared: the
+    # hoisted step's optimizer scatters into the named packs only, r2_rmsprop_pack_all)
+    out = {"master": eng.master, "target": eng.target, "opt_a": eng.opt_a, "opt_b": eng.opt_b,
+           "lstm_b": eng.lstm_b, "lstm_b_t": eng.lstm_b_t, "priority": rp.priority,
+           "tree": rp.tree, "step": rp.step, "loss": eng.loss}
+    for tag, (bf, f32) in {"": (eng.bf, eng.f32), "_t": (eng.bf_t, eng.f32_t)}.items():
+        for plane in range(bf.shape[0]):
+            for k, v in eng.layout.packed_views(bf[plane], f32).items():
+                out["%s%s.%d" % (k, tag, plane)] = v
+    return out
 
 
 @pytest.mark.parametrize("graph", [True, False])

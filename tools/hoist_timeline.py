@@ -13,10 +13,14 @@ def main(pattern, which=-2):
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     S = lambda r: int(r["Start_Timestamp"])   # noqa: E731
     E = lambda r: int(r["End_Timestamp"])     # noqa: E731
-    # the step's main torso launch: the full-chip grid (the side launch has fewer workgroups)
-    grid = max(int(r["Grid_Size_X"]) for r in rows if "torso_fwd_sp2" in r["Kernel_Name"])
-    starts = [i for i, r in enumerate(rows)
-              if "torso_fwd_sp2" in r["Kernel_Name"] and int(r["Grid_Size_X"]) == grid]
+    # the step's main torso launch: the torso launch followed on its queue by the x-projection
+    def main_torso(i):
+        r = rows[i]
+        if "torso_fwd_sp2" not in r["Kernel_Name"]:
+            return False
+        nxt = next((o for o in rows[i + 1:] if o["Queue_Id"] == r["Queue_Id"]), None)
+        return nxt is not None and "gemm6_kernel<true, 192, 256" in nxt["Kernel_Name"]
+    starts = [i for i in range(len(rows)) if main_torso(i)]
     i0, i1 = starts[which], starts[which + 1] if which + 1 < len(starts) else len(rows)
     t0 = S(rows[i0])
     print("%-44s %5s %9s %9s %8s" % ("kernel", "queue", "start", "end", "us"))
