@@ -197,8 +197,7 @@ def main(argv=None):
                 # step k's priority tail, step k+1's sample and part of its target-net torso
                 # run on a side stream beside step k's BPTT (learner.hoist; bit-identical)
                 "hoisted_step": bool(getattr(eng, "hoist", False)),
-                "dp_graph": ("one graph, RCCL captured" if getattr(eng, "_one_dp_graph", False)
-                             else "segment graphs") if eng.dp else None,
+                "dp_graph": eng.dp_graph_label(),
             },
             "optimizer_steps_per_sec": round(opt_steps, 3),
             "sequences_per_sec": round(opt_steps * lc.batch_size * world, 1),

@@ -179,6 +179,10 @@ class LearnerConfig:
     hoist_torso: bool = True
     # the side branch's priority tail and next-step sample in one launch (r2_prio_tail_sample)
     hoist_fuse_sample: bool = True
+    # the optimizer writes every packed layout itself (r2_rmsprop_pack_all) instead of the
+    # pack_step launch after it: measured slower (rmsprop 14.5 -> 25.2 us against 6.4 us for the
+    # gather launch: the transposed W_hh^T / W1^T packs as 2-byte scattered stores), off
+    hoist_full_repack: bool = False
     # where the side branch joins the main stream: "bwd" (before the conv backward) | "end"
     hoist_join: str = "bwd"
     # BPTT recurrence groups packed two per XCD (lstm_persist.hip xcd_map 3): whole XCDs free
@@ -250,10 +254,14 @@ class DistConfig:
     # machinery's overhead at one forced rank 1.180 -> 1.122 ms against 1.102 for the plain step
     # (tools/dp_overhead_ab.sh, profiles/r03_force_dp_ab.txt)
     graph_collectives: bool = True
-    # ... also at world > 1.  Off until a run with two or more RCCL ranks has shown matching
-    # weights across ranks and a zero error word (the multi-rank DP path runs the segment graphs
-    # with the collectives issued between them, the form the multi-rank tests pin)
-    graph_collectives_multi: bool = False
+    # ... also at world > 1, rolled out per run (parallel/graph_rollout.py): the first
+    # one_graph_warm steps replay the segment graphs, then the one graph with a one_graph_validate
+    # step window in which every rank records a weight checksum + its error word on the device,
+    # checked by ONE all-reduce at the window's end; any mismatch sends every rank back to the
+    # segment graphs (rank 0's state re-broadcast) and bench.py labels the run
+    graph_collectives_multi: bool = True
+    one_graph_warm: int = 3
+    one_graph_validate: int = 50
     learner_steps_per_round: int = 1    # run_split default run length: rounds x this
 
 

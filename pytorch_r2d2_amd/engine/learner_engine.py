@@ -187,7 +187,7 @@ class LearnerEngine:
         # hoisted step: the optimizer writes EVERY packed layout itself (r2_rmsprop_pack_all; the
         # pack_step launch is gone from the step's tail)
         self._rms_all = None
-        if self.hoist and self.row_dst4 is not None:
+        if self.hoist and self.row_dst4 is not None and cfg.learner.hoist_full_repack:
             t = L.rms_scatter_tables()
             if t is not None:
                 xq0, xA, xB, xF, bq0, binv = t
@@ -1445,18 +1445,16 @@ class LearnerEngine:
             self.graph = True
             return
         one = self.cfg.dist.graph_collectives and (self.world == 1 or self.cfg.dist.graph_collectives_multi)
-        if self.dp and one and self._pg_backend() == "nccl":
-            # the whole DP step in ONE graph: the bucket all-reduces and the shard-stats
-            # all-gather are captured on their side streams (fork / join as graph edges), so the
-            # ~15 us gap of every segment boundary disappears
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._dp_step_body()
-            self.graphs.append(g)
-            self._one_dp_graph = True
-            torch.cuda.synchronize(self.device)
-            self.graph = True
-            return
+        if self.dp:
+            # the segment graphs first; the whole DP step as ONE graph (collectives captured on
+            # their side streams) replaces them after dist.one_graph_warm steps and, at world > 1,
+            # a validation window (parallel/graph_rollout.py)
+            from ..parallel.graph_rollout import GraphRollout
+            dc = self.cfg.dist
+            self._rollout = GraphRollout(self.pg, self.rank, self.world,
+                                         enabled=one and self._pg_backend() == "nccl",
+                                         warm=int(dc.one_graph_warm), validate=int(dc.one_graph_validate),
+                                         device=self.device)
         if self.dp:
             segs = [self._seg_core, self._seg_torso, self._seg_prio, self._seg_update]
             if self.dp_global:
@@ -1508,6 +1506,52 @@ class LearnerEngine:
         self._sync().finish()
         self._seg_update()
 
+    def _capture_one_dp(self) -> None:
+        """The whole DP step in ONE graph: the bucket all-reduces and the shard-stats all-gather
+        are captured on their side streams (fork / join as graph edges), so the ~15 us gap of
+        every segment boundary disappears."""
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=self.graphs[0].pool() if self.graphs else None):
+            self._dp_step_body()
+        torch.cuda.synchronize(self.device)
+        self._one_graph = g
+        self._one_dp_graph = True
+
+    def _dp_checksum(self) -> torch.Tensor:
+        """A fingerprint of this rank's weights (0-d float64, on the device): equal on every rank
+        while the ranks stay in lock-step."""
+        return self.master.double().sum() + 3.0 * self.target.double().sum()
+
+    def _dp_repair(self) -> None:
+        """After a one-graph validation mismatch: every rank takes rank 0's weights and optimizer
+        state, and re-packs its kernel layouts."""
+        import torch.distributed as dist
+        src = dist.get_global_rank(self.pg, 0) if hasattr(dist, "get_global_rank") else 0
+        for t in (self.master, self.target, self.opt_a, self.opt_b):
+            dist.broadcast(t, src=src, group=self.pg)
+        self._pack(always=True)
+        self._one_dp_graph = False
+
+    def _dp_rollout_after_step(self) -> None:
+        ro = getattr(self, "_rollout", None)
+        if ro is None:
+            return
+        if ro.validating():
+            if ro.record(self._dp_checksum(), self.err, self.steps_done) is False:
+                self._dp_repair()
+        elif ro.want_promote(self.steps_done):
+            self._capture_one_dp()
+            ro.promoted()
+
+    def dp_graph_label(self) -> Optional[str]:
+        """How the DP step is replayed (bench.py JSON): segment graphs, the one graph (validated
+        or still validating), or the fallback after a mismatch; None without DP."""
+        if not self.dp:
+            return None
+        ro = getattr(self, "_rollout", None)
+        return ro.label() if ro is not None else "eager"
+
     def step(self):
         if self.hoist and self.graph:
             self._hoist_step()
@@ -1515,8 +1559,13 @@ class LearnerEngine:
         if not self.graph:
             self.step_eager()
             return
-        if not self.dp or getattr(self, "_one_dp_graph", False):
+        if not self.dp:
             self.graphs[0].replay()
+        elif getattr(self, "_rollout", None) is not None and self._rollout.mode == "one":
+            self._one_graph.replay()
+            self.steps_done += 1
+            self._dp_rollout_after_step()
+            return
         else:
             L = self.layout
             if self.dp_global:
@@ -1541,6 +1590,9 @@ class LearnerEngine:
             g_prio.replay()
             self._sync().finish()
             g_update.replay()
+            self.steps_done += 1
+            self._dp_rollout_after_step()
+            return
         self.steps_done += 1
 
     def dp_imbalance(self) -> float:

@@ -8,6 +8,8 @@ processes) or programmatically, as ``;``-separated specs:
     learner:0:crash_at=<step>
     push:<id>:drop=<prob>             drop a trajectory push with probability p
     weights:<id>:stale=<n>            ignore the first n weight publications
+    dpcheck:<rank>:corrupt_at=<step>  perturb that rank's weight checksum in the one-graph DP
+                                      rollout's validation at that step (parallel/graph_rollout.py)
 
 Add ``once=1`` to a crash / hang rule (``actor:3:crash_at=500,once=1``) to fire it only in the
 process's first incarnation: the supervisor exports ``R2D2_INCARNATION`` (its restart count) to
@@ -55,6 +57,10 @@ class FaultPlan:
     def drop(self, role: str, rid: int) -> bool:
         r = self._r(role, rid)
         return bool(r and "drop" in r and self.rng.random() < r["drop"])
+
+    def corrupt(self, role: str, rid: int, step: int) -> bool:
+        r = self._r(role, rid)
+        return bool(r and "corrupt_at" in r and int(step) == int(r["corrupt_at"]))
 
     def stale(self, role: str, rid: int, n_seen: int) -> bool:
         r = self._r(role, rid)

@@ -368,11 +368,14 @@ def _force_dp_worker(rank, port, outdir):
                             init_module=QNet("cpu", cfg.model, cfg.env))
         assert eng.dp == force and eng.dp_global == force
         eng.capture(warmup=1)
-        assert len(eng.graphs) == (6 if force and not one else 1)
-        for _ in range(3):
+        if force:       # the segment graphs; the one graph after dist.one_graph_warm steps
+            assert len(eng.graphs) == 6
+        for _ in range(5):
             eng.step()
         torch.cuda.synchronize()
         assert eng.error_word() == 0
+        if force:
+            assert eng._rollout.mode == ("one" if one else "segments"), eng.dp_graph_label()
         out[(force, one)] = {"master": eng.master.cpu(), "loss": eng.loss_value()}
     torch.save(out, os.path.join(outdir, "force_dp.pt"))
     dist.destroy_process_group()
@@ -381,8 +384,9 @@ def _force_dp_worker(rank, port, outdir):
 def test_forced_dp_step_over_rccl_matches_plain_step(tmp_path):
     """The N-GPU step machinery at ONE rank over RCCL (dist.force_dp): six graph segments, the
     bucketed all-reduces on the comm stream and the shard-stats all-gather as one-rank
-    collectives -- the same trajectory as the plain single-graph step (what the 8-GPU run uses,
-    exercised on the real backend instead of gloo)."""
+    collectives, then (dist.graph_collectives) the one captured graph after the warm-up steps --
+    the same trajectory as the plain single-rank step (what the 8-GPU run uses, exercised on the
+    real backend instead of gloo)."""
     import torch.multiprocessing as tmp
     tmp.spawn(_force_dp_worker, args=(_free_port(), str(tmp_path)), nprocs=1, join=True)
     r = torch.load(tmp_path / "force_dp.pt", weights_only=True)

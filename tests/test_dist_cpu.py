@@ -292,3 +292,48 @@ def test_async_links_decouple_learner_from_slow_actor(tmp_path):
             assert ra["weights"] and ra["weights"] == sorted(ra["weights"])
     print("learner steps/s, fast actors vs one slow actor:", rates)
     assert rates[2] >= 0.7 * rates[0], rates
+
+
+def _rollout_worker(rank, port, fault, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2")
+    import torch.distributed as dist
+    from pytorch_r2d2_amd.parallel.graph_rollout import GraphRollout
+    from pytorch_r2d2_amd.utils.faults import set_faults
+    set_faults(fault)
+    dist.init_process_group("gloo")
+    ro = GraphRollout(dist.group.WORLD, rank, 2, enabled=True, warm=3, validate=4)
+    events = []
+    w = torch.zeros(16, dtype=torch.float64)
+    for step in range(1, 12):
+        w += step          # both ranks hold the same "weights"
+        if ro.validating():
+            v = ro.record(w.sum(), torch.tensor(0), step)
+            if v is not None:
+                events.append(("verdict", step, bool(v)))
+        elif ro.want_promote(step):
+            ro.promoted()
+            events.append(("promote", step))
+    torch.save({"events": events, "mode": ro.mode, "fallback": ro.fallback,
+                "mismatch": ro.mismatch_step, "label": ro.label()}, "%s.%d" % (out, rank))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fault", ["", "dpcheck:1:corrupt_at=5"])
+def test_one_graph_rollout_falls_back_on_checksum_mismatch(tmp_path, fault):
+    """parallel/graph_rollout.py at gloo world 2 (round-6 verdict item 7): segment graphs for the
+    warm-up steps, the one graph after them, a 4-step validation window decided by ONE
+    all-reduce; a checksum perturbed on rank 1 at step 5 (R2D2_FAULTS) sends BOTH ranks back to
+    the segment graphs with the same mismatch step; without the fault both stay on the one graph."""
+    import torch.multiprocessing as tmp
+    out = str(tmp_path / "ro")
+    tmp.spawn(_rollout_worker, args=(_free_port(), fault, out), nprocs=2, join=True)
+    r = [torch.load("%s.%d" % (out, k), weights_only=True) for k in range(2)]
+    assert r[0]["events"] == r[1]["events"]
+    assert r[0]["events"][0] == ("promote", 3)
+    if fault:
+        assert r[0]["events"][1] == ("verdict", 7, False)
+        assert all(x["fallback"] and x["mode"] == "segments" and x["mismatch"] == 5 for x in r)
+        assert "fallback at step 5" in r[0]["label"]
+    else:
+        assert r[0]["events"][1] == ("verdict", 7, True)
+        assert all(not x["fallback"] and x["mode"] == "one" for x in r)

@@ -37,14 +37,16 @@ def _state(rp, eng):
     return out
 
 
-@pytest.mark.parametrize("graph", [True, False])
-def test_hoisted_step_is_bitwise_the_plain_step(graph):
+@pytest.mark.parametrize("graph,full_repack", [(True, False), (False, False), (True, True)])
+def test_hoisted_step_is_bitwise_the_plain_step(graph, full_repack):
     """Bench shape (B=64, 40 + 40, n=5, fixed target), target sync every 3 steps (steps 2, 5, 8
     sync: the step after each runs the full target torso), one invalidation in the middle (the
     next step samples at its start): weights, optimizer moments, every packed layout, priorities,
-    sum tree and step counter equal the plain engine's after every step; error word 0."""
+    sum tree and step counter equal the plain engine's after every step; error word 0.
+    ``full_repack``: the optimizer scatters every packed layout itself (r2_rmsprop_pack_all)."""
     rp0, plain = _engine(False, graph=graph)
-    rp1, hoist = _engine(True, graph=graph)
+    rp1, hoist = _engine(True, graph=graph, **{"learner.hoist_full_repack": full_repack})
+    assert (hoist._rms_all is not None) == full_repack
     assert hoist.hoist and not plain.hoist
     if graph:
         plain.capture(warmup=0)

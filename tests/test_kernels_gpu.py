@@ -610,11 +610,56 @@ def test_fused_prio_tail_matches_refresh_and_tree_repair(cap):
                                  f"offs {offs} sync {a.prio_sync.tolist()}")
         assert int(a.step.item()) == int(b.step.item()) == rnd + 1
         assert int(a.dirty_count.item()) == 0
-        assert a.prio_sync.tolist() == [0, 0, 0, 0], a.prio_sync.tolist()
+        assert a.prio_sync.tolist() == [0] * 8, a.prio_sync.tolist()
     # without end_step the counter and the dirty list are left alone
     a.prio_tail(idx, 64, 0, cfg.replay.seq_len, end_step=False)
     torch.cuda.synchronize()
     assert int(a.step.item()) == 4 and int(a.dirty_count.item()) > 0
+
+
+@pytest.mark.parametrize("skip", [0, 2])
+def test_fused_prio_tail_sample_matches_tail_then_sample(skip):
+    """replay.hip r2_prio_tail_sample (the hoisted step's side branch: priority tail ending the
+    step, then the NEXT batch sampled from the repaired tree inside the same launch, the tail's
+    workgroups kept off the first ``skip`` XCD slots) == prio_tail + sample_batch, bit for bit:
+    tree, step counter, starts, probabilities, row list, stored states; the frame-queue words are
+    zeroed; every sync word is back to 0."""
+    from pytorch_r2d2_amd.engine.replay_hbm import HBMReplay
+    cfg = get_config("atari57", **{"replay.capacity": 64000, "replay.n_subrings": 8})
+    a = HBMReplay(cfg, DEV)
+    a.fill_synthetic(episode_len=200, seed=3)
+    b = HBMReplay(cfg, DEV)
+    b.fill_synthetic(episode_len=200, seed=3)
+    B, H, Tn = 64, cfg.model.hidden, cfg.replay.seq_len + cfg.replay.n_step
+    g = torch.Generator(device=DEV).manual_seed(9)
+    z = lambda *s, dt=torch.float32: torch.zeros(s, dtype=dt, device=DEV)   # noqa: E731
+    for rnd in range(3):
+        idx = z(B, dt=torch.int32)
+        a.sample(B, idx, z(B))
+        pr = torch.rand(a.capacity, generator=g, device=DEV) * 3
+        for r in (a, b):
+            r.priority.copy_(pr)
+        outs = []
+        for r in (a, b):
+            st, pb, rows = z(B, dt=torch.int32), z(B), z(Tn * B, dt=torch.int32)
+            hs = [(r.hs_cs, 0, z(B, H), z(B, H)), (r.target_hs_cs, 5, z(B, H), z(B, H)),
+                  (r.hs_cs, 5, z(B, H), z(B, H))]
+            q = torch.full((4,), 7, dtype=torch.int32, device=DEV)
+            outs.append((st, pb, rows, hs, q))
+            if r is a:
+                assert r.prio_tail_sample(idx, B, 40, 80, st, pb, rows, Tn, hs, True, q, skip_xcds=skip)
+            else:
+                assert r.prio_tail(idx, B, 40, 80, True)
+                r.sample_batch(B, st, pb, rows, Tn, hs, h_f32=True, qreset=q)
+        torch.cuda.synchronize()
+        assert torch.equal(a.tree, b.tree) and torch.equal(a.step, b.step)
+        (s0, p0, r0, h0, q0), (s1, p1, r1, h1, q1) = outs
+        assert torch.equal(s0, s1) and torch.equal(p0, p1) and torch.equal(r0, r1)
+        for (_, _, ha, ca), (_, _, hb, cb) in zip(h0, h1):
+            assert torch.equal(ha, hb) and torch.equal(ca, cb)
+        assert q0[:2].tolist() == [0, 0] and q0[2:].tolist() == [7, 7]
+        assert a.prio_sync.tolist() == [0] * 8, a.prio_sync.tolist()
+        assert int(a.dirty_count.item()) == 0
 
 
 @pytest.mark.parametrize("N", [2560, 333])
