@@ -47,6 +47,7 @@ struct TSJob {
   // A grabbed frame is always finished, so [0, min(q[0], n)) is done once the qmode-1 launch ends.
   unsigned* q;
   int n, wbegin, wcount, qmode;
+  int avoid, pad_j;                // qmode 1: bit x set = workgroups on XCD x leave at once (job word 19)
 };
 struct TSArgs {
   const uint8_t* frames;
@@ -317,6 +318,11 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
   int f = wk - wbeg;
   int row_f = 0, row_q1 = 0, f_q1 = 0;
   if (qjob) {
+    if (J.qmode == 1 && J.avoid) {   // keep the hoisted frames off the recurrence's XCDs
+      unsigned x;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+      if ((J.avoid >> (x & 15)) & 1) return;
+    }
     // first two frames of this workgroup from the queue (before any setup: a workgroup that
     // finds the queue empty or stopped leaves at once)
     if (tid == 0) {
@@ -710,6 +716,7 @@ extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs,
     J.s1 = (bf16*)p[13]; J.s1l = (bf16*)p[14]; J.s2 = (bf16*)p[15]; J.s2l = (bf16*)p[16];
     J.q = (unsigned*)p[17];
     J.qmode = J.q ? (int)p[18] : 0;
+    J.avoid = J.q ? (int)p[19] : 0;
     if (!J.w1l || !J.w2l || !J.w3l || !J.out_l || (J.s1 && !J.s1l) || (J.s2 && !J.s2l)) return -4;
     // queue jobs: no activation saves (the saved frames are indexed by launch order), mode 1 / 2
     if (J.q && (J.s1 || J.s2 || (J.qmode != 1 && J.qmode != 2))) return -5;

@@ -183,6 +183,8 @@ class LearnerConfig:
     # pack_step launch after it: measured slower (rmsprop 14.5 -> 25.2 us against 6.4 us for the
     # gather launch: the transposed W_hh^T / W1^T packs as 2-byte scattered stores), off
     hoist_full_repack: bool = False
+    # XCD bit mask the hoisted torso frames stay off (their workgroups leave at once there)
+    hoist_avoid_xcds: int = 0
     # where the side branch joins the main stream: "bwd" (before the conv backward) | "end"
     hoist_join: str = "bwd"
     # BPTT recurrence groups packed two per XCD (lstm_persist.hip xcd_map 3): whole XCDs free

@@ -116,7 +116,6 @@ class LearnerEngine:
                 arr = (ctypes.c_int * 8)(*xcd_cus)
                 kernels().r2_set_xcd_cus(arr)
             kernels().r2_lstm_persist_force_slow(0 if cfg.learner.lstm_xcd_pairs else 2)
-            kernels().r2_lstm_bwd_xcd_pairs(1 if cfg.learner.bptt_xcd_pairs else 0)
             # gemm_sp.hip launcher mode: bit 0 interleaved fragment loads, bit 2 gemm5, bit 6 the
             # tile-major item order instead of the K-split-major one
             kernels().r2_gemm5_set_mode(1 | (0 if cfg.learner.sp_gemm6 else 4)
@@ -184,6 +183,10 @@ class LearnerEngine:
         self.graph = None
         self.stats: Dict[str, float] = {}
         self._alloc()
+        if d.type == "cuda":
+            # the BPTT packed two groups per XCD only beside the hoisted torso frames (alone it
+            # runs faster one group per XCD: 100 vs 113 us, profiles/r06_hoist_bptt_placement.txt)
+            kernels().r2_lstm_bwd_xcd_pairs(1 if (self.hoist and cfg.learner.bptt_xcd_pairs) else 0)
         # hoisted step: the optimizer writes EVERY packed layout itself (r2_rmsprop_pack_all; the
         # pack_step launch is gone from the step's tail)
         self._rms_all = None
@@ -477,21 +480,28 @@ class LearnerEngine:
             if torso:
                 lc = self.cfg.learner
                 rows = self._sets[nxt]["rows"][self.t_lo_tg * B:]
-                job = self._torso_job_sp(self.pk_t, self.pk_t_lo, rows, self.X_tg, self.X_tg_lo, qmode=1)
+                job = self._torso_job_sp(self.pk_t, self.pk_t_lo, rows, self.X_tg, self.X_tg_lo, qmode=1,
+                                         avoid=int(lc.hoist_avoid_xcds))
                 arr = np.asarray([job], dtype=np.int64)
                 self._side_job = arr      # (the launcher copies it into the kernel arguments)
-                grid = int(lc.hoist_grid) or (self.n_cus if lc.bptt_xcd_pairs
+                grid = int(lc.hoist_grid) or (self.n_cus if lc.bptt_xcd_pairs or lc.hoist_avoid_xcds
                                               else max(1, self.n_cus - self._bptt_groups_wgs()))
                 check(kernels().r2_torso_fwd_sp_multi(ptr(rp.frames), arr.ctypes.data, 1, grid,
                                                       stream_handle(side)), "torso_fwd_sp (hoisted)")
         return side
 
     def _bptt_xcds(self) -> int:
-        """XCDs 0 .. n-1 hold the BPTT recurrence when it is packed two groups per XCD
-        (learner.bptt_xcd_pairs; lstm_persist.hip xcd_map 3), else 0."""
-        if not self.cfg.learner.bptt_xcd_pairs or self.layout.H // UNITS != 16:
-            return 0
-        return min(4, (-(-self.B // 16) + 1) // 2)
+        """The first n XCDs, which hold the BPTT recurrence's workgroups, for the hoisted
+        branch's tail workgroups to stay off: packed two groups per XCD (learner.bptt_xcd_pairs;
+        lstm_persist.hip xcd_map 3) -> ceil(batch tiles / 2); else the low run of
+        learner.hoist_avoid_xcds (one group per XCD: XCDs 0 .. tiles-1)."""
+        lc = self.cfg.learner
+        if lc.bptt_xcd_pairs and self.layout.H // UNITS == 16:
+            return min(4, (-(-self.B // 16) + 1) // 2)
+        m, n = int(lc.hoist_avoid_xcds), 0
+        while n < 4 and (m >> n) & 1:
+            n += 1
+        return n
 
     def _bptt_groups_wgs(self) -> int:
         """Workgroups of the BPTT recurrence (batch tiles x hidden / 16)."""
@@ -663,7 +673,8 @@ class LearnerEngine:
         return [ptr(rows), rows.numel(), ptr(pk["conv1"]), ptr(pk["b1"]), ptr(pk["conv2"]),
                 ptr(pk["b2"]), ptr(pk["conv3"]), ptr(pk["b3"]), ptr(out), s1, s2, 0]
 
-    def _torso_job_sp(self, pk, pkl, rows, out, out_lo, save_at=None, qmode: int = 0):
+    def _torso_job_sp(self, pk, pkl, rows, out, out_lo, save_at=None, qmode: int = 0,
+                      avoid: int = 0):
         """torso_sp.hip job (20 int64): weights hi / lo, features hi / lo, saved activations, and
         (qmode 1 / 2, the hoisted step) the frame-queue words ``self.tq``."""
         B = self.B
@@ -672,10 +683,10 @@ class LearnerEngine:
             r0, r1 = save_at * B, save_at * B + rows.numel()
             s = [ptr(self.act1[r0:r1]), ptr(self.act1_lo[r0:r1]), ptr(self.act2[r0:r1]),
                  ptr(self.act2_lo[r0:r1])]
-        q = [ptr(self.tq), qmode] if qmode else [0, 0]
+        q = [ptr(self.tq), qmode, avoid] if qmode else [0, 0, 0]
         return [ptr(rows), rows.numel(), ptr(pk["conv1"]), ptr(pkl["conv1"]), ptr(pk["b1"]),
                 ptr(pk["conv2"]), ptr(pkl["conv2"]), ptr(pk["b2"]), ptr(pk["conv3"]),
-                ptr(pkl["conv3"]), ptr(pk["b3"]), ptr(out), ptr(out_lo)] + s + q + [0]
+                ptr(pkl["conv3"]), ptr(pk["b3"]), ptr(out), ptr(out_lo)] + s + q
 
     # ------------------------------------------------------------------ the step
     def _forward_loss(self):
