@@ -53,7 +53,8 @@ struct TSArgs {
   const uint8_t* frames;
   TSJob job[TS_MAX_JOBS];
   int njobs, dbg;            // dbg: timing-probe bits (r2_torso_sp_debug), 0 in production
-  int dyn, pad_;             // dyn: workgroups dealt on the device (a qmode-2 job's size is q-dependent)
+  int dyn;                   // dyn: workgroups dealt on the device (a qmode-2 job's size is q-dependent)
+  int save_w;                // deal weight of a frame with activation saves, per mille of a plain one
   long long* trace;          // optional per-phase clock stamps (r2_torso_sp_trace), null in production
 };
 
@@ -270,6 +271,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
     // the host's deal (r2_torso_fwd_sp_multi) with a qmode-2 job counted at its remaining frames
     // n - min(q[0], n): every workgroup computes the same table from the same words
     int ne[TS_MAX_JOBS];
+    int64_t nw_[TS_MAX_JOBS];   // frames weighted by their cost (saves: args.save_w per mille)
     int64_t total = 0;
 #pragma unroll
     for (int i = 0; i < TS_MAX_JOBS; ++i) {
@@ -278,7 +280,8 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
       if (i < args.njobs && Ji.qmode == 2)
         v -= (int)min(__hip_atomic_load(Ji.q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), (unsigned)Ji.n);
       ne[i] = v;
-      total += v;
+      nw_[i] = v > 0 ? (int64_t)v * (i < args.njobs && Ji.s1 ? args.save_w : 1000) : 0;
+      total += nw_[i];
     }
     const int nw = gridDim.x;
     int wb = 0, left = 0;
@@ -290,7 +293,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
     for (int i = 0; i < TS_MAX_JOBS; ++i) {
       if (ne[i] <= 0) continue;
       --left;   // non-empty jobs after this one: each keeps at least one workgroup (nw >= njobs)
-      seen += ne[i];
+      seen += nw_[i];
       int end = (int)((seen * nw + total - 1) / total);
       end = min(end, nw - left);
       const int cnt = min(max(end - wb, 1), ne[i]);
@@ -683,6 +686,13 @@ extern "C" int r2_torso_sp_trace(long long* p) { g_tsp_trace = p; return 0; }
 // timing probes only (tools/sp_micro.py): bit 0 skips conv1, bit 1 conv2, bit 2 conv3, bit 4 the
 // next-frame staging, bit 6 the act1 save
 extern "C" int r2_torso_sp_debug(int bits) { g_tsp_dbg = bits; return 0; }
+// deal weight of a frame with activation saves, per mille of a plain frame (learner.torso_save_weight)
+static int g_tsp_save_w = 1000;
+extern "C" int r2_torso_sp_save_weight(int per_mille) {
+  if (per_mille < 500 || per_mille > 4000) return -1;
+  g_tsp_save_w = per_mille;
+  return 0;
+}
 
 extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs, int njobs,
                                      int grid, void* stream) {
@@ -691,8 +701,13 @@ extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs,
   a.frames = frames;
   a.dbg = g_tsp_dbg;
   a.trace = g_tsp_trace;
+  a.save_w = g_tsp_save_w;
+  // frames weighted by cost: a frame whose activations are saved (job word 13) takes longer
+  auto wt = [&](const int64_t* p) -> int64_t {
+    return p[1] > 0 ? p[1] * (p[13] ? g_tsp_save_w : 1000) : 0;
+  };
   int64_t total = 0;
-  for (int i = 0; i < njobs; ++i) total += jobs[TS_JOB_WORDS * i + 1] > 0 ? jobs[TS_JOB_WORDS * i + 1] : 0;
+  for (int i = 0; i < njobs; ++i) total += wt(jobs + TS_JOB_WORDS * i);
   if (total <= 0) return 0;
   if (grid <= 0) grid = 256;
   const int nw = grid;
@@ -701,7 +716,7 @@ extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs,
   for (int i = 0; i < njobs; ++i) {
     const int64_t* p = jobs + TS_JOB_WORDS * i;
     if (p[1] <= 0) continue;
-    seen += p[1];
+    seen += wt(p);
     int end = (int)((seen * nw + total - 1) / total);
     if (end > nw) end = nw;
     int cnt = end - wb;

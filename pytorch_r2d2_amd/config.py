@@ -152,6 +152,9 @@ class LearnerConfig:
     # split precision: the dueling head's gradient reduction on the BPTT launch's idle workgroups
     # (r2_lstm_bwd_tag_sp_hg) instead of its own 28 us launch
     sp_head_grads_in_bptt: bool = True
+    # fused split-precision torso forward: how much a frame whose activations are saved for the
+    # backward costs relative to a plain frame, for the deal of workgroups over the frame lists
+    torso_save_weight: float = 1.0
     torso_bwd: str = "fused"         # fused (HIP kernel) | library (MIOpen convolution_backward)
     # library conv path (frame geometries without the fused HIP torso, e.g. DMLab): MIOpen find
     # mode (torch.backends.cudnn.benchmark) instead of its immediate-mode heuristics

@@ -116,6 +116,8 @@ class LearnerEngine:
                 arr = (ctypes.c_int * 8)(*xcd_cus)
                 kernels().r2_set_xcd_cus(arr)
             kernels().r2_lstm_persist_force_slow(0 if cfg.learner.lstm_xcd_pairs else 2)
+            check(kernels().r2_torso_sp_save_weight(int(round(1000 * cfg.learner.torso_save_weight))),
+                  "torso_sp_save_weight")
             # gemm_sp.hip launcher mode: bit 0 interleaved fragment loads, bit 2 gemm5, bit 6 the
             # tile-major item order instead of the K-split-major one
             kernels().r2_gemm5_set_mode(1 | (0 if cfg.learner.sp_gemm6 else 4)
