@@ -43,8 +43,9 @@ struct TSJob {
   bf16* s2; bf16* s2l;             // optional (n, 81, 32)
   // frame queue (job words 17 / 18; null = the static grid-stride deal).  qmode 1 (the hoisted
   // target-net frames beside the BPTT): frames q[0]++ until q[0] >= n or the stop word q[2] is set;
-  // qmode 2 (the same job's remainder in the next step's launch): frames min(q[0], n) + q[1]++.
-  // A grabbed frame is always finished, so [0, min(q[0], n)) is done once the qmode-1 launch ends.
+  // a taken frame is always finished, so [0, min(q[0], n)) is done once the qmode-1 launch ends.
+  // qmode 2 (the same job's remainder in the next step's launch): frames [min(q[0], n), n) dealt
+  // with the static stride over the job's workgroups (their number set on the device, TSArgs::dyn).
   unsigned* q;
   int n, wbegin, wcount, qmode;
   int avoid, pad_j;                // qmode 1: bit x set = workgroups on XCD x leave at once (job word 19)
@@ -58,17 +59,13 @@ struct TSArgs {
   long long* trace;          // optional per-phase clock stamps (r2_torso_sp_trace), null in production
 };
 
-// Frame of a queue job (one thread): qmode 1 stops at the stop word, qmode 2 continues after the
-// qmode-1 launch's frames.  n when the job is exhausted.
+// Frame of a qmode-1 queue job (one thread; the workgroup's first two frames -- later ones are
+// taken with the round trips hidden under phase A, in the frame loop): n once the job is
+// exhausted or the stop word is set.
 __device__ __forceinline__ int ts_grab(const TSJob& J) {
   unsigned* q = J.q;
-  if (J.qmode == 1) {
-    if (__hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return J.n;
-    const unsigned g = __hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return g < (unsigned)J.n ? (int)g : J.n;
-  }
-  const unsigned base = min(__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), (unsigned)J.n);
-  const unsigned g = base + __hip_atomic_fetch_add(q + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (__hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) return J.n;
+  const unsigned g = __hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return g < (unsigned)J.n ? (int)g : J.n;
 }
 
@@ -316,9 +313,13 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
   const int stride = wcnt;
   if (wk - wbeg >= stride) return;
   const int n_frames = J.n;
-  const bool qjob = J.q != nullptr;
+  // qmode 1 frames come from the queue; a qmode-2 job deals the frames the qmode-1 launch left,
+  // [min(q[0], n), n), over its workgroups with the static stride (no per-frame atomics)
+  const bool qjob = J.q != nullptr && J.qmode == 1;
   __shared__ int s_q[4];
   int f = wk - wbeg;
+  if (J.q != nullptr && J.qmode == 2)
+    f += (int)min(__hip_atomic_load(J.q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), (unsigned)n_frames);
   int row_f = 0, row_q1 = 0, f_q1 = 0;
   if (qjob) {
     if (J.qmode == 1 && J.avoid) {   // keep the hoisted frames off the recurrence's XCDs
@@ -394,6 +395,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
 
   int fprev = -1;
   int it_dbg = 0;
+  unsigned q_g = 0u, q_st = 0u, q_stop = 0u;   // queue job, thread 192 only
   long long* tr = (args.trace && blockIdx.x == 0 && lane == 0) ? args.trace + wave * 16 * 5 : nullptr;
 #define TS2_STAMP(k) \
   if (tr && it_dbg < 16) tr[it_dbg * 5 + (k)] = (long long)__builtin_readcyclecounter();
@@ -407,6 +409,12 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
     // hoisted out of the frame loop (32+ VGPRs held across every phase otherwise)
     int oz;
     asm volatile("v_mov_b32 %0, 0" : "=v"(oz));
+    // queue job: wave 3's first lane takes fnn here and hands it over at the end of phase A; its
+    // row is loaded in phase B (both round trips hidden under the phases' work)
+    if (qjob && tid == 192 && fn < n_frames && !q_stop) {
+      q_st = __hip_atomic_load(J.q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      q_g = __hip_atomic_fetch_add(J.q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     // =================== phase A: conv1(f) || conv3(f-1) on wave 2; frame f+1 -> registers
     // (nothing in phase A waits on vmcnt: conv1 / conv3 operands come from LDS / registers)
     if (have && fn < n_frames && !(args.dbg & 16)) {
@@ -567,6 +575,11 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
         }
       }
     }
+    if (qjob && tid == 192) {
+      s_q[0] = (fn < n_frames && !q_stop) ? (int)min(q_g, (unsigned)n_frames) : n_frames;
+      q_stop |= q_st;     // the stop word seen: this frame is the workgroup's last grab
+      q_st = 0u;
+    }
     TS2_STAMP(1);
     lds_sync();
     TS2_STAMP(2);
@@ -582,9 +595,8 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
           ((u32x4*)fr)[c] = __builtin_bit_cast(u32x4, wfl[8 + q]) ^ 0x80808080u;
       }
     }
-    if (qjob && tid == 192) {   // fnn of a queue job and its row, read after the barrier below
-      const int g = fn < n_frames ? ts_grab(J) : n_frames;
-      s_q[0] = g;
+    if (qjob && tid == 192) {   // fnn's row (fnn taken in phase A), read after the barrier below
+      const int g = s_q[0];
       s_q[1] = g < n_frames ? (J.rows ? J.rows[g] : g) : 0;
     }
     if (conv2_wave) {

@@ -122,7 +122,6 @@ def test_torso_queue_jobs_match_static_job():
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
     assert torch.equal(other, other_ref)
-    assert int(eng.tq[1]) >= n - n // 3
 
 
 @pytest.mark.parametrize("hoist", [False, True])
