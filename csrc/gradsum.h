@@ -103,43 +103,35 @@ __device__ __forceinline__ void head_grads_body(const HeadGradArgs& a, int cb, i
   float s = 0.f, dvs = 0.f, w[gs::MAXW];
 #pragma unroll
   for (int i = 0; i < gs::MAXW; ++i) w[i] = 0.f;
-  // rows r0+rg, +4, ...: loads of U rows issued together, then accumulated in row order.  The
-  // item's dva rows are staged in LDS chunks (the partials' buffer, free until the epilogue) and
-  // read as broadcasts: per row a thread loads only its zr / dz / dz_lo column, so 16 rows fit in
-  // flight (round 6: 5 rows with 8 dva loads each left the item latency-bound, ~59 us for 320 rows)
-  constexpr int U = 16;
-  float* dvl = &red[0][0][0];
-  const int cap = ((4 * 64 * gs::NV) / W) & ~3;   // rows per chunk, a multiple of the 4 row groups
-  for (int q0 = r0; q0 < r1; q0 += cap) {
-    const int q1 = min(q0 + cap, r1);
-    __syncthreads();                               // the previous chunk's readers are done
-    for (int i = tid; act && i < (q1 - q0) * W; i += 256) dvl[i] = a.dva[(size_t)q0 * W + i];
-    __syncthreads();
-    for (int rb = q0 + rg; act && rb < q1; rb += 4 * U) {
-      float z[U], d[U];
+  // rows r0+rg, +4, ...: loads of U rows issued together, then accumulated in row order
+  constexpr int U = 5;
+  for (int rb = r0 + rg; act && rb < r1; rb += 4 * U) {
+    float z[U], d[U], dvv[U][gs::MAXW], dsl[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int r = min(rb + 4 * u, q1 - 1);
-        const size_t o = (size_t)r * C + col;
-        z[u] = vcol ? (a.zr32 ? a.zr32[o] : (float)a.zr[o]) : 0.f;
-        d[u] = vcol ? (float)a.dz[o] + (a.dz_lo ? (float)a.dz_lo[o] : 0.f) : 0.f;
+    for (int u = 0; u < U; ++u) {
+      const int r = min(rb + 4 * u, r1 - 1);
+      const float* dv = a.dva + (size_t)r * W;
+      const size_t o = (size_t)r * C + col;
+      z[u] = vcol ? (a.zr32 ? a.zr32[o] : (float)a.zr[o]) : 0.f;
+      d[u] = vcol ? (float)a.dz[o] + (a.dz_lo ? (float)a.dz_lo[o] : 0.f) : 0.f;
+      dvv[u][0] = dv[0];
+#pragma unroll
+      for (int i = 1; i < gs::MAXW; ++i) dvv[u][i] = 7 * p + i < W ? dv[7 * p + i] : 0.f;
+      dsl[u] = (cb == 0 && p == 0 && c < W) ? dv[c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (rb + 4 * u >= r1) break;
+      s += d[u];
+      if (!adv) {
+        w[0] += dvv[u][0] * z[u];
+      } else {
+#pragma unroll
+        for (int i = 0; i < gs::MAXW - 1; ++i) w[i] += dvv[u][1 + i] * z[u];
       }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (rb + 4 * u >= q1) break;
-        const float* dv = dvl + (rb + 4 * u - q0) * W;
-        s += d[u];
-        if (!adv) {
-          w[0] += dv[0] * z[u];
-        } else {
-#pragma unroll
-          for (int i = 0; i < gs::MAXW - 1; ++i) w[i] += (7 * p + 1 + i < W ? dv[7 * p + 1 + i] : 0.f) * z[u];
-        }
-        dvs += (cb == 0 && p == 0 && c < W) ? dv[c] : 0.f;
-      }
+      dvs += dsl[u];
     }
   }
-  __syncthreads();                                 // dvl (= red) is rewritten below
   if (act) {
     red[rg][c][0] = s;
     red[rg][c][1] = dvs;

@@ -1781,10 +1781,12 @@ static int lstm_bwd_tag_launch(const float* dh_ext, const float* gates, const fl
   args.dgates_lo = dgates_lo;
   args.dz = dz[0]; args.dz_lo = dz[1]; args.w1t = dz[2]; args.w1t_lo = dz[3];
   if (args.dz && (!sp || H != 256 || g_pl_bwd8)) return -13;   // split-precision T4 BPTT, H 256 only
-  // one workgroup per CU (the PL_LDS_RESERVE rule, comment at its definition): the dz path's own
-  // dynamic LDS (iteration 0's dz rows + the dh partials) is smaller than the reserve
-  const int dyn_lds = args.dz ? max(PL_LDS_RESERVE, PT_DZ_LDS + 4 * PT_ROWS * PL_UNITS * 4)
-                              : PL_LDS_RESERVE;
+  // one workgroup per CU (the PL_LDS_RESERVE rule, comment at its definition): the dz path's
+  // dynamic LDS (iteration 0's dz rows + the dh partials, 36 KB) plus the kernel's 54 KB of static
+  // LDS (LDS_Block_Size in the rocprofv3 trace) is 90 KB > 80 KB, so two workgroups never share a
+  // CU either way; reserving the full 84 KB there as well measured +7 us per BPTT (97 -> 104 us)
+  const int dyn_lds = args.dz ? PT_DZ_LDS + 4 * PT_ROWS * PL_UNITS * 4 : PL_LDS_RESERVE;
+  static_assert(PT_DZ_LDS + 4 * PT_ROWS * PL_UNITS * 4 + 48 * 1024 > 80 * 1024, "1 WG per CU");
   hipStream_t s = (hipStream_t)stream;   // counters are left zeroed by the previous launch
   dim3 grid(nh ? 256 : (xmap == 3 ? 16 * nwg : xmap ? 8 * nwg : MB * nwg)), block(320);
 #define R2_BWD_LAUNCH1(HH, SPP, T4)                                                            \

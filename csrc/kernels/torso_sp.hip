@@ -248,6 +248,10 @@ __device__ __forceinline__ void c1_frags(const uint8_t* dig, int lane, bf16x8 (&
 __constant__ int c_s2_begin[8] = {0, 2, 4, 4, 6, 8, 10, 11};
 __constant__ int c_s2_count[8] = {2, 2, 0, 2, 2, 2, 1, 2};
 
+// QUEUE: the hoisted launch's qmode-1 queue job (frames taken one by one); false: every job on
+// the static grid-stride deal (the frame loop as before the queue existed -- its register
+// allocation and schedule do not carry the queue's code)
+template <bool QUEUE>
 __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
   using namespace tsp2;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -315,7 +319,8 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
   const int n_frames = J.n;
   // qmode 1 frames come from the queue; a qmode-2 job deals the frames the qmode-1 launch left,
   // [min(q[0], n), n), over its workgroups with the static stride (no per-frame atomics)
-  const bool qjob = J.q != nullptr && J.qmode == 1;
+  const bool qjob = QUEUE && J.q != nullptr && J.qmode == 1;
+  if (!QUEUE && J.q != nullptr && J.qmode == 1) return;   // (the launcher never pairs these)
   __shared__ int s_q[4];
   int f = wk - wbeg;
   if (J.q != nullptr && J.qmode == 2)
@@ -755,14 +760,22 @@ extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs,
   // the device-side deal (dyn) may give every workgroup of the grid a job: keep the whole grid
   if (grid > wb && !a.dyn) grid = wb;
   if (a.dyn && grid < a.njobs) return -3;
+  bool queue = false;
+  for (int i = 0; i < a.njobs; ++i) queue = queue || a.job[i].qmode == 1;
   static bool attr2 = false;
   if (!attr2) {
-    hipFuncSetAttribute((const void*)torso_fwd_sp2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipFuncSetAttribute((const void*)torso_fwd_sp2_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        tsp2::LDS_BYTES_I8);
+    hipFuncSetAttribute((const void*)torso_fwd_sp2_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                         tsp2::LDS_BYTES_I8);
     attr2 = true;
   }
-  hipLaunchKernelGGL(torso_fwd_sp2_kernel, dim3(grid), dim3(tsp::NT), tsp2::LDS_BYTES_I8,
-                     (hipStream_t)stream, a);
+  if (queue)
+    hipLaunchKernelGGL(torso_fwd_sp2_kernel<true>, dim3(grid), dim3(tsp::NT), tsp2::LDS_BYTES_I8,
+                       (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(torso_fwd_sp2_kernel<false>, dim3(grid), dim3(tsp::NT), tsp2::LDS_BYTES_I8,
+                       (hipStream_t)stream, a);
   R2_CHECK_LAUNCH();
   return 0;
 }

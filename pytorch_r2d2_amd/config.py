@@ -173,9 +173,9 @@ class LearnerConfig:
     # the BPTT raises the side torso's stop word this many iterations before its last one (the
     # side workgroups finish the frame in hand and the one already taken: ~1.5 frames)
     hoist_stop_lead: int = 5
-    # BPTT helper workgroups that take the dueling head's gradient reduction items in the hoisted
-    # step (0 = all 192); the others leave at once so the side torso gets their CUs
-    hoist_hg_wgs: int = 0
+    # BPTT helper workgroups that take the dueling head's gradient reduction items, one item each
+    # (0 = all 192); the others leave at once (the hoisted step's side torso takes their CUs)
+    bptt_hg_wgs: int = 0
     # workgroups of the side torso launch (0 = the CUs outside the BPTT recurrence's groups)
     hoist_grid: int = 0
     # A/B probe: False = the side stream runs only the priority tail and the next sample

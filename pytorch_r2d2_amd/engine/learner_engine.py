@@ -952,12 +952,12 @@ class LearnerEngine:
         if dz_on:
             check(k.r2_lstm_bwd_set_dz(ptr(self.dz), ptr(self.dz_lo), ptr(pk["head1T"]),
                                        ptr(pkl["head1T"]), 2 * HD), "lstm_bwd_set_dz")
-        if self.hoist:
-            # the hoisted target torso beside this launch stops taking frames hoist_stop_lead
-            # iterations before the recurrence ends; hoist_hg_wgs helpers take the head gradients
-            lc = self.cfg.learner
-            check(k.r2_lstm_bwd_set_stop(ptr(self.tq[2:]), max(0, self.Ll - int(lc.hoist_stop_lead)),
-                                         int(lc.hoist_hg_wgs)), "lstm_bwd_set_stop")
+        # the hoisted target torso beside this launch stops taking frames hoist_stop_lead
+        # iterations before the recurrence ends; bptt_hg_wgs helpers take the head gradients
+        lc = self.cfg.learner
+        check(k.r2_lstm_bwd_set_stop(ptr(self.tq[2:]) if self.hoist else 0,
+                                     max(0, self.Ll - int(lc.hoist_stop_lead)), int(lc.bptt_hg_wgs)),
+              "lstm_bwd_set_stop")
         if side_hg:
             rc = k.r2_lstm_bwd_tag_sp_hg(*bptt, *hg, s)   # >= 0: bit 0 = head grads done here
         else:

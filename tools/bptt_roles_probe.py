@@ -1,7 +1,7 @@
 """Per-role clock stamps of the fp32 BPTT launch (lstm_persist.hip lstm_bwd_tag_kernel, PTBArgs::dbg)
 at the bench config, one eager engine step per arm, arms as learner.* override sets:
 
-    python tools/bptt_roles_probe.py hoist=0 hoist_torso=0 off hoist_hg_wgs=64 ...
+    python tools/bptt_roles_probe.py hoist=0 hoist_torso=0 off bptt_hg_wgs=64 ...
 
 Per arm: launch span (first workgroup start -> last workgroup end), the recurrence's end (its
 last workgroup), the helpers' end (head-gradient reduction), the median / max BPTT iteration of
