@@ -28,28 +28,35 @@ __global__ void rmsprop_centered_kernel(float* __restrict__ p, const float* __re
     f32x4 sv = ((f32x4*)sq)[i], av = ((f32x4*)ga)[i];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const float gr = gv[e] * scale;
-      sv[e] = alpha * sv[e] + (1.f - alpha) * gr * gr;
-      av[e] = alpha * av[e] + (1.f - alpha) * gr;
-      pv[e] -= lr * gr / (sqrtf(sv[e] - av[e] * av[e]) + eps);
+      float s = sv[e], m = av[e];
+      pv[e] = rms_elem(s, m, pv[e], gv[e] * scale, lr, alpha, eps);
+      sv[e] = s;
+      av[e] = m;
     }
     ((f32x4*)p)[i] = pv;
     ((f32x4*)sq)[i] = sv;
     ((f32x4*)ga)[i] = av;
   }
   for (int64_t i = (n4 << 2) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
-    const float gr = g[i] * scale;
-    sq[i] = alpha * sq[i] + (1.f - alpha) * gr * gr;
-    ga[i] = alpha * ga[i] + (1.f - alpha) * gr;
-    p[i] -= lr * gr / (sqrtf(sq[i] - ga[i] * ga[i]) + eps);
+    float sv = sq[i], av = ga[i];
+    p[i] = rms_elem(sv, av, p[i], g[i] * scale, lr, alpha, eps);
+    sq[i] = sv;
+    ga[i] = av;
   }
 }
 
 // rmsprop_centered_kernel + the row packs (rms_pack.h rmsprop_pack_items): same arithmetic
 // (bit-identical master), one HBM pass fewer over the big LSTM / head weights than
 // update-then-gather.
-__global__ void rmsprop_pack_kernel(const RmsPackArgs a) {
-  rmsprop_pack_items(a, blockIdx.x * (int64_t)blockDim.x + threadIdx.x, (int64_t)gridDim.x * blockDim.x);
+// With a torso section (r2_rmsprop_pack_slab) the first tblocks workgroups reduce + update the
+// torso elements and the rest run the quad loop up to quad tq.
+__global__ __launch_bounds__(256) void rmsprop_pack_kernel(const RmsPackArgs a) {
+  const int b = (int)blockIdx.x - a.tblocks;
+  if (b < 0) {
+    rmsprop_torso_items(a, blockIdx.x);
+    return;
+  }
+  rmsprop_pack_items(a, b * (int64_t)blockDim.x + threadIdx.x, (int64_t)(gridDim.x - a.tblocks) * blockDim.x);
 }
 
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
@@ -150,6 +157,30 @@ extern "C" int r2_rmsprop_pack(float* p, const float* g, float* sq, float* ga, i
   a.xA = nullptr;
   if (!rms_pack_args_ok(a)) return -1;
   hipLaunchKernelGGL(rmsprop_pack_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, a);
+  R2_CHECK_LAUNCH();
+  return 0;
+}
+
+// r2_rmsprop_pack with the torso slab reduction folded in (world 1, no clipping): the torso
+// backward's slabs (grid x SL floats, torso_bwd.hip) are summed by the first ceil(SL / 64)
+// workgroups, which update master element dst[e] with gradient scale[e] * sum (and write it to g
+// like torso_grad_reduce); the quad loop stops at quad tq (the caller guarantees every master
+// element from 4 * tq on is a torso element or zero padding, with no row pack there).
+extern "C" int r2_rmsprop_pack_slab(float* p, float* g, float* sq, float* ga, int64_t n, float lr,
+                                    float alpha, float eps, float gscale, const int* dst4, bf16* bf,
+                                    bf16* bf_t, int64_t lo_off, float* target, const int64_t* step,
+                                    int64_t interval, const float* slab, int grid, int SL,
+                                    const int* dst, const float* scale, int64_t tq, void* stream) {
+  RmsPackArgs a{p, g, sq, ga, n, lr, alpha, eps, gscale, nullptr, 0.f, dst4, bf, bf_t,
+                lo_off, target, step, interval};
+  a.xA = nullptr;
+  a.slab = slab; a.tdst = dst; a.tscale = scale; a.gw = g;
+  a.tG = grid; a.tSL = SL; a.tblocks = (SL + 63) / 64; a.tq = tq;
+  if (!rms_pack_args_ok(a) || !slab || !dst || !scale || grid <= 0 || SL <= 0 || tq < 0 ||
+      4 * tq > n)
+    return -1;
+  hipLaunchKernelGGL(rmsprop_pack_kernel, dim3(a.tblocks + grid_for(4 * tq, 4)), dim3(256), 0,
+                     (hipStream_t)stream, a);
   R2_CHECK_LAUNCH();
   return 0;
 }

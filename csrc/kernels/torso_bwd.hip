@@ -28,6 +28,7 @@
 // into the flat gradient buffer (deterministic; torch layout via an index map,
 // engine/layout.py torso_grad_map).
 #include "../common.h"
+#include "../slab_reduce.h"
 
 // Geometry of the fused backward (template parameter): CIN uint8 planes of H x W (multiples of
 // 4); instantiated for the Atari stack 4x84x84 and DMLab-30 RGB 3x72x96.
@@ -465,32 +466,16 @@ __global__ __launch_bounds__(512) void torso_dw3_kernel(const TBArgs a) {
   if (wave == 7 && lane < 32) sl[Gb::OFF_B + 64 + lane] = db3p;
 }
 
-// grad[dst[e]] = scale[e] * sum_g slab[g][e].  Block = 64 columns x 4 row-groups (coalesced 256-B
-// row segments, 16 independent loads in flight per thread), partials combined through LDS;
-// ~530 blocks fill the chip.
+// grad[dst[e]] = scale[e] * sum_g slab[g][e] (slab_reduce.h: 64 columns x 4 row-groups a block;
+// ~1200 blocks fill the chip).  At world 1 the learner folds this into the optimizer launch
+// instead (rms_pack.h torso section).
 __global__ __launch_bounds__(256) void torso_grad_reduce_kernel(
     const float* __restrict__ slab, int G, int SL, const int* __restrict__ dst,
     const float* __restrict__ scale, float* __restrict__ grad) {
   __shared__ float part[4][64];
-  const int c = threadIdx.x & 63, gq = threadIdx.x >> 6;
-  const int e = blockIdx.x * 64 + c;
-  float s = 0.f;
-  if (e < SL) {
-    const float* p = slab + e;
-    int g = gq;
-    for (; g + 60 < G; g += 64) {
-      float v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = p[(size_t)(g + 4 * u) * SL];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) s += v[u];
-    }
-    for (; g < G; g += 4) s += p[(size_t)g * SL];
-  }
-  part[gq][c] = s;
-  __syncthreads();
-  if (gq == 0 && e < SL)
-    grad[dst[e]] = (part[0][c] + part[1][c] + part[2][c] + part[3][c]) * scale[e];
+  const float s = slab_column_sum(slab, G, SL, blockIdx.x, part);
+  const int e = blockIdx.x * 64 + threadIdx.x;
+  if (threadIdx.x < 64 && e < SL) grad[dst[e]] = s * scale[e];
 }
 
 static long long* g_tb_dbg = nullptr;

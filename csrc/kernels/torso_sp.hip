@@ -1369,6 +1369,7 @@ extern "C" int r2_torso_bwd_sp_trace(long long* p) { g_tbs_trace = p; return 0; 
 
 // Split-precision torso backward: every activation / gradient operand as hi / lo planes (out3:
 // the torso output's hi plane, a ReLU mask only).  slab: grid x r2_torso_bwd_slab_floats().
+// grad == nullptr: the slabs are left for the optimizer launch (optim.hip r2_rmsprop_pack_slab).
 extern "C" int r2_torso_bwd_sp(const uint8_t* frames, const int* rows, int n, const bf16* act1,
                                const bf16* act1l, const bf16* act2, const bf16* act2l,
                                const bf16* dx3, const bf16* dx3l, const bf16* out3,
@@ -1390,5 +1391,6 @@ extern "C" int r2_torso_bwd_sp(const uint8_t* frames, const int* rows, int n, co
   hipLaunchKernelGGL(torso_bwd_sp_kernel, dim3(grid), dim3(tbs::NT), tbs::LDS, s, a);
   hipLaunchKernelGGL(torso_dw3_sp_kernel, dim3(grid), dim3(1024), 0, s, a);
   R2_CHECK_LAUNCH();
+  if (!grad) return 0;
   return r2_torso_grad_reduce(slab, grid, dst, scale, grad, stream);
 }

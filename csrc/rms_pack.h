@@ -9,6 +9,7 @@
 // target master and target packs are written too.
 #pragma once
 #include "common.h"
+#include "slab_reduce.h"
 
 struct RmsPackArgs {
   float* p;
@@ -41,7 +42,26 @@ struct RmsPackArgs {
   float* f32_t;
   float* lstm_b;
   float* lstm_b_t;
+  // optional torso section (r2_rmsprop_pack_slab, world 1): the first tblocks workgroups sum the
+  // torso backward's slabs (slab_reduce.h, tG slabs of tSL floats) and update master elements
+  // tdst[e] with gradient tscale[e] * sum (written to gw too) -- the torso_grad_reduce launch
+  // folded in; the quad loop then ends at quad tq (every master element from 4 * tq on is a
+  // torso element or zero padding: the torso bucket is the master's tail, layout.py)
+  const float* slab;
+  const int* tdst;
+  const float* tscale;
+  float* gw;
+  int tG, tSL, tblocks, pad_;
+  int64_t tq;
 };
+
+// one element of the centered update (every path below: the same expression, the same bits)
+__device__ __forceinline__ float rms_elem(float& sq, float& ga, float p, float gr, float lr,
+                                          float alpha, float eps) {
+  sq = alpha * sq + (1.f - alpha) * gr * gr;
+  ga = alpha * ga + (1.f - alpha) * gr;
+  return p - lr * gr / (sqrtf(sq - ga * ga) + eps);
+}
 
 __device__ __forceinline__ void rmsprop_pack_items(const RmsPackArgs& a, int64_t first, int64_t stride) {
   float scale = a.gscale;
@@ -65,10 +85,10 @@ __device__ __forceinline__ void rmsprop_pack_items(const RmsPackArgs& a, int64_t
     const int d = a.dst4[q];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const float gr = gv[e] * scale;
-      sv[e] = alpha * sv[e] + (1.f - alpha) * gr * gr;
-      av[e] = alpha * av[e] + (1.f - alpha) * gr;
-      pv[e] -= lr * gr / (sqrtf(sv[e] - av[e] * av[e]) + eps);
+      float s = sv[e], m = av[e];
+      pv[e] = rms_elem(s, m, pv[e], gv[e] * scale, lr, alpha, eps);
+      sv[e] = s;
+      av[e] = m;
     }
     ((f32x4*)p)[q] = pv;
     ((f32x4*)sq)[q] = sv;
@@ -120,7 +140,8 @@ __device__ __forceinline__ void rmsprop_pack_items(const RmsPackArgs& a, int64_t
     }
     return pv;
   };
-  for (int64_t i = first; i < n4; i += stride) {
+  const int64_t qend = a.tblocks ? a.tq : n4;
+  for (int64_t i = first; i < qend; i += stride) {
     if (full && i >= a.bq0 + gq && i < a.bq0 + 2 * gq) continue;   // bias_hh: with its partner
     const f32x4 pv = quad(i);
     if (full && i >= a.bq0 && i < a.bq0 + gq) {
@@ -135,13 +156,31 @@ __device__ __forceinline__ void rmsprop_pack_items(const RmsPackArgs& a, int64_t
       }
     }
   }
-  for (int64_t i = (n4 << 2) + first; i < n; i += stride) {
-    const float gr = g[i] * scale;
-    sq[i] = alpha * sq[i] + (1.f - alpha) * gr * gr;
-    ga[i] = alpha * ga[i] + (1.f - alpha) * gr;
-    p[i] -= lr * gr / (sqrtf(sq[i] - ga[i] * ga[i]) + eps);
+  for (int64_t i = (n4 << 2) + first; i < n && !a.tblocks; i += stride) {
+    float sv = sq[i], av = ga[i];
+    p[i] = rms_elem(sv, av, p[i], g[i] * scale, lr, alpha, eps);
+    sq[i] = sv;
+    ga[i] = av;
     if (due) a.target[i] = p[i];
   }
+}
+
+// torso section block blk: column sums of 64 slab columns, then the element update at tdst[e]
+// (the same per-element arithmetic as the quad path; gscale 1 at world 1, no clipping)
+__device__ __forceinline__ void rmsprop_torso_items(const RmsPackArgs& a, int blk) {
+  __shared__ float part[4][64];
+  const float s = slab_column_sum(a.slab, a.tG, a.tSL, blk, part);
+  const int e = blk * 64 + (int)threadIdx.x;
+  if (threadIdx.x >= 64 || e >= a.tSL) return;
+  const int m = a.tdst[e];
+  const float gv = s * a.tscale[e];
+  a.gw[m] = gv;
+  float sv = a.sq[m], av = a.ga[m];
+  const float pv = rms_elem(sv, av, a.p[m], gv * a.gscale, a.lr, a.alpha, a.eps);
+  a.sq[m] = sv;
+  a.ga[m] = av;
+  a.p[m] = pv;
+  if (a.interval <= 1 || ((*a.step) + 1) % a.interval == 0) a.target[m] = pv;
 }
 
 // host-side argument checks: 16-B master / grad / state / target, 8-B packs

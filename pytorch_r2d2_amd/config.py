@@ -115,6 +115,9 @@ class LearnerConfig:
     # rmsprop writes the LSTM / head row packs itself (optim.hip rmsprop_pack_kernel) instead of
     # a gather over the updated master in the pack launch
     fuse_opt_pack: bool = True
+    # world 1: the torso backward's slab reduction folded into that optimizer launch (its first
+    # workgroups; optim.hip r2_rmsprop_pack_slab) instead of its own torso_grad_reduce launch
+    fold_torso_reduce: bool = True
     td_fuse_head_bwd: bool = True     # dueling-head backward inside the TD launch (td_duel_kernel)
     # ... and the heads' dueling FORWARD too (fixed / reference target modes: the TD launch forms
     # relu(z + b1) and the Q rows of all three heads itself; no separate dueling_fwd launch)

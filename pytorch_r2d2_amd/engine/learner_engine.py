@@ -199,6 +199,15 @@ class LearnerEngine:
                 self._rms_all = dict(xq0=xq0, bq0=bq0, xA=torch.from_numpy(xA).to(d),
                                      xB=torch.from_numpy(xB).to(d), xF=torch.from_numpy(xF).to(d),
                                      binv=torch.from_numpy(binv).to(d))
+        # world 1 (no gradient all-reduce, no clipping): the torso backward's slab reduction rides
+        # on the optimizer launch (r2_rmsprop_pack_slab: one launch fewer); the torso bucket is the
+        # master's tail, so the update's quad loop stops at its first quad
+        self._fold_tq = None
+        if (self.sp and not self.sp_lib and not self.dp and self.world == 1 and lc.fold_torso_reduce
+                and lc.optimizer != "adam" and lc.grad_clip <= 0 and self.row_dst4 is not None
+                and self._rms_all is None and self.fwd_geom is not None and L.torso_offset % 4 == 0
+                and bool((L.row_dst4[L.torso_offset // 4:] < 0).all())):
+            self._fold_tq = L.torso_offset // 4
         self._pack(always=True)
         if d.type == "cuda":
             torch.cuda.synchronize(d)
@@ -1190,7 +1199,8 @@ class LearnerEngine:
                 ptr(self.act1_lo), ptr(self.act2), ptr(self.act2_lo), ptr(self.dX), ptr(self.dX_lo),
                 ptr(self.X_on[Lb * B: T * B]), ptr(pk["conv3_dg"]), ptr(pkl["conv3_dg"]),
                 ptr(pk["conv2_dg"]), ptr(pkl["conv2_dg"]), ptr(self._tb_slab), self._tb_grid,
-                ptr(self._tb_dst), ptr(self._tb_scale), ptr(self.grad), stream_handle()), "torso_bwd_sp")
+                ptr(self._tb_dst), ptr(self._tb_scale),
+                0 if self._fold_tq is not None else ptr(self.grad), stream_handle()), "torso_bwd_sp")
             return
         if self.cfg.learner.torso_bwd == "fused" and self.fwd_geom is not None:
             self._backward_torso_fused()
@@ -1289,6 +1299,18 @@ class LearnerEngine:
                                         ptr(r["xA"]), ptr(r["xB"]), ptr(r["xF"]), r["bq0"], L.G,
                                         ptr(r["binv"]), ptr(self.f32), ptr(self.f32_t),
                                         ptr(self.lstm_b), ptr(self.lstm_b_t), s), "rmsprop_pack_all")
+            return
+        elif self._fold_tq is not None:
+            # + the torso slab reduction (its first workgroups; _backward_torso left the slabs)
+            check(k.r2_rmsprop_pack_slab(ptr(self.master), ptr(self.grad), ptr(self.opt_a),
+                                         ptr(self.opt_b), n, float(lc.lr), float(lc.rms_alpha),
+                                         float(lc.eps), gscale, ptr(self.row_dst4), ptr(self.bf),
+                                         ptr(self.bf_t), L.bf_numel if self.sp else 0,
+                                         ptr(self.target), ptr(self.replay.step),
+                                         self._baked_interval(), ptr(self._tb_slab), self._tb_grid,
+                                         int(kernels().r2_torso_bwd_slab_floats()), ptr(self._tb_dst),
+                                         ptr(self._tb_scale), self._fold_tq, s), "rmsprop_pack_slab")
+            self._pack_step(self._baked_interval(), s, rows_done=True)
             return
         elif self.row_dst4 is not None:
             # the update writes the row packs (w_ih / w_hh / head1) and, when due, the target

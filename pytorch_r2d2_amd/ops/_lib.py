@@ -78,6 +78,7 @@ _SIGS = {
     "r2_step_end": [P, P, P],
     "r2_rmsprop_centered": [P, P, P, P, I64, F, F, F, F, P, F, P],
     "r2_rmsprop_pack": [P, P, P, P, I64, F, F, F, F, P, F, P, P, P, I64, P, P, I64, P],
+    "r2_rmsprop_pack_slab": [P, P, P, P, I64, F, F, F, F, P, P, P, I64, P, P, I64, P, I, I, P, P, I64, P],
     "r2_rmsprop_pack_all": [P, P, P, P, I64, F, F, F, F, P, F, P, P, P, I64, P, P, I64, I64, P, P, P,
                             I64, I64, P, P, P, P, P, P],
     "r2_adam": [P, P, P, P, I64, F, F, F, F, F, P, P, F, P],

@@ -208,3 +208,13 @@ def test_kernel_library_loads_with_every_symbol_resolved():
     from pytorch_r2d2_amd.ops._lib import kernels
     k = kernels()
     assert int(k.r2_ingest_args_bytes()) > 0
+
+def test_torso_fold_precondition():
+    """The folded torso reduction (r2_rmsprop_pack_slab) needs the torso bucket at the master's
+    tail with no row pack there, and the slab map to cover exactly its elements."""
+    cfg = get_config("atari57")
+    L = ParamLayout(cfg.model, cfg.env)
+    tq = L.torso_offset // 4
+    assert L.torso_offset % 4 == 0 and bool((L.row_dst4[tq:] < 0).all())
+    dst, _ = L.torso_grad_map()
+    assert torch.equal(torch.sort(dst.long()).values, torch.arange(L.torso_offset, L.numel))
