@@ -83,12 +83,6 @@ __device__ __forceinline__ bf16x8 g5_frag(const uint8_t* tile, int i0, int ks, i
   return gm_tr8((const bf16*)b0, (const bf16*)(b0 + 4 * 256));
 }
 
-template <int N>
-__device__ __forceinline__ void g5_vmwait() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");
-}
-
 struct G5Args {
   GemmProb p[gm::MAXP];
   int split[gm::MAXP];
@@ -97,7 +91,6 @@ struct G5Args {
   int ticket_base[gm::MAXP];
   int tiles_m[gm::MAXP];
   int np, total;
-  int dbg;   // probe (r2_gemm5_set_mode bits 4-5): 1 = operand staging only, 2 = no staging
   int order; // item order of K-split problems (g5_coords)
   float* ws;
   unsigned* tickets;
@@ -124,118 +117,6 @@ __device__ __forceinline__ void g5_coords(const G5Args& a, int pi, int S, int it
     ksp = item % S;
     tm = tile / P.tiles_n;
     tn = tile % P.tiles_n;
-  }
-}
-
-// K loop of one item: acc += A[m0.., k] B[k, n0..] over K tiles [kt0, kt1), NS-stage LDS ring,
-// every operand split (A_hi, A_lo, B_hi, B_lo staged; 3 MFMAs per fragment pair)
-template <bool AK, bool BKM, int BM, int BN, int BK, int NS, bool IL>
-__device__ __forceinline__ void g5_mainloop(const GemmProb& P, int m0, int n0, int kt0, int kt1,
-                                            uint8_t* lds, int wave, int lane,
-                                            f32x4 (&acc)[BM / 32][BN / 64], int dbg = 0) {
-  constexpr int FM = BM / 32, FN = BN / 64;
-  constexpr int OPA = BM * BK * 2, OPB = BN * BK * 2, STB = 2 * (OPA + OPB);
-  constexpr int NDMA = 2 * (BM + BN) * BK * 2 / (512 * 16);   // DMA instructions per thread per tile
-  static_assert(NS == 2 || ((BM * BK * 2 / 1024) % 8 == 0 && (BN * BK * 2 / 1024) % 8 == 0),
-                "uneven staging needs the 2-stage ring (vmcnt(0) waits)");
-  const int wr = wave >> 2, wc = wave & 3;
-  auto stage = [&](int kt) {
-    if (dbg & 2) return;
-    int oz;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(oz));
-    uint8_t* st = lds + ((kt - kt0) % NS) * STB;
-    const int k0 = kt * BK;
-    g5_stage<AK, BM, BK>(P.A, P.lda, m0, P.M, k0, P.K, st, wave, lane, oz);
-    g5_stage<AK, BM, BK>(P.A_lo, P.lda, m0, P.M, k0, P.K, st + OPA, wave, lane, oz);
-    g5_stage<BKM, BN, BK>(P.B, P.ldb, n0, P.N, k0, P.K, st + 2 * OPA, wave, lane, oz);
-    g5_stage<BKM, BN, BK>(P.B_lo, P.ldb, n0, P.N, k0, P.K, st + 2 * OPA + OPB, wave, lane, oz);
-  };
-#pragma unroll
-  for (int s = 0; s < NS - 1; ++s)
-    if (kt0 + s < kt1) stage(kt0 + s);
-  for (int kt = kt0; kt < kt1; ++kt) {
-    // tile kt has landed once only the DMAs of tiles kt+1 .. kt+NS-2 (those issued) remain
-    const int ahead = kt1 - 1 - kt;
-    if (NS >= 4 && ahead >= 2) g5_vmwait<(NS >= 4 ? 2 : 0) * NDMA>();
-    else if (NS >= 3 && ahead >= 1) g5_vmwait<(NS >= 3 ? 1 : 0) * NDMA>();
-    else g5_vmwait<0>();
-    __builtin_amdgcn_s_barrier();     // tile kt visible; everyone finished reading tile kt-1
-    if (kt + NS - 1 < kt1) stage(kt + NS - 1);
-    if (dbg & 1) continue;
-    const uint8_t* ah = lds + ((kt - kt0) % NS) * STB;
-    const uint8_t* al = ah + OPA;
-    const uint8_t* bh = ah + 2 * OPA;
-    const uint8_t* bl = bh + OPB;
-    if constexpr (IL) {
-      // fragments of k-step ks+1 are read from LDS while the MFMAs of k-step ks issue, one
-      // ds_read per MFMA pair (sched_group_barrier), so neither pipe waits for the other
-      constexpr int KS = BK / 32, NF = 2 * (FM + FN);
-      bf16x8 fr[2][NF];   // [buffer][B hi (FN), B lo (FN), A hi (FM), A lo (FM)]
-      auto load = [&](int ks, bf16x8 (&f)[NF]) {
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          f[j] = g5_frag<BKM, BK>(bh, wc * (BN / 4) + 16 * j, ks, lane);
-          f[FN + j] = g5_frag<BKM, BK>(bl, wc * (BN / 4) + 16 * j, ks, lane);
-        }
-#pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          f[2 * FN + i] = g5_frag<AK, BK>(ah, wr * (BM / 2) + 16 * i, ks, lane);
-          f[2 * FN + FM + i] = g5_frag<AK, BK>(al, wr * (BM / 2) + 16 * i, ks, lane);
-        }
-      };
-      load(0, fr[0]);
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        bf16x8 (&f)[NF] = fr[ks & 1];
-        if (ks + 1 < KS) load(ks + 1, fr[(ks + 1) & 1]);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j) {
-            acc[i][j] = g5_mfma(f[2 * FN + FM + i], f[j], acc[i][j]);
-            acc[i][j] = g5_mfma(f[2 * FN + i], f[FN + j], acc[i][j]);
-            acc[i][j] = g5_mfma(f[2 * FN + i], f[j], acc[i][j]);
-          }
-        __builtin_amdgcn_s_setprio(0);
-        if (ks + 1 < KS) {
-          // interleave: NF fragment reads (ds_read_b128 or 2 x ds_read_b64_tr) over 3 FM FN MFMAs
-#pragma unroll
-          for (int q = 0; q < NF; ++q) {
-            __builtin_amdgcn_sched_group_barrier(0x100, BKM && AK ? 1 : 2, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, (3 * FM * FN) / NF, 0);
-          }
-          __builtin_amdgcn_sched_group_barrier(0x008, 3 * FM * FN - NF * ((3 * FM * FN) / NF), 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    } else {
-#pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      bf16x8 fbh[FN], fbl[FN], fah[FM], fal[FM];
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        fbh[j] = g5_frag<BKM, BK>(bh, wc * (BN / 4) + 16 * j, ks, lane);
-        fbl[j] = g5_frag<BKM, BK>(bl, wc * (BN / 4) + 16 * j, ks, lane);
-      }
-#pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        fah[i] = g5_frag<AK, BK>(ah, wr * (BM / 2) + 16 * i, ks, lane);
-        fal[i] = g5_frag<AK, BK>(al, wr * (BM / 2) + 16 * i, ks, lane);
-      }
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < FM; ++i)
-#pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          acc[i][j] = g5_mfma(fal[i], fbh[j], acc[i][j]);
-          acc[i][j] = g5_mfma(fah[i], fbl[j], acc[i][j]);
-          acc[i][j] = g5_mfma(fah[i], fbh[j], acc[i][j]);
-        }
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    }
   }
 }
 
@@ -285,7 +166,7 @@ __device__ __forceinline__ void g5_emit(const GemmProb& P, int row, int col, f32
   }
 }
 
-// Epilogue of an 8-wave (2 x 4) tile, shared by gemm5 and gemm6: the BM x BN accumulators pass
+// Epilogue of gemm6's 8-wave (2 x 4) tile: the BM x BN accumulators pass
 // through LDS 64 rows at a time (row-contiguous, 4 columns per thread); with a K split, the
 // partial tile goes write-through to the workspace and the tile's last arriver sums the splits
 // in split order (bit-reproducible) and runs the epilogue.
@@ -372,50 +253,12 @@ __device__ __forceinline__ void g5_epilogue(const G5Args& a, const GemmProb& P, 
   }
 }
 
-template <bool BKM, int BM, int BN, int BK, int NS, bool IL>
-__global__ __launch_bounds__(512) void gemm5_kernel(const G5Args a) {
-  constexpr int FM = BM / 32, FN = BN / 64;
-  extern __shared__ __attribute__((aligned(1024))) uint8_t lds5[];
-  int bid;
-  {
-    const int b = blockIdx.x, x = b & 7, qn = a.total >> 3, r = a.total & 7;
-    bid = (x < r ? x * (qn + 1) : r * (qn + 1) + (x - r) * qn) + (b >> 3);
-  }
-  int pi = 0;
-#pragma unroll
-  for (int i = 1; i < gm::MAXP; ++i)
-    if (i < a.np && bid >= a.item_base[i]) pi = i;
-  const GemmProb& P = a.p[pi];
-  const int S = a.split[pi];
-  const int item = bid - a.item_base[pi];
-  int tm, tn, ksp;
-  g5_coords(a, pi, S, item, tm, tn, ksp);
-  const int tile = tm * P.tiles_n + tn;
-  const int m0 = tm * BM, n0 = tn * BN;
-  const int nk = (P.K + BK - 1) / BK, per = (nk + S - 1) / S;
-  const int kt0 = min(nk, ksp * per), kt1 = min(nk, kt0 + per);
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int wr = wave >> 2, wc = wave & 3;
-  f32x4 acc[FM][FN];
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (BM % 128 == 0) {
-    if (P.a_kmajor) g5_mainloop<true, BKM, BM, BN, BK, NS, IL>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc, a.dbg);
-    else g5_mainloop<false, BKM, BM, BN, BK, NS, IL>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc, a.dbg);
-  } else {
-    g5_mainloop<true, BKM, BM, BN, BK, NS, IL>(P, m0, n0, kt0, kt1, lds5, wave, lane, acc, a.dbg);
-  }
-
-  g5_epilogue<BM, BN>(a, P, pi, tile, ksp, S, m0, n0, acc, lds5, tid, wave, lane);
-}
-
 // ============================================================================================
 // gemm6: the split GEMM mainloop with the fragment registers refilled between the three product
-// passes.  gemm5 reads all of a K step's fragments (A / B hi and lo) and then issues its MFMAs;
-// with two waves per SIMD released together by the per-tile barrier, both read LDS at the same
-// moment and the MFMA pipe idles through the read burst (PMC: ~42 % busy, waves waiting 35 %).
+// passes.  (Its predecessor gemm5 read all of a K step's fragments and then issued its MFMAs; with
+// two waves per SIMD released together by the per-tile barrier both read LDS at the same moment
+// and the MFMA pipe idled through the read burst -- PMC ~42 % busy, profiles/r03_pmc_gemm6.txt,
+// r03_gemm6_ab.txt; gemm5 was deleted in round 6.)
 // Here every K step runs its products as three passes over all FM x FN accumulators in the order
 // A hi.B lo, A hi.B hi, A lo.B hi -- the only order whose last pass frees the operands the next
 // step's first pass does not need -- and each plane's registers take the next step's fragments
@@ -423,7 +266,7 @@ __global__ __launch_bounds__(512) void gemm5_kernel(const G5Args a) {
 // the next step's pass 1), so fragment reads always overlap MFMAs without a second register set.
 // The one barrier per LDS tile follows pass 1 of its last K step (the tile's last LDS reads): the
 // next tile has landed, and the DMA of the tile after it refills this buffer with a whole tile
-// of MFMAs to land.  Same 8-wave 2 x 4 layout, staging and epilogue (split-K included) as gemm5.
+// of MFMAs to land.  8 waves in a 2 x 4 layout; split-K partials through g5_epilogue.
 __device__ __forceinline__ void g6_dma(const bf16* src, uint8_t* dst) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
@@ -442,7 +285,7 @@ __device__ __forceinline__ void g6_mix() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <bool AK, bool BKM, int BM, int BN, int BK>
+template <bool AK, bool BKM, int BM, int BN, int BK, bool FOK>
 __device__ __forceinline__ void g6_mainloop(const GemmProb& P, int m0, int n0, int kt0, int kt1,
                                             uint8_t* lds6, int wave, int lane,
                                             f32x4 (&acc)[BM / 32][BN / 64]) {
@@ -450,9 +293,10 @@ __device__ __forceinline__ void g6_mainloop(const GemmProb& P, int m0, int n0, i
   constexpr int FM = BM / 32, FN = BN / 64;
   constexpr int OPA = BM * BK * 2, OPB = BN * BK * 2, STB = 2 * (OPA + OPB);
   const int wr = wave >> 2, wc = wave & 3;
-  // both operands k-major, no K tail (the x-projection): each thread's 1-KB staging blocks as
-  // element offsets fixed for the whole K loop (a tile adds k0); else gemm5's generic staging
-  constexpr bool FAST = AK && BKM && BK == 32;
+  // both operands k-major, no K tail (FOK: K % 32 == 0 in every problem of the launch; the
+  // x-projection): each thread's 1-KB staging blocks as element offsets fixed for the whole K
+  // loop (a tile adds k0); else the generic staging (g5_stage, K tail zero-filled)
+  constexpr bool FAST = FOK && AK && BKM && BK == 32;
   constexpr int NBA = BM * BK * 2 / 1024, NBB = BN * BK * 2 / 1024;
   constexpr int PA = (NBA + NW - 1) / NW, PB = (NBB + NW - 1) / NW;
   uint32_t offa[FAST ? PA : 1], offb[FAST ? PB : 1];
@@ -555,7 +399,7 @@ __device__ __forceinline__ void g6_mainloop(const GemmProb& P, int m0, int n0, i
   }
 }
 
-template <bool BKM, int BM, int BN, int BK>
+template <bool BKM, int BM, int BN, int BK, bool FOK>
 __global__ __launch_bounds__(512) void gemm6_kernel(const G5Args a) {
   constexpr int FM = BM / 32, FN = BN / 64;           // 16 x 16 fragments of the (BM/2) x (BN/4) wave tile
   extern __shared__ __attribute__((aligned(1024))) uint8_t lds6[];
@@ -584,10 +428,10 @@ __global__ __launch_bounds__(512) void gemm6_kernel(const G5Args a) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   if constexpr (BM % 128 == 0) {
-    if (P.a_kmajor) g6_mainloop<true, BKM, BM, BN, BK>(P, m0, n0, kt0, kt1, lds6, wave, lane, acc);
-    else g6_mainloop<false, BKM, BM, BN, BK>(P, m0, n0, kt0, kt1, lds6, wave, lane, acc);
+    if (P.a_kmajor) g6_mainloop<true, BKM, BM, BN, BK, FOK>(P, m0, n0, kt0, kt1, lds6, wave, lane, acc);
+    else g6_mainloop<false, BKM, BM, BN, BK, FOK>(P, m0, n0, kt0, kt1, lds6, wave, lane, acc);
   } else {
-    g6_mainloop<true, BKM, BM, BN, BK>(P, m0, n0, kt0, kt1, lds6, wave, lane, acc);
+    g6_mainloop<true, BKM, BM, BN, BK, FOK>(P, m0, n0, kt0, kt1, lds6, wave, lane, acc);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();            // every wave past its last LDS read before the epilogue
@@ -598,53 +442,36 @@ __global__ __launch_bounds__(512) void gemm6_kernel(const G5Args a) {
 // on every shape and removed: profiles/r05_gemm7_deep_ring_rejected.txt)
 
 
-static int g6_off = 0;   // r2_gemm5_set_mode bit 2: every launch on gemm5
-
-template <bool BKM, int BM, int BN, int BK>
+template <bool BKM, int BM, int BN, int BK, bool FOK>
 static void g6_kernel_launch(const G5Args& a, hipStream_t s) {
   constexpr int LDS = 2 * 2 * (BM + BN) * BK * 2;
   static_assert(LDS <= 160 * 1024 && 64 * (BN + 16) * 4 + 4 <= LDS, "LDS");
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)gemm6_kernel<BKM, BM, BN, BK>,
+    hipFuncSetAttribute((const void*)gemm6_kernel<BKM, BM, BN, BK, FOK>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm6_kernel<BKM, BM, BN, BK>), dim3(a.total), dim3(512), LDS, s, a);
+  hipLaunchKernelGGL((gemm6_kernel<BKM, BM, BN, BK, FOK>), dim3(a.total), dim3(512), LDS, s, a);
+}
+// the fast staging only where it applies (k-major A and B, BK 32, no K tail)
+template <bool BKM, int BM, int BN, int BK>
+static void g6_launch(const G5Args& a, bool k32, hipStream_t s) {
+  if (BKM && BK == 32 && k32) g6_kernel_launch<BKM, BM, BN, BK, true>(a, s);
+  else g6_kernel_launch<BKM, BM, BN, BK, false>(a, s);
 }
 
-static int g5_il = 1;   // interleaved fragment loads (r2_gemm5_set_mode)
-static int g5_dbg = 0;  // probe bits (G5Args::dbg)
-// K-split-major item order (g5_coords); r2_gemm5_set_mode bit 6 = the tile-major order instead.
-// Group of the paper config (tools/gemm_order_probe.py): 94-103 -> 92-96 us, bitwise-equal output
+// K-split-major item order (g5_coords); r2_gemm5_set_mode bit 6 = the tile-major order instead
+// (the probe's A/B: tools/gemm_order_probe.py, profiles/r05_gemm_item_order.txt -- the group of
+// the paper config 94-103 -> 92-96 us, bitwise-equal output).  Other bits are ignored (the gemm5
+// and probe modes were removed in round 6).
 static int g5_order = 1;
 extern "C" int r2_gemm5_set_mode(int m) {
-  g5_il = m & 1;
-  g6_off = (m >> 2) & 1;
-  g5_dbg = (m >> 4) & 3;
   g5_order = !((m >> 6) & 1);
   return 0;
 }
 
-template <bool BKM, int BM, int BN, int BK, int NS, bool IL>
-static void g5_kernel_launch_il(const G5Args& a, hipStream_t s) {
-  constexpr int LDS = NS * 2 * (BM + BN) * BK * 2;
-  static_assert(LDS <= 160 * 1024, "LDS");
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)gemm5_kernel<BKM, BM, BN, BK, NS, IL>,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
-    attr = true;
-  }
-  hipLaunchKernelGGL((gemm5_kernel<BKM, BM, BN, BK, NS, IL>), dim3(a.total), dim3(512), LDS, s, a);
-}
-template <bool BKM, int BM, int BN, int BK, int NS>
-static void g5_kernel_launch(const G5Args& a, hipStream_t s) {
-  if (g5_il) g5_kernel_launch_il<BKM, BM, BN, BK, NS, true>(a, s);
-  else g5_kernel_launch_il<BKM, BM, BN, BK, NS, false>(a, s);
-}
-
-// tile configurations: {BM, BN, BK, NS}
+// tile configurations: {BM, BN, BK, (unused)}
 static const int g5_cfgs[][4] = {{192, 128, 64, 2}, {128, 128, 64, 2}, {256, 128, 32, 3},
                                  {256, 256, 32, 2}, {256, 64, 64, 2}, {128, 64, 64, 2},
                                  {128, 128, 32, 4}, {192, 256, 32, 2}};
@@ -704,7 +531,7 @@ extern "C" int r2_gemm5(const int64_t* descs, const int* split, int np, int cfg,
                         long long ws_bytes, unsigned* tickets, int n_tickets, int n_cus, void* stream) {
   if (np < 1 || np > gm::MAXP) return -1;
   G5Args a;
-  a.np = np; a.ws = ws; a.tickets = tickets; a.dbg = g5_dbg;
+  a.np = np; a.ws = ws; a.tickets = tickets;
   int bkm = -1;
   bool all_k = true;
   for (int i = 0; i < np; ++i) {
@@ -768,49 +595,25 @@ extern "C" int r2_gemm5(const int64_t* descs, const int* split, int np, int cfg,
   a.order = g5_order;
   if (slabs * bm * bn * 4 > ws_bytes || tks > n_tickets) return -7;
   hipStream_t s = (hipStream_t)stream;
-  // gemm6 (refilled fragment registers) for every configuration; gemm5 under r2_gemm5_set_mode
-  // bit 2 or the probe bits.  gemm6's fast staging (k-major A and B, BK 32) has no K tail.
   bool k32 = true;
   for (int i = 0; i < np; ++i) k32 = k32 && a.p[i].K % 32 == 0;
-  if (!g6_off && !a.dbg && (k32 || !(bkm && all_k))) {
-    switch (cfg * 2 + bkm) {
-      case 0: g6_kernel_launch<false, 192, 128, 64>(a, s); break;
-      case 1: g6_kernel_launch<true, 192, 128, 64>(a, s); break;
-      case 2: g6_kernel_launch<false, 128, 128, 64>(a, s); break;
-      case 3: g6_kernel_launch<true, 128, 128, 64>(a, s); break;
-      case 4: g6_kernel_launch<false, 256, 128, 32>(a, s); break;
-      case 5: g6_kernel_launch<true, 256, 128, 32>(a, s); break;
-      case 6: g6_kernel_launch<false, 256, 256, 32>(a, s); break;
-      case 7: g6_kernel_launch<true, 256, 256, 32>(a, s); break;
-      case 9: g6_kernel_launch<true, 256, 64, 64>(a, s); break;
-      case 11: g6_kernel_launch<true, 128, 64, 64>(a, s); break;
-      case 12: g6_kernel_launch<false, 128, 128, 32>(a, s); break;
-      case 13: g6_kernel_launch<true, 128, 128, 32>(a, s); break;
-      case 14: g6_kernel_launch<false, 192, 256, 32>(a, s); break;
-      case 15: g6_kernel_launch<true, 192, 256, 32>(a, s); break;
-      default: return -8;
-    }
-    R2_CHECK_LAUNCH();
-    return cfg;
-  }
   switch (cfg * 2 + bkm) {
-    case 0: g5_kernel_launch<false, 192, 128, 64, 2>(a, s); break;
-    case 1: g5_kernel_launch<true, 192, 128, 64, 2>(a, s); break;
-    case 2: g5_kernel_launch<false, 128, 128, 64, 2>(a, s); break;
-    case 3: g5_kernel_launch<true, 128, 128, 64, 2>(a, s); break;
-    case 4: g5_kernel_launch<false, 256, 128, 32, 3>(a, s); break;
-    case 5: g5_kernel_launch<true, 256, 128, 32, 3>(a, s); break;
-    case 6: g5_kernel_launch<false, 256, 256, 32, 2>(a, s); break;
-    case 7: g5_kernel_launch<true, 256, 256, 32, 2>(a, s); break;
-    case 9: g5_kernel_launch<true, 256, 64, 64, 2>(a, s); break;
-    case 11: g5_kernel_launch<true, 128, 64, 64, 2>(a, s); break;
-    case 12: g5_kernel_launch<false, 128, 128, 32, 4>(a, s); break;
-    case 13: g5_kernel_launch<true, 128, 128, 32, 4>(a, s); break;
+    case 0: g6_launch<false, 192, 128, 64>(a, k32, s); break;
+    case 1: g6_launch<true, 192, 128, 64>(a, k32, s); break;
+    case 2: g6_launch<false, 128, 128, 64>(a, k32, s); break;
+    case 3: g6_launch<true, 128, 128, 64>(a, k32, s); break;
+    case 4: g6_launch<false, 256, 128, 32>(a, k32, s); break;
+    case 5: g6_launch<true, 256, 128, 32>(a, k32, s); break;
+    case 6: g6_launch<false, 256, 256, 32>(a, k32, s); break;
+    case 7: g6_launch<true, 256, 256, 32>(a, k32, s); break;
+    case 9: g6_launch<true, 256, 64, 64>(a, k32, s); break;
+    case 11: g6_launch<true, 128, 64, 64>(a, k32, s); break;
+    case 12: g6_launch<false, 128, 128, 32>(a, k32, s); break;
+    case 13: g6_launch<true, 128, 128, 32>(a, k32, s); break;
     // 192 x 256: one round of tiles for the x-projection's 10,560 x 1,024 on 256 CUs (224 items;
-    // 192 x 128 took 2.6 rounds).  Wave tile 96 x 64 -- 20 fragments per 72 MFMAs -- leaves no
-    // VGPRs for the interleaved (double-buffered) fragment loads, so always the plain k-loop
-    case 14: g5_kernel_launch_il<false, 192, 256, 32, 2, false>(a, s); break;
-    case 15: g5_kernel_launch_il<true, 192, 256, 32, 2, false>(a, s); break;
+    // 192 x 128 took 2.6 rounds)
+    case 14: g6_launch<false, 192, 256, 32>(a, k32, s); break;
+    case 15: g6_launch<true, 192, 256, 32>(a, k32, s); break;
     default: return -8;
   }
   R2_CHECK_LAUNCH();

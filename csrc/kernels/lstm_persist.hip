@@ -696,7 +696,8 @@ __device__ __forceinline__ int pt_swz16(int r, int col) {      // 16-float rows,
 //    the previous launch's step of the same parity, whose epoch parity differs because every
 //    launch of one launch SITE (fixed chain set, one ring, one ctr) advances the epoch by one.
 //    Requirement (the engine keeps it): a ring + ctr pair serves one launch site.
-//  * !T4 (r2_lstm_sp_handoff8(1), A/B probes): {fp32 h[u], 32-bit tag} 8-byte granules.
+//  * !T4 (the bf16 kernel): {bf16 h pair, 32-bit tag} 8-byte granules.  (The split-precision
+//    8-byte form lost the round-2 A/B, profiles/archive/bench_r02_tag_words_ab.log; removed.)
 template <int H, bool SP, bool T4 = false>
 __global__ __launch_bounds__(320) void lstm_fwd_tag_kernel(const PTArgs a) {
   static_assert(!T4 || SP, "T4 is a split-precision hand-off");
@@ -1051,10 +1052,6 @@ extern "C" int r2_lstm_tag_ring_bytes(int n_chains, int B, int H) {
   return n < (1ll << 31) ? (int)n : -1;
 }
 
-// A/B probe switch: 1 = split-precision forward on the 8-byte {h, tag} granules (previous path)
-static int g_pl_sp8 = 0;
-extern "C" int r2_lstm_sp_handoff8(int v) { g_pl_sp8 = v; return 0; }
-
 // Same chain layout / ctr as r2_lstm_fwd_persist; ring: r2_lstm_tag_ring_bytes bytes.  bf16: any
 // content.  Split precision (4-bit tagged words): zero- or (-1)-filled at allocation, and one
 // ring + ctr pair per launch site (a fixed chain set), see lstm_fwd_tag_kernel.
@@ -1094,7 +1091,7 @@ static int lstm_fwd_tag_launch(const int64_t* chain_ptrs, int words, int n_chain
   hipStream_t s = (hipStream_t)stream;   // counters are left zeroed by the previous launch
   const int nblk = args.xcd_map == 1 ? 8 * nwg : args.xcd_map == 2 ? 16 * nwg : groups * nwg;
   dim3 grid(nblk), block(320);   // 4 compute waves + 1 I/O wave
-  if (SP && !g_pl_sp8) {   // 4-byte tagged-word hand-off (lstm_fwd_tag_kernel T4)
+  if constexpr (SP) {   // 4-byte tagged-word hand-off (lstm_fwd_tag_kernel T4)
 #define PT_T4(HH)                                                                              \
   hipFuncSetAttribute((const void*)lstm_fwd_tag_kernel<HH, true, true>,                       \
                       hipFuncAttributeMaxDynamicSharedMemorySize, PL_LDS_RESERVE);             \
@@ -1108,16 +1105,16 @@ static int lstm_fwd_tag_launch(const int64_t* chain_ptrs, int words, int n_chain
     R2_CHECK_LAUNCH();
     return 0;
   }
-  const void* fn = H == 64 ? (const void*)lstm_fwd_tag_kernel<64, SP>
-                 : H == 128 ? (const void*)lstm_fwd_tag_kernel<128, SP>
-                 : H == 256 ? (const void*)lstm_fwd_tag_kernel<256, SP>
-                            : (const void*)lstm_fwd_tag_kernel<(SP ? 256 : 512), SP>;
+  const void* fn = H == 64 ? (const void*)lstm_fwd_tag_kernel<64, false>
+                 : H == 128 ? (const void*)lstm_fwd_tag_kernel<128, false>
+                 : H == 256 ? (const void*)lstm_fwd_tag_kernel<256, false>
+                            : (const void*)lstm_fwd_tag_kernel<512, false>;
   hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, PL_LDS_RESERVE);
   switch (H) {
-    case 64: hipLaunchKernelGGL((lstm_fwd_tag_kernel<64, SP>), grid, block, PL_LDS_RESERVE, s, args); break;
-    case 128: hipLaunchKernelGGL((lstm_fwd_tag_kernel<128, SP>), grid, block, PL_LDS_RESERVE, s, args); break;
-    case 256: hipLaunchKernelGGL((lstm_fwd_tag_kernel<256, SP>), grid, block, PL_LDS_RESERVE, s, args); break;
-    default: hipLaunchKernelGGL((lstm_fwd_tag_kernel<(SP ? 256 : 512), SP>), grid, block, PL_LDS_RESERVE, s, args); break;
+    case 64: hipLaunchKernelGGL((lstm_fwd_tag_kernel<64, false>), grid, block, PL_LDS_RESERVE, s, args); break;
+    case 128: hipLaunchKernelGGL((lstm_fwd_tag_kernel<128, false>), grid, block, PL_LDS_RESERVE, s, args); break;
+    case 256: hipLaunchKernelGGL((lstm_fwd_tag_kernel<256, false>), grid, block, PL_LDS_RESERVE, s, args); break;
+    default: hipLaunchKernelGGL((lstm_fwd_tag_kernel<512, false>), grid, block, PL_LDS_RESERVE, s, args); break;
   }
   R2_CHECK_LAUNCH();
   return 0;
@@ -1211,7 +1208,7 @@ __device__ __forceinline__ int dzs_f(int r) { return (0x1230 >> (4 * (r >> 2))) 
 
 // SP (split precision, split.h): W_hh^T hi / lo fragments, dgates tile kept as hi / lo images for
 // the partial-dh MFMAs (3 passes) and written as hi / lo planes for the weight-gradient GEMMs.
-// T4 (default, r2_lstm_bwd_handoff8(1) = the 8-byte granules): each partial travels as ONE 4-byte
+// T4 (every launch; the 8-byte granule form was removed in round 6): each partial travels as ONE 4-byte
 // word, fp32 rounded to 19 mantissa bits | 4-bit {epoch parity, (k + 1) mod 8} tag (the forward's
 // T4 scheme, lstm_fwd_tag_kernel): half the ring bytes; a consumer wave gathers 4 units x 4 sources
 // per 16-B load and the 4 waves split the 16 sources (sums in source order, then wave order).
@@ -1245,8 +1242,12 @@ __global__ __launch_bounds__(320) void lstm_bwd_tag_kernel(const PTBArgs a) {
     const int b = blockIdx.x, g = b & 7, jj = b >> 3;
     int h;   // helper ordinal: blocks before b that are not recurrence blocks
     if (a.xcd_map == 3) {
-      const int xr = (a.MB + 1) / 2, lr = 2 * NWG;   // recurrence rows l < lr on XCDs x < xr
-      h = jj < lr ? jj * (8 - xr) + (g - xr) : lr * (8 - xr) + (jj - lr) * 8 + g;
+      // rows jj < NWG (slot 0) hold recurrence blocks on XCDs x < r0, rows NWG .. 2 NWG - 1
+      // (slot 1) on XCDs x < r1 (one fewer when MB is odd), later rows none
+      const int r0 = (a.MB + 1) / 2, r1 = a.MB / 2;
+      h = jj < NWG ? jj * (8 - r0) + (g - r0)
+        : jj < 2 * NWG ? NWG * (8 - r0) + (jj - NWG) * (8 - r1) + (g - r1)
+                       : NWG * (16 - r0 - r1) + (jj - 2 * NWG) * 8 + g;
     } else {
       h = b - (min(jj, NWG) * a.MB + (jj < NWG ? min(g, a.MB) : 0));
     }
@@ -1703,10 +1704,6 @@ extern "C" int r2_lstm_bwd_set_stop(unsigned* stop, int stop_at, int hg_wgs) {
 static int g_bwd_pairs = 0;
 extern "C" int r2_lstm_bwd_xcd_pairs(int v) { g_bwd_pairs = v; return 0; }
 
-// A/B probe switch: 1 = the BPTT on 8-byte {partial, tag} granules (the previous hand-off)
-static int g_pl_bwd8 = 0;
-extern "C" int r2_lstm_bwd_handoff8(int v) { g_pl_bwd8 = v; return 0; }
-
 extern "C" int r2_lstm_bwd_tag_ring_bytes(int B, int H) {
   const long long n = 2ll * (H / PL_UNITS) * ((B + PT_ROWS - 1) / PT_ROWS) * PT_ROWS * H * 8;
   return n < (1ll << 31) ? (int)n : -1;
@@ -1780,7 +1777,7 @@ static int lstm_bwd_tag_launch(const float* dh_ext, const float* gates, const fl
   args.whhT_lo = whhT_lo;
   args.dgates_lo = dgates_lo;
   args.dz = dz[0]; args.dz_lo = dz[1]; args.w1t = dz[2]; args.w1t_lo = dz[3];
-  if (args.dz && (!sp || H != 256 || g_pl_bwd8)) return -13;   // split-precision T4 BPTT, H 256 only
+  if (args.dz && (!sp || H != 256)) return -13;   // split-precision T4 BPTT, H 256 only
   // one workgroup per CU (the PL_LDS_RESERVE rule, comment at its definition): the dz path's
   // dynamic LDS (iteration 0's dz rows + the dh partials, 36 KB) plus the kernel's 54 KB of static
   // LDS (LDS_Block_Size in the rocprofv3 trace) is 90 KB > 80 KB, so two workgroups never share a
@@ -1795,11 +1792,7 @@ static int lstm_bwd_tag_launch(const float* dh_ext, const float* gates, const fl
                         hipFuncAttributeMaxDynamicSharedMemorySize, dyn_lds);                  \
     hipLaunchKernelGGL((lstm_bwd_tag_kernel<HH, SPP, T4>), grid, block, dyn_lds, s, args);     \
   } while (0)
-#define R2_BWD_LAUNCH(HH, SPP)                                                                 \
-  do {                                                                                         \
-    if (g_pl_bwd8) R2_BWD_LAUNCH1(HH, SPP, false);                                             \
-    else R2_BWD_LAUNCH1(HH, SPP, true);                                                        \
-  } while (0)
+#define R2_BWD_LAUNCH(HH, SPP) R2_BWD_LAUNCH1(HH, SPP, true)
   if (sp) {
     switch (H) {
       case 64: R2_BWD_LAUNCH(64, true); break;

@@ -154,7 +154,6 @@ extern "C" int r2_rmsprop_pack(float* p, const float* g, float* sq, float* ga, i
                                float* target, const int64_t* step, int64_t interval, void* stream) {
   RmsPackArgs a{p, g, sq, ga, n, lr, alpha, eps, gscale, clip_sumsq, max_norm, dst4, bf, bf_t,
                 lo_off, target, step, interval};
-  a.xA = nullptr;
   if (!rms_pack_args_ok(a)) return -1;
   hipLaunchKernelGGL(rmsprop_pack_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, a);
   R2_CHECK_LAUNCH();
@@ -173,7 +172,6 @@ extern "C" int r2_rmsprop_pack_slab(float* p, float* g, float* sq, float* ga, in
                                     const int* dst, const float* scale, int64_t tq, void* stream) {
   RmsPackArgs a{p, g, sq, ga, n, lr, alpha, eps, gscale, nullptr, 0.f, dst4, bf, bf_t,
                 lo_off, target, step, interval};
-  a.xA = nullptr;
   a.slab = slab; a.tdst = dst; a.tscale = scale; a.gw = g;
   a.tG = grid; a.tSL = SL; a.tblocks = (SL + 63) / 64; a.tq = tq;
   if (!rms_pack_args_ok(a) || !slab || !dst || !scale || grid <= 0 || SL <= 0 || tq < 0 ||
@@ -181,31 +179,6 @@ extern "C" int r2_rmsprop_pack_slab(float* p, float* g, float* sq, float* ga, in
     return -1;
   hipLaunchKernelGGL(rmsprop_pack_kernel, dim3(a.tblocks + grid_for(4 * tq, 4)), dim3(256), 0,
                      (hipStream_t)stream, a);
-  R2_CHECK_LAUNCH();
-  return 0;
-}
-
-// r2_rmsprop_pack + every other kernel layout (rms_pack.h "full repack"): the per-element
-// destination tables of the quads from xq0 on (layout.py ParamLayout.rms_scatter_tables), the fp32
-// gathers and the packed LSTM bias -- the state pack_step leaves, without its launch.
-extern "C" int r2_rmsprop_pack_all(float* p, const float* g, float* sq, float* ga, int64_t n,
-                                   float lr, float alpha, float eps, float gscale,
-                                   const float* clip_sumsq, float max_norm, const int* dst4, bf16* bf,
-                                   bf16* bf_t, int64_t lo_off, float* target, const int64_t* step,
-                                   int64_t interval, int64_t xq0, const int* xA, const int* xB,
-                                   const int* xF, int64_t bq0, int64_t G, const int* binv,
-                                   float* f32, float* f32_t, float* lstm_b, float* lstm_b_t,
-                                   void* stream) {
-  RmsPackArgs a{p, g, sq, ga, n, lr, alpha, eps, gscale, clip_sumsq, max_norm, dst4, bf, bf_t,
-                lo_off, target, step, interval};
-  a.xq0 = xq0; a.bq0 = bq0; a.G = G;
-  a.xA = (const int4*)xA; a.xB = (const int4*)xB; a.xF = (const int4*)xF; a.binv = binv;
-  a.f32 = f32; a.f32_t = f32_t; a.lstm_b = lstm_b; a.lstm_b_t = lstm_b_t;
-  if (!rms_pack_args_ok(a) || !xA || !xB || !xF || !binv || !f32 || !f32_t || !lstm_b || !lstm_b_t ||
-      (G & 3) || xq0 < 0 || (((uintptr_t)xA | (uintptr_t)xB | (uintptr_t)xF) & 15) ||
-      xq0 > bq0 || bq0 + G / 2 > n / 4)
-    return -1;
-  hipLaunchKernelGGL(rmsprop_pack_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, a);
   R2_CHECK_LAUNCH();
   return 0;
 }

@@ -48,14 +48,14 @@ struct TSJob {
   // with the static stride over the job's workgroups (their number set on the device, TSArgs::dyn).
   unsigned* q;
   int n, wbegin, wcount, qmode;
-  int avoid, pad_j;                // qmode 1: bit x set = workgroups on XCD x leave at once (job word 19)
+  int pad_j[2];                    // (job word 19: reserved, 0)
 };
 struct TSArgs {
   const uint8_t* frames;
   TSJob job[TS_MAX_JOBS];
   int njobs, dbg;            // dbg: timing-probe bits (r2_torso_sp_debug), 0 in production
   int dyn;                   // dyn: workgroups dealt on the device (a qmode-2 job's size is q-dependent)
-  int save_w;                // deal weight of a frame with activation saves, per mille of a plain one
+  int pad_;
   long long* trace;          // optional per-phase clock stamps (r2_torso_sp_trace), null in production
 };
 
@@ -272,7 +272,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
     // the host's deal (r2_torso_fwd_sp_multi) with a qmode-2 job counted at its remaining frames
     // n - min(q[0], n): every workgroup computes the same table from the same words
     int ne[TS_MAX_JOBS];
-    int64_t nw_[TS_MAX_JOBS];   // frames weighted by their cost (saves: args.save_w per mille)
+    int64_t nw_[TS_MAX_JOBS];
     int64_t total = 0;
 #pragma unroll
     for (int i = 0; i < TS_MAX_JOBS; ++i) {
@@ -281,7 +281,7 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
       if (i < args.njobs && Ji.qmode == 2)
         v -= (int)min(__hip_atomic_load(Ji.q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), (unsigned)Ji.n);
       ne[i] = v;
-      nw_[i] = v > 0 ? (int64_t)v * (i < args.njobs && Ji.s1 ? args.save_w : 1000) : 0;
+      nw_[i] = v > 0 ? v : 0;
       total += nw_[i];
     }
     const int nw = gridDim.x;
@@ -327,11 +327,6 @@ __global__ __launch_bounds__(512) void torso_fwd_sp2_kernel(const TSArgs args) {
     f += (int)min(__hip_atomic_load(J.q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), (unsigned)n_frames);
   int row_f = 0, row_q1 = 0, f_q1 = 0;
   if (qjob) {
-    if (J.qmode == 1 && J.avoid) {   // keep the hoisted frames off the recurrence's XCDs
-      unsigned x;
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-      if ((J.avoid >> (x & 15)) & 1) return;
-    }
     // first two frames of this workgroup from the queue (before any setup: a workgroup that
     // finds the queue empty or stopped leaves at once)
     if (tid == 0) {
@@ -703,13 +698,6 @@ extern "C" int r2_torso_sp_trace(long long* p) { g_tsp_trace = p; return 0; }
 // timing probes only (tools/sp_micro.py): bit 0 skips conv1, bit 1 conv2, bit 2 conv3, bit 4 the
 // next-frame staging, bit 6 the act1 save
 extern "C" int r2_torso_sp_debug(int bits) { g_tsp_dbg = bits; return 0; }
-// deal weight of a frame with activation saves, per mille of a plain frame (learner.torso_save_weight)
-static int g_tsp_save_w = 1000;
-extern "C" int r2_torso_sp_save_weight(int per_mille) {
-  if (per_mille < 500 || per_mille > 4000) return -1;
-  g_tsp_save_w = per_mille;
-  return 0;
-}
 
 extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs, int njobs,
                                      int grid, void* stream) {
@@ -718,11 +706,9 @@ extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs,
   a.frames = frames;
   a.dbg = g_tsp_dbg;
   a.trace = g_tsp_trace;
-  a.save_w = g_tsp_save_w;
-  // frames weighted by cost: a frame whose activations are saved (job word 13) takes longer
-  auto wt = [&](const int64_t* p) -> int64_t {
-    return p[1] > 0 ? p[1] * (p[13] ? g_tsp_save_w : 1000) : 0;
-  };
+  // workgroups dealt in proportion to the frames (weighting the frames with activation saves
+  // 1.15x / 1.3x measured slower, round 6)
+  auto wt = [&](const int64_t* p) -> int64_t { return p[1] > 0 ? p[1] : 0; };
   int64_t total = 0;
   for (int i = 0; i < njobs; ++i) total += wt(jobs + TS_JOB_WORDS * i);
   if (total <= 0) return 0;
@@ -748,7 +734,6 @@ extern "C" int r2_torso_fwd_sp_multi(const uint8_t* frames, const int64_t* jobs,
     J.s1 = (bf16*)p[13]; J.s1l = (bf16*)p[14]; J.s2 = (bf16*)p[15]; J.s2l = (bf16*)p[16];
     J.q = (unsigned*)p[17];
     J.qmode = J.q ? (int)p[18] : 0;
-    J.avoid = J.q ? (int)p[19] : 0;
     if (!J.w1l || !J.w2l || !J.w3l || !J.out_l || (J.s1 && !J.s1l) || (J.s2 && !J.s2l)) return -4;
     // queue jobs: no activation saves (the saved frames are indexed by launch order), mode 1 / 2
     if (J.q && (J.s1 || J.s2 || (J.qmode != 1 && J.qmode != 2))) return -5;

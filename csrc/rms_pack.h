@@ -27,21 +27,6 @@ struct RmsPackArgs {
   float* target;
   const int64_t* step;
   int64_t interval;
-  // optional full repack (r2_rmsprop_pack_all: no pack_step launch after the update).  Quads
-  // q >= xq0 carry per-element destinations: xA / xB = up to two bf16 prefix-pack slots (conv
-  // layouts, W_hh^T, W1^T; -1 none), xF = the fp32 gather slot (-1 none), indexed q - xq0.  The
-  // bias_ih quads [bq0, bq0 + G/4) are updated together with their bias_hh partners (+G/4), so
-  // one thread forms the packed LSTM bias lstm_b[binv[k]] = b_ih[k] + b_hh[k] from both new values
-  // (pack_step.h's gather order and rounding).
-  int64_t xq0, bq0, G;
-  const int4* xA;
-  const int4* xB;
-  const int4* xF;
-  const int* binv;
-  float* f32;
-  float* f32_t;
-  float* lstm_b;
-  float* lstm_b_t;
   // optional torso section (r2_rmsprop_pack_slab, world 1): the first tblocks workgroups sum the
   // torso backward's slabs (slab_reduce.h, tG slabs of tSL floats) and update master elements
   // tdst[e] with gradient tscale[e] * sum (written to gw too) -- the torso_grad_reduce launch
@@ -76,10 +61,8 @@ __device__ __forceinline__ void rmsprop_pack_items(const RmsPackArgs& a, int64_t
   float* __restrict__ ga = a.ga;
   const bool due = a.interval <= 1 || ((*a.step) + 1) % a.interval == 0;
   const int64_t n = a.n, n4 = n >> 2;
-  const bool full = a.xA != nullptr;
-  const int64_t gq = a.G >> 2;
-  // quad q: update, row pack (dst4), and (full) the per-element prefix / fp32 destinations
-  auto quad = [&](int64_t q) -> f32x4 {
+  // quad q: update, row pack (dst4)
+  auto quad = [&](int64_t q) {
     f32x4 pv = ((f32x4*)p)[q], gv = ((const f32x4*)g)[q];
     f32x4 sv = ((f32x4*)sq)[q], av = ((f32x4*)ga)[q];
     const int d = a.dst4[q];
@@ -108,54 +91,9 @@ __device__ __forceinline__ void rmsprop_pack_items(const RmsPackArgs& a, int64_t
         if (a.lo_off) *(bf16x4*)(a.bf_t + a.lo_off + d) = l;
       }
     }
-    if (full && q >= a.xq0) {
-      const int4 xa = a.xA[q - a.xq0], xb = a.xB[q - a.xq0], xf = a.xF[q - a.xq0];
-      const int sa[4] = {xa.x, xa.y, xa.z, xa.w}, sb[4] = {xb.x, xb.y, xb.z, xb.w};
-      const int sf[4] = {xf.x, xf.y, xf.z, xf.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const bf16 h = (bf16)pv[e];
-        const bf16 l = (bf16)(pv[e] - (float)h);
-        if (sa[e] >= 0) {
-          a.bf[sa[e]] = h;
-          if (a.lo_off) a.bf[sa[e] + a.lo_off] = l;
-          if (due) {
-            a.bf_t[sa[e]] = h;
-            if (a.lo_off) a.bf_t[sa[e] + a.lo_off] = l;
-          }
-        }
-        if (sb[e] >= 0) {
-          a.bf[sb[e]] = h;
-          if (a.lo_off) a.bf[sb[e] + a.lo_off] = l;
-          if (due) {
-            a.bf_t[sb[e]] = h;
-            if (a.lo_off) a.bf_t[sb[e] + a.lo_off] = l;
-          }
-        }
-        if (sf[e] >= 0) {
-          a.f32[sf[e]] = pv[e];
-          if (due) a.f32_t[sf[e]] = pv[e];
-        }
-      }
-    }
-    return pv;
   };
   const int64_t qend = a.tblocks ? a.tq : n4;
-  for (int64_t i = first; i < qend; i += stride) {
-    if (full && i >= a.bq0 + gq && i < a.bq0 + 2 * gq) continue;   // bias_hh: with its partner
-    const f32x4 pv = quad(i);
-    if (full && i >= a.bq0 && i < a.bq0 + gq) {
-      const f32x4 ph = quad(i + gq);
-      const int k0 = (int)(i - a.bq0) * 4;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int j = a.binv[k0 + e];
-        const float b = pv[e] + ph[e];
-        a.lstm_b[j] = b;
-        if (due) a.lstm_b_t[j] = b;
-      }
-    }
-  }
+  for (int64_t i = first; i < qend; i += stride) quad(i);
   for (int64_t i = (n4 << 2) + first; i < n && !a.tblocks; i += stride) {
     float sv = sq[i], av = ga[i];
     p[i] = rms_elem(sv, av, p[i], g[i] * scale, lr, alpha, eps);

@@ -105,10 +105,6 @@ class LearnerConfig:
     # persistent forward hand-off: "tagged" (8-byte {h pair, tag} granules polled directly, 16-row
     # batch tiles; falls back when the grid does not fit) | "counter" (payload + arrival counter)
     lstm_handoff: str = "tagged"
-    # tagged kernels: h (forward, split precision) and the recurrent dh partials (BPTT) as 4-byte
-    # words with a 4-bit tag (lstm_persist.hip T4) -- False = the 8-byte {value, tag} granules
-    # (A/B probes; process-wide kernel switch, set by the engine at construction)
-    lstm_tag_words: bool = True
     # post-BPTT GEMMs: "group" = weight gradients + dX in one grid (58 us vs 85 separate),
     # "group:a,b,c,d" = with K splits, "separate"
     bwd_gemm: str = "group"
@@ -139,25 +135,9 @@ class LearnerConfig:
     # tile config of that group: ops/gemm.py G5_CFGS index, -1 = the launcher's CU model, -2 =
     # learner_engine._auto_group_splits' choice (paper shape: 128x128, 4-deep 32-K ring)
     sp_group_cfg: int = -2
-    # split GEMMs on gemm6 (gemm_sp.hip: the fragment planes refilled between the three product
-    # passes, one barrier per LDS tile; the heads' layer-1 GEMMs join the one-pass kernel too):
-    # x-projection 115-129 -> 102-110 us, tools/gemm6_probe.py
-    sp_gemm6: bool = True
-    # item order of K-split split GEMMs (gemm_sp.hip g5_coords): 0 = tile-major, 1 = K split
-    # slowest, tm fastest (a weight gradient's big B operand read by ~one XCD instead of several:
-    # post-BPTT group -2 us in the micro, step -4.5 us on the same box, bitwise-equal results;
-    # profiles/r05_gemm_item_order.txt)
-    sp_gemm_order: int = 1
-    # tile config of the heads' layer-1 split GEMM (ops/gemm.py G5_CFGS index; -1 = the
-    # launcher's CU model, which picks 128x128x64; same-box sweep: -1 0.943 / 0.945, 192x128x64
-    # 0.949 / 0.948, 256x128x32 0.959 / 0.958, 256x256x32 0.990 / 0.989 ms per step)
-    sp_heads_cfg: int = -1
     # split precision: the dueling head's gradient reduction on the BPTT launch's idle workgroups
     # (r2_lstm_bwd_tag_sp_hg) instead of its own 28 us launch
     sp_head_grads_in_bptt: bool = True
-    # fused split-precision torso forward: how much a frame whose activations are saved for the
-    # backward costs relative to a plain frame, for the deal of workgroups over the frame lists
-    torso_save_weight: float = 1.0
     torso_bwd: str = "fused"         # fused (HIP kernel) | library (MIOpen convolution_backward)
     # library conv path (frame geometries without the fused HIP torso, e.g. DMLab): MIOpen find
     # mode (torch.backends.cudnn.benchmark) instead of its immediate-mode heuristics
@@ -176,26 +156,12 @@ class LearnerConfig:
     # the BPTT raises the side torso's stop word this many iterations before its last one (the
     # side workgroups finish the frame in hand and the one already taken: ~1.5 frames)
     hoist_stop_lead: int = 5
-    # BPTT helper workgroups that take the dueling head's gradient reduction items, one item each
-    # (0 = all 192); the others leave at once (the hoisted step's side torso takes their CUs)
-    bptt_hg_wgs: int = 0
-    # workgroups of the side torso launch (0 = the CUs outside the BPTT recurrence's groups)
-    hoist_grid: int = 0
-    # A/B probe: False = the side stream runs only the priority tail and the next sample
-    hoist_torso: bool = True
-    # the side branch's priority tail and next-step sample in one launch (r2_prio_tail_sample)
-    hoist_fuse_sample: bool = True
-    # the optimizer writes every packed layout itself (r2_rmsprop_pack_all) instead of the
-    # pack_step launch after it: measured slower (rmsprop 14.5 -> 25.2 us against 6.4 us for the
-    # gather launch: the transposed W_hh^T / W1^T packs as 2-byte scattered stores), off
-    hoist_full_repack: bool = False
-    # XCD bit mask the hoisted torso frames stay off (their workgroups leave at once there)
-    hoist_avoid_xcds: int = 0
-    # where the side branch joins the main stream: "bwd" (before the conv backward) | "end"
-    hoist_join: str = "bwd"
-    # BPTT recurrence groups packed two per XCD (lstm_persist.hip xcd_map 3): whole XCDs free
-    # for the hoisted torso frames, whose L2 traffic then stays off the recurrence's hand-offs
-    bptt_xcd_pairs: bool = True
+    # (removed A/B knobs whose alternative lost, record in profiles/: lstm_tag_words = False, the
+    # 8-byte hand-off granules (archive/bench_r02_tag_words_ab.log); sp_gemm6 = False, gemm5
+    # (r03_gemm6_ab.txt); sp_gemm_order = 0 (r05_gemm_item_order.txt); sp_heads_cfg
+    # (r03_heads_cfg_ab.txt); torso_save_weight 1.15 / 1.3, hoist_full_repack, hoist_join "end",
+    # hoist_avoid_xcds, bptt_hg_wgs 64, bptt_xcd_pairs off (r06_tree_ab_knobs.txt,
+    # r06_hoist_knobs_rejected.txt))
     # single-rank step: the weight repack after the optimizer (pack_step) runs on extra
     # workgroups of the priority tail's launch (replay.hip r2_prio_tail_pack): one launch fewer
     fuse_pack_tail: bool = True

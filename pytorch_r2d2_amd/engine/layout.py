@@ -268,54 +268,6 @@ class ParamLayout:
             return None
         return torch.from_numpy(dst.astype(np.int32))
 
-    def rms_scatter_tables(self):
-        """Per-element destinations for the optimizer's full repack (optim.hip
-        r2_rmsprop_pack_all, rms_pack.h): every master element from lstm.weight_hh on gets up to
-        two bf16 prefix-pack slots (the packs before ``bf_rows_begin``: conv layouts, W_hh^T,
-        W1^T; the row packs stay on ``row_dst4``) and its fp32 gather slot.  Returns
-        (xq0, xA, xB, xF, bq0, binv) as numpy int32 arrays (xA / xB / xF: 4 entries per quad from
-        quad xq0 on, -1 = none) or None when an element has more than two prefix slots or a
-        destination lies before xq0."""
-        e0 = self.segs["lstm.weight_hh"].offset
-        if e0 % 4 or self.segs["lstm.bias_ih"].offset % 4:
-            return None
-        n = self.padded - e0
-        A = np.full(n, -1, dtype=np.int64)
-        Bt = np.full(n, -1, dtype=np.int64)
-        F = np.full(n, -1, dtype=np.int64)
-        bf_idx = self.bf_index.numpy().astype(np.int64)
-        for name, (o, shp) in self.bf_offsets.items():
-            if o >= self.bf_rows_begin:
-                continue
-            cnt = int(np.prod(shp))
-            src = bf_idx[o:o + cnt] - e0
-            slots = np.arange(o, o + cnt)
-            if (src < 0).any():
-                return None
-            for sv, sl in ((src, slots),):
-                first = A[sv] < 0
-                # an element may appear in two prefix packs (conv2 / conv2_dg, conv3 / conv3_dg),
-                # never twice in one
-                if np.unique(sv).size != sv.size:
-                    return None
-                A[sv[first]] = sl[first]
-                rest = ~first
-                if (Bt[sv[rest]] >= 0).any():
-                    return None
-                Bt[sv[rest]] = sl[rest]
-        f_idx = self.f_index.numpy().astype(np.int64)
-        for name, (o, shp) in self.f_offsets.items():
-            cnt = int(np.prod(shp))
-            src = f_idx[o:o + cnt] - e0
-            if (src < 0).any() or np.unique(src).size != src.size or (F[src] >= 0).any():
-                return None
-            F[src] = np.arange(o, o + cnt)
-        b0 = self.segs["lstm.bias_ih"].offset
-        if self.segs["lstm.bias_hh"].offset != b0 + self.G:
-            return None
-        binv = self.gate_inv.numpy().astype(np.int32)     # bias element k -> packed slot
-        return (e0 // 4, A.astype(np.int32), Bt.astype(np.int32), F.astype(np.int32), b0 // 4, binv)
-
     def torso_grad_map(self):
         """(dst index into the flat grad buffer, scale) for every element of the fused torso
         backward slab: [dW1 (co, ci*64) | dW2 (co, (kh,kw,ci)) | dW3 (co, (kh,kw,ci)) | db1 | db2 | db3]."""

@@ -116,12 +116,6 @@ class LearnerEngine:
                 arr = (ctypes.c_int * 8)(*xcd_cus)
                 kernels().r2_set_xcd_cus(arr)
             kernels().r2_lstm_persist_force_slow(0 if cfg.learner.lstm_xcd_pairs else 2)
-            check(kernels().r2_torso_sp_save_weight(int(round(1000 * cfg.learner.torso_save_weight))),
-                  "torso_sp_save_weight")
-            # gemm_sp.hip launcher mode: bit 0 interleaved fragment loads, bit 2 gemm5, bit 6 the
-            # tile-major item order instead of the K-split-major one
-            kernels().r2_gemm5_set_mode(1 | (0 if cfg.learner.sp_gemm6 else 4)
-                                        | (0 if cfg.learner.sp_gemm_order else 64))
         if init_module is None:
             torch.manual_seed(cfg.seed)
             init_module = QNet("cpu", m, e)
@@ -188,24 +182,14 @@ class LearnerEngine:
         if d.type == "cuda":
             # the BPTT packed two groups per XCD only beside the hoisted torso frames (alone it
             # runs faster one group per XCD: 100 vs 113 us, profiles/r06_hoist_bptt_placement.txt)
-            kernels().r2_lstm_bwd_xcd_pairs(1 if (self.hoist and cfg.learner.bptt_xcd_pairs) else 0)
-        # hoisted step: the optimizer writes EVERY packed layout itself (r2_rmsprop_pack_all; the
-        # pack_step launch is gone from the step's tail)
-        self._rms_all = None
-        if self.hoist and self.row_dst4 is not None and cfg.learner.hoist_full_repack:
-            t = L.rms_scatter_tables()
-            if t is not None:
-                xq0, xA, xB, xF, bq0, binv = t
-                self._rms_all = dict(xq0=xq0, bq0=bq0, xA=torch.from_numpy(xA).to(d),
-                                     xB=torch.from_numpy(xB).to(d), xF=torch.from_numpy(xF).to(d),
-                                     binv=torch.from_numpy(binv).to(d))
+            kernels().r2_lstm_bwd_xcd_pairs(1 if self.hoist else 0)
         # world 1 (no gradient all-reduce, no clipping): the torso backward's slab reduction rides
         # on the optimizer launch (r2_rmsprop_pack_slab: one launch fewer); the torso bucket is the
         # master's tail, so the update's quad loop stops at its first quad
         self._fold_tq = None
         if (self.sp and not self.sp_lib and not self.dp and self.world == 1 and lc.fold_torso_reduce
                 and lc.optimizer != "adam" and lc.grad_clip <= 0 and self.row_dst4 is not None
-                and self._rms_all is None and self.fwd_geom is not None and L.torso_offset % 4 == 0
+                and self.fwd_geom is not None and L.torso_offset % 4 == 0
                 and bool((L.row_dst4[L.torso_offset // 4:] < 0).all())):
             self._fold_tq = L.torso_offset // 4
         self._pack(always=True)
@@ -254,9 +238,6 @@ class LearnerEngine:
         # the fused FORWARD kernel also covers DMLab-30 RGB (3x72x96); its backward then runs on
         # the library convs from the saved activations
         self.fwd_geom = fused_torso_fwd_geom(cfg.env, cfg.model) if d.type == "cuda" else None
-        if d.type == "cuda":
-            kernels().r2_lstm_sp_handoff8(0 if lc.lstm_tag_words else 1)
-            kernels().r2_lstm_bwd_handoff8(0 if lc.lstm_tag_words else 1)
         if sp and not (cfg.model.torso == "atari" and d.type == "cuda" and L.H <= 256
                        and lc.lstm_impl == "persistent" and lc.lstm_handoff == "tagged"):
             raise NotImplementedError(
@@ -479,9 +460,9 @@ class LearnerEngine:
             # one launch: the tail ends the step (counter + 1) and samples the next batch from the
             # repaired tree (replay.hip r2_prio_tail_sample); else the separate launches
             S, states = self._sample_dst(nxt)
-            if not (self.cfg.learner.hoist_fuse_sample and rp.prio_tail_sample(
-                    self.starts, B, self.Lb, self.T, S["starts"], S["probs"], S["rows"], self.Tn,
-                    states, self.sp, self.tq, skip_xcds=self._bptt_xcds())):
+            if not rp.prio_tail_sample(self.starts, B, self.Lb, self.T, S["starts"], S["probs"],
+                                       S["rows"], self.Tn, states, self.sp, self.tq,
+                                       skip_xcds=self._bptt_xcds()):
                 if not rp.prio_tail(self.starts, B, self.Lb, self.T, True):
                     rp.refresh_sequences(self.starts, B, self.Lb, self.T)
                     if not rp.update_tree_and_end_step(True):
@@ -489,30 +470,28 @@ class LearnerEngine:
                         rp.step_end()
                 self._sample(set_idx=nxt, qreset=self.tq)
             if torso:
-                lc = self.cfg.learner
                 rows = self._sets[nxt]["rows"][self.t_lo_tg * B:]
-                job = self._torso_job_sp(self.pk_t, self.pk_t_lo, rows, self.X_tg, self.X_tg_lo, qmode=1,
-                                         avoid=int(lc.hoist_avoid_xcds))
+                job = self._torso_job_sp(self.pk_t, self.pk_t_lo, rows, self.X_tg, self.X_tg_lo, qmode=1)
                 arr = np.asarray([job], dtype=np.int64)
                 self._side_job = arr      # (the launcher copies it into the kernel arguments)
-                grid = int(lc.hoist_grid) or (self.n_cus if lc.bptt_xcd_pairs or lc.hoist_avoid_xcds
-                                              else max(1, self.n_cus - self._bptt_groups_wgs()))
+                # every CU when the recurrence packs two groups per XCD (its helpers leave at
+                # once), else the CUs outside its groups
+                grid = (self.n_cus if self._bptt_pairs()
+                        else max(1, self.n_cus - self._bptt_groups_wgs()))
                 check(kernels().r2_torso_fwd_sp_multi(ptr(rp.frames), arr.ctypes.data, 1, grid,
                                                       stream_handle(side)), "torso_fwd_sp (hoisted)")
         return side
 
+    def _bptt_pairs(self) -> bool:
+        """The hoisted BPTT packs its recurrence groups two per XCD (lstm_persist.hip xcd_map 3,
+        hidden / 16 = 16 workgroups a group; alone it runs faster one group per XCD, 97 vs 105
+        us, so only beside the hoisted torso frames: profiles/r06_tree_ab_knobs.txt "np")."""
+        return self.layout.H // UNITS == 16
+
     def _bptt_xcds(self) -> int:
         """The first n XCDs, which hold the BPTT recurrence's workgroups, for the hoisted
-        branch's tail workgroups to stay off: packed two groups per XCD (learner.bptt_xcd_pairs;
-        lstm_persist.hip xcd_map 3) -> ceil(batch tiles / 2); else the low run of
-        learner.hoist_avoid_xcds (one group per XCD: XCDs 0 .. tiles-1)."""
-        lc = self.cfg.learner
-        if lc.bptt_xcd_pairs and self.layout.H // UNITS == 16:
-            return min(4, (-(-self.B // 16) + 1) // 2)
-        m, n = int(lc.hoist_avoid_xcds), 0
-        while n < 4 and (m >> n) & 1:
-            n += 1
-        return n
+        branch's tail workgroups to stay off: ceil(batch tiles / 2) when packed in pairs."""
+        return min(4, (-(-self.B // 16) + 1) // 2) if self._bptt_pairs() else 0
 
     def _bptt_groups_wgs(self) -> int:
         """Workgroups of the BPTT recurrence (batch tiles x hidden / 16)."""
@@ -536,14 +515,12 @@ class LearnerEngine:
         # path does not pay a cross-queue hand-off (measured: the BPTT started 11 us after the TD
         # when the side branch was captured first)
         self._backward_core()
-        side = self._hoist_side(torso=not due and self.cfg.learner.hoist_torso, after_td=after_td)
-        end_join = self.cfg.learner.hoist_join == "end"
-        if not end_join:
-            main.wait_stream(side)   # before the conv backward: the side branch ends with the BPTT
+        side = self._hoist_side(torso=not due, after_td=after_td)
+        # join before the conv backward: the side branch ends with the BPTT (joining at the end of
+        # the step instead let the side torso slow the conv backward: measured slower)
+        main.wait_stream(side)
         self._seg_torso()
         self._update()
-        if end_join:
-            main.wait_stream(side)
 
     def _hoist_step(self):
         k = self.steps_done
@@ -651,9 +628,10 @@ class LearnerEngine:
         if self.sp:
             probs = [Gemm(h, pk["head1"].t(), zb, a_lo=hl, b_lo=pkl["head1"].t())
                      for (pk, h, zb, _, _), (pkl, hl) in zip(jobs, lo)]
-            if self.cfg.learner.sp_gemm6 and self.cfg.learner.sp_gemm == "fused":
-                self._gemm_sp("heads", probs, splits=[0] * len(probs),
-                              cfg=int(self.cfg.learner.sp_heads_cfg))   # gemm6
+            if self.cfg.learner.sp_gemm == "fused":
+                # the launcher's CU model picks 128x128x64 (same-box sweep of the tile configs:
+                # profiles/r03_heads_cfg_ab.txt)
+                self._gemm_sp("heads", probs, splits=[0] * len(probs), cfg=-1)
             else:
                 gemm(*probs)
             zs = [zb for _, _, zb, _, _ in jobs]
@@ -684,8 +662,7 @@ class LearnerEngine:
         return [ptr(rows), rows.numel(), ptr(pk["conv1"]), ptr(pk["b1"]), ptr(pk["conv2"]),
                 ptr(pk["b2"]), ptr(pk["conv3"]), ptr(pk["b3"]), ptr(out), s1, s2, 0]
 
-    def _torso_job_sp(self, pk, pkl, rows, out, out_lo, save_at=None, qmode: int = 0,
-                      avoid: int = 0):
+    def _torso_job_sp(self, pk, pkl, rows, out, out_lo, save_at=None, qmode: int = 0):
         """torso_sp.hip job (20 int64): weights hi / lo, features hi / lo, saved activations, and
         (qmode 1 / 2, the hoisted step) the frame-queue words ``self.tq``."""
         B = self.B
@@ -694,7 +671,7 @@ class LearnerEngine:
             r0, r1 = save_at * B, save_at * B + rows.numel()
             s = [ptr(self.act1[r0:r1]), ptr(self.act1_lo[r0:r1]), ptr(self.act2[r0:r1]),
                  ptr(self.act2_lo[r0:r1])]
-        q = [ptr(self.tq), qmode, avoid] if qmode else [0, 0, 0]
+        q = [ptr(self.tq), qmode, 0] if qmode else [0, 0, 0]
         return [ptr(rows), rows.numel(), ptr(pk["conv1"]), ptr(pkl["conv1"]), ptr(pk["b1"]),
                 ptr(pk["conv2"]), ptr(pkl["conv2"]), ptr(pk["b2"]), ptr(pk["conv3"]),
                 ptr(pkl["conv3"]), ptr(pk["b3"]), ptr(out), ptr(out_lo)] + s + q
@@ -924,7 +901,7 @@ class LearnerEngine:
         instead of the TD launch streaming all of W1^T through each of its workgroups."""
         lc, L = self.cfg.learner, self.layout
         return bool(self.sp and lc.bptt_dh and lc.td_fuse_head_bwd and L.H == 256 and 2 * L.HD == 512
-                    and lc.lstm_tag_words and self.device.type == "cuda")
+                    and self.device.type == "cuda")
 
     def _backward_core_sp(self):
         """Split-precision backward core: head gradients, dh GEMM, BPTT, weight-gradient + dX
@@ -962,10 +939,10 @@ class LearnerEngine:
             check(k.r2_lstm_bwd_set_dz(ptr(self.dz), ptr(self.dz_lo), ptr(pk["head1T"]),
                                        ptr(pkl["head1T"]), 2 * HD), "lstm_bwd_set_dz")
         # the hoisted target torso beside this launch stops taking frames hoist_stop_lead
-        # iterations before the recurrence ends; bptt_hg_wgs helpers take the head gradients
+        # iterations before the recurrence ends; every helper takes head-gradient items
         lc = self.cfg.learner
         check(k.r2_lstm_bwd_set_stop(ptr(self.tq[2:]) if self.hoist else 0,
-                                     max(0, self.Ll - int(lc.hoist_stop_lead)), int(lc.bptt_hg_wgs)),
+                                     max(0, self.Ll - int(lc.hoist_stop_lead)), 0),
               "lstm_bwd_set_stop")
         if side_hg:
             rc = k.r2_lstm_bwd_tag_sp_hg(*bptt, *hg, s)   # >= 0: bit 0 = head grads done here
@@ -1150,10 +1127,9 @@ class LearnerEngine:
                     ptr(pk["w_hhT"]), ptr(self.dgates), B, T, Lb, H, ptr(self.ctr), ptr(self.err),
                     ptr(self.ring_b), ptr(self.bias_ws), ptr(self.gate_perm_i32),
                     ptr(L.view(g, "lstm.bias_ih")), ptr(L.view(g, "lstm.bias_hh"))]
-            self._gdesc = np.zeros(1, dtype=np.int64)    # no GEMM side jobs (kept alive for capture)
-            rc = k.r2_lstm_bwd_tag(*base, *self._hg_job, self._gdesc.ctypes.data, 0, 0, 0, s)
+            rc = k.r2_lstm_bwd_tag(*base, *self._hg_job, s)
             if rc in (-6, -10):   # not enough idle workgroups for the side job: recurrence alone
-                rc = k.r2_lstm_bwd_tag(*base, *([0] * 11), self._gdesc.ctypes.data, 0, 0, 0, s)
+                rc = k.r2_lstm_bwd_tag(*base, *([0] * 11), s)
             if rc != -3:          # -3: grid too large for one workgroup per CU
                 if rc < 0:
                     check(rc, "lstm_bwd_tag")
@@ -1183,7 +1159,11 @@ class LearnerEngine:
             return out
         return grad * (act > 0)
 
-    def _backward_torso(self):
+    def _backward_torso(self, defer_reduce: bool = False):
+        """Conv-torso backward into self.grad.  ``defer_reduce`` (split precision, world 1): the
+        per-workgroup gradient slabs are left for the optimizer launch, which sums them
+        (r2_rmsprop_pack_slab); the torso entries of self.grad are written there."""
+        self._torso_deferred = False
         if self.sp_lib:
             B, Lb, T = self.B, self.Lb, self.T
             torso_backward_library_sp(self.replay.frames, self.rows[Lb * B: T * B], self.layout,
@@ -1200,7 +1180,8 @@ class LearnerEngine:
                 ptr(self.X_on[Lb * B: T * B]), ptr(pk["conv3_dg"]), ptr(pkl["conv3_dg"]),
                 ptr(pk["conv2_dg"]), ptr(pkl["conv2_dg"]), ptr(self._tb_slab), self._tb_grid,
                 ptr(self._tb_dst), ptr(self._tb_scale),
-                0 if self._fold_tq is not None else ptr(self.grad), stream_handle()), "torso_bwd_sp")
+                0 if defer_reduce else ptr(self.grad), stream_handle()), "torso_bwd_sp")
+            self._torso_deferred = defer_reduce
             return
         if self.cfg.learner.torso_bwd == "fused" and self.fwd_geom is not None:
             self._backward_torso_fused()
@@ -1287,20 +1268,7 @@ class LearnerEngine:
                             float(lc.lr), float(lc.adam_betas[0]), float(lc.adam_betas[1]),
                             float(lc.eps), gscale, ptr(self.replay.step), clip,
                             float(lc.grad_clip), s), "adam")
-        elif self._rms_all is not None:
-            # the update writes every packed layout and, when due, the target master and packs
-            r = self._rms_all
-            check(k.r2_rmsprop_pack_all(ptr(self.master), ptr(self.grad), ptr(self.opt_a),
-                                        ptr(self.opt_b), n, float(lc.lr), float(lc.rms_alpha),
-                                        float(lc.eps), gscale, clip, float(lc.grad_clip),
-                                        ptr(self.row_dst4), ptr(self.bf), ptr(self.bf_t),
-                                        L.bf_numel if self.sp else 0, ptr(self.target),
-                                        ptr(self.replay.step), self._baked_interval(), r["xq0"],
-                                        ptr(r["xA"]), ptr(r["xB"]), ptr(r["xF"]), r["bq0"], L.G,
-                                        ptr(r["binv"]), ptr(self.f32), ptr(self.f32_t),
-                                        ptr(self.lstm_b), ptr(self.lstm_b_t), s), "rmsprop_pack_all")
-            return
-        elif self._fold_tq is not None:
+        elif self._fold_tq is not None and getattr(self, "_torso_deferred", False):
             # + the torso slab reduction (its first workgroups; _backward_torso left the slabs)
             check(k.r2_rmsprop_pack_slab(ptr(self.master), ptr(self.grad), ptr(self.opt_a),
                                          ptr(self.opt_b), n, float(lc.lr), float(lc.rms_alpha),
@@ -1381,7 +1349,8 @@ class LearnerEngine:
         self._backward_core()
 
     def _seg_torso(self):
-        self._backward_torso()
+        # the update that follows (same segment) sums the slabs itself when folded
+        self._backward_torso(defer_reduce=self._fold_tq is not None)
 
     def _seg_tail(self):
         self._update()

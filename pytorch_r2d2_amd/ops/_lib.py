@@ -68,7 +68,6 @@ _SIGS = {
     "r2_sample_batch_q": [P, P, P, I, I, U64, P, P, P, P, I, I, I, I, P, P, P, P, I, P, P],
     "r2_torso_fwd_sp_multi": [P, P, I, I, P],
     "r2_torso_sp_debug": [I],
-    "r2_torso_sp_save_weight": [I],
     "r2_torso_sp_trace": [P],
     "r2_torso_bwd_sp_trace": [P],
     "r2_torso_bwd_sp_debug": [I],
@@ -79,8 +78,6 @@ _SIGS = {
     "r2_rmsprop_centered": [P, P, P, P, I64, F, F, F, F, P, F, P],
     "r2_rmsprop_pack": [P, P, P, P, I64, F, F, F, F, P, F, P, P, P, I64, P, P, I64, P],
     "r2_rmsprop_pack_slab": [P, P, P, P, I64, F, F, F, F, P, P, P, I64, P, P, I64, P, I, I, P, P, I64, P],
-    "r2_rmsprop_pack_all": [P, P, P, P, I64, F, F, F, F, P, F, P, P, P, I64, P, P, I64, I64, P, P, P,
-                            I64, I64, P, P, P, P, P, P],
     "r2_adam": [P, P, P, P, I64, F, F, F, F, F, P, P, F, P],
     "r2_sumsq": [P, I64, P, P],
     "r2_pack_bf16": [P, P, P, I64, P],
@@ -105,8 +102,6 @@ _SIGS = {
     "r2_torso_fwd_set_debug": [P],
     "r2_lstm_persist_set_debug": [P],
     "r2_lstm_fwd_set_stamps": [P],
-    "r2_lstm_sp_handoff8": [I],
-    "r2_lstm_bwd_handoff8": [I],
     "r2_td_duel_fwd_set": [P],
     "r2_prio_tail": [P, I, P, P, P, P, P, I, I, I, I, I, F, P, P, I, P, P, I, P],
     "r2_lstm_bwd_set_dz": [P, P, P, P, I],
@@ -181,8 +176,33 @@ def kernels():
                 continue
             fn.argtypes = argtypes
             fn.restype = ctypes.c_longlong if ("_ws_bytes" in name) else ctypes.c_int
-        _lib = lib
-        return lib
+        _lib = _Strict(lib)
+        return _lib
+
+
+class _Strict:
+    """The loaded library with an argument-count check on every declared entry point: ctypes
+    passes surplus arguments through as C varargs, so a stale call site (one argument list longer
+    than the entry point's) would silently shift the trailing stream argument."""
+
+    def __init__(self, lib):
+        self._cdll = lib
+
+    def __getattr__(self, name):
+        fn = getattr(self._cdll, name)
+        sig = _SIGS.get(name)
+        if sig is None:
+            return fn
+        n = len(sig)
+
+        def call(*args):
+            if len(args) != n:
+                raise TypeError(f"{name}: {len(args)} arguments, the entry point takes {n}")
+            return fn(*args)
+
+        call.__name__ = name
+        self.__dict__[name] = call
+        return call
 
 
 def ptr(t) -> int:

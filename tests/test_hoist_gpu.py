@@ -25,8 +25,7 @@ def _engine(hoist, B=64, interval=3, graph=True, **kw):
 
 
 def _state(rp, eng):
-    # the packed layouts by name (their alignment padding is never read and not compared: the
-    # hoisted step's optimizer scatters into the named packs only, r2_rmsprop_pack_all)
+    # the packed layouts by name (their alignment padding is never read and not compared)
     out = {"master": eng.master, "target": eng.target, "opt_a": eng.opt_a, "opt_b": eng.opt_b,
            "lstm_b": eng.lstm_b, "lstm_b_t": eng.lstm_b_t, "priority": rp.priority,
            "tree": rp.tree, "step": rp.step, "loss": eng.loss}
@@ -37,16 +36,16 @@ def _state(rp, eng):
     return out
 
 
-@pytest.mark.parametrize("graph,full_repack", [(True, False), (False, False), (True, True)])
-def test_hoisted_step_is_bitwise_the_plain_step(graph, full_repack):
+@pytest.mark.parametrize("graph,B", [(True, 64), (False, 64), (True, 16), (False, 8)])
+def test_hoisted_step_is_bitwise_the_plain_step(graph, B):
     """Bench shape (B=64, 40 + 40, n=5, fixed target), target sync every 3 steps (steps 2, 5, 8
     sync: the step after each runs the full target torso), one invalidation in the middle (the
     next step samples at its start): weights, optimizer moments, every packed layout, priorities,
-    sum tree and step counter equal the plain engine's after every step; error word 0.
-    ``full_repack``: the optimizer scatters every packed layout itself (r2_rmsprop_pack_all)."""
-    rp0, plain = _engine(False, graph=graph)
-    rp1, hoist = _engine(True, graph=graph, **{"learner.hoist_full_repack": full_repack})
-    assert (hoist._rms_all is not None) == full_repack
+    sum tree and step counter equal the plain engine's after every step; error word 0.  B 8 / 16:
+    one batch tile, an odd count of recurrence groups packed in XCD pairs (the head-gradient
+    helpers' ordinals, lstm_persist.hip xcd_map 3)."""
+    rp0, plain = _engine(False, B=B, graph=graph)
+    rp1, hoist = _engine(True, B=B, graph=graph)
     assert hoist.hoist and not plain.hoist
     if graph:
         plain.capture(warmup=0)

@@ -142,7 +142,7 @@ def test_lstm_backward_matches_autograd(B, H, impl):
         for _ in range(2):      # second launch: stale granules of the first must be ignored
             assert k.r2_lstm_bwd_tag(ptr(dh_ext), ptr(gates), ptr(cseq), ptr(c0), ptr(pk["w_hhT"]),
                                      ptr(dg), B, T, t0, H, ptr(ctr), ptr(err), ptr(ring),
-                                     ptr(bias_ws), ptr(perm_i), ptr(db1), ptr(db2), *([0] * 15),
+                                     ptr(bias_ws), ptr(perm_i), ptr(db1), ptr(db2), *([0] * 11),
                                      stream_handle()) == 0
         rest = ctr.clone()
         rest[3072 + 32] = rest[3072 + 64] = 0        # the two launch epochs (lstm_persist.hip PT_EPOCH_*)

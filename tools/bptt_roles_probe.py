@@ -1,7 +1,7 @@
 """Per-role clock stamps of the fp32 BPTT launch (lstm_persist.hip lstm_bwd_tag_kernel, PTBArgs::dbg)
 at the bench config, one eager engine step per arm, arms as learner.* override sets:
 
-    python tools/bptt_roles_probe.py hoist=0 hoist_torso=0 off bptt_hg_wgs=64 ...
+    python tools/bptt_roles_probe.py hoist=0 off hoist_stop_lead=3 ...
 
 Per arm: launch span (first workgroup start -> last workgroup end), the recurrence's end (its
 last workgroup), the helpers' end (head-gradient reduction), the median / max BPTT iteration of
@@ -90,7 +90,7 @@ def arm(spec: str, reps: int = 3):
 
 
 def main():
-    arms = sys.argv[1:] or ["hoist=0", "hoist_torso=0", "off"]
+    arms = sys.argv[1:] or ["hoist=0", "off"]
     for a in arms:
         print(json.dumps(arm(a)), flush=True)
 

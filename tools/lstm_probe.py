@@ -67,7 +67,7 @@ bwd = lambda: k.r2_lstm_bwd_persist(ptr(dh), ptr(bufs[2]), ptr(bufs[1]), ptr(c0)
 res["bwd_counter_us_per_step"] = timeit(bwd) / 40
 ring_b = torch.zeros(k.r2_lstm_bwd_tag_ring_bytes(B, H) // 4, dtype=torch.int32, device=DEV)
 bwd_tag = lambda: k.r2_lstm_bwd_tag(ptr(dh), ptr(bufs[2]), ptr(bufs[1]), ptr(c0), ptr(pk["w_hhT"]),
-                                    ptr(dg), B, 80, 40, H, ptr(ctr), ptr(err), ptr(ring_b), 0, 0, 0, 0, *([0] * 15),
+                                    ptr(dg), B, 80, 40, H, ptr(ctr), ptr(err), ptr(ring_b), 0, 0, 0, 0, *([0] * 11),
                                     stream_handle())
 res["bwd_us_per_step"] = timeit(bwd_tag) / 40
 dbg = torch.zeros(32 * 8 + 256, dtype=torch.int64, device=DEV)

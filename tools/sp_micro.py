@@ -124,11 +124,8 @@ if which in ("xproj", "both"):
             xh, xl = split(x)
             yh, yl = split(y)
             probs.append(Gemm(xh, yh, torch.zeros(M, N, device=DEV), a_lo=xl, b_lo=yl))
-        for il in (0, 1):
-            kernels().r2_gemm5_set_mode(il)
-            for c in (0, 1, 3, 6):
-                res[f"xproj_il{il}_cfg{c}_us"] = timeit(lambda: gemm_sp(xp, cfg=c))
-            for c in (1, 3, 6):
-                res[f"group_il{il}_cfg{c}_us"] = timeit(lambda: gemm_sp(probs, splits=[4, 4, 4, 1], cfg=c))
-        kernels().r2_gemm5_set_mode(1)
+        for c in (0, 1, 3, 6):
+            res[f"xproj_cfg{c}_us"] = timeit(lambda: gemm_sp(xp, cfg=c))
+        for c in (1, 3, 6):
+            res[f"group_cfg{c}_us"] = timeit(lambda: gemm_sp(probs, splits=[4, 4, 4, 1], cfg=c))
 print(json.dumps(res))
