@@ -38,6 +38,9 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
              "-Wno-unused-result", "-Wno-unused-variable"]
+if os.environ.get("R2D2_PROBES"):
+    # the LSTM kernels' clock-stamp hooks (csrc/lstm_common.h PL_PROBE): probe builds only
+    HIP_FLAGS.append("-DR2_LSTM_PROBES=1")
 CXX = os.environ.get("CXX", "g++")
 CXX_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
 

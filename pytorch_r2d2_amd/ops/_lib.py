@@ -107,6 +107,7 @@ _SIGS = {
     "r2_lstm_bwd_set_dz": [P, P, P, P, I],
     "r2_lstm_bwd_set_stop": [P, I, I],
     "r2_lstm_bwd_xcd_pairs": [I],
+    "r2_lstm_probes": [],
     "r2_prio_tail_sample": [P, I, P, P, P, P, P, I, I, I, I, I, F, P, P, I, P, P, U64, P, P, P, I,
                             I, I, P, P, P, P, I, P, I, P],
     "r2_prio_tail_pack": [P, I, P, P, P, P, P, I, I, I, I, I, F, P, P, I, P, P, I,

@@ -42,6 +42,9 @@ def arm(spec: str, reps: int = 3):
         eng.step()
     torch.cuda.synchronize()
     k = kernels()
+    if not k.r2_lstm_probes():
+        raise SystemExit("the LSTM stamp hooks are compiled out: rebuild with "
+                         "R2D2_PROBES=1 python -m pytorch_r2d2_amd._build")
     out = []
     for _ in range(reps):
         dbg = torch.zeros(4096, dtype=torch.int64, device=DEV)

@@ -36,6 +36,9 @@ def main(reps: int = 3):
         eng.step()
     torch.cuda.synchronize()
     k = kernels()
+    if not k.r2_lstm_probes():
+        raise SystemExit("the LSTM stamp hooks are compiled out: rebuild with "
+                         "R2D2_PROBES=1 python -m pytorch_r2d2_amd._build")
     for _ in range(reps):
         fs = torch.zeros(4 * 512, dtype=torch.int64, device=DEV)
         dbg = torch.zeros(4096, dtype=torch.int64, device=DEV)
