@@ -1545,8 +1545,21 @@ class LearnerEngine:
             if ro.record(self._dp_checksum(), self.err, self.steps_done) is False:
                 self._dp_repair()
         elif ro.want_promote(self.steps_done):
-            self._capture_one_dp()
-            ro.promoted()
+            err = None
+            try:
+                self._capture_one_dp()
+            except Exception as e:   # noqa: BLE001 -- the runtime refused the capture
+                err = "%s: %s" % (type(e).__name__, str(e).splitlines()[0][:120] if str(e) else "")
+                self._one_graph, self._one_dp_graph = None, False
+                # host-side step state a half-captured body may have left behind
+                self._pack_deferred = None
+                self._gsync = None
+                torch.cuda.synchronize(self.device)
+            if ro.agree(err is None):
+                ro.promoted()
+            else:
+                self._one_graph, self._one_dp_graph = None, False
+                ro.refused(err or "on another rank")
 
     def dp_graph_label(self) -> Optional[str]:
         """How the DP step is replayed (bench.py JSON): segment graphs, the one graph (validated

@@ -16,6 +16,8 @@ run (round-6 verdict item 7; reference: a single learner, /root/reference/learne
      checksum of its weights and its error word on the device (no host sync per step), and at the
      end of the window ONE all-reduce (MAX) of ``[checksums, -checksums, error words]`` decides:
      identical weights on every rank give max - min = 0 at every step;
+  (a capture that raises on any rank -- agreed by one all-reduce -- keeps every rank on the
+  segment graphs;)
   3. any mismatch or a non-zero error word switches EVERY rank back to the segment graphs for the
      rest of the run (the decision is taken on the all-reduced values, so all ranks agree), the
      engine re-broadcasts rank 0's weights / optimizer state, and ``fallback`` is reported
@@ -49,6 +51,7 @@ class GraphRollout:
         self.fallback = False
         self.checked = 0
         self.mismatch_step: Optional[int] = None
+        self.refusal: Optional[str] = None
         self._buf = None
         self._steps = []
 
@@ -56,6 +59,22 @@ class GraphRollout:
         """Capture and switch to the one graph now (after the warm-up segment steps)?"""
         return (self.enabled and not self.fallback and self.mode == "segments"
                 and steps_done >= self.warm)
+
+    def agree(self, ok: bool) -> bool:
+        """Did the one-graph capture succeed on EVERY rank?  One all-reduce (MIN) of the local
+        flag, issued outside any capture: a rank whose capture raised keeps every rank on the
+        segment graphs (their collective sequences must stay identical)."""
+        if not (dist.is_initialized() and self.world > 1):
+            return bool(ok)
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=self.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(int(t.item()))
+
+    def refused(self, reason: str) -> None:
+        """The one graph could not be captured (on some rank): segments for the rest of the run."""
+        self.mode = "segments"
+        self.fallback = True
+        self.refusal = reason
 
     def promoted(self) -> None:
         self.mode = "one"
@@ -100,6 +119,8 @@ class GraphRollout:
         return True
 
     def label(self) -> str:
+        if self.refusal is not None:
+            return "segment graphs (one-graph capture refused: %s)" % self.refusal
         if self.fallback:
             return "segment graphs (one-graph fallback at step %d)" % self.mismatch_step
         if self.mode == "one":

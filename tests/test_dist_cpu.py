@@ -294,7 +294,7 @@ def test_async_links_decouple_learner_from_slow_actor(tmp_path):
     assert rates[2] >= 0.7 * rates[0], rates
 
 
-def _rollout_worker(rank, port, fault, out):
+def _rollout_worker(rank, port, fault, out, refuse_rank=-1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE="2")
     import torch.distributed as dist
     from pytorch_r2d2_amd.parallel.graph_rollout import GraphRollout
@@ -311,8 +311,12 @@ def _rollout_worker(rank, port, fault, out):
             if v is not None:
                 events.append(("verdict", step, bool(v)))
         elif ro.want_promote(step):
-            ro.promoted()
-            events.append(("promote", step))
+            if ro.agree(rank != refuse_rank):    # the capture "raised" on refuse_rank
+                ro.promoted()
+                events.append(("promote", step))
+            else:
+                ro.refused("test")
+                events.append(("refused", step))
     torch.save({"events": events, "mode": ro.mode, "fallback": ro.fallback,
                 "mismatch": ro.mismatch_step, "label": ro.label()}, "%s.%d" % (out, rank))
     dist.destroy_process_group()
@@ -337,3 +341,15 @@ def test_one_graph_rollout_falls_back_on_checksum_mismatch(tmp_path, fault):
     else:
         assert r[0]["events"][1] == ("verdict", 7, True)
         assert all(not x["fallback"] and x["mode"] == "one" for x in r)
+
+
+def test_one_graph_capture_refused_on_one_rank_keeps_every_rank_on_segments(tmp_path):
+    """A one-graph capture that raises on rank 1 only: the all-reduced flag keeps BOTH ranks on
+    the segment graphs (their collective sequences stay identical) and labels the run."""
+    import torch.multiprocessing as tmp
+    out = str(tmp_path / "rf")
+    tmp.spawn(_rollout_worker, args=(_free_port(), "", out, 1), nprocs=2, join=True)
+    r = [torch.load("%s.%d" % (out, k), weights_only=True) for k in range(2)]
+    assert r[0]["events"] == r[1]["events"] == [("refused", 3)]
+    assert all(x["mode"] == "segments" and x["fallback"] for x in r)
+    assert "capture refused" in r[0]["label"]
