@@ -285,7 +285,10 @@ __device__ __forceinline__ void g6_mix() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <bool AK, bool BKM, int BM, int BN, int BK, bool FOK>
+// PM (decomposition probe, r2_gemm5_set_mode bits 8-9; the 192 x 256 fast tile only): 1 =
+// operand staging alone (no fragment reads, no MFMAs), 2 = the compute loop alone (no staging);
+// tools/xproj_decomp.py, profiles/r06_xproj_decomposition.txt
+template <bool AK, bool BKM, int BM, int BN, int BK, bool FOK, int PM = 0>
 __device__ __forceinline__ void g6_mainloop(const GemmProb& P, int m0, int n0, int kt0, int kt1,
                                             uint8_t* lds6, int wave, int lane,
                                             f32x4 (&acc)[BM / 32][BN / 64]) {
@@ -315,7 +318,9 @@ __device__ __forceinline__ void g6_mainloop(const GemmProb& P, int m0, int n0, i
   }
   auto stage = [&](int kt) {
     uint8_t* st = lds6 + ((kt - kt0) & 1) * STB;
-    if constexpr (FAST) {
+    if constexpr (PM == 2) {
+      return;
+    } else if constexpr (FAST) {
       const uint32_t k0 = (uint32_t)(kt * BK);
 #pragma unroll
       for (int j = 0; j < PA; ++j) {
@@ -346,11 +351,13 @@ __device__ __forceinline__ void g6_mainloop(const GemmProb& P, int m0, int n0, i
   bf16x8 ahi[FM], alo[FM], bhi[FN], blo[FN];
   // K step q = (LDS tile kt, step ks of it); its planes in buffer (kt - kt0) & 1
   auto ldA = [&](bf16x8 (&f)[FM], int kt, int ks, int plane) {
+    if constexpr (PM == 1) return;
     const uint8_t* pl = lds6 + ((kt - kt0) & 1) * STB + plane * OPA;
 #pragma unroll
     for (int i = 0; i < FM; ++i) f[i] = g5_frag<AK, BK>(pl, wr * (BM / 2) + 16 * i, ks, lane);
   };
   auto ldB = [&](bf16x8 (&f)[FN], int kt, int ks, int plane) {
+    if constexpr (PM == 1) return;
     const uint8_t* pl = lds6 + ((kt - kt0) & 1) * STB + 2 * OPA + plane * OPB;
 #pragma unroll
     for (int j = 0; j < FN; ++j) f[j] = g5_frag<BKM, BK>(pl, wc * (BN / 4) + 16 * j, ks, lane);
@@ -364,7 +371,8 @@ __device__ __forceinline__ void g6_mainloop(const GemmProb& P, int m0, int n0, i
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = g5_mfma(ahi[i], blo[j], acc[i][j]);
+      for (int j = 0; j < FN; ++j)
+        if constexpr (PM != 1) acc[i][j] = g5_mfma(ahi[i], blo[j], acc[i][j]);
     g6_mix<FM + FN, FM * FN>();
     if (ks == KS - 1) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // tile kt+1 landed; kt read
@@ -376,14 +384,16 @@ __device__ __forceinline__ void g6_mainloop(const GemmProb& P, int m0, int n0, i
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = g5_mfma(ahi[i], bhi[j], acc[i][j]);
+      for (int j = 0; j < FN; ++j)
+        if constexpr (PM != 1) acc[i][j] = g5_mfma(ahi[i], bhi[j], acc[i][j]);
     if (more) g6_mix<FN, FM * FN>(); else g6_mix<0, FM * FN>();
     // pass 3: A lo x B hi; A hi <- the next step's
     if (more) ldA(ahi, nkt, nks, 0);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) acc[i][j] = g5_mfma(alo[i], bhi[j], acc[i][j]);
+      for (int j = 0; j < FN; ++j)
+        if constexpr (PM != 1) acc[i][j] = g5_mfma(alo[i], bhi[j], acc[i][j]);
     if (more) g6_mix<FM, FM * FN>(); else g6_mix<0, FM * FN>();
   };
   if (kt0 < kt1) {
@@ -399,7 +409,7 @@ __device__ __forceinline__ void g6_mainloop(const GemmProb& P, int m0, int n0, i
   }
 }
 
-template <bool BKM, int BM, int BN, int BK, bool FOK>
+template <bool BKM, int BM, int BN, int BK, bool FOK, int PM = 0>
 __global__ __launch_bounds__(512) void gemm6_kernel(const G5Args a) {
   constexpr int FM = BM / 32, FN = BN / 64;           // 16 x 16 fragments of the (BM/2) x (BN/4) wave tile
   extern __shared__ __attribute__((aligned(1024))) uint8_t lds6[];
@@ -427,7 +437,9 @@ __global__ __launch_bounds__(512) void gemm6_kernel(const G5Args a) {
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (BM % 128 == 0) {
+  if constexpr (PM != 0) {
+    g6_mainloop<true, BKM, BM, BN, BK, FOK, PM>(P, m0, n0, kt0, kt1, lds6, wave, lane, acc);
+  } else if constexpr (BM % 128 == 0) {
     if (P.a_kmajor) g6_mainloop<true, BKM, BM, BN, BK, FOK>(P, m0, n0, kt0, kt1, lds6, wave, lane, acc);
     else g6_mainloop<false, BKM, BM, BN, BK, FOK>(P, m0, n0, kt0, kt1, lds6, wave, lane, acc);
   } else {
@@ -442,17 +454,17 @@ __global__ __launch_bounds__(512) void gemm6_kernel(const G5Args a) {
 // on every shape and removed: profiles/r05_gemm7_deep_ring_rejected.txt)
 
 
-template <bool BKM, int BM, int BN, int BK, bool FOK>
+template <bool BKM, int BM, int BN, int BK, bool FOK, int PM = 0>
 static void g6_kernel_launch(const G5Args& a, hipStream_t s) {
   constexpr int LDS = 2 * 2 * (BM + BN) * BK * 2;
   static_assert(LDS <= 160 * 1024 && 64 * (BN + 16) * 4 + 4 <= LDS, "LDS");
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)gemm6_kernel<BKM, BM, BN, BK, FOK>,
+    hipFuncSetAttribute((const void*)gemm6_kernel<BKM, BM, BN, BK, FOK, PM>,
                         hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((gemm6_kernel<BKM, BM, BN, BK, FOK>), dim3(a.total), dim3(512), LDS, s, a);
+  hipLaunchKernelGGL((gemm6_kernel<BKM, BM, BN, BK, FOK, PM>), dim3(a.total), dim3(512), LDS, s, a);
 }
 // the fast staging only where it applies (k-major A and B, BK 32, no K tail)
 template <bool BKM, int BM, int BN, int BK>
@@ -465,9 +477,10 @@ static void g6_launch(const G5Args& a, bool k32, hipStream_t s) {
 // (the probe's A/B: tools/gemm_order_probe.py, profiles/r05_gemm_item_order.txt -- the group of
 // the paper config 94-103 -> 92-96 us, bitwise-equal output).  Other bits are ignored (the gemm5
 // and probe modes were removed in round 6).
-static int g5_order = 1;
+static int g5_order = 1, g5_probe = 0;
 extern "C" int r2_gemm5_set_mode(int m) {
   g5_order = !((m >> 6) & 1);
+  g5_probe = (m >> 8) & 3;      // decomposition probe instances (192 x 256 fast tile)
   return 0;
 }
 
@@ -613,7 +626,11 @@ extern "C" int r2_gemm5(const int64_t* descs, const int* split, int np, int cfg,
     // 192 x 256: one round of tiles for the x-projection's 10,560 x 1,024 on 256 CUs (224 items;
     // 192 x 128 took 2.6 rounds)
     case 14: g6_launch<false, 192, 256, 32>(a, k32, s); break;
-    case 15: g6_launch<true, 192, 256, 32>(a, k32, s); break;
+    case 15:
+      if (k32 && all_k && g5_probe == 1) g6_kernel_launch<true, 192, 256, 32, true, 1>(a, s);
+      else if (k32 && all_k && g5_probe == 2) g6_kernel_launch<true, 192, 256, 32, true, 2>(a, s);
+      else g6_launch<true, 192, 256, 32>(a, k32, s);
+      break;
     default: return -8;
   }
   R2_CHECK_LAUNCH();
