@@ -4,7 +4,7 @@ eager engine steps).  Forward: per-workgroup stamps of lstm_fwd_tag_kernel
 PTBArgs::dbg words of lstm_bwd_tag_kernel (start [0], end [1], role [2], rendezvous done [6],
 loop entry [7]).  us from each launch's first workgroup start (s_memrealtime, 100 MHz).
 
-    python tools/lstm_startup_probe.py
+    python tools/lstm_startup_probe.py [key=value ...]
 """
 import json
 import os
@@ -27,8 +27,12 @@ def med(x):
     return round(float(np.median(x)) / 100.0, 2)
 
 
-def main(reps: int = 3):
-    cfg = get_config("atari57", **{"seed": 1234, "learner.use_graph": False})
+def main(reps: int = 3, overrides=()):
+    ov = {"seed": 1234, "learner.use_graph": False}
+    for kv in overrides:        # key=value config overrides (ints / floats / bools / strings)
+        key, v = kv.split("=", 1)
+        ov[key] = {"True": True, "False": False}.get(v, int(v) if v.lstrip("-").isdigit() else v)
+    cfg = get_config("atari57", **ov)
     replay = HBMReplay(cfg, DEV, capacity=200_000)
     replay.fill_synthetic(episode_len=400, seed=0)
     eng = LearnerEngine(cfg, replay, DEV)
@@ -67,4 +71,4 @@ def main(reps: int = 3):
 
 
 if __name__ == "__main__":
-    main()
+    main(overrides=sys.argv[1:])
