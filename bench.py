@@ -129,14 +129,14 @@ def main(argv=None):
     use_graph = cfg.learner.use_graph and not args.no_graph
     if use_graph:
         eng.capture(warmup=2)
-    for _ in range(args.warmup):
-        eng.step()
+    # run_steps: the same steps as a step() loop; the hoisted graph mode replays runs of
+    # learner.graph_chunk steps as one graph each (LearnerEngine.run_steps)
+    eng.run_steps(args.warmup)
     if use_pg:
         dist.barrier()
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.step()
+    eng.run_steps(args.steps)
     torch.cuda.synchronize(device)
     if use_pg:
         dist.barrier()
@@ -197,6 +197,8 @@ def main(argv=None):
                 # step k's priority tail, step k+1's sample and part of its target-net torso
                 # run on a side stream beside step k's BPTT (learner.hoist; bit-identical)
                 "hoisted_step": bool(getattr(eng, "hoist", False)),
+                # consecutive hoisted steps replayed per graph (1 = one graph per step)
+                "graph_chunk": eng._chunk_len() if use_graph else 0,
                 "dp_graph": eng.dp_graph_label(),
             },
             "optimizer_steps_per_sec": round(opt_steps, 3),

@@ -156,6 +156,10 @@ class LearnerConfig:
     # the BPTT raises the side torso's stop word this many iterations before its last one (the
     # side workgroups finish the frame in hand and the one already taken: ~1.5 frames)
     hoist_stop_lead: int = 5
+    # hoisted step, graph mode: LearnerEngine.run_steps(n) replays runs of this many consecutive
+    # steps (no target sync inside, the previous step sampled) as ONE captured graph, so the
+    # ~5 us boundary between two graph replays is paid once per chunk; 1 = a graph per step
+    graph_chunk: int = 8
     # (removed A/B knobs whose alternative lost, record in profiles/: lstm_tag_words = False, the
     # 8-byte hand-off granules (archive/bench_r02_tag_words_ab.log); sp_gemm6 = False, gemm5
     # (r03_gemm6_ab.txt); sp_gemm_order = 0 (r05_gemm_item_order.txt); sp_heads_cfg

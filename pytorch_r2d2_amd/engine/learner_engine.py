@@ -58,6 +58,21 @@ from ..ops.torso_lib import (fused_torso_fwd_geom, fused_torso_supported, gather
 from .layout import ParamLayout, UNITS
 from .replay_hbm import HBMReplay
 
+
+def _graph_upload(g) -> None:
+    """Upload an instantiated graph's executable to the device (hipGraphUpload on the current
+    stream), so its first replay -- possibly inside a timed loop -- does not pay for it.  Best
+    effort: without the runtime entry point the first replay uploads as before."""
+    import os
+    try:
+        exec_h = int(g.raw_cuda_graph_exec())
+        lib = ctypes.CDLL(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))
+        lib.hipGraphUpload.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        lib.hipGraphUpload(ctypes.c_void_p(exec_h), ctypes.c_void_p(stream_handle()))
+    except (AttributeError, OSError, RuntimeError):
+        pass
+
+
 def device_cus(device) -> int:
     """Multiprocessor (CU) count of ``device`` (256 on a whole MI355X; 256 for CPU tensors)."""
     d = torch.device(device)
@@ -536,6 +551,33 @@ class LearnerEngine:
             self._hoist_body(p, inm, due)
         self._hoist_ready = True
         self.steps_done += 1
+
+    def _chunk_len(self) -> int:
+        return max(1, int(getattr(self.cfg.learner, "graph_chunk", 1))) if self.hoist else 1
+
+    def run_steps(self, n: int) -> None:
+        """``n`` learner steps, the same work and results as ``n`` calls of ``step``.  In the
+        hoisted graph mode a run of ``learner.graph_chunk`` steps that starts at an even step,
+        follows a hoisted step and has no target sync inside replays as ONE captured graph
+        (the hoisted bodies back to back on the same streams): the ~5 us boundary between two
+        graph replays (profiles/r06_step_timeline.txt) is paid once per chunk."""
+        m = self._chunk_len()
+        while n > 0:
+            k = self.steps_done
+            off = getattr(self, "_dev_step_off", None)
+            if (n >= m and m > 1 and self.graph and getattr(self, "_cgraph", None) is not None
+                    and (k & 1) == 0 and getattr(self, "_hoist_ready", False) and off is not None
+                    and not any(self._due(k + j + off) for j in range(m))):
+                self._use_set(0)
+                self._cgraph.replay()
+                self.chunks_run = getattr(self, "chunks_run", 0) + 1
+                self._use_set((m - 1) & 1)
+                self._hoist_due = False
+                self.steps_done += m
+                n -= m
+            else:
+                self.step()
+                n -= 1
 
     def state_dict(self):
         return self.layout.state_dict(self.master)
@@ -1443,6 +1485,17 @@ class LearnerEngine:
                 if self._hpool is None:
                     self._hpool = g.pool()
                 self._hgraphs[key] = g
+            # runs of graph_chunk steps starting at an even step, none due, previous step sampled
+            # (run_steps): one graph, so the inter-replay boundary is paid once per chunk
+            self._cgraph = None
+            m = self._chunk_len()
+            if m > 1:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self._hpool):
+                    for j in range(m):
+                        self._hoist_body(j & 1, "H", False)
+                self._cgraph = g
+                _graph_upload(g)
             self._use_set(cur)
             self._hoist_due = due
             torch.cuda.synchronize(self.device)

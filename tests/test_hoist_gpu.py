@@ -160,3 +160,26 @@ def test_folded_torso_reduce_matches_separate_launch(hoist):
         sa["grad"], sb["grad"] = a.grad, b.grad
         bad = [k for k in sa if not torch.equal(sa[k], sb[k])]
         assert not bad, (i, bad)
+
+
+def test_chunked_graph_matches_step_loop():
+    """learner.graph_chunk: run_steps replays runs of m consecutive hoisted steps (even start, no
+    target sync inside, previous step hoisted) as one graph.  Against the plain step loop, target
+    sync every 7 steps (chunks around the sync steps fall back to single-step graphs): the same
+    state bitwise after every run_steps call; at least two chunks replayed; error word 0."""
+    rp0, plain = _engine(False, B=16, interval=7)
+    rp1, ch = _engine(True, B=16, interval=7, **{"learner.graph_chunk": 4})
+    plain.capture(warmup=0)
+    ch.capture(warmup=0)
+    assert ch._cgraph is not None
+    for n in (1, 9, 4, 5, 8):
+        for _ in range(n):
+            plain.step()
+        ch.run_steps(n)
+        torch.cuda.synchronize()
+        a, b = _state(rp0, plain), _state(rp1, ch)
+        bad = [k for k in a if not torch.equal(a[k], b[k])]
+        assert not bad, (n, ch.steps_done, bad)
+    assert ch.steps_done == plain.steps_done == 27
+    assert getattr(ch, "chunks_run", 0) >= 2
+    assert plain.error_word() == 0 and ch.error_word() == 0
