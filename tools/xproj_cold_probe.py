@@ -1,6 +1,6 @@
 """Why does the split x-projection take ~120 us inside the learner step but ~97 us back to back
-(tools/xproj_wg_scaling.py)?  The bench-shape launch (5440 + 5120 rows, 192x256 tile) timed alone
-per rep after: nothing (warm), a 512 MB scratch write (cold MALL / L2, dirty lines), a 64 MB rewrite
+(tools/xproj_wg_scaling.py)?  The bench-shape launch (5440 + 5120 rows, 192x256 tile) timed per rep
+(events around it, no host sync between reps) after: nothing (warm), a 512 MB scratch write (cold MALL / L2, dirty lines), a 64 MB rewrite
 of its own A operand (A just produced, as the torso kernel leaves it).  Medians of 30 reps, us.
   python tools/xproj_cold_probe.py"""
 import json
@@ -50,14 +50,15 @@ def pre_rewrite_a():
 res = {}
 for name, pre in (("warm", pre_none), ("after_512MB_write", pre_scratch), ("after_A_rewrite", pre_rewrite_a),
                   ("warm2", pre_none)):
-    ts = []
-    for _ in range(35):
+    evs = []
+    for _ in range(35):   # no host sync between reps: the GPU stays busy (clocks steady)
         pre()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         gemm_sp(pr, cfg=7, ws=ws, tickets=tk)
         e1.record()
-        torch.cuda.synchronize()
-        ts.append(e0.elapsed_time(e1) * 1e3)
+        evs.append((e0, e1))
+    torch.cuda.synchronize()
+    ts = [a.elapsed_time(b) * 1e3 for a, b in evs]
     res[name] = round(statistics.median(ts[5:]), 1)
 print(json.dumps(res))
