@@ -414,7 +414,8 @@ __global__ __launch_bounds__(256) void prio_tail_kernel(
     const float* __restrict__ priority, float* __restrict__ tree, TreeGeom g, int T, int upd_lo,
     int upd_hi, int cap_e, float eta, int* __restrict__ dirty, int* __restrict__ count,
     int max_dirty, unsigned* __restrict__ sync, int64_t* __restrict__ step, int reset_count,
-    int nprio, int npart, int skip, const PackStepArgs pk, const SampleBatchArgs sb) {
+    int nprio, int npart, int skip, const PackStepArgs pk, const SampleBatchArgs sb,
+    unsigned* __restrict__ wait) {
   __shared__ int last;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   // role of this block among the npart participants.  skip > 0 (the hoisted step): blocks b with
@@ -428,6 +429,23 @@ __global__ __launch_bounds__(256) void prio_tail_kernel(
     role = (blockIdx.x >> 3) * (8 - skip) + x - skip;
   }
   if (role >= npart) return;
+  if (wait && role < nprio) {
+    // the hoisted step's early fork: launched beside the TD kernel, the tail workgroups wait for
+    // its done flag (the priorities it wrote are performed write-through), then acquire; bounded
+    // (sync[3] bit 2 on a timeout); the last arriver below clears the flag
+    if (threadIdx.x == 0) {
+      unsigned spins = 0;
+      while (__hip_atomic_load(wait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 22)) {
+          __hip_atomic_fetch_or(sync + 3, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+  }
   if (role >= nprio) {
     const int64_t pb = role - nprio, npb = npart - nprio;
     pack_step_items(pk, pb * blockDim.x + threadIdx.x, npb * blockDim.x);
@@ -499,6 +517,7 @@ __global__ __launch_bounds__(256) void prio_tail_kernel(
         *step += 1;
     }
     if (reset_count) *count = 0;
+    if (wait) __hip_atomic_store(wait, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (sb.B > 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_store(sync + 4, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -794,12 +813,21 @@ extern "C" int r2_seqprio_refresh(const int* starts, int B, const uint8_t* is_st
 // allow the fold (tree_update_fused's conditions) or B > 256 (all workgroups must be resident)
 extern "C" int r2_get_num_cus();   // lstm_persist.hip: CUs of the learner's stream
 
+// TD done flag the NEXT r2_prio_tail_sample launch on this host thread waits for (consumed by it):
+// the hoisted step forks its side branch before the TD launch (td.hip TdDuelArgs::done)
+static thread_local unsigned* g_prio_wait = nullptr;
+extern "C" int r2_prio_tail_set_wait(unsigned* wait) {
+  g_prio_wait = wait;
+  return 0;
+}
+
 static int prio_tail_launch(const int* starts, int B, const uint8_t* is_start, const float* priority,
                             float* tree, const int64_t* offs, const int64_t* sizes, int levels,
                             int T, int upd_lo, int upd_hi, int cap_e, float eta, int* dirty,
                             int* count, int max_dirty, unsigned* sync, int64_t* step,
                             int reset_count, const PackStepArgs* pk, void* stream,
-                            const SampleBatchArgs* sb = nullptr, int skip = 0) {
+                            const SampleBatchArgs* sb = nullptr, int skip = 0,
+                            unsigned* wait = nullptr) {
   if (upd_hi - upd_lo + T - 1 > 2048) return -2;
   if (B <= 0 || B > 256) return -3;
   {   // every workgroup must be resident at once (grid barriers): B <= CUs x blocks per CU
@@ -829,7 +857,7 @@ static int prio_tail_launch(const int* starts, int B, const uint8_t* is_start, c
   if (skip) grid = (npart + 8 - skip - 1) / (8 - skip) * 8;
   hipLaunchKernelGGL(prio_tail_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, starts, is_start,
                      priority, tree, g, T, upd_lo, upd_hi, cap_e, eta, dirty, count, max_dirty, sync,
-                     step, reset_count, B, npart, skip, pk ? *pk : none, sb ? *sb : no_sample);
+                     step, reset_count, B, npart, skip, pk ? *pk : none, sb ? *sb : no_sample, wait);
   R2_CHECK_LAUNCH();
   return 0;
 }
@@ -924,10 +952,12 @@ extern "C" int r2_prio_tail_sample(const int* starts, int B, const uint8_t* is_s
                                    const int64_t* c, int h_f32, unsigned* qreset, int skip_xcds,
                                    void* stream) {
   if (!step || nstate < 0 || nstate > 3) return -1;
+  unsigned* const wait = g_prio_wait;
+  g_prio_wait = nullptr;
   const SampleBatchArgs sb = make_sample_args(tree, offs, sizes, levels, B, seed, step, s_starts,
                                               s_probs, s_rows, Tn, cap_e, H, nstate, hs, off, h, c,
                                               h_f32, qreset);
   return prio_tail_launch(starts, B, is_start, priority, tree, offs, sizes, levels, T, upd_lo, upd_hi,
                           cap_e, eta, dirty, count, max_dirty, sync, step, 1, nullptr, stream, &sb,
-                          skip_xcds);
+                          skip_xcds, wait);
 }

@@ -216,6 +216,10 @@ struct TdDuelArgs {
   int fuse_fwd;
   // optional stage stamps (r2_td_duel_set_trace): [workgroup][wave][12] s_memrealtime (100 MHz)
   long long* trace;
+  // optional (r2_td_duel_set_done, the hoisted step's early fork): the row priorities go out
+  // write-through and drained before the arrival ticket, and the last arriver stores 1 here --
+  // the priority tail launched beside this kernel waits for it (replay.hip prio_tail_kernel)
+  unsigned* done;
 };
 
 // head.hip dueling_fwd_kernel for one row on one wave (same order of operations, same
@@ -443,7 +447,11 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
       lsum = wb * 0.5f * delta * delta;
       const float ad = fabsf(delta);
       if (a.td_abs) a.td_abs[i] = ad;
-      if (own) a.priority[row] = powf(ad + a.prio_eps, a.alpha);
+      if (own) {
+        const float pv = powf(ad + a.prio_eps, a.alpha);
+        if (args.done) __hip_atomic_store(a.priority + row, pv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else a.priority[row] = pv;
+      }
     }
     if (lane < a.A) a.dq[(size_t)i * a.A + lane] = lane == act ? g : 0.f;
     TD_STAMP(9);
@@ -517,6 +525,7 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
   // ---- loss: wave partial (lane 0) -> workgroup partial -> arrival ticket (before dh: the
   // atomic's round trip overlaps the product) -> the last arriver sums in workgroup order
   if (lane == 0) lred[wave] = lsum;
+  if (args.done) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // priorities performed
   __syncthreads();
   TD_STAMP(4);
   unsigned tk = 0;
@@ -559,6 +568,7 @@ __global__ __launch_bounds__(1024) void td_duel_kernel(const TdDuelArgs args) {
   __syncthreads();
   TD_STAMP(6);
   if (!last) return;
+  if (args.done && tid == 0) __hip_atomic_store(args.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   float s = 0.f;
   for (unsigned g = tid; g < gridDim.x; g += NW * 64)
     s += __hip_atomic_load(a.part + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -609,6 +619,12 @@ extern "C" int r2_td_duel_set_trace(long long* tr) {
   g_td_trace = tr;
   return 0;
 }
+// done flag of the NEXT r2_td_duel_dh launch on this host thread (consumed by it; TdDuelArgs::done)
+static thread_local unsigned* g_td_done = nullptr;
+extern "C" int r2_td_duel_set_done(unsigned* done) {
+  g_td_done = done;
+  return 0;
+}
 extern "C" int r2_td_duel_fwd_set(const int64_t* fwd) {
   g_td_fwd_on = fwd != nullptr;
   if (fwd)
@@ -644,6 +660,8 @@ extern "C" int r2_td_duel_dh(const float* q_sa, const float* q_arg, const float*
                              const float* w2, bf16* dz, float* dva, int HD, bf16* dz_lo,
                              const float* dp, const bf16* w1t, const bf16* w1t_lo, float* dh, int H,
                              void* stream) {
+  unsigned* const td_done = g_td_done;
+  g_td_done = nullptr;
   if (B > 256) return -1;
   if (A < 1 || A > 64) return -3;             // one lane per action
   const int grid = (Tl * B + 15) / 16;
@@ -654,6 +672,8 @@ extern "C" int r2_td_duel_dh(const float* q_sa, const float* q_arg, const float*
                 prio_eps, beta, value_rescale, dp},
                zr, w2, dz, dva, dz_lo, w1t, w1t_lo, dh};
   d.fuse_fwd = 0;
+  d.done = td_done;
+  if (td_done && !priority) return -8;
   {   // never bake a stamp buffer into a captured launch
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     const bool cap = hipStreamIsCapturing((hipStream_t)stream, &st) == hipSuccess &&

@@ -160,6 +160,9 @@ class LearnerConfig:
     # steps (no target sync inside, the previous step sampled) as ONE captured graph, so the
     # ~5 us boundary between two graph replays is paid once per chunk; 1 = a graph per step
     graph_chunk: int = 8
+    # hoisted step: fork the side branch before the TD launch instead of after it; the priority
+    # tail, launched beside TD, waits for TD's done flag on the device (td.hip TdDuelArgs::done)
+    hoist_early_fork: bool = True
     # (removed A/B knobs whose alternative lost, record in profiles/: lstm_tag_words = False, the
     # 8-byte hand-off granules (archive/bench_r02_tag_words_ab.log); sp_gemm6 = False, gemm5
     # (r03_gemm6_ab.txt); sp_gemm_order = 0 (r05_gemm_item_order.txt); sp_heads_cfg

@@ -331,6 +331,9 @@ class LearnerEngine:
         self.gamma_n = float(lc.gamma ** n)
         self.td_part = z(4096)                          # TD loss partials, one per workgroup
         self.td_ticket = z(1, dt=torch.int32)           # reset by the kernel's last workgroup
+        # the TD launch's done flag (hoisted step, early fork): set by its last workgroup, waited
+        # on and cleared by the priority tail beside it
+        self.td_done = z(1, dt=torch.int32) if self.device.type == "cuda" else None
         # fused torso backward: per-workgroup gradient slabs + destination map (allocated here,
         # never lazily: the step must be capturable without warm-up)
         if self.fwd_geom is not None:
@@ -463,7 +466,7 @@ class LearnerEngine:
             self._side = torch.cuda.Stream(device=self.device)
         return self._side
 
-    def _hoist_side(self, torso: bool, after_td):
+    def _hoist_side(self, torso: bool, after_td, td_wait: bool = False):
         """The side branch, forked at event ``after_td`` (recorded right after the TD launch):
         priority tail(k) + step counter, sample(k+1) into the other set (zeroing the frame
         queue), and (``torso``) the target-net frames of step k+1."""
@@ -475,9 +478,14 @@ class LearnerEngine:
             # one launch: the tail ends the step (counter + 1) and samples the next batch from the
             # repaired tree (replay.hip r2_prio_tail_sample); else the separate launches
             S, states = self._sample_dst(nxt)
-            if not rp.prio_tail_sample(self.starts, B, self.Lb, self.T, S["starts"], S["probs"],
-                                       S["rows"], self.Tn, states, self.sp, self.tq,
-                                       skip_xcds=self._bptt_xcds()):
+            if td_wait:
+                check(kernels().r2_prio_tail_set_wait(ptr(self.td_done)), "prio_tail_set_wait")
+            ok = rp.prio_tail_sample(self.starts, B, self.Lb, self.T, S["starts"], S["probs"],
+                                     S["rows"], self.Tn, states, self.sp, self.tq,
+                                     skip_xcds=self._bptt_xcds())
+            if not ok and td_wait:   # the separate launches cannot wait for TD on the device
+                raise RuntimeError("prio_tail_sample refused the early-fork launch")
+            if not ok:
                 if not rp.prio_tail(self.starts, B, self.Lb, self.T, True):
                     rp.refresh_sequences(self.starts, B, self.Lb, self.T)
                     if not rp.update_tree_and_end_step(True):
@@ -521,16 +529,25 @@ class LearnerEngine:
         self._hoist_due = due
         if inm == "P":
             self._sample(qreset=self.tq)
-        self._forward_rest()
+        early = bool(self.cfg.learner.hoist_early_fork) and self.td_done is not None
+        if early:
+            # fork before the TD launch (the side queue's start latency, ~13 us after its fork
+            # event, then overlaps TD); the priority tail waits for TD's done flag on the device
+            self._early_fork = torch.cuda.Event()
+        try:
+            self._forward_rest()
+        finally:
+            after_td, self._early_fork = getattr(self, "_early_fork", None), None
         main = torch.cuda.current_stream(self.device)
-        after_td = torch.cuda.Event()
-        after_td.record(main)
+        if not early:
+            after_td = torch.cuda.Event()
+            after_td.record(main)
         # the BPTT and the weight-gradient group are issued (captured) BEFORE the side branch:
         # the graph keeps the first dependent of the TD node on the TD's queue, so the critical
         # path does not pay a cross-queue hand-off (measured: the BPTT started 11 us after the TD
         # when the side branch was captured first)
         self._backward_core()
-        side = self._hoist_side(torso=not due, after_td=after_td)
+        side = self._hoist_side(torso=not due, after_td=after_td, td_wait=early)
         # join before the conv backward: the side branch ends with the BPTT (joining at the end of
         # the step instead let the side torso slow the conv backward: measured slower)
         main.wait_stream(side)
@@ -915,6 +932,12 @@ class LearnerEngine:
             fuse_dh = lc.td_fuse_dh and L.H == 256 and not self._dh_in_bptt()
             w1t = ptr(pk["head1T"]) if fuse_dh else 0
             w1t_lo = ptr(self.pk_lo["head1T"]) if fuse_dh and self.sp else 0
+            ef = getattr(self, "_early_fork", None)
+            if ef is not None:
+                # hoisted step, early fork: the side branch forks here, before the TD launch, and
+                # its priority tail waits on the device for this launch's done flag
+                ef.record(torch.cuda.current_stream(self.device))
+                k.r2_td_duel_set_done(ptr(self.td_done))
             if fuse_fwd:
                 z_on, z_tg, z_nx = self._zs[0], self._zs[1], self._zs[2]
                 self._fwd_arr = np.asarray(
@@ -925,6 +948,8 @@ class LearnerEngine:
             rc_ = k.r2_td_duel_dh(*targs, ptr(self.zr_on[: Ll * B]), ptr(pk["head_w2"]), ptr(self.dz),
                                   ptr(self.dva), L.HD, ptr(self.dz_lo), dp, w1t, w1t_lo,
                                   ptr(self.dh) if fuse_dh else 0, L.H, s)
+            if ef is not None and rc_ != 0:
+                raise RuntimeError("td_duel refused the early-fork launch (code %d)" % rc_)
             if rc_ == 0:
                 self._duel_done = True
                 self._dh_done = fuse_dh or self._dh_in_bptt()

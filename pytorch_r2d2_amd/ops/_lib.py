@@ -68,6 +68,8 @@ _SIGS = {
     "r2_sample_batch_q": [P, P, P, I, I, U64, P, P, P, P, I, I, I, I, P, P, P, P, I, P, P],
     "r2_torso_fwd_sp_multi": [P, P, I, I, P],
     "r2_torso_sp_debug": [I],
+    "r2_td_duel_set_done": [P],
+    "r2_prio_tail_set_wait": [P],
     "r2_torso_sp_trace": [P],
     "r2_torso_bwd_sp_trace": [P],
     "r2_torso_bwd_sp_debug": [I],

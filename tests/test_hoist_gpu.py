@@ -36,16 +36,18 @@ def _state(rp, eng):
     return out
 
 
-@pytest.mark.parametrize("graph,B", [(True, 64), (False, 64), (True, 16), (False, 8)])
-def test_hoisted_step_is_bitwise_the_plain_step(graph, B):
+@pytest.mark.parametrize("graph,B,early", [(True, 64, False), (False, 64, False), (True, 16, False),
+                                           (False, 8, False), (True, 64, True), (False, 16, True)])
+def test_hoisted_step_is_bitwise_the_plain_step(graph, B, early):
     """Bench shape (B=64, 40 + 40, n=5, fixed target), target sync every 3 steps (steps 2, 5, 8
     sync: the step after each runs the full target torso), one invalidation in the middle (the
     next step samples at its start): weights, optimizer moments, every packed layout, priorities,
     sum tree and step counter equal the plain engine's after every step; error word 0.  B 8 / 16:
     one batch tile, an odd count of recurrence groups packed in XCD pairs (the head-gradient
-    helpers' ordinals, lstm_persist.hip xcd_map 3)."""
+    helpers' ordinals, lstm_persist.hip xcd_map 3).  ``early``: the side branch forks before the
+    TD launch and its priority tail waits for TD's done flag on the device."""
     rp0, plain = _engine(False, B=B, graph=graph)
-    rp1, hoist = _engine(True, B=B, graph=graph)
+    rp1, hoist = _engine(True, B=B, graph=graph, **{"learner.hoist_early_fork": early})
     assert hoist.hoist and not plain.hoist
     if graph:
         plain.capture(warmup=0)
