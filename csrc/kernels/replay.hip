@@ -951,9 +951,9 @@ extern "C" int r2_prio_tail_sample(const int* starts, int B, const uint8_t* is_s
                                    const int64_t* hs, const int* off, const int64_t* h,
                                    const int64_t* c, int h_f32, unsigned* qreset, int skip_xcds,
                                    void* stream) {
-  if (!step || nstate < 0 || nstate > 3) return -1;
-  unsigned* const wait = g_prio_wait;
+  unsigned* const wait = g_prio_wait;   // consumed by this call whatever it returns
   g_prio_wait = nullptr;
+  if (!step || nstate < 0 || nstate > 3) return -1;
   const SampleBatchArgs sb = make_sample_args(tree, offs, sizes, levels, B, seed, step, s_starts,
                                               s_probs, s_rows, Tn, cap_e, H, nstate, hs, off, h, c,
                                               h_f32, qreset);

@@ -73,6 +73,18 @@ def _graph_upload(g) -> None:
         pass
 
 
+def _dispatch_serialized() -> bool:
+    """True when kernel dispatches run one at a time (rocprofv3 counter collection / thread trace,
+    AMD_SERIALIZE_KERNEL, HIP_LAUNCH_BLOCKING).  The hoisted step's early fork has a kernel on the
+    side queue wait on the device for the TD kernel of the main queue, which a serialised
+    dispatcher never runs beside it (a bounded stall and an error word), so it forks after TD there."""
+    import os
+    env = os.environ
+    on = lambda k: env.get(k, "0").strip().lower() not in ("", "0", "false", "no", "off")  # noqa: E731
+    return (on("ROCPROF_COUNTER_COLLECTION") or on("ROCPROF_ADVANCED_THREAD_TRACE")
+            or on("HIP_LAUNCH_BLOCKING") or env.get("AMD_SERIALIZE_KERNEL", "0") not in ("", "0"))
+
+
 def device_cus(device) -> int:
     """Multiprocessor (CU) count of ``device`` (256 on a whole MI355X; 256 for CPU tensors)."""
     d = torch.device(device)
@@ -483,8 +495,14 @@ class LearnerEngine:
             ok = rp.prio_tail_sample(self.starts, B, self.Lb, self.T, S["starts"], S["probs"],
                                      S["rows"], self.Tn, states, self.sp, self.tq,
                                      skip_xcds=self._bptt_xcds())
-            if not ok and td_wait:   # the separate launches cannot wait for TD on the device
-                raise RuntimeError("prio_tail_sample refused the early-fork launch")
+            if not ok and td_wait:
+                # refused on the host (shape / co-residency, e.g. ranks sharing the GPU): the
+                # separate launches cannot wait for TD on the device, so this branch also waits for
+                # the event after the TD launch; TD's unconsumed done flag is cleared, and this
+                # engine stops forking early
+                side.wait_event(self._early_post)
+                self.td_done.zero_()
+                self._early_refused = True
             if not ok:
                 if not rp.prio_tail(self.starts, B, self.Lb, self.T, True):
                     rp.refresh_sequences(self.starts, B, self.Lb, self.T)
@@ -529,7 +547,8 @@ class LearnerEngine:
         self._hoist_due = due
         if inm == "P":
             self._sample(qreset=self.tq)
-        early = bool(self.cfg.learner.hoist_early_fork) and self.td_done is not None
+        early = (bool(self.cfg.learner.hoist_early_fork) and self.td_done is not None
+                 and not getattr(self, "_early_refused", False) and not _dispatch_serialized())
         if early:
             # fork before the TD launch (the side queue's start latency, ~13 us after its fork
             # event, then overlaps TD); the priority tail waits for TD's done flag on the device
@@ -950,6 +969,9 @@ class LearnerEngine:
                                   ptr(self.dh) if fuse_dh else 0, L.H, s)
             if ef is not None and rc_ != 0:
                 raise RuntimeError("td_duel refused the early-fork launch (code %d)" % rc_)
+            if ef is not None:   # the fallback's fork point (_hoist_side: a refused fused tail)
+                self._early_post = torch.cuda.Event()
+                self._early_post.record(torch.cuda.current_stream(self.device))
             if rc_ == 0:
                 self._duel_done = True
                 self._dh_done = fuse_dh or self._dh_in_bptt()
