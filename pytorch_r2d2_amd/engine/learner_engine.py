@@ -1568,12 +1568,19 @@ class LearnerEngine:
         pool = None
         for fn in segs:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, pool=pool):
+            with torch.cuda.graph(g, pool=pool, capture_error_mode=self._capture_mode()):
                 fn()
             pool = g.pool()
             self.graphs.append(g)
         torch.cuda.synchronize(self.device)
         self.graph = True
+
+    def _capture_mode(self) -> str:
+        """Graph capture error mode: with a process group the RCCL watchdog thread polls the events
+        of earlier collectives while this thread captures, which global mode turns into a capture
+        error (hipErrorStreamCaptureUnsupported on the watchdog, seen as a flaky forced-DP test);
+        thread-local mode confines the capture rules to this thread."""
+        return "thread_local" if self.dp else "global"
 
     def _pg_backend(self) -> str:
         """Backend of the DP process group (only RCCL collectives can be graph-captured; gloo
@@ -1616,7 +1623,8 @@ class LearnerEngine:
         every segment boundary disappears."""
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, pool=self.graphs[0].pool() if self.graphs else None):
+        with torch.cuda.graph(g, pool=self.graphs[0].pool() if self.graphs else None,
+                              capture_error_mode=self._capture_mode()):
             self._dp_step_body()
         torch.cuda.synchronize(self.device)
         self._one_graph = g
