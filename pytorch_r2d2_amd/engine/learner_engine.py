@@ -553,10 +553,14 @@ class LearnerEngine:
             # fork before the TD launch (the side queue's start latency, ~13 us after its fork
             # event, then overlaps TD); the priority tail waits for TD's done flag on the device
             self._early_fork = torch.cuda.Event()
+            self._early_post = None
         try:
             self._forward_rest()
         finally:
             after_td, self._early_fork = getattr(self, "_early_fork", None), None
+        # (the fork is recorded only by the fused TD + head launch, td_fuse_head_bwd; without it
+        # the side branch forks after TD as before)
+        early = early and getattr(self, "_early_post", None) is not None
         main = torch.cuda.current_stream(self.device)
         if not early:
             after_td = torch.cuda.Event()

@@ -185,3 +185,22 @@ def test_chunked_graph_matches_step_loop():
     assert ch.steps_done == plain.steps_done == 27
     assert getattr(ch, "chunks_run", 0) >= 2
     assert plain.error_word() == 0 and ch.error_word() == 0
+
+
+def test_hoisted_step_without_fused_td_forks_after_td():
+    """learner.td_fuse_head_bwd off: the TD launch is not the fused kernel that records the early
+    fork and sets the done flag, so the side branch forks after TD as before -- still bitwise the
+    plain step, error word 0."""
+    kw = {"learner.td_fuse_head_bwd": False}
+    rp0, plain = _engine(False, B=16, **kw)
+    rp1, hoist = _engine(True, B=16, **kw)
+    plain.capture(warmup=0)
+    hoist.capture(warmup=0)
+    for i in range(4):
+        plain.step()
+        hoist.step()
+        torch.cuda.synchronize()
+        a, b = _state(rp0, plain), _state(rp1, hoist)
+        bad = [k for k in a if not torch.equal(a[k], b[k])]
+        assert not bad, (i, bad)
+    assert plain.error_word() == 0 and hoist.error_word() == 0
